@@ -1,0 +1,176 @@
+"""ctypes wrapper for the C oracle (oracle/sa_oracle.c) -- TEST INFRASTRUCTURE.
+
+Only tests/, bench.py's cpu_baseline leg and __graft_entry__.smoke() may import
+this module, and only as the checker / CPU baseline.  The product path
+(sequence-aligner_amd/) never links or calls it.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "liborc.so")
+
+ORC_OK, ORC_E_INPUT, ORC_E_NPE, ORC_E_MATCH, ORC_E_INDEX = 0, -1, -2, -3, -4
+
+
+class Settings(C.Structure):
+    _fields_ = [("kmer_size", C.c_int32), ("min_overlap", C.c_int32), ("max_ignore", C.c_int32),
+                ("gap_open", C.c_int32), ("gap_extend", C.c_int32), ("min_collisions", C.c_int32),
+                ("max_collisions", C.c_int32), ("min_identity", C.c_float), ("kmer_edge", C.c_float),
+                ("kmer_center", C.c_float), ("cost", C.c_int32 * 16)]
+
+
+class Align(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("lead", "trail", "is_dud", "start_i", "start_j", "end_i", "end_j",
+                                         "correct", "error", "len_a", "len_b", "valid", "ovl_valid",
+                                         "ahg", "bhg")]
+
+
+ALIGN_FIELDS = [f[0] for f in Align._fields_]
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = C.CDLL(LIB)
+        P = C.POINTER
+        L.orc_default_settings.argtypes = [P(Settings)]
+        L.orc_create_from_fasta.argtypes = [C.c_char_p, P(C.c_void_p)]
+        L.orc_create_from_buffers.argtypes = [C.c_char_p, P(C.c_uint64), C.c_uint32, P(C.c_void_p)]
+        L.orc_destroy.argtypes = [C.c_void_p]
+        L.orc_num_reads.argtypes = [C.c_void_p]
+        L.orc_num_reads.restype = C.c_uint32
+        L.orc_run.argtypes = [C.c_void_p, P(Settings), C.c_int]
+        for fn in ("orc_num_kmers", "orc_num_buckets", "orc_num_pairs", "orc_num_dispatch"):
+            getattr(L, fn).argtypes = [C.c_void_p]
+            getattr(L, fn).restype = C.c_size_t
+        L.orc_kmers.argtypes = [C.c_void_p, P(P(C.c_int32)), P(P(C.c_int32)), P(P(C.c_float))]
+        L.orc_bucket_order.argtypes = [C.c_void_p]
+        L.orc_bucket_order.restype = P(C.c_int32)
+        L.orc_pairs.argtypes = [C.c_void_p, P(P(C.c_int32)), P(P(C.c_int32)), P(P(C.c_int32))]
+        L.orc_pairs_first_order.argtypes = [C.c_void_p, P(P(C.c_int32)), P(P(C.c_int32))]
+        L.orc_dispatch.argtypes = [C.c_void_p, P(P(C.c_int32)), P(P(C.c_int32))]
+        L.orc_aligns.argtypes = [C.c_void_p]
+        L.orc_aligns.restype = P(Align)
+        L.orc_ovl.argtypes = [C.c_void_p, P(C.c_char_p)]
+        L.orc_ovl.restype = C.c_size_t
+        L.orc_align_pair.argtypes = [C.c_char_p, C.c_int32, C.c_char_p, C.c_int32, C.c_int32, C.c_int32,
+                                     P(Settings), P(Align)]
+        L.orc_trove_order.argtypes = [P(C.c_int32), C.c_size_t, P(C.c_int32), P(C.c_int32)]
+        _lib = L
+    return _lib
+
+
+def default_settings(**kw):
+    s = Settings()
+    lib().orc_default_settings(C.byref(s))
+    for k, v in kw.items():
+        if k == "cost":
+            for i, x in enumerate(np.asarray(v).reshape(16)):
+                s.cost[i] = int(x)
+        else:
+            setattr(s, k, v)
+    return s
+
+
+def _arr(ptr, n, dtype):
+    if n == 0:
+        return np.zeros(0, dtype=dtype)
+    return np.ctypeslib.as_array(ptr, shape=(n,)).astype(dtype, copy=True)
+
+
+class OracleError(RuntimeError):
+    def __init__(self, rc):
+        super().__init__("oracle error %d" % rc)
+        self.rc = rc
+
+
+class Run:
+    """Result of one calc-overlaps run of the oracle."""
+
+    def __init__(self, reads=None, fasta=None, settings=None, wide=False, keep_kmers=False):
+        L = lib()
+        h = C.c_void_p()
+        if fasta is not None:
+            rc = L.orc_create_from_fasta(fasta.encode(), C.byref(h))
+        else:
+            bases = b"".join(r.encode() if isinstance(r, str) else bytes(r) for r in reads)
+            off = np.zeros(len(reads) + 1, dtype=np.uint64)
+            off[1:] = np.cumsum([len(r) for r in reads])
+            rc = L.orc_create_from_buffers(bases, off.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                           len(reads), C.byref(h))
+        if rc:
+            raise OracleError(rc)
+        self.settings = settings or default_settings()
+        try:
+            rc = L.orc_run(h, C.byref(self.settings), 1 if wide else 0)
+            self.rc = rc
+            self.n_reads = L.orc_num_reads(h)
+            if keep_kmers:
+                hp, ip, lp = C.POINTER(C.c_int32)(), C.POINTER(C.c_int32)(), C.POINTER(C.c_float)()
+                L.orc_kmers(h, C.byref(hp), C.byref(ip), C.byref(lp))
+                nk = L.orc_num_kmers(h)
+                self.kmer_hash = _arr(hp, nk, np.int32)
+                self.kmer_id = _arr(ip, nk, np.int32)
+                self.kmer_loc = _arr(lp, nk, np.float32)
+                nb = L.orc_num_buckets(h)
+                self.bucket_order = _arr(L.orc_bucket_order(h), nb, np.int32)
+            if rc:
+                raise OracleError(rc)
+            f, s_, c = C.POINTER(C.c_int32)(), C.POINTER(C.c_int32)(), C.POINTER(C.c_int32)()
+            L.orc_pairs(h, C.byref(f), C.byref(s_), C.byref(c))
+            n = L.orc_num_pairs(h)
+            self.pair_fst, self.pair_snd, self.pair_cnt = (_arr(f, n, np.int32), _arr(s_, n, np.int32),
+                                                           _arr(c, n, np.int32))
+            if not wide:
+                L.orc_pairs_first_order(h, C.byref(f), C.byref(s_))
+                self.first_fst, self.first_snd = _arr(f, n, np.int32), _arr(s_, n, np.int32)
+            d1, d2 = C.POINTER(C.c_int32)(), C.POINTER(C.c_int32)()
+            L.orc_dispatch(h, C.byref(d1), C.byref(d2))
+            nd = L.orc_num_dispatch(h)
+            self.lead, self.trail = _arr(d1, nd, np.int32), _arr(d2, nd, np.int32)
+            ap = L.orc_aligns(h)
+            self.aligns = np.zeros((nd, len(ALIGN_FIELDS)), dtype=np.int32)
+            if nd:
+                raw = np.ctypeslib.as_array(C.cast(ap, C.POINTER(C.c_int32)), shape=(nd * len(ALIGN_FIELDS),))
+                self.aligns[:] = raw.reshape(nd, len(ALIGN_FIELDS))
+            t = C.c_char_p()
+            ln = L.orc_ovl(h, C.byref(t))
+            self.ovl = C.string_at(t, ln) if ln else b""
+        finally:
+            L.orc_destroy(h)
+
+    def align_field(self, name):
+        return self.aligns[:, ALIGN_FIELDS.index(name)]
+
+
+def align_pair(A, B, id_a=1, id_b=2, settings=None):
+    s = settings or default_settings()
+    out = Align()
+    rc = lib().orc_align_pair(A.encode(), len(A), B.encode(), len(B), id_a, id_b, C.byref(s), C.byref(out))
+    if rc:
+        raise OracleError(rc)
+    return {n: getattr(out, n) for n in ALIGN_FIELDS}
+
+
+def trove_order(keys):
+    keys = np.ascontiguousarray(keys, dtype=np.int32)
+    out = np.zeros(len(keys), dtype=np.int32)
+    cap = C.c_int32()
+    rc = lib().orc_trove_order(keys.ctypes.data_as(C.POINTER(C.c_int32)), len(keys),
+                               out.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(cap))
+    if rc:
+        raise OracleError(rc)
+    return out, cap.value

@@ -1,0 +1,153 @@
+"""Oracle pinning: the C restatement against every known answer available.
+
+No output of the Scala reference exists (no JVM; none shipped), so the oracle is
+pinned by (a) the Scala-literal Python transliteration's golden vectors for
+crp177 (tests/golden/make_crp177_golden.py), (b) known answers taken from the
+reference's own files (HOXD1.txt, the README record sample, Trove's prime
+table read from lib/trove.jar as data), and (c) arithmetic facts derived from
+the code (SURVEY.md E2 cut table, E5 widths, E1 capacity chain).
+"""
+import bisect
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+import helpers as H
+
+GOLD = H.GOLDEN
+
+
+@pytest.mark.parametrize("k", [12, 15])
+def test_crp177_matches_literal_restatement(oracle_mod, k):
+    r = oracle_mod.Run(fasta=H.crp177_path(), settings=oracle_mod.default_settings(kmer_size=k),
+                       keep_kmers=True)
+    g = np.load(os.path.join(GOLD, "crp177_k%d.npz" % k))
+    assert open(os.path.join(GOLD, "crp177_k%d.ovl" % k), "rb").read() == r.ovl
+    np.testing.assert_array_equal(r.pair_fst, g["pair_fst"])
+    np.testing.assert_array_equal(r.pair_snd, g["pair_snd"])
+    np.testing.assert_array_equal(r.pair_cnt, g["pair_cnt"])
+    np.testing.assert_array_equal(r.first_fst, g["first_fst"])
+    np.testing.assert_array_equal(r.first_snd, g["first_snd"])
+    np.testing.assert_array_equal(r.lead, g["lead"])
+    np.testing.assert_array_equal(r.trail, g["trail"])
+    np.testing.assert_array_equal(r.bucket_order, g["bucket_order"])
+
+
+def test_small_random_matches_literal(oracle_mod):
+    import literal as L
+    reads = H.synth_reads(60, 80, 900, gc=0.4, seed=7)
+    text = H.reads_fasta_bytes(reads).decode()
+    for k, wid in ((10, 0.95), (13, 0.98)):
+        s = oracle_mod.default_settings(kmer_size=k, min_identity=wid, min_collisions=3)
+        r = oracle_mod.Run(reads=reads, settings=s)
+        out, _, _ = L.run(text, L.AlignSettings(k=k, min_identity=wid, min_coll=3))
+        assert r.ovl.decode() == out
+
+
+def test_hoxd1_equals_default_matrix(oracle_mod):
+    """amos/HOXD1.txt (readHOXD format) == defaultHOXD (BioLibs.scala:122-140)."""
+    rows = [l.split(",") for l in open(os.path.join(GOLD, "HOXD1.txt")).read().strip().split("\n")[1:]]
+    cols = [c.strip() for c in rows[0][1:]]
+    idx = {"A": 0, "C": 1, "G": 2, "T": 3}
+    m = np.zeros((4, 4), dtype=np.int32)
+    for row in rows[1:]:
+        for j, v in enumerate(row[1:]):
+            m[idx[row[0].strip()], idx[cols[j]]] = int(v)
+    s = oracle_mod.default_settings()
+    np.testing.assert_array_equal(np.array(list(s.cost)).reshape(4, 4), m)
+
+
+def test_trove_capacity_chain_and_order(oracle_mod):
+    """E1: THash(10,0.5f) starts at nextPrime(20)=23, grows to nextPrime(cap<<1)."""
+    primes = json.load(open(os.path.join(GOLD, "trove_primes.json")))["sorted"]
+    assert len(primes) == 245
+    np_ = lambda x: primes[bisect.bisect_left(primes, x)]
+    chain = [np_(20)]
+    for _ in range(20):
+        chain.append(np_(chain[-1] << 1))
+    assert chain[:21] == [23, 47, 97, 197, 397, 797, 1597, 3203, 6421, 12853, 25717, 51437, 102877,
+                          205759, 411527, 823117, 1646237, 3292489, 6584983, 13169977, 26339969]
+    # keys smaller than the capacity iterate in descending order
+    order, cap = oracle_mod.trove_order(np.arange(1, 12, dtype=np.int32))
+    assert cap == 23 and list(order) == list(range(11, 0, -1))
+    # the 12th key overflows maxSize = min(22, (int)(23*0.5f)) = 11 -> rehash to 47
+    order, cap = oracle_mod.trove_order(np.arange(1, 13, dtype=np.int32))
+    assert cap == 47
+    # collisions probe downward by 1 + h % (cap-2): keys 0 and 23 share slot 0
+    order, cap = oracle_mod.trove_order(np.array([0, 23], dtype=np.int32))
+    assert cap == 23 and list(order) == [23, 0]  # 23 lands at 0 - (1 + 23 % 21) + 23 = 20
+
+
+def _cuts(L, k, edge=np.float32(0.4), center=np.float32(0.4)):
+    d = np.float32(L - k)
+    loc = np.arange(L - k + 1, dtype=np.float32) / d
+    head, tail = edge, np.float32(1) - edge
+    ml, mt = np.float32(0.5) - center * np.float32(0.5), np.float32(0.5) + center * np.float32(0.5)
+    st = np.nonzero(loc <= head)[0]
+    md = np.nonzero((ml <= loc) & (loc <= mt))[0]
+    en = np.nonzero(tail <= loc)[0]
+    return (st.min(), st.max()), (md.min(), md.max()), (en.min(), en.max())
+
+
+@pytest.mark.parametrize("L,k,st,md,en", [
+    (100, 12, (0, 35), (27, 61), (53, 88)), (100, 15, (0, 34), (26, 59), (51, 85)),
+    (500, 15, (0, 194), (146, 339), (291, 485)), (500, 12, (0, 195), (147, 341), (293, 488)),
+    (1000, 15, (0, 394), (296, 689), (591, 985))])
+def test_region_cut_table(oracle_mod, L, k, st, md, en):
+    """E2: float32 region tags; the oracle's k-mer locs reproduce the cuts."""
+    assert _cuts(L, k) == (st, md, en)
+    r = oracle_mod.Run(reads=["ACGT" * (L // 4)], settings=oracle_mod.default_settings(kmer_size=k),
+                       keep_kmers=True)
+    loc = r.kmer_loc
+    np.testing.assert_array_equal(loc, np.arange(L - k + 1, dtype=np.float32) / np.float32(L - k))
+
+
+@pytest.mark.parametrize("L,k,w", [(100, 12, 12), (100, 15, 15), (500, 15, 15), (1000, 15, 20)])
+def test_band_width(L, k, w):
+    """E5: width = max(k, floor(|A| * (1 - 0.98f)) + 1) with a float32 product."""
+    prod = np.float32(L) * (np.float32(1) - np.float32(0.98))
+    assert max(k, int(np.floor(prod)) + 1) == w
+
+
+def test_record_format_matches_readme(oracle_mod):
+    """README:164-175 sample record; every oracle record has exactly that shape."""
+    r = oracle_mod.Run(fasta=H.crp177_path())
+    recs = r.ovl.decode().split("}\n")[:-1]
+    assert len(recs) == r.ovl.count(b"{OVL")
+    pat = re.compile(r"^\{OVL\nadj:N\nrds:\d+,\d+\nscr:0\nahg:-?\d+\nbhg:-?\d+\n$")
+    assert all(pat.match(x) for x in recs)
+
+
+def test_recall_against_amos_hash_overlap(oracle_mod):
+    """Set-level sanity only (not a parity gate): the AMOS overlapper's crp177.ovl
+    pairs (a<b, ahg==bhg) vs ours (lead,trail) -- most true dovetails recovered."""
+    amos = set(tuple(map(int, m)) for m in re.findall(r"rds:(\d+),(\d+)", open(
+        os.path.join(GOLD, "crp177_amos.ovl")).read()))
+    r = oracle_mod.Run(fasta=H.crp177_path(), settings=oracle_mod.default_settings(kmer_size=15))
+    ours = set((min(a, b), max(a, b)) for a, b in re.findall(rb"rds:(\d+),(\d+)", r.ovl) for a, b in [(int(a), int(b))])
+    recall = len(ours & amos) / len(amos)
+    assert recall > 0.85, recall
+
+
+def test_c_ruddii_reconstruction():
+    reads = H.c_ruddii_reads()
+    assert len(reads) == 32000 and all(len(x) == 100 for x in reads)
+    assert H.sha256("".join(x + "\n" for x in reads).encode()).startswith("3d8724e6")
+
+
+def test_degenerate_and_dud_cases(oracle_mod):
+    # |B| < width -> StringIndexOutOfBounds in phase 1
+    with pytest.raises(oracle_mod.OracleError):
+        oracle_mod.align_pair("ACGT" * 25, "ACGTACG", settings=oracle_mod.default_settings(kmer_size=12))
+    # no positive phase-1 cell -> degenerate backtrack (AIOOBE)
+    with pytest.raises(oracle_mod.OracleError):
+        oracle_mod.align_pair("A" * 50, "C" * 20, settings=oracle_mod.default_settings(kmer_size=12))
+    # non-ACGT aligned -> MatchError
+    with pytest.raises(oracle_mod.OracleError):
+        oracle_mod.align_pair("ACGTN" * 10, "ACGTACGTACGTACGT", settings=oracle_mod.default_settings(kmer_size=12))
+    # B's prefix absent from A's band -> dud
+    a = oracle_mod.align_pair("ACGT" * 20, "GGGGACGTACGTACGT" * 2, settings=oracle_mod.default_settings(kmer_size=12))
+    assert a["is_dud"] == 1 and a["valid"] == 0
