@@ -1,0 +1,225 @@
+"""bench.py -- MI355X hash-overlap stage benchmark (BASELINE.json configs[1] and [2]).
+
+Workload: a synthetic splitmix64 genome of
+2.5 Mbp per GPU (GC 0.50, seed 1 + rank), 100,000 error-free forward reads of
+500 bp per GPU (20x coverage), k = 15, reference defaults otherwise, wide ids
+(N >= 32,768 is outside the reference's 16-bit id domain).
+
+A step = one pass of the hash stage over the device-resident reads:
+pack -> k-mer emit -> (hash, loc) radix sort -> bucket/list build ->
+edge<->middle pair count + collision filter -> candidate ordering
+(KmerTable.calcPairData + calcDispatchData).  `value` = candidate k-mer (role)
+pairs per second summed over ranks.  The end-to-end config (banded HOXD
+dovetail alignment of every dispatched pair) is timed in a second loop and
+reported as aligned_read_pairs_per_s.
+
+Multi-GPU: one process per GPU (torchrun); each rank owns its own read shard
+and genome (weak scaling, no data-path collective: "replicas" until the
+RCCL-sharded exchange lands), barrier + max-over-ranks timing.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "sequence-aligner_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
+
+
+def splitmix64(seed, n):
+    """n consecutive outputs of splitmix64 starting from `seed` (vectorised)."""
+    x = (np.uint64(seed) + np.arange(1, n + 1, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15))
+    z = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def synth_workload(n_reads, read_len, genome_len, gc, seed):
+    """Genome: base i from splitmix64(seed) (GC with probability gc); reads start
+    uniformly in [0, G-L] (splitmix64(seed ^ 0xABCDEF)), forward strand, error-free."""
+    with np.errstate(over="ignore"):
+        z = splitmix64(seed, genome_len)
+        u = (z >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
+        bit = (z & np.uint64(1)).astype(np.uint8)
+        genome = np.where(u < gc, np.where(bit == 1, ord("G"), ord("C")),
+                          np.where(bit == 1, ord("T"), ord("A"))).astype(np.uint8)
+        starts = (splitmix64(seed ^ 0xABCDEF, n_reads) % np.uint64(genome_len - read_len + 1)).astype(np.int64)
+    idx = starts[:, None] + np.arange(read_len, dtype=np.int64)[None, :]
+    bases = genome[idx].reshape(-1)
+    offsets = np.arange(n_reads + 1, dtype=np.uint64) * np.uint64(read_len)
+    return bases, offsets
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--reads", type=int, default=100_000)
+    ap.add_argument("--len", type=int, default=500)
+    ap.add_argument("--k", type=int, default=15)
+    ap.add_argument("--gc", type=float, default=0.50)
+    ap.add_argument("--coverage", type=float, default=20.0)
+    ap.add_argument("--align-steps", type=int, default=None)
+    ap.add_argument("--cpu-sample-reads", type=int, default=10_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    ws, rank, local = dist_env()
+    dist = None
+    if ws > 1:
+        import torch
+        import torch.distributed as dist_
+        dist = dist_
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import saoverlap as sao
+
+    G = int(args.reads * args.len / args.coverage)
+    bases, offsets = synth_workload(args.reads, args.len, G, args.gc, seed=1 + rank)
+    ov = sao.Overlapper(device=local if ws > 1 else 0, timing=True, kmer_size=args.k,
+                        id_mode=sao.SA_IDS_WIDE)
+    ov.add_packed(bases.tobytes(), offsets)
+
+    def barrier():
+        if dist is not None:
+            import torch
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    def max_over_ranks(x):
+        if dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum_over_ranks(x):
+        if dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return float(t.item())
+
+    # ---- hash stage (configs[1]) ------------------------------------------
+    ov.device_build()  # allocations happen here, outside the timed region
+    for _ in range(args.warmup):
+        ov.device_build()
+    ov.reset_stage_times()
+    barrier()
+    ov.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ov.device_build()
+    ov.sync()
+    barrier()
+    t_build = max_over_ranks(time.perf_counter() - t0)
+    st = ov.stats()
+    stages = ov.stage_times()
+    role_pairs_total = sum_over_ranks(float(st["role_pairs"])) * args.steps
+    value = role_pairs_total / t_build
+
+    # ---- end-to-end incl. banded HOXD alignment (configs[2]) --------------
+    asteps = args.align_steps if args.align_steps is not None else max(1, args.steps // 2)
+    ov.device_align()
+    ov.reset_stage_times()
+    barrier()
+    ov.sync()
+    t0 = time.perf_counter()
+    for _ in range(asteps):
+        ov.device_align()
+    ov.sync()
+    barrier()
+    t_align = max_over_ranks(time.perf_counter() - t0)
+    ast = ov.stats()
+    astages = ov.stage_times()
+    aligned_total = sum_over_ranks(float(ast["aligned"])) * asteps
+
+    # ---- roofline of the dominant hash-stage kernel ----------------------
+    # pair_count is one launch per step; algorithmic HBM bytes per launch
+    # ("pair_count"): per k-mer 8 B (group id + partner range) + per
+    # candidate (role) pair 4 B (partner id) + per distinct pair 12 B written.
+    pc_ms, pc_n = stages["pairs"]
+    pc_avg_ms = pc_ms / max(pc_n, 1)
+    alg_bytes = 8.0 * st["kmers"] + 4.0 * st["role_pairs"] + 12.0 * st["dispatched"]
+    achieved = alg_bytes / (pc_avg_ms * 1e-3) / 1e9 if pc_avg_ms > 0 else 0.0
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": "pair_count_kernel<false>", "launch_ms": round(pc_avg_ms, 4),
+                "algorithmic_bytes_per_launch": int(alg_bytes)}
+
+    # ---- CPU baseline: the C oracle (port of the reference), 1 thread -----
+    cpu = None
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        n_s = args.cpu_sample_reads
+        G_s = int(n_s * args.len / args.coverage)
+        b_s, o_s = synth_workload(n_s, args.len, G_s, args.gc, seed=1)
+        s = oracle.default_settings(kmer_size=args.k)
+        t0 = time.perf_counter()
+        r = oracle.Run(packed=(b_s.tobytes(), o_s), settings=s, wide=True, skip_align=True)
+        t_cpu = time.perf_counter() - t0
+        # role pairs of the sample counted exactly as the GPU counts them
+        ovs = sao.Overlapper(kmer_size=args.k, id_mode=sao.SA_IDS_WIDE)
+        ovs.add_packed(b_s.tobytes(), o_s)
+        ovs.build()
+        rp_s = ovs.stats()["role_pairs"]
+        assert len(r.lead) == ovs.stats()["dispatched"], "CPU/GPU candidate mismatch on the baseline sample"
+        ovs.close()
+        cpu = {"value": round(rp_s / t_cpu, 1), "unit": "candidate k-mer pairs/s", "cores": 1, "kind": "port",
+               "sample": "%d reads x %d bp, %d bp genome (same 20x coverage), k=%d, hash stage "
+                         "(KmerTable.calcPairData+calcDispatchData restated in C, wide ids), %.1f s"
+                         % (n_s, args.len, G_s, args.k, t_cpu)}
+
+    if rank == 0:
+        line = {
+            "metric": "candidate k-mer pairs/sec (hash stage) + aligned read-pairs/sec, k=15, 500 bp reads",
+            "value": round(value, 1),
+            "unit": "candidate k-mer pairs/s",
+            "n_gpus": ws,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_build / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic (splitmix64 genome, error-free 500 bp reads)",
+            "config": {"workload": "configs[1]: %dk synthetic %d bp reads/GPU, k=%d, bucket build + "
+                                   "edge/middle pair filter" % (args.reads // 1000, args.len, args.k),
+                       "reads_per_gpu": args.reads, "read_len": args.len, "k": args.k,
+                       "genome_bp_per_gpu": G, "ids": "wide",
+                       "parallelism": "replicas" if ws > 1 else "single"},
+            "aligned_read_pairs_per_s": round(aligned_total / t_align, 1),
+            "ms_per_align_step": round(t_align / asteps * 1e3, 3),
+            "per_gpu": {k: int(v) for k, v in st.items() if k not in ("aligned", "ovl_records", "dp_cells")},
+            "dp_cells_per_align_step": int(ast["dp_cells"]),
+            "stage_ms_per_step": {k: round(v[0] / max(args.steps, 1), 4) for k, v in stages.items() if v[1]},
+            "align_kernel_ms": round(astages["align"][0] / max(astages["align"][1], 1), 4),
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    ov.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

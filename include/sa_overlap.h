@@ -1,0 +1,168 @@
+/*
+ * sa_overlap.h -- C ABI of the MI355X hash-overlap stage (libsa_overlap.so).
+ *
+ * Drop-in boundary for the reference's hot path (rohit507/Sequence-Aligner):
+ *   KmerTable.scala   k-mer hashing, edge<->middle candidate-pair counting, filter
+ *   BioLibs.scala     banded HOXD dovetail alignment (generateFastDovetailAlignmentSet)
+ *   Project4.scala    calc-overlaps driver and AMOS .ovl writer
+ * Plain pointers and sizes only; no torch or HIP types cross this boundary.
+ * Each entry point names the reference interface it replaces (file:line,
+ * /root/reference/src/...).  INTEGRATION.md shows the JNI / ctypes bindings.
+ *
+ * Ownership: the library owns device buffers and every array it returns by
+ * pointer (valid until the next call on the same context or sa_ctx_destroy);
+ * the caller owns its inputs.  One context per host thread.
+ * Errors: every int-returning call returns SA_OK (0) or a negative SA_E_* code;
+ * sa_last_error() gives the message.  The HIP path is the only compute path:
+ * without a usable gfx950 device, sa_ctx_create fails with SA_E_HIP.
+ */
+#ifndef SA_OVERLAP_H
+#define SA_OVERLAP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SA_ABI_VERSION 1
+
+enum sa_status {
+    SA_OK = 0,
+    SA_E_ARG = -1,         /* bad argument / flag (Project4.readArgs exit 1) */
+    SA_E_INPUT = -2,       /* unreadable FASTA / first line not '>' (BioLibs.scala:32-33) */
+    SA_E_NON_ACGT = -3,    /* non-ACGT base reached the HOXD cost closure (BioLibs.scala:142-160 MatchError) */
+    SA_E_ID_RANGE = -4,    /* strict ids: a dispatched id does not survive the 16-bit key packing (KmerTable.scala:73,169-170) */
+    SA_E_SHORT_READ = -5,  /* |B| < band width: B.charAt(j-1) out of range (BioLibs.scala:648) */
+    SA_E_DEGENERATE = -6,  /* no positive phase-1 cell: backtrack leaves the matrix (BioLibs.scala:679-689) */
+    SA_E_HIP = -7,         /* HIP runtime failure or no gfx950 device */
+    SA_E_NOMEM = -8,
+    SA_E_RCCL = -9,
+    SA_E_STATE = -10,      /* call out of order (e.g. sa_align before sa_build_candidates) */
+    SA_E_OVERFLOW = -11    /* a size limit of this implementation was exceeded */
+};
+
+/* Id policy.  STRICT reproduces the reference's 32-bit
+ * (fst<<16)^snd PairData keys and its GNU Trove iteration order, so the .ovl is
+ * byte-identical; it is defined for < 32,768 reads (the reference crashes
+ * beyond).  WIDE keys pairs by two 32-bit ids and orders records canonically
+ * (lead descending, trail ascending).  AUTO = STRICT below 32,768 reads, else WIDE. */
+enum sa_id_mode { SA_IDS_AUTO = 0, SA_IDS_STRICT = 1, SA_IDS_WIDE = 2 };
+
+/* AlignSettings (ObjectStore.scala:17-36) with Project4 defaults (Project4.scala:104-114). */
+typedef struct sa_settings {
+    int32_t kmer_size;       /* -k, --kmer-size        12   */
+    int32_t min_overlap;     /* --min-overlap          40   */
+    int32_t max_ignore;      /* --max-ignore           90   (compared as Float) */
+    int32_t gap_open;        /* -gO, --gap-open        -200 */
+    int32_t gap_extend;      /* -gE, --gap-extend      -20  */
+    int32_t min_collisions;  /* --min-collisions       7    */
+    int32_t max_collisions;  /* --max-collisions       222  */
+    float min_identity;      /* --min-identity         0.98f */
+    float kmer_edge;         /* --kmer-edge            0.4f */
+    float kmer_center;       /* --kmer-center          0.4f */
+    int32_t cost[16];        /* HOXD matrix, [a*4+b], bases A0 C1 G2 T3 (BioLibs.scala:122-140) */
+    int32_t id_mode;         /* enum sa_id_mode */
+} sa_settings;
+
+/* One alignment per dispatched pair (Alignment + Overlap, ObjectStore.scala:89-142). */
+typedef struct sa_alignment {
+    int32_t lead, trail;             /* read ids, 1-based (rds:lead,trail) */
+    int32_t start_i, start_j;        /* Alignment.start */
+    int32_t end_i, end_j;            /* Alignment.end */
+    int32_t correct, error;          /* c, e (alignA.length == c + e) */
+    int32_t ahg, bhg;                /* Overlap.ahg / bhg */
+    int32_t flags;                   /* SA_ALN_* bits */
+    int32_t reserved;
+} sa_alignment;
+#define SA_ALN_DUD 1        /* phase-1 backtrack missed j==0 -> BioLibs.dud (BioLibs.scala:694-695) */
+#define SA_ALN_VALID 2      /* Alignment.valid (ObjectStore.scala:102-107) */
+#define SA_ALN_OVL_VALID 4  /* Overlap.valid (ObjectStore.scala:137-141) -> written to the .ovl */
+
+typedef struct sa_ctx sa_ctx;
+
+/* Project4.readArgs defaults (Project4.scala:104-114) + defaultHOXD. */
+void sa_default_settings(sa_settings *s);
+
+/* new AlignSettings + new KmerTable (KmerTable.scala:26-37) on HIP device `device`. */
+int sa_ctx_create(const sa_settings *s, int device, sa_ctx **out);
+void sa_ctx_destroy(sa_ctx *ctx);
+const char *sa_last_error(const sa_ctx *ctx);
+
+/* BioLibs.readHOXD (BioLibs.scala:66-114): -m / --matrix FILE into s->cost. */
+int sa_load_hoxd(sa_settings *s, const char *path);
+
+/* Reads.  Ids are assigned 1..N in call order (BioLibs.readSeq ordinal ids,
+ * BioLibs.scala:27-47).  Bases are copied; lower case is upper-cased as
+ * readSeq's toUpperCase does.  Replaces KmerTable.addKmerSet (KmerTable.scala:41)
+ * fed by BioLibs.generateKmerSet (BioLibs.scala:54). */
+int sa_add_reads(sa_ctx *ctx, const char *bases, const uint64_t *offsets, uint32_t n);
+/* BioLibs.readSeq (BioLibs.scala:26-50) + sa_add_reads. */
+int sa_read_fasta(sa_ctx *ctx, const char *path);
+uint32_t sa_num_reads(const sa_ctx *ctx);
+
+/* KmerTable.calcPairData + calcDispatchData (KmerTable.scala:85-187): device
+ * k-mer emission, bucket build, edge<->middle pair counting, collision filter. */
+int sa_build_candidates(sa_ctx *ctx);
+/* DispatchData in dispatch order (KmerTable.scala:251-271): one entry per
+ * (lead, trail) with its collision count. */
+int sa_get_dispatch(sa_ctx *ctx, const int32_t **lead, const int32_t **trail,
+                    const int32_t **count, size_t *n);
+/* PairData (every counted ordered pair, not only dispatched ones), in the
+ * reference's iteration order (STRICT) or by (fst, snd) ascending (WIDE).
+ * Requires sa_set_option(ctx, SA_OPT_KEEP_PAIRS, 1) before sa_build_candidates. */
+int sa_get_pairs(sa_ctx *ctx, const int32_t **fst, const int32_t **snd,
+                 const int32_t **count, size_t *n);
+
+/* genBlockMTAlign -> generateFastDovetailAlignmentSet for every dispatched pair
+ * (Project4.scala:725-790, BioLibs.scala:596-822). */
+int sa_align(sa_ctx *ctx);
+int sa_get_alignments(sa_ctx *ctx, const sa_alignment **out, size_t *n);
+
+/* calcOverlaps (Project4.scala:795-825): AMOS {OVL} records of valid overlaps in
+ * dispatch order.  path == NULL writes to stdout; an existing file is replaced. */
+int sa_write_ovl(sa_ctx *ctx, const char *path);
+/* The same bytes into a library-owned buffer. */
+int sa_get_ovl(sa_ctx *ctx, const char **text, size_t *len);
+
+/* Options. */
+enum sa_option {
+    SA_OPT_KEEP_PAIRS = 1,   /* also materialise PairData for sa_get_pairs */
+    SA_OPT_TIMING = 2        /* record HIP events per stage (sa_get_stage_times) */
+};
+int sa_set_option(sa_ctx *ctx, int option, int64_t value);
+
+/* Statistics of the last sa_build_candidates / sa_align. */
+typedef struct sa_stats {
+    uint64_t kmers;            /* k-mer occurrences (Kmer objects) */
+    uint64_t buckets;          /* distinct k-mer hashes (KmerData.size) */
+    uint64_t role_pairs;       /* (st x md) + (en x md) occurrence pairs visited by calcPairData */
+    uint64_t pairs;            /* distinct ordered read pairs (PairData.size) */
+    uint64_t dispatched;       /* pairs with min <= count <= max */
+    uint64_t aligned;          /* alignments computed */
+    uint64_t ovl_records;      /* valid overlaps */
+    uint64_t dp_cells;         /* DP cells evaluated (phase 1 + phase 2) */
+    int32_t id_mode;           /* resolved mode (STRICT or WIDE) */
+    int32_t reserved;
+} sa_stats;
+int sa_get_stats(const sa_ctx *ctx, sa_stats *out);
+
+/* Per-stage device time accumulated since the last reset (SA_OPT_TIMING). */
+enum sa_stage {
+    SA_STAGE_PACK = 0, SA_STAGE_EMIT, SA_STAGE_SORT, SA_STAGE_BUCKETS, SA_STAGE_PAIRS,
+    SA_STAGE_ORDER, SA_STAGE_ALIGN, SA_NUM_STAGES
+};
+int sa_get_stage_times(const sa_ctx *ctx, double *ms, uint64_t *launches, int n);
+int sa_reset_stage_times(sa_ctx *ctx);
+
+/* Benchmark hooks: reads stay resident on the device; each call re-runs the
+ * hot path on them with no host<->device copies of bulk data. */
+int sa_device_build(sa_ctx *ctx);   /* == sa_build_candidates without host readback */
+int sa_device_align(sa_ctx *ctx);   /* == sa_align without host readback */
+int sa_sync(sa_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -210,6 +210,7 @@ class Alignment:  # ObjectStore.scala:89-107
 
 
 DUD = Alignment(0, 0, 0, 0, (0, 0), (0, 0), 0, 1)  # BioLibs.scala:22
+DUD.alen = 0  # its alignA is "" although error == 1
 
 
 # --------------------------------------------------------------------------

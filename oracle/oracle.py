@@ -100,10 +100,16 @@ class OracleError(RuntimeError):
 class Run:
     """Result of one calc-overlaps run of the oracle."""
 
-    def __init__(self, reads=None, fasta=None, settings=None, wide=False, keep_kmers=False):
+    def __init__(self, reads=None, fasta=None, settings=None, wide=False, keep_kmers=False, skip_align=False,
+                 packed=None):
         L = lib()
         h = C.c_void_p()
-        if fasta is not None:
+        if packed is not None:
+            bases, off = packed
+            off = np.ascontiguousarray(off, dtype=np.uint64)
+            rc = L.orc_create_from_buffers(bases, off.ctypes.data_as(C.POINTER(C.c_uint64)), len(off) - 1,
+                                           C.byref(h))
+        elif fasta is not None:
             rc = L.orc_create_from_fasta(fasta.encode(), C.byref(h))
         else:
             bases = b"".join(r.encode() if isinstance(r, str) else bytes(r) for r in reads)
@@ -115,7 +121,7 @@ class Run:
             raise OracleError(rc)
         self.settings = settings or default_settings()
         try:
-            rc = L.orc_run(h, C.byref(self.settings), 1 if wide else 0)
+            rc = L.orc_run(h, C.byref(self.settings), (1 if wide else 0) | (2 if skip_align else 0))
             self.rc = rc
             self.n_reads = L.orc_num_reads(h)
             if keep_kmers:

@@ -494,7 +494,8 @@ static int align_one(dp_buf *b, const char *A, int32_t la, const char *B, int32_
 /* Alignment.valid / Overlap (ObjectStore.scala:99-141) */
 static void judge(orc_align_t *o, const orc_settings *s) {
     float ratio = (float)o->correct / ((float)o->correct + (float)o->error);
-    int32_t alen = o->correct + o->error; /* alignA.length */
+    /* alignA.length: one char per backtrack step, but "" for the dud (BioLibs.scala:22) */
+    int32_t alen = o->is_dud ? 0 : o->correct + o->error;
     o->valid = (ratio >= s->min_identity) && (alen >= s->min_overlap) &&
                ((o->start_i == 0 && o->len_b == o->end_j) || (o->start_j == 0 && o->len_a == o->end_i));
     o->ahg = o->start_i - o->start_j;
@@ -520,7 +521,8 @@ static int cmp_wide_pair(const void *a, const void *b) {
     return (*x > *y) - (*x < *y);
 }
 
-int orc_run(orc_ctx *c, const orc_settings *s, int wide) {
+int orc_run(orc_ctx *c, const orc_settings *s, int flags) {
+    const int wide = flags & 1, skip_align = flags & 2;
     free_results(c);
     const int k = s->kmer_size;
     /* AlignSettings derived edges, ObjectStore.scala:30-35 */
@@ -727,6 +729,10 @@ out_kd:
 
     /* genBlockMTAlign (Project4.scala:725-790) + calcOverlaps (:795-825) */
     c->aligns = (orc_align_t *)calloc(c->nd + 1, sizeof(orc_align_t));
+    if (skip_align) {
+        c->ovl = (char *)calloc(1, 1);
+        return ORC_OK;
+    }
     size_t ocap = 4096, olen = 0;
     char *ovl = (char *)malloc(ocap);
     dp_buf db = {0};

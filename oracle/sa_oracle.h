@@ -73,10 +73,11 @@ int orc_create_from_buffers(const char *bases, const uint64_t *offsets, uint32_t
 void orc_destroy(orc_ctx *c);
 uint32_t orc_num_reads(const orc_ctx *c);
 
-/* Run the whole calc-overlaps path.  wide = 0: reference emulation with 32-bit
- * (fst<<16)^snd keys and Trove order (E1/E4).  wide = 1: 64-bit (fst,snd) keys,
- * canonical order (lead descending, trail ascending). */
-int orc_run(orc_ctx *c, const orc_settings *s, int wide);
+/* Run the whole calc-overlaps path.  flags bit 0 (wide) = 0: reference emulation
+ * with 32-bit (fst<<16)^snd keys and Trove order (E1/E4); = 1: 64-bit (fst,snd)
+ * keys, canonical order (lead descending, trail ascending).  flags bit 1: stop
+ * after DispatchData (candidate stage only, for the CPU baseline). */
+int orc_run(orc_ctx *c, const orc_settings *s, int flags);
 
 /* Results of orc_run (arrays owned by ctx, valid until destroy/next run). */
 size_t orc_num_kmers(const orc_ctx *c);

@@ -1,0 +1,918 @@
+// api.cpp -- C ABI (include/sa_overlap.h) and host orchestration of the
+// MI355X hash-overlap stage.
+//
+// Pipeline (one HIP stream; bulk data never leaves HBM between stages):
+//   pack_reads      ASCII -> 2-bit words                       (BioLibs.readSeq output)
+//   kmer_emit       (seqHash << lb | locrank, g) per k-mer     (BioLibs.generateKmerSet)
+//   radix_sort      group by hash, loc order, g-stable          (KmerData, KmerTable.scala:41-53)
+//   build_buckets   middle / edge lists + partner ranges        (calcPairData split, :97-115)
+//   pair_count      per-read LDS aggregation + [min,max] filter (addKmerPair / calcDispatchData)
+//   order           wide: lead desc / trail asc; strict: first-occurrence rank -> host Trove replay
+//   dovetail        banded two-phase DP + validity             (generateFastDovetailAlignmentSet)
+// then the .ovl writer (Project4.calcOverlaps) on the host.
+#include "../../../include/sa_overlap.h"
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../sa_internal.h"
+#include "trove.h"
+
+namespace sa {
+int read_fasta(const char *path, std::vector<char> &bases, std::vector<uint64_t> &offsets);
+int read_hoxd(const char *path, int32_t cost[16]);
+size_t pair_count_lds_bytes(bool strict);
+hipError_t launch_bucket_first(const uint64_t *skeys, const uint32_t *svals, const Buckets &b, int lb,
+                               uint32_t *hash_out, uint32_t *first_out, hipStream_t s);
+}  // namespace sa
+
+using namespace sa;
+
+namespace {
+
+struct DBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+};
+
+struct Counters {                    // device-resident scalars, one memset per build
+    unsigned long long cursor;
+    unsigned long long role_pairs;
+    unsigned long long role_pairs_dummy;
+    unsigned long long distinct;
+    unsigned long long cells;
+    uint32_t overflow_n;
+    int32_t err;
+    uint32_t totals[4];
+};
+
+}  // namespace
+
+struct sa_ctx {
+    sa_settings set{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // reads (host)
+    std::vector<char> bases;
+    std::vector<uint64_t> boff{0};
+    bool reads_dirty = true, uploaded = false;
+    // derived (host)
+    std::vector<int32_t> len;
+    std::vector<uint64_t> woff, occ_off;
+    std::vector<uint32_t> lbase, lrank;
+    std::vector<uint8_t> tagtab;
+    int lb = 1, m = 0, maxd = 0, maxL = 0;
+    uint32_t uniform_npr = 0;
+    uint64_t n_occ = 0, n_words = 0;
+    uint32_t max_occ = 0;
+    int32_t mode = SA_IDS_WIDE;
+    // device buffers
+    DBuf d_ascii, d_boff, d_woff, d_len, d_codes, d_bad, d_occ_off, d_lbase, d_lrank, d_tagtab;
+    DBuf d_keys, d_vals, d_keys2, d_vals2, d_sorttmp;
+    DBuf d_md, d_ed, d_bmdo, d_bedo, d_bstart, d_gbid, d_gmds, d_gede, d_ogid, d_bkttmp;
+    DBuf d_mdidx, d_edidx, d_occidx, d_bnst, d_brank, d_bhash, d_bfirst;
+    DBuf d_pf, d_ps, d_pc, d_pr, d_ovl, d_cnt;
+    DBuf d_okeys, d_ovals, d_okeys2, d_ovals2, d_osort;
+    DBuf d_lead, d_trail, d_count, d_aln;
+    uint64_t pair_cap = 0;
+    uint64_t n_disp = 0;
+    Buckets bk{};
+    // options / state
+    bool keep_pairs = false, timing = false;
+    bool built = false, aligned = false;
+    // results (host)
+    std::vector<int32_t> lead, trail, count;
+    std::vector<int32_t> pfst, psnd, pcnt;
+    std::vector<sa_alignment> alns;
+    std::string ovl;
+    sa_stats stats{};
+    // timing
+    struct Pending { int stage; hipEvent_t a, b; };
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> ev_pool;
+    double stage_ms[SA_NUM_STAGES] = {0};
+    uint64_t stage_n[SA_NUM_STAGES] = {0};
+};
+
+namespace {
+
+int fail(sa_ctx *c, int code, const std::string &msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                            \
+    do {                                                                                        \
+        hipError_t e_ = (expr);                                                                 \
+        if (e_ != hipSuccess)                                                                   \
+            return fail(c, SA_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));       \
+    } while (0)
+
+template <class T>
+int ensure(sa_ctx *c, DBuf &b, size_t count, T **out) {
+    const size_t need = std::max<size_t>(count, 1) * sizeof(T);
+    if (b.bytes < need) {
+        if (b.p) (void)hipFree(b.p);
+        b.p = nullptr;
+        b.bytes = 0;
+        const size_t alloc = need + need / 8;
+        hipError_t e = hipMalloc(&b.p, alloc);
+        if (e != hipSuccess) return fail(c, SA_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+        b.bytes = alloc;
+    }
+    *out = (T *)b.p;
+    return SA_OK;
+}
+
+#define ENSURE(buf, n, ptr)                          \
+    do {                                             \
+        int r_ = ensure(c, (buf), (size_t)(n), ptr); \
+        if (r_) return r_;                           \
+    } while (0)
+
+hipEvent_t get_event(sa_ctx *c) {
+    if (!c->ev_pool.empty()) {
+        hipEvent_t e = c->ev_pool.back();
+        c->ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+struct StageScope {
+    sa_ctx *c;
+    int stage;
+    hipEvent_t a = nullptr;
+    StageScope(sa_ctx *c_, int s) : c(c_), stage(s) {
+        if (c->timing) {
+            a = get_event(c);
+            (void)hipEventRecord(a, c->stream);
+        }
+    }
+    ~StageScope() {
+        if (c->timing && a) {
+            hipEvent_t b = get_event(c);
+            (void)hipEventRecord(b, c->stream);
+            c->pending.push_back({stage, a, b});
+        }
+    }
+};
+
+void resolve_timing(sa_ctx *c) {
+    for (auto &p : c->pending) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+            c->stage_ms[p.stage] += ms;
+            c->stage_n[p.stage] += 1;
+        }
+        c->ev_pool.push_back(p.a);
+        c->ev_pool.push_back(p.b);
+    }
+    c->pending.clear();
+}
+
+int bits_for(uint64_t v) {  // bits to represent 0..v
+    int b = 1;
+    while (b < 64 && (v >> b)) ++b;
+    return b;
+}
+
+// ---------------------------------------------------------------------------
+// host-side read metadata: lengths, word/occurrence offsets, loc ranks, tags
+// ---------------------------------------------------------------------------
+int prepare_reads(sa_ctx *c) {
+    const uint32_t n = (uint32_t)(c->boff.size() - 1);
+    const int k = c->set.kmer_size;
+    if (k < 1) return fail(c, SA_E_ARG, "kmer size must be >= 1");
+    c->m = k < 16 ? k : 16;
+    c->len.resize(n);
+    c->woff.resize(n + 1);
+    c->occ_off.resize(n + 1);
+    c->woff[0] = 0;
+    c->occ_off[0] = 0;
+    c->maxL = 0;
+    c->max_occ = 0;
+    std::vector<char> has_d;
+    int maxd = -1;
+    int32_t uni = -1;
+    bool uniform = true;
+    for (uint32_t r = 0; r < n; ++r) {
+        const uint64_t L64 = c->boff[r + 1] - c->boff[r];
+        if (L64 > (1u << 20) - 2) return fail(c, SA_E_OVERFLOW, "read longer than 1,048,574 bases");
+        const int32_t L = (int32_t)L64;
+        c->len[r] = L;
+        c->maxL = std::max(c->maxL, L);
+        c->woff[r + 1] = c->woff[r] + (uint64_t)((L + 15) / 16);
+        const int32_t nk = L - k + 1 > 0 ? L - k + 1 : 0;
+        c->occ_off[r + 1] = c->occ_off[r] + (uint64_t)nk;
+        c->max_occ = std::max<uint32_t>(c->max_occ, (uint32_t)nk);
+        if (uni < 0) uni = L;
+        if (L != uni || L < k) uniform = false;
+        if (L >= k) {
+            const int d = L - k;
+            if (d > maxd) { maxd = d; has_d.resize(d + 1, 0); }
+            has_d[d] = 1;
+        }
+    }
+    c->n_occ = c->occ_off[n];
+    if (c->n_occ >= 0xFFFFFFF0ull) return fail(c, SA_E_OVERFLOW, "more than 2^32 k-mers on one device");
+    c->n_words = c->woff[n] + 2;  // pad: windows read one word past a read
+    c->uniform_npr = (uniform && n > 0) ? (uint32_t)(uni - k + 1) : 0;
+    c->maxd = maxd < 0 ? 0 : maxd;
+    // distinct float32 locs i/d (BioLibs.scala:56-58) -> ranks; NaN (d == 0) ranks last, untagged
+    std::vector<float> vals;
+    bool nan_loc = false;
+    for (int d = 0; d <= maxd; ++d) {
+        if (!has_d[d]) continue;
+        if (d == 0) { nan_loc = true; continue; }
+        const float fd = (float)d;
+        for (int i = 0; i <= d; ++i) vals.push_back((float)i / fd);
+    }
+    std::sort(vals.begin(), vals.end());
+    vals.erase(std::unique(vals.begin(), vals.end()), vals.end());
+    const uint32_t nan_rank = (uint32_t)vals.size();
+    c->lbase.assign((size_t)c->maxd + 1, 0);
+    c->lrank.clear();
+    for (int d = 0; d <= maxd; ++d) {
+        c->lbase[d] = (uint32_t)c->lrank.size();
+        if (!has_d[d]) continue;
+        if (d == 0) { c->lrank.push_back(nan_rank); continue; }
+        const float fd = (float)d;
+        for (int i = 0; i <= d; ++i) {
+            const float v = (float)i / fd;
+            c->lrank.push_back((uint32_t)(std::lower_bound(vals.begin(), vals.end(), v) - vals.begin()));
+        }
+    }
+    if (c->lrank.empty()) c->lrank.push_back(0);
+    // AlignSettings edges (ObjectStore.scala:32-35), float32
+    const float head = c->set.kmer_edge;
+    const float tail = 1.0f - c->set.kmer_edge;
+    const float half_c = c->set.kmer_center * 0.5f;
+    const float midLead = 0.5f - half_c;
+    const float midTail = 0.5f + half_c;
+    c->tagtab.assign(vals.size() + 1 + (nan_loc ? 1 : 0), 0);
+    for (size_t q = 0; q < vals.size(); ++q) {
+        const float v = vals[q];
+        uint8_t t = 0;
+        if (v <= head) t |= TAG_ST;  // KmerTable.scala:106-115
+        if (midLead <= v && v <= midTail) t |= TAG_MD;
+        if (tail <= v) t |= TAG_EN;
+        c->tagtab[q] = t;
+    }
+    c->lb = bits_for(nan_rank);
+    if (2 * c->m + c->lb > 64) return fail(c, SA_E_OVERFLOW, "sort key wider than 64 bits");
+    // tag table indexed by (key & lbmask): pad to 1 << lb
+    c->tagtab.resize((size_t)1 << c->lb, 0);
+    return SA_OK;
+}
+
+int upload_reads(sa_ctx *c) {
+    const uint32_t n = (uint32_t)(c->boff.size() - 1);
+    uint8_t *ascii; uint64_t *boff, *woff, *occ; int32_t *len; uint32_t *codes; int32_t *bad;
+    uint32_t *lbase, *lrank; uint8_t *tag;
+    ENSURE(c->d_ascii, c->bases.size() + 16, &ascii);
+    ENSURE(c->d_boff, n + 1, &boff);
+    ENSURE(c->d_woff, n + 1, &woff);
+    ENSURE(c->d_len, n + 1, &len);
+    ENSURE(c->d_codes, c->n_words, &codes);
+    ENSURE(c->d_bad, n + 1, &bad);
+    ENSURE(c->d_occ_off, n + 1, &occ);
+    ENSURE(c->d_lbase, c->lbase.size(), &lbase);
+    ENSURE(c->d_lrank, c->lrank.size(), &lrank);
+    ENSURE(c->d_tagtab, c->tagtab.size(), &tag);
+    if (!c->bases.empty()) HIPCHK(hipMemcpyAsync(ascii, c->bases.data(), c->bases.size(), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(boff, c->boff.data(), (n + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(woff, c->woff.data(), (n + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    if (n) HIPCHK(hipMemcpyAsync(len, c->len.data(), n * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(occ, c->occ_off.data(), (n + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(lbase, c->lbase.data(), c->lbase.size() * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(lrank, c->lrank.data(), c->lrank.size() * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(tag, c->tagtab.data(), c->tagtab.size(), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemsetAsync(codes, 0, c->n_words * 4, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->uploaded = true;
+    return SA_OK;
+}
+
+DevReads dev_reads(sa_ctx *c) {
+    DevReads r;
+    r.n = (uint32_t)(c->boff.size() - 1);
+    r.ascii = (const uint8_t *)c->d_ascii.p;
+    r.boff = (const uint64_t *)c->d_boff.p;
+    r.woff = (const uint64_t *)c->d_woff.p;
+    r.len = (const int32_t *)c->d_len.p;
+    r.codes = (uint32_t *)c->d_codes.p;
+    r.bad = (int32_t *)c->d_bad.p;
+    return r;
+}
+
+EmitParams emit_params(sa_ctx *c) {
+    EmitParams e;
+    e.k = c->set.kmer_size;
+    e.m = c->m;
+    e.lb = c->lb;
+    e.occ_off = (const uint64_t *)c->d_occ_off.p;
+    e.lbase = (const uint32_t *)c->d_lbase.p;
+    e.lrank = (const uint32_t *)c->d_lrank.p;
+    e.maxd = c->maxd;
+    return e;
+}
+
+int ensure_prepared(sa_ctx *c) {
+    if (c->reads_dirty) {
+        int rc = prepare_reads(c);
+        if (rc) return rc;
+        c->reads_dirty = false;
+        c->uploaded = false;
+    }
+    if (!c->uploaded) {
+        int rc = upload_reads(c);
+        if (rc) return rc;
+    }
+    const uint32_t n = (uint32_t)(c->boff.size() - 1);
+    int mode = c->set.id_mode;
+    if (mode == SA_IDS_AUTO) mode = n < 32768 ? SA_IDS_STRICT : SA_IDS_WIDE;
+    if (mode == SA_IDS_STRICT && n >= 65536)
+        return fail(c, SA_E_ID_RANGE, "strict ids: >= 65,536 reads alias in the reference's (fst<<16)^snd keys; use wide ids");
+    c->mode = mode;
+    return SA_OK;
+}
+
+// ---------------------------------------------------------------------------
+// candidate build (device), optional host readback
+// ---------------------------------------------------------------------------
+int device_build(sa_ctx *c, bool readback) {
+    int rc = ensure_prepared(c);
+    if (rc) return rc;
+    c->built = false;
+    c->aligned = false;
+    const bool strict = c->mode == SA_IDS_STRICT;
+    const uint32_t nr = (uint32_t)(c->boff.size() - 1);
+    const uint64_t n = c->n_occ;
+    DevReads R = dev_reads(c);
+    EmitParams E = emit_params(c);
+    Counters *cnt;
+    ENSURE(c->d_cnt, 1, &cnt);
+    HIPCHK(hipMemsetAsync(cnt, 0, sizeof(Counters), c->stream));
+
+    uint64_t *keys, *keys2; uint32_t *vals, *vals2; void *stmp;
+    ENSURE(c->d_keys, n, &keys);
+    ENSURE(c->d_keys2, n, &keys2);
+    ENSURE(c->d_vals, n, &vals);
+    ENSURE(c->d_vals2, n, &vals2);
+    uint8_t *stmp8;
+    ENSURE(c->d_sorttmp, std::max(radix_sort_temp_bytes(n), buckets_temp_bytes(n)), &stmp8);
+    stmp = stmp8;
+    {
+        StageScope st(c, SA_STAGE_PACK);
+        HIPCHK(launch_pack_reads(R, c->stream));
+    }
+    {
+        StageScope st(c, SA_STAGE_EMIT);
+        HIPCHK(launch_kmer_emit(R, E, keys, vals, c->stream));
+    }
+    {
+        StageScope st(c, SA_STAGE_SORT);
+        HIPCHK(radix_sort(&keys, &vals, &keys2, &vals2, n, 0, c->lb + 2 * c->m, stmp, c->stream));
+    }
+    Buckets &B = c->bk;
+    B.n_occ = n;
+    ENSURE(c->d_md, n, &B.md_list);
+    ENSURE(c->d_ed, 2 * n, &B.ed_list);
+    ENSURE(c->d_bmdo, n + 2, &B.bkt_mdo);
+    ENSURE(c->d_bedo, n + 2, &B.bkt_edo);
+    ENSURE(c->d_bstart, n + 2, &B.bkt_start);
+    ENSURE(c->d_gbid, n + 1, &B.grp_bid);
+    ENSURE(c->d_gmds, n + 1, &B.grp_mds);
+    ENSURE(c->d_gede, n + 1, &B.grp_ede);
+    ENSURE(c->d_ogid, n + 1, &B.occ_gid);
+    const uint8_t *tagtab = (const uint8_t *)c->d_tagtab.p;
+    {
+        StageScope st(c, SA_STAGE_BUCKETS);
+        HIPCHK(build_buckets(keys, vals, n, c->lb, tagtab, (const uint64_t *)c->d_occ_off.p, nr, c->uniform_npr, B,
+                             cnt->totals, stmp, c->stream));
+        if (strict) {
+            ENSURE(c->d_mdidx, n + 1, &B.md_idx);
+            ENSURE(c->d_edidx, 2 * n + 1, &B.ed_idx);
+            ENSURE(c->d_occidx, 3 * n + 3, &B.occ_idx);
+            ENSURE(c->d_bnst, n + 1, &B.bkt_nst);
+            ENSURE(c->d_brank, n + 1, &B.bkt_rank);
+            HIPCHK(build_strict_index(keys, vals, n, c->lb, tagtab, B, c->stream));
+        }
+    }
+    uint32_t totals[4] = {0, 0, 0, 0};
+    if (strict || readback) {
+        HIPCHK(hipMemcpyAsync(totals, cnt->totals, sizeof(totals), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        B.n_buckets = totals[0]; B.n_groups = totals[1]; B.n_md = totals[2]; B.n_ed = totals[3];
+    }
+    if (strict) {
+        // KmerData iteration rank of every bucket: replay its Trove layout over the
+        // distinct hashes in first-occurrence order (KmerTable.scala:45-50)
+        uint32_t *bh, *bf;
+        ENSURE(c->d_bhash, B.n_buckets + 1, &bh);
+        ENSURE(c->d_bfirst, B.n_buckets + 1, &bf);
+        HIPCHK(launch_bucket_first(keys, vals, B, c->lb, bh, bf, c->stream));
+        std::vector<uint32_t> hh(B.n_buckets), ff(B.n_buckets);
+        if (B.n_buckets) {
+            HIPCHK(hipMemcpyAsync(hh.data(), bh, B.n_buckets * 4, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipMemcpyAsync(ff.data(), bf, B.n_buckets * 4, hipMemcpyDeviceToHost, c->stream));
+        }
+        HIPCHK(hipStreamSynchronize(c->stream));
+        std::vector<uint32_t> order(B.n_buckets);
+        for (uint32_t i = 0; i < B.n_buckets; ++i) order[i] = i;
+        std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return ff[x] < ff[y]; });
+        TroveLayout kd;
+        for (uint32_t i : order) kd.insert((int32_t)hh[i]);
+        // bucket ids are ascending unsigned hash order
+        std::vector<uint32_t> rank(B.n_buckets);
+        uint32_t rk = 0;
+        std::vector<std::pair<uint32_t, uint32_t>> hid(B.n_buckets);
+        for (uint32_t i = 0; i < B.n_buckets; ++i) hid[i] = {hh[i], i};
+        std::sort(hid.begin(), hid.end());
+        kd.for_each([&](int32_t key) {
+            auto it = std::lower_bound(hid.begin(), hid.end(), std::make_pair((uint32_t)key, 0u));
+            rank[it->second] = rk++;
+        });
+        if (rk >= (1u << 26)) return fail(c, SA_E_OVERFLOW, "strict ids: more than 2^26 distinct k-mers");
+        if (B.n_buckets) HIPCHK(hipMemcpyAsync(B.bkt_rank, rank.data(), B.n_buckets * 4, hipMemcpyHostToDevice, c->stream));
+    }
+
+    // ---- pair counting -------------------------------------------------
+    PairParams P;
+    P.min_coll = c->set.min_collisions;
+    P.max_coll = c->set.max_collisions;
+    P.emit_all = (strict || c->keep_pairs) ? 1 : 0;
+    P.strict = strict ? 1 : 0;
+    P.split = 1;
+    P.max_occ = c->max_occ;
+    if (c->pair_cap == 0) c->pair_cap = std::max<uint64_t>(1 << 16, (uint64_t)nr * (P.emit_all ? 64 : 24));
+    unsigned long long cursor = 0;
+    uint32_t ovn = 0;
+    for (int attempt = 0; attempt < 4; ++attempt) {
+        PairOut O;
+        ENSURE(c->d_pf, c->pair_cap, &O.fst);
+        ENSURE(c->d_ps, c->pair_cap, &O.snd);
+        ENSURE(c->d_pc, c->pair_cap, &O.cnt);
+        O.rank = nullptr;
+        if (strict) ENSURE(c->d_pr, c->pair_cap, &O.rank);
+        ENSURE(c->d_ovl, nr + 1, &O.overflow_list);
+        O.cursor = &cnt->cursor;
+        O.cap = c->pair_cap;
+        O.role_pairs = &cnt->role_pairs;
+        O.overflow_n = &cnt->overflow_n;
+        O.distinct = &cnt->distinct;
+        HIPCHK(hipMemsetAsync(&cnt->cursor, 0, 4 * sizeof(unsigned long long), c->stream));
+        HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(uint32_t), c->stream));
+        {
+            StageScope st(c, SA_STAGE_PAIRS);
+            HIPCHK(launch_pair_count(R, E, B, tagtab, P, O, nullptr, nr, c->stream));
+        }
+        HIPCHK(hipMemcpyAsync(&cursor, &cnt->cursor, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(&ovn, &cnt->overflow_n, 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        // split passes for reads whose LDS table overflowed (rare; high-copy repeats)
+        uint32_t split = 8;
+        uint32_t *ovl_list = O.overflow_list;
+        while (ovn > 0 && cursor <= c->pair_cap) {
+            if (split > (1u << 16)) return fail(c, SA_E_OVERFLOW, "pair table overflow beyond 65536-way split");
+            std::vector<uint32_t> lst(ovn);
+            HIPCHK(hipMemcpyAsync(lst.data(), ovl_list, ovn * 4, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            uint32_t *dl;
+            ENSURE(c->d_bfirst, ovn + 1, &dl);  // reuse as read list (strict bucket_first data already consumed)
+            HIPCHK(hipMemcpyAsync(dl, lst.data(), ovn * 4, hipMemcpyHostToDevice, c->stream));
+            PairParams P2 = P;
+            P2.split = (int32_t)split;
+            PairOut O2 = O;
+            O2.role_pairs = &cnt->role_pairs_dummy;
+            HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(uint32_t), c->stream));
+            {
+                StageScope st(c, SA_STAGE_PAIRS);
+                HIPCHK(launch_pair_count(R, E, B, tagtab, P2, O2, dl, ovn * split, c->stream));
+            }
+            HIPCHK(hipMemcpyAsync(&cursor, &cnt->cursor, 8, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipMemcpyAsync(&ovn, &cnt->overflow_n, 4, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            if (ovn) {
+                // the split pass itself overflowed: rerun the whole read set at the next split
+                return fail(c, SA_E_OVERFLOW, "pair table overflow in split pass");
+            }
+            split *= 8;
+        }
+        if (cursor <= c->pair_cap) break;
+        c->pair_cap = cursor + cursor / 4 + 1024;  // grow and recount
+        if (attempt == 3) return fail(c, SA_E_OVERFLOW, "pair output did not fit");
+    }
+    const uint64_t np = cursor;
+
+    // ---- ordering --------------------------------------------------------
+    uint64_t *ok, *ok2; uint32_t *ov, *ov2; uint8_t *otmp;
+    ENSURE(c->d_okeys, np, &ok);
+    ENSURE(c->d_okeys2, np, &ok2);
+    ENSURE(c->d_ovals, np, &ov);
+    ENSURE(c->d_ovals2, np, &ov2);
+    ENSURE(c->d_osort, radix_sort_temp_bytes(np), &otmp);
+    int32_t *dlead, *dtrail, *dcount;
+    ENSURE(c->d_lead, np, &dlead);
+    ENSURE(c->d_trail, np, &dtrail);
+    ENSURE(c->d_count, np, &dcount);
+    {
+        StageScope st(c, SA_STAGE_ORDER);
+        const int idb = bits_for(nr ? nr - 1 : 0);
+        HIPCHK(launch_make_order_keys((const uint32_t *)c->d_pf.p, (const uint32_t *)c->d_ps.p,
+                                      (const uint64_t *)c->d_pr.p, np, strict ? 1 : 0, idb, ok, ov, c->stream));
+        const int hi = strict ? 64 : 2 * idb;
+        HIPCHK(radix_sort(&ok, &ov, &ok2, &ov2, np, 0, hi, otmp, c->stream));
+        HIPCHK(launch_gather_pairs(ov, np, (const uint32_t *)c->d_pf.p, (const uint32_t *)c->d_ps.p,
+                                   (const uint32_t *)c->d_pc.p, dlead, dtrail, dcount, c->stream));
+    }
+    Counters hc;
+    HIPCHK(hipMemcpyAsync(&hc, cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    resolve_timing(c);
+    B.n_buckets = hc.totals[0]; B.n_groups = hc.totals[1]; B.n_md = hc.totals[2]; B.n_ed = hc.totals[3];
+    c->stats = sa_stats{};
+    c->stats.kmers = n;
+    c->stats.buckets = B.n_buckets;
+    c->stats.role_pairs = hc.role_pairs;
+    c->stats.pairs = hc.distinct;
+    c->stats.id_mode = c->mode;
+
+    c->lead.clear(); c->trail.clear(); c->count.clear();
+    c->pfst.clear(); c->psnd.clear(); c->pcnt.clear();
+    if (!strict && !P.emit_all) {
+        c->n_disp = np;
+        if (readback && np) {
+            c->lead.resize(np); c->trail.resize(np); c->count.resize(np);
+            HIPCHK(hipMemcpy(c->lead.data(), dlead, np * 4, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(c->trail.data(), dtrail, np * 4, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(c->count.data(), dcount, np * 4, hipMemcpyDeviceToHost));
+        }
+    } else {
+        // every distinct pair came back (strict: in first-insertion order; wide: lead desc)
+        std::vector<int32_t> f(np), s(np), k(np);
+        if (np) {
+            HIPCHK(hipMemcpy(f.data(), dlead, np * 4, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(s.data(), dtrail, np * 4, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(k.data(), dcount, np * 4, hipMemcpyDeviceToHost));
+        }
+        if (strict) {
+            // PairData: Trove layout of keys (fst<<16)^snd inserted in first-occurrence order
+            TroveLayout pd;
+            std::vector<std::pair<int32_t, uint32_t>> key_ix(np);
+            for (uint64_t i = 0; i < np; ++i) {
+                const int32_t key = (int32_t)(((uint32_t)f[i] << 16) ^ (uint32_t)s[i]);
+                pd.insert(key);
+                key_ix[i] = {key, (uint32_t)i};
+            }
+            std::sort(key_ix.begin(), key_ix.end());
+            auto find = [&](int32_t key) {
+                return std::lower_bound(key_ix.begin(), key_ix.end(), std::make_pair(key, 0u))->second;
+            };
+            // calcDispatchData (KmerTable.scala:155-187) over PairData iteration order
+            TroveLayout dd;
+            std::vector<std::vector<int32_t>> lists;
+            std::unordered_map<int32_t, int32_t> list_of;  // lead -> list index
+            bool id_err = false;
+            pd.for_each([&](int32_t key) {
+                const uint32_t ix = find(key);
+                const int32_t cnt_ = k[ix];
+                const int32_t a = key >> 16;
+                const int32_t b = (int32_t)((uint32_t)key << 16) >> 16;
+                if (c->keep_pairs) { c->pfst.push_back(a); c->psnd.push_back(b); c->pcnt.push_back(cnt_); }
+                if (c->set.min_collisions <= cnt_ && cnt_ <= c->set.max_collisions) {
+                    if (dd.insert(a)) { list_of[a] = (int32_t)lists.size(); lists.emplace_back(); }
+                    lists[list_of[a]].push_back(b);
+                    if (a < 1 || a > (int32_t)nr || b < 1 || b > (int32_t)nr) id_err = true;
+                }
+            });
+            if (id_err)
+                return fail(c, SA_E_ID_RANGE, "strict ids: a dispatched pair decodes to an id outside 1..N "
+                                              "(reference NullPointerException, KmerTable.scala:263-265)");
+            dd.for_each([&](int32_t a) {
+                const auto &vec = lists[list_of[a]];
+                for (int32_t b : vec) {
+                    c->lead.push_back(a);
+                    c->trail.push_back(b);
+                    const int32_t key = (int32_t)(((uint32_t)a << 16) ^ (uint32_t)b);
+                    c->count.push_back(k[find(key)]);
+                }
+            });
+        } else {
+            // wide + keep_pairs: PairData sorted (fst, snd); dispatch = filter, lead desc
+            std::vector<uint32_t> ix(np);
+            for (uint64_t i = 0; i < np; ++i) ix[i] = (uint32_t)i;
+            std::sort(ix.begin(), ix.end(), [&](uint32_t x, uint32_t y) {
+                return f[x] != f[y] ? f[x] < f[y] : s[x] < s[y];
+            });
+            for (uint32_t i : ix) { c->pfst.push_back(f[i]); c->psnd.push_back(s[i]); c->pcnt.push_back(k[i]); }
+            for (uint64_t i = 0; i < np; ++i)
+                if (c->set.min_collisions <= k[i] && k[i] <= c->set.max_collisions) {
+                    c->lead.push_back(f[i]); c->trail.push_back(s[i]); c->count.push_back(k[i]);
+                }
+        }
+        c->n_disp = c->lead.size();
+        if (c->n_disp) {
+            HIPCHK(hipMemcpy(dlead, c->lead.data(), c->n_disp * 4, hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(dtrail, c->trail.data(), c->n_disp * 4, hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(dcount, c->count.data(), c->n_disp * 4, hipMemcpyHostToDevice));
+        }
+    }
+    c->stats.dispatched = c->n_disp;
+    c->built = true;
+    return SA_OK;
+}
+
+int device_align(sa_ctx *c, bool readback) {
+    if (!c->built) return fail(c, SA_E_STATE, "sa_align before sa_build_candidates");
+    const uint64_t nd = c->n_disp;
+    const float omm = 1.0f - c->set.min_identity;
+    const float prod = (float)c->maxL * omm;
+    const int32_t wmax = std::max(c->set.kmer_size, (int32_t)floor((double)prod) + 1);
+    int G = wmax <= 15 ? 16 : (wmax <= 31 ? 32 : (wmax <= 63 ? 64 : 0));
+    if (!G) return fail(c, SA_E_OVERFLOW, "band width above 63 (min-identity too low for the read length)");
+    uint32_t rw = (uint32_t)((c->maxL + 1 + 15) / 16) | 1u;
+    if ((size_t)256 * rw * 4 > 160 * 1024)
+        return fail(c, SA_E_OVERFLOW, "reads too long for the LDS traceback (max ~2,500 bp this build)");
+    AlignParams P;
+    P.k = c->set.kmer_size;
+    P.gap_open = c->set.gap_open;
+    P.gap_extend = c->set.gap_extend;
+    P.min_overlap = c->set.min_overlap;
+    P.one_minus_minid = omm;
+    P.min_identity = c->set.min_identity;
+    P.max_ignore = (float)c->set.max_ignore;
+    memcpy(P.cost, c->set.cost, sizeof(P.cost));
+    P.rw = rw;
+    Counters *cnt = (Counters *)c->d_cnt.p;
+    DevAlignment *out;
+    ENSURE(c->d_aln, nd, &out);
+    HIPCHK(hipMemsetAsync(&cnt->err, 0, 4, c->stream));
+    HIPCHK(hipMemsetAsync(&cnt->cells, 0, 8, c->stream));
+    {
+        StageScope st(c, SA_STAGE_ALIGN);
+        HIPCHK(launch_dovetail(dev_reads(c), (const int32_t *)c->d_lead.p, (const int32_t *)c->d_trail.p, nd, P, G,
+                               out, &cnt->err, &cnt->cells, c->stream));
+    }
+    int32_t err = 0;
+    unsigned long long cells = 0;
+    HIPCHK(hipMemcpyAsync(&err, &cnt->err, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(&cells, &cnt->cells, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    resolve_timing(c);
+    c->stats.aligned = nd;
+    c->stats.dp_cells = cells;
+    if (err) {
+        const char *msg = err == SA_E_NON_ACGT ? "non-ACGT base in an aligned region (HOXD MatchError)"
+                        : err == SA_E_SHORT_READ ? "trail shorter than the band width (StringIndexOutOfBounds)"
+                        : err == SA_E_DEGENERATE ? "no positive phase-1 cell (degenerate backtrack)"
+                        : "alignment limit exceeded";
+        return fail(c, err, msg);
+    }
+    if (readback) {
+        c->alns.resize(nd);
+        if (nd) HIPCHK(hipMemcpy(c->alns.data(), out, nd * sizeof(sa_alignment), hipMemcpyDeviceToHost));
+        uint64_t rec = 0;
+        c->ovl.clear();
+        char buf[160];
+        for (uint64_t i = 0; i < nd; ++i) {
+            const sa_alignment &a = c->alns[i];
+            if (!(a.flags & SA_ALN_OVL_VALID)) continue;
+            const int ra = (a.flags & SA_ALN_DUD) ? 0 : a.lead, rb = (a.flags & SA_ALN_DUD) ? 0 : a.trail;
+            const int m = snprintf(buf, sizeof(buf), "{OVL\nadj:N\nrds:%d,%d\nscr:0\nahg:%d\nbhg:%d\n}\n", ra, rb,
+                                   a.ahg, a.bhg);
+            c->ovl.append(buf, (size_t)m);
+            ++rec;
+        }
+        c->stats.ovl_records = rec;
+    }
+    c->aligned = true;
+    return SA_OK;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" {
+
+void sa_default_settings(sa_settings *s) {
+    static const int32_t hoxd[16] = {91, -114, -31, -123, -114, 100, -125, -31,
+                                     -31, -125, 100, -114, -123, -31, -114, 91};
+    memset(s, 0, sizeof(*s));
+    s->kmer_size = 12;
+    s->min_overlap = 40;
+    s->max_ignore = 90;
+    s->gap_open = -200;
+    s->gap_extend = -20;
+    s->min_collisions = 7;
+    s->max_collisions = 222;
+    s->min_identity = 0.98f;
+    s->kmer_edge = 0.4f;
+    s->kmer_center = 0.4f;
+    memcpy(s->cost, hoxd, sizeof(hoxd));
+    s->id_mode = SA_IDS_AUTO;
+}
+
+int sa_ctx_create(const sa_settings *s, int device, sa_ctx **out) {
+    if (!s || !out) return SA_E_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) return SA_E_HIP;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return SA_E_HIP;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return SA_E_HIP;  // code objects are gfx950 only
+    if (hipSetDevice(device) != hipSuccess) return SA_E_HIP;
+    sa_ctx *c = new sa_ctx();
+    c->set = *s;
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return SA_E_HIP;
+    }
+    *out = c;
+    return SA_OK;
+}
+
+void sa_ctx_destroy(sa_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    DBuf *bufs[] = {&c->d_ascii, &c->d_boff, &c->d_woff, &c->d_len, &c->d_codes, &c->d_bad, &c->d_occ_off,
+                    &c->d_lbase, &c->d_lrank, &c->d_tagtab, &c->d_keys, &c->d_vals, &c->d_keys2, &c->d_vals2,
+                    &c->d_sorttmp, &c->d_md, &c->d_ed, &c->d_bmdo, &c->d_bedo, &c->d_bstart, &c->d_gbid,
+                    &c->d_gmds, &c->d_gede, &c->d_ogid, &c->d_bkttmp, &c->d_mdidx, &c->d_edidx, &c->d_occidx,
+                    &c->d_bnst, &c->d_brank, &c->d_bhash, &c->d_bfirst, &c->d_pf, &c->d_ps, &c->d_pc, &c->d_pr,
+                    &c->d_ovl, &c->d_cnt, &c->d_okeys, &c->d_ovals, &c->d_okeys2, &c->d_ovals2, &c->d_osort,
+                    &c->d_lead, &c->d_trail, &c->d_count, &c->d_aln};
+    for (DBuf *b : bufs)
+        if (b->p) (void)hipFree(b->p);
+    for (auto &p : c->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
+    for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char *sa_last_error(const sa_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int sa_add_reads(sa_ctx *c, const char *bases, const uint64_t *offsets, uint32_t n) {
+    if (!c || (n && (!bases || !offsets))) return SA_E_ARG;
+    const uint64_t base0 = c->bases.size();
+    for (uint32_t r = 0; r < n; ++r) {
+        if (offsets[r + 1] < offsets[r]) return fail(c, SA_E_ARG, "offsets must be non-decreasing");
+    }
+    c->bases.insert(c->bases.end(), bases + offsets[0], bases + offsets[n]);
+    for (uint32_t r = 0; r < n; ++r) c->boff.push_back(base0 + (offsets[r + 1] - offsets[0]));
+    c->reads_dirty = true;
+    c->built = c->aligned = false;
+    return SA_OK;
+}
+
+int sa_read_fasta(sa_ctx *c, const char *path) {
+    if (!c || !path) return SA_E_ARG;
+    std::vector<char> b;
+    std::vector<uint64_t> off;
+    if (read_fasta(path, b, off) != 0) return fail(c, SA_E_INPUT, std::string("Invalid Sequence File: ") + path);
+    return sa_add_reads(c, b.data(), off.data(), (uint32_t)(off.size() - 1));
+}
+
+uint32_t sa_num_reads(const sa_ctx *c) { return c ? (uint32_t)(c->boff.size() - 1) : 0; }
+
+int sa_build_candidates(sa_ctx *c) {
+    if (!c) return SA_E_ARG;
+    (void)hipSetDevice(c->device);
+    return device_build(c, true);
+}
+
+int sa_device_build(sa_ctx *c) {
+    if (!c) return SA_E_ARG;
+    (void)hipSetDevice(c->device);
+    return device_build(c, false);
+}
+
+int sa_get_dispatch(sa_ctx *c, const int32_t **lead, const int32_t **trail, const int32_t **count, size_t *n) {
+    if (!c || !n) return SA_E_ARG;
+    if (!c->built) return fail(c, SA_E_STATE, "no candidates built");
+    if (c->lead.size() != c->n_disp) {  // device-only build: fetch now
+        c->lead.resize(c->n_disp); c->trail.resize(c->n_disp); c->count.resize(c->n_disp);
+        if (c->n_disp) {
+            HIPCHK(hipMemcpy(c->lead.data(), c->d_lead.p, c->n_disp * 4, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(c->trail.data(), c->d_trail.p, c->n_disp * 4, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(c->count.data(), c->d_count.p, c->n_disp * 4, hipMemcpyDeviceToHost));
+        }
+    }
+    if (lead) *lead = c->lead.data();
+    if (trail) *trail = c->trail.data();
+    if (count) *count = c->count.data();
+    *n = c->n_disp;
+    return SA_OK;
+}
+
+int sa_get_pairs(sa_ctx *c, const int32_t **fst, const int32_t **snd, const int32_t **count, size_t *n) {
+    if (!c || !n) return SA_E_ARG;
+    if (!c->built || !c->keep_pairs) return fail(c, SA_E_STATE, "pairs not kept (SA_OPT_KEEP_PAIRS)");
+    if (fst) *fst = c->pfst.data();
+    if (snd) *snd = c->psnd.data();
+    if (count) *count = c->pcnt.data();
+    *n = c->pfst.size();
+    return SA_OK;
+}
+
+int sa_align(sa_ctx *c) {
+    if (!c) return SA_E_ARG;
+    (void)hipSetDevice(c->device);
+    return device_align(c, true);
+}
+
+int sa_device_align(sa_ctx *c) {
+    if (!c) return SA_E_ARG;
+    (void)hipSetDevice(c->device);
+    return device_align(c, false);
+}
+
+int sa_get_alignments(sa_ctx *c, const sa_alignment **out, size_t *n) {
+    if (!c || !out || !n) return SA_E_ARG;
+    if (!c->aligned) return fail(c, SA_E_STATE, "no alignments");
+    if (c->alns.size() != c->n_disp) {
+        c->alns.resize(c->n_disp);
+        if (c->n_disp)
+            HIPCHK(hipMemcpy(c->alns.data(), c->d_aln.p, c->n_disp * sizeof(sa_alignment), hipMemcpyDeviceToHost));
+    }
+    *out = c->alns.data();
+    *n = c->alns.size();
+    return SA_OK;
+}
+
+int sa_get_ovl(sa_ctx *c, const char **text, size_t *len) {
+    if (!c || !text || !len) return SA_E_ARG;
+    if (!c->aligned) return fail(c, SA_E_STATE, "no alignments");
+    *text = c->ovl.data();
+    *len = c->ovl.size();
+    return SA_OK;
+}
+
+int sa_write_ovl(sa_ctx *c, const char *path) {
+    if (!c) return SA_E_ARG;
+    if (!c->aligned) return fail(c, SA_E_STATE, "no alignments");
+    FILE *f = path ? fopen(path, "wb") : stdout;  // the file is deleted and recreated (Project4.scala:797-805)
+    if (!f) return fail(c, SA_E_INPUT, std::string("cannot write ") + path);
+    const size_t w = fwrite(c->ovl.data(), 1, c->ovl.size(), f);
+    if (path) fclose(f); else fflush(f);
+    return w == c->ovl.size() ? SA_OK : fail(c, SA_E_INPUT, "short write");
+}
+
+int sa_set_option(sa_ctx *c, int option, int64_t value) {
+    if (!c) return SA_E_ARG;
+    switch (option) {
+    case SA_OPT_KEEP_PAIRS: c->keep_pairs = value != 0; return SA_OK;
+    case SA_OPT_TIMING: c->timing = value != 0; return SA_OK;
+    default: return fail(c, SA_E_ARG, "unknown option");
+    }
+}
+
+int sa_get_stats(const sa_ctx *c, sa_stats *out) {
+    if (!c || !out) return SA_E_ARG;
+    *out = c->stats;
+    return SA_OK;
+}
+
+int sa_get_stage_times(const sa_ctx *c, double *ms, uint64_t *launches, int n) {
+    if (!c) return SA_E_ARG;
+    for (int i = 0; i < n && i < SA_NUM_STAGES; ++i) {
+        if (ms) ms[i] = c->stage_ms[i];
+        if (launches) launches[i] = c->stage_n[i];
+    }
+    return SA_OK;
+}
+
+int sa_reset_stage_times(sa_ctx *c) {
+    if (!c) return SA_E_ARG;
+    for (int i = 0; i < SA_NUM_STAGES; ++i) { c->stage_ms[i] = 0; c->stage_n[i] = 0; }
+    return SA_OK;
+}
+
+int sa_sync(sa_ctx *c) {
+    if (!c) return SA_E_ARG;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return SA_OK;
+}
+
+int sa_load_hoxd(sa_settings *s, const char *path) {
+    if (!s || !path) return SA_E_ARG;
+    return read_hoxd(path, s->cost) == 0 ? SA_OK : SA_E_INPUT;
+}
+
+}  // extern "C"

@@ -1,0 +1,114 @@
+// pack_emit.hip -- 2-bit read packing and per-read k-mer emission (gfx950).
+//
+// Replaces BioLibs.generateKmerSet (BioLibs.scala:54-61) + Kmer.seqHash
+// (ObjectStore.scala:48-67).  One wavefront per read; lanes walk positions, so
+// every k-mer record write is a coalesced 8-byte (key) + 4-byte (payload) store.
+// Bound: HBM (integer byte work; no MFMA).
+#include "../sa_internal.h"
+
+namespace sa {
+
+// ASCII -> 2-bit HOXD code (A0 C1 G2 T3), after readSeq's toUpperCase.
+__device__ __forceinline__ int base_code(uint32_t ch, bool &ok) {
+    ch |= 0x20u;  // fold to lower case (non-letters stay non-ACGT)
+    ok = true;
+    switch (ch) {
+    case 'a': return 0;
+    case 'c': return 1;
+    case 'g': return 2;
+    case 't': return 3;
+    default: ok = false; return 0;
+    }
+}
+
+// One wave per read, lane = one 16-base word.
+__global__ __launch_bounds__(256) void pack_reads_kernel(DevReads r) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t rd = wave; rd < r.n; rd += nwaves) {
+        const uint64_t b0 = r.boff[rd];
+        const int32_t L = (int32_t)(r.boff[rd + 1] - b0);
+        const uint64_t w0 = r.woff[rd];
+        const int32_t nw = (L + 15) >> 4;
+        int32_t first_bad = INT32_MAX;
+        for (int32_t q = lane; q < nw; q += 64) {
+            uint32_t word = 0;
+            const int32_t p0 = q << 4;
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                const int32_t p = p0 + t;
+                if (p < L) {
+                    bool ok;
+                    const int c = base_code(r.ascii[b0 + p], ok);
+                    word |= (uint32_t)c << (30 - 2 * t);
+                    if (!ok && p < first_bad) first_bad = p;
+                }
+            }
+            r.codes[w0 + q] = word;
+        }
+        // wave-wide min of first_bad
+        for (int off = 32; off > 0; off >>= 1) {
+            const int32_t o = __shfl_xor(first_bad, off, 64);
+            first_bad = o < first_bad ? o : first_bad;
+        }
+        if (lane == 0) r.bad[rd] = first_bad;
+    }
+}
+
+// 16 codes starting at base position p of a read whose first word is `w`
+// (MSB-first window), used for hashing and diagonal compares.
+__device__ __forceinline__ uint32_t window16(const uint32_t *w, int32_t p) {
+    const uint32_t a = w[p >> 4];
+    const int s = p & 15;
+    if (s == 0) return a;
+    const uint32_t b = w[(p >> 4) + 1];
+    return (a << (2 * s)) | (b >> (32 - 2 * s));
+}
+
+// One wave per read, lane = position.  key = seqHash << lb | locrank, val = g.
+__global__ __launch_bounds__(256) void kmer_emit_kernel(DevReads r, EmitParams e, uint64_t *keys,
+                                                        uint32_t *vals) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    const int shift = 32 - 2 * e.m;
+    for (uint32_t rd = wave; rd < r.n; rd += nwaves) {
+        const int32_t L = r.len[rd];
+        const int32_t nk = L - e.k + 1;
+        if (nk <= 0) continue;
+        const uint32_t *w = r.codes + r.woff[rd];
+        const uint64_t g0 = e.occ_off[rd];
+        const int32_t d = L - e.k;
+        const uint32_t *lr = e.lrank + e.lbase[d];
+        for (int32_t i = lane; i < nk; i += 64) {
+            uint32_t x = window16(w, i);
+            x = shift == 32 ? 0u : (x >> shift);
+            // HOXD order (A0 C1 G2 T3) -> seqHash order (A0 C1 T2 G3): c ^ (c >> 1)
+            x ^= (x >> 1) & 0x55555555u;
+            keys[g0 + i] = ((uint64_t)x << e.lb) | (uint64_t)lr[i];
+            vals[g0 + i] = (uint32_t)(g0 + i);
+        }
+    }
+}
+
+static uint32_t grid_for_waves(uint64_t waves) {
+    uint64_t blocks = (waves + 3) / 4;
+    if (blocks > 8192) blocks = 8192;
+    return (uint32_t)(blocks ? blocks : 1);
+}
+
+hipError_t launch_pack_reads(const DevReads &r, hipStream_t s) {
+    if (r.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(pack_reads_kernel, dim3(grid_for_waves(r.n)), dim3(256), 0, s, r);
+    return hipGetLastError();
+}
+
+hipError_t launch_kmer_emit(const DevReads &r, const EmitParams &p, uint64_t *keys, uint32_t *vals,
+                            hipStream_t s) {
+    if (r.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(kmer_emit_kernel, dim3(grid_for_waves(r.n)), dim3(256), 0, s, r, p, keys, vals);
+    return hipGetLastError();
+}
+
+}  // namespace sa

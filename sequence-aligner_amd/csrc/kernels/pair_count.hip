@@ -1,0 +1,308 @@
+// pair_count.hip -- edge<->middle candidate-pair counting and collision filter.
+//
+// Device replacement of KmerTable.calcPairData / addKmerPair / calcDispatchData
+// (KmerTable.scala:57-187).  Organised by the pair's FIRST read (the occurrence
+// with the larger loc, KmerTable.scala:65-71): one workgroup per read `a`
+// enumerates exactly the role pairs whose fst is `a` --
+//   each edge (st/en) k-mer of a  x  middle k-mers of its bucket with loc <  own
+//   each middle k-mer of a        x  edge roles of its bucket with loc <= own
+// -- so every (st x md) / (en x md) pair of the reference is visited once, by
+// the read that becomes `fst`, and all counts of key (a, b) land in ONE LDS hash
+// table: no global atomics, no role-pair materialisation.  The [min, max]
+// collision filter is applied on chip.  Strict mode also tracks each key's
+// first-occurrence rank in calcPairData's traversal order, from which the host
+// replays GNU Trove's PairData layout.
+// Work is load-balanced inside the workgroup over the prefix sum of per-k-mer
+// partner counts.  Bound: gather latency / LDS atomics; HBM bytes are small.
+#include "../sa_internal.h"
+
+namespace sa {
+
+constexpr int PC_THREADS = 256;
+constexpr int PC_TAB = 2048;             // LDS hash slots per read
+constexpr int PC_FILL_MAX = PC_TAB * 3 / 4;
+constexpr int PC_CHUNK = 1024;           // occurrences per pass over a read
+constexpr uint32_t PC_EMPTY = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t pc_hash(uint32_t p) { return (p * 0x9E3779B1u) >> (32 - 11); }
+
+struct PcShared {
+    uint32_t key[PC_TAB];
+    uint32_t cnt[PC_TAB];
+    uint32_t pref[PC_CHUNK + 1];
+    uint32_t e0[PC_CHUNK];     // first md-list entry of the bucket (edge role partners)
+    uint32_t d0[PC_CHUNK];     // first edge-list entry of the bucket (middle role partners)
+    uint32_t ne[PC_CHUNK];     // number of edge-role partners; bits 30-31 = edge multiplicity
+    uint32_t lds4[4];
+    uint32_t fill, overflow, total, out_base;
+};
+struct PcSharedStrict {
+    unsigned long long rank[PC_TAB];
+    uint32_t bid[PC_CHUNK];
+    uint32_t own_e[PC_CHUNK];  // (phase<<31) | own st/en index
+    uint32_t own_m[PC_CHUNK];  // own md index
+};
+
+__device__ __forceinline__ uint32_t pc_block_excl_scan(uint32_t v, uint32_t *lds4, uint32_t *total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += t;
+    }
+    if (lane == 63) lds4[w] = inc;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < PC_THREADS / 64; ++i) {
+        const uint32_t x = lds4[i];
+        if (i < w) off += x;
+        tot += x;
+    }
+    __syncthreads();
+    *total = tot;
+    return off + inc - v;
+}
+
+template <bool STRICT>
+__global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(DevReads r, EmitParams e, Buckets b,
+                                                                const uint8_t *tagtab, PairParams p, PairOut o,
+                                                                const uint32_t *read_list) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    PcShared &S = *reinterpret_cast<PcShared *>(smem);
+    PcSharedStrict &X = *reinterpret_cast<PcSharedStrict *>(smem + ((sizeof(PcShared) + 15) & ~size_t(15)));
+    const int tid = threadIdx.x;
+    const uint32_t split = (uint32_t)p.split;
+    const uint32_t item = blockIdx.x / split;
+    const uint32_t residue = blockIdx.x % split;
+    const uint32_t a = read_list ? read_list[item] : item;
+
+    for (int i = tid; i < PC_TAB; i += PC_THREADS) {
+        S.key[i] = PC_EMPTY;
+        S.cnt[i] = 0;
+        if constexpr (STRICT) X.rank[i] = ~0ull;
+    }
+    if (tid == 0) { S.fill = 0; S.overflow = 0; }
+
+    const uint64_t g0 = e.occ_off[a];
+    const uint32_t nocc = (uint32_t)(e.occ_off[a + 1] - g0);
+    const int32_t L = r.len[a];
+    const uint32_t *lr = nocc ? e.lrank + e.lbase[L - e.k] : nullptr;
+    const uint64_t lbm = (1ull << e.lb) - 1;
+    unsigned long long role_pairs = 0;
+    __syncthreads();
+
+    for (uint32_t c0 = 0; c0 < nocc; c0 += PC_CHUNK) {
+        const uint32_t cn = min((uint32_t)PC_CHUNK, nocc - c0);
+        // --- per-occurrence partner ranges -------------------------------
+        uint32_t mytot[PC_CHUNK / PC_THREADS];
+#pragma unroll
+        for (int j = 0; j < PC_CHUNK / PC_THREADS; ++j) {
+            const uint32_t oi = tid * (PC_CHUNK / PC_THREADS) + j;  // thread-contiguous
+            uint32_t tot = 0;
+            if (oi < cn) {
+                const uint64_t g = g0 + c0 + oi;
+                const uint32_t t = tagtab[lr[c0 + oi] & lbm];
+                const uint32_t gid = b.occ_gid[g];
+                const uint32_t bid = b.grp_bid[gid];
+                const uint32_t me = ((t & TAG_ST) ? 1u : 0u) + ((t & TAG_EN) ? 1u : 0u);
+                const uint32_t mdo = b.bkt_mdo[bid], edo = b.bkt_edo[bid];
+                const uint32_t nE = me ? (b.grp_mds[gid] - mdo) : 0u;
+                const uint32_t nD = (t & TAG_MD) ? (b.grp_ede[gid] - edo) : 0u;
+                S.e0[oi] = mdo;
+                S.d0[oi] = edo;
+                S.ne[oi] = nE | (me << 30);
+                tot = nE + nD;
+                if constexpr (STRICT) {
+                    X.bid[oi] = bid;
+                    X.own_e[oi] = (t & TAG_ST) ? b.occ_idx[3 * g + 0] : ((1u << 31) | b.occ_idx[3 * g + 2]);
+                    X.own_m[oi] = b.occ_idx[3 * g + 1];
+                }
+            }
+            mytot[j] = tot;
+        }
+        uint32_t s = 0;
+#pragma unroll
+        for (int j = 0; j < PC_CHUNK / PC_THREADS; ++j) s += mytot[j];
+        uint32_t total;
+        uint32_t ex = pc_block_excl_scan(s, S.lds4, &total);
+#pragma unroll
+        for (int j = 0; j < PC_CHUNK / PC_THREADS; ++j) {
+            const uint32_t oi = tid * (PC_CHUNK / PC_THREADS) + j;
+            if (oi <= cn) S.pref[oi] = ex;   // pref[cn] = total (exclusive prefix of padding = total)
+            ex += mytot[j];
+        }
+        if (tid == PC_THREADS - 1 && cn == PC_CHUNK) S.pref[PC_CHUNK] = total;
+        role_pairs += total;
+        __syncthreads();
+
+        // --- load-balanced enumeration: thread takes a contiguous chunk ------
+        const uint32_t per = (total + PC_THREADS - 1) / PC_THREADS;
+        const uint32_t t0 = min(total, tid * per), t1 = min(total, t0 + per);
+        if (t0 < t1) {
+            uint32_t lo = 0, hi = cn;  // last oi with pref[oi] <= t0
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (S.pref[mid] <= t0) lo = mid; else hi = mid;
+            }
+            uint32_t oi = lo;
+            uint32_t nxt = S.pref[oi + 1];
+            for (uint32_t t = t0; t < t1; ++t) {
+                while (t >= nxt) { ++oi; nxt = S.pref[oi + 1]; }
+                const uint32_t off = t - S.pref[oi];
+                const uint32_t nev = S.ne[oi];
+                const uint32_t nE = nev & 0x3FFFFFFFu;
+                uint32_t partner, w;
+                unsigned long long rank = 0;
+                if (off < nE) {
+                    const uint32_t q = S.e0[oi] + off;
+                    partner = b.md_list[q];
+                    w = nev >> 30;
+                    if constexpr (STRICT) {
+                        const uint32_t bid = X.bid[oi];
+                        const uint32_t nmd = b.bkt_mdo[bid + 1] - b.bkt_mdo[bid];
+                        const uint32_t nst = b.bkt_nst[bid];
+                        const uint32_t oe = X.own_e[oi];
+                        const unsigned long long within =
+                            (unsigned long long)(oe >> 31) * nst * nmd +
+                            (unsigned long long)(oe & 0x7FFFFFFFu) * nmd + b.md_idx[q];
+                        rank = ((unsigned long long)b.bkt_rank[bid] << 37) | within;
+                    }
+                } else {
+                    const uint32_t q = S.d0[oi] + (off - nE);
+                    partner = b.ed_list[q];
+                    w = 1;
+                    if constexpr (STRICT) {
+                        const uint32_t bid = X.bid[oi];
+                        const uint32_t nmd = b.bkt_mdo[bid + 1] - b.bkt_mdo[bid];
+                        const uint32_t nst = b.bkt_nst[bid];
+                        const uint32_t pe = b.ed_idx[q];
+                        const unsigned long long within =
+                            (unsigned long long)(pe >> 31) * nst * nmd +
+                            (unsigned long long)(pe & 0x7FFFFFFFu) * nmd + X.own_m[oi];
+                        rank = ((unsigned long long)b.bkt_rank[bid] << 37) | within;
+                    }
+                }
+                if (partner == a) continue;                 // same read (KmerTable.scala:61-63)
+                if (split > 1 && (partner % split) != residue) continue;
+                if (S.overflow) break;
+                uint32_t slot = pc_hash(partner);
+                for (int probe = 0; probe < PC_TAB; ++probe) {
+                    const uint32_t old = atomicCAS(&S.key[slot], PC_EMPTY, partner);
+                    if (old == PC_EMPTY || old == partner) {
+                        if (old == PC_EMPTY && atomicAdd(&S.fill, 1u) >= (uint32_t)PC_FILL_MAX) S.overflow = 1;
+                        atomicAdd(&S.cnt[slot], w);
+                        if constexpr (STRICT) atomicMin(&X.rank[slot], rank);
+                        break;
+                    }
+                    slot = (slot + 1) & (PC_TAB - 1);
+                }
+            }
+        }
+        __syncthreads();
+    }
+
+    if (tid == 0 && residue == 0 && role_pairs) atomicAdd(o.role_pairs, role_pairs);
+    if (tid == 0 && !S.overflow) atomicAdd(o.distinct, (unsigned long long)S.fill);
+    if (S.overflow) {
+        if (tid == 0 && residue == 0) {
+            const uint32_t at = atomicAdd(o.overflow_n, 1u);
+            o.overflow_list[at] = a;
+        }
+        return;
+    }
+    // --- emit (a, partner, count[, rank]) --------------------------------
+    constexpr int PER = PC_TAB / PC_THREADS;
+    uint32_t keep = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const uint32_t sl = tid * PER + j;
+        const uint32_t c = S.cnt[sl];
+        if (S.key[sl] != PC_EMPTY && (p.emit_all || ((int32_t)c >= p.min_coll && (int32_t)c <= p.max_coll)))
+            keep |= 1u << j;
+    }
+    uint32_t total;
+    uint32_t ex = pc_block_excl_scan(__popc(keep), S.lds4, &total);
+    if (total == 0) return;
+    if (tid == 0) S.out_base = (uint32_t)atomicAdd(o.cursor, (unsigned long long)total);
+    __syncthreads();
+    const unsigned long long base = (unsigned long long)S.out_base + ex;
+    uint32_t k = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        if (!(keep & (1u << j))) continue;
+        const uint32_t sl = tid * PER + j;
+        const unsigned long long at = base + k++;
+        if (at < o.cap) {
+            o.fst[at] = a;
+            o.snd[at] = S.key[sl];
+            o.cnt[at] = S.cnt[sl];
+            if constexpr (STRICT) o.rank[at] = X.rank[sl];
+        }
+    }
+}
+
+size_t pair_count_lds_bytes(bool strict) {
+    size_t s = (sizeof(PcShared) + 15) & ~size_t(15);
+    if (strict) s += sizeof(PcSharedStrict);
+    return s;
+}
+
+hipError_t launch_pair_count(const DevReads &r, const EmitParams &e, const Buckets &b, const uint8_t *tagtab,
+                             const PairParams &p, PairOut &o, const uint32_t *read_list, uint32_t n_blocks,
+                             hipStream_t s) {
+    if (n_blocks == 0) return hipSuccess;
+    const size_t lds = pair_count_lds_bytes(p.strict != 0);
+    if (p.strict) {
+        (void)hipFuncSetAttribute((const void *)pair_count_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(pair_count_kernel<true>, dim3(n_blocks), dim3(PC_THREADS), lds, s, r, e, b, tagtab, p, o,
+                           read_list);
+    } else {
+        (void)hipFuncSetAttribute((const void *)pair_count_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(pair_count_kernel<false>, dim3(n_blocks), dim3(PC_THREADS), lds, s, r, e, b, tagtab, p,
+                           o, read_list);
+    }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// output ordering helpers
+// ---------------------------------------------------------------------------
+__global__ void make_order_keys_kernel(const uint32_t *fst, const uint32_t *snd, const uint64_t *rank, uint64_t n,
+                                       int by_rank, int idbits, uint64_t *keys, uint32_t *vals) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    // wide: lead descending then trail ascending; strict: first-occurrence rank
+    const uint64_t top = (1ull << idbits) - 1;
+    keys[i] = by_rank ? rank[i] : (((top - fst[i]) << idbits) | snd[i]);
+    vals[i] = (uint32_t)i;
+}
+
+hipError_t launch_make_order_keys(const uint32_t *fst, const uint32_t *snd, const uint64_t *rank, uint64_t n,
+                                  int by_rank, int idbits, uint64_t *keys, uint32_t *vals, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(make_order_keys_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, fst, snd, rank, n,
+                       by_rank, idbits, keys, vals);
+    return hipGetLastError();
+}
+
+__global__ void gather_pairs_kernel(const uint32_t *perm, uint64_t n, const uint32_t *fst, const uint32_t *snd,
+                                    const uint32_t *cnt, int32_t *lead, int32_t *trail, int32_t *count) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t j = perm[i];
+    lead[i] = (int32_t)fst[j] + 1;  // reference ids are 1-based
+    trail[i] = (int32_t)snd[j] + 1;
+    count[i] = (int32_t)cnt[j];
+}
+
+hipError_t launch_gather_pairs(const uint32_t *perm, uint64_t n, const uint32_t *fst, const uint32_t *snd,
+                               const uint32_t *cnt, int32_t *lead, int32_t *trail, int32_t *count, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(gather_pairs_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, perm, n, fst, snd,
+                       cnt, lead, trail, count);
+    return hipGetLastError();
+}
+
+}  // namespace sa

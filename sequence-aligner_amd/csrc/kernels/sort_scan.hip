@@ -1,0 +1,224 @@
+// sort_scan.hip -- hand-written device primitives for gfx950:
+//   * exclusive prefix scan of u32 (reduce-then-scan, 3 launches)
+//   * stable LSD radix sort of (u64 key, u32 value) over a key bit range,
+//     8-bit digits, per-wave 64-lane ballot multisplit for stable local ranks.
+// These group k-mer records by hash (the device replacement of KmerData,
+// KmerTable.scala:26-53) and order candidate pairs.  Bound: HBM.
+#include "../sa_internal.h"
+
+namespace sa {
+
+constexpr int SC_THREADS = 256;
+constexpr int SC_ITEMS = 8;
+constexpr int SC_TILE = SC_THREADS * SC_ITEMS;
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = __shfl_up(v, off, 64);
+        if (lane >= off) v += t;
+    }
+    return v;
+}
+
+// Block-wide exclusive scan of one value per thread (256 threads); returns the
+// exclusive prefix, *total = block sum.
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *lds4, uint32_t *total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t inc = wave_incl_scan(v, lane);
+    if (lane == 63) lds4[w] = inc;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < SC_THREADS / 64; ++i) {
+        const uint32_t x = lds4[i];
+        if (i < w) off += x;
+        tot += x;
+    }
+    __syncthreads();
+    *total = tot;
+    return off + inc - v;
+}
+
+__global__ __launch_bounds__(SC_THREADS) void scan_reduce_kernel(const uint32_t *in, uint64_t n,
+                                                                 uint32_t *partial) {
+    __shared__ uint32_t lds4[4];
+    const uint64_t base = (uint64_t)blockIdx.x * SC_TILE;
+    uint32_t s = 0;
+#pragma unroll
+    for (int j = 0; j < SC_ITEMS; ++j) {
+        const uint64_t i = base + (uint64_t)j * SC_THREADS + threadIdx.x;
+        if (i < n) s += in[i];
+    }
+    uint32_t tot;
+    block_excl_scan(s, lds4, &tot);
+    if (threadIdx.x == 0) partial[blockIdx.x] = tot;
+}
+
+// single block: exclusive scan of partial[0..m) in place, total -> *total
+__global__ __launch_bounds__(SC_THREADS) void scan_partials_kernel(uint32_t *partial, uint32_t m,
+                                                                   uint32_t *total) {
+    __shared__ uint32_t lds4[4];
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < m; base += SC_THREADS) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t v = i < m ? partial[i] : 0;
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan(v, lds4, &tot);
+        if (i < m) partial[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0 && total) *total = carry;
+}
+
+__global__ __launch_bounds__(SC_THREADS) void scan_down_kernel(const uint32_t *in, uint32_t *out,
+                                                               uint64_t n, const uint32_t *partial) {
+    __shared__ uint32_t lds4[4];
+    __shared__ uint32_t tile[SC_TILE];
+    const uint64_t base = (uint64_t)blockIdx.x * SC_TILE;
+#pragma unroll
+    for (int j = 0; j < SC_ITEMS; ++j) {  // coalesced load into LDS
+        const uint64_t i = base + (uint64_t)j * SC_THREADS + threadIdx.x;
+        tile[j * SC_THREADS + threadIdx.x] = i < n ? in[i] : 0;
+    }
+    __syncthreads();
+    uint32_t v[SC_ITEMS], s = 0;
+#pragma unroll
+    for (int j = 0; j < SC_ITEMS; ++j) {  // thread-contiguous items
+        v[j] = tile[threadIdx.x * SC_ITEMS + j];
+        s += v[j];
+    }
+    uint32_t tot;
+    uint32_t ex = block_excl_scan(s, lds4, &tot) + partial[blockIdx.x];
+#pragma unroll
+    for (int j = 0; j < SC_ITEMS; ++j) {
+        tile[threadIdx.x * SC_ITEMS + j] = ex;
+        ex += v[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < SC_ITEMS; ++j) {
+        const uint64_t i = base + (uint64_t)j * SC_THREADS + threadIdx.x;
+        if (i < n) out[i] = tile[j * SC_THREADS + threadIdx.x];
+    }
+}
+
+size_t scan_temp_bytes(uint64_t n) {
+    const uint64_t nb = (n + SC_TILE - 1) / SC_TILE;
+    return (nb + 64) * sizeof(uint32_t);
+}
+
+hipError_t exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *total_dev,
+                              void *tmp, hipStream_t s) {
+    if (n == 0) {
+        if (total_dev) return hipMemsetAsync(total_dev, 0, sizeof(uint32_t), s);
+        return hipSuccess;
+    }
+    const uint64_t nb = (n + SC_TILE - 1) / SC_TILE;
+    uint32_t *partial = (uint32_t *)tmp;
+    hipLaunchKernelGGL(scan_reduce_kernel, dim3((uint32_t)nb), dim3(SC_THREADS), 0, s, in, n, partial);
+    hipLaunchKernelGGL(scan_partials_kernel, dim3(1), dim3(SC_THREADS), 0, s, partial, (uint32_t)nb, total_dev);
+    hipLaunchKernelGGL(scan_down_kernel, dim3((uint32_t)nb), dim3(SC_THREADS), 0, s, in, out, n,
+                       (const uint32_t *)partial);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// radix sort
+// ---------------------------------------------------------------------------
+constexpr int RS_THREADS = 256;
+constexpr int RS_ITEMS = 16;
+constexpr int RS_TILE = RS_THREADS * RS_ITEMS;
+
+__global__ __launch_bounds__(RS_THREADS) void rs_upsweep_kernel(const uint64_t *keys, uint64_t n, int shift,
+                                                                uint32_t *hist, uint32_t nblocks) {
+    __shared__ uint32_t cnt[256];
+    cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+#pragma unroll 4
+    for (int j = 0; j < RS_ITEMS; ++j) {
+        const uint64_t i = base + (uint64_t)j * RS_THREADS + threadIdx.x;
+        if (i < n) atomicAdd(&cnt[(uint32_t)(keys[i] >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    hist[(uint64_t)threadIdx.x * nblocks + blockIdx.x] = cnt[threadIdx.x];
+}
+
+// Stable scatter: elements keep tile order (slice j, then thread) inside each digit.
+__global__ __launch_bounds__(RS_THREADS) void rs_downsweep_kernel(const uint64_t *kin, const uint32_t *vin,
+                                                                  uint64_t *kout, uint32_t *vout, uint64_t n,
+                                                                  int shift, const uint32_t *hist,
+                                                                  uint32_t nblocks) {
+    __shared__ uint32_t run[256];     // next output position of each digit for this block
+    __shared__ uint32_t wcnt[4][256]; // per-wave digit counts of the current slice
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    run[tid] = hist[(uint64_t)tid * nblocks + blockIdx.x];
+    const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int j = 0; j < RS_ITEMS; ++j) {
+        const uint64_t i = base + (uint64_t)j * RS_THREADS + tid;
+        const bool valid = i < n;
+        const uint64_t key = valid ? kin[i] : 0ull;
+        const uint32_t val = valid ? vin[i] : 0u;
+        const uint32_t d = (uint32_t)(key >> shift) & 255u;
+        uint64_t peer = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            peer &= bit ? bb : ~bb;
+        }
+        const uint32_t rank_w = __popcll(peer & lt_mask);
+        const uint32_t cnt_w = __popcll(peer);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) wcnt[w][lane * 4 + q] = 0;
+        __syncthreads();
+        if (valid && rank_w == 0) wcnt[w][d] = cnt_w;
+        __syncthreads();
+        {   // digit tid: exclusive prefix across the 4 waves, in place
+            uint32_t acc = run[tid];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t c = wcnt[q][tid];
+                wcnt[q][tid] = acc;
+                acc += c;
+            }
+            run[tid] = acc;
+        }
+        __syncthreads();
+        if (valid) {
+            const uint32_t pos = wcnt[w][d] + rank_w;
+            kout[pos] = key;
+            vout[pos] = val;
+        }
+        __syncthreads();
+    }
+}
+
+size_t radix_sort_temp_bytes(uint64_t n) {
+    const uint64_t nb = (n + RS_TILE - 1) / RS_TILE;
+    const uint64_t hist = 256 * (nb ? nb : 1);
+    return hist * sizeof(uint32_t) + scan_temp_bytes(hist) + 256;
+}
+
+hipError_t radix_sort(uint64_t **keys, uint32_t **vals, uint64_t **keys_alt, uint32_t **vals_alt,
+                      uint64_t n, int lo, int hi, void *tmp, hipStream_t s) {
+    if (n <= 1 || hi <= lo) return hipSuccess;
+    const uint64_t nb = (n + RS_TILE - 1) / RS_TILE;
+    uint32_t *hist = (uint32_t *)tmp;
+    void *stmp = (void *)(hist + 256 * nb);
+    for (int shift = lo; shift < hi; shift += 8) {
+        hipLaunchKernelGGL(rs_upsweep_kernel, dim3((uint32_t)nb), dim3(RS_THREADS), 0, s, *keys, n, shift, hist,
+                           (uint32_t)nb);
+        hipError_t e = exclusive_scan_u32(hist, hist, 256 * nb, nullptr, stmp, s);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(rs_downsweep_kernel, dim3((uint32_t)nb), dim3(RS_THREADS), 0, s, *keys, *vals,
+                           *keys_alt, *vals_alt, n, shift, (const uint32_t *)hist, (uint32_t)nb);
+        uint64_t *tk = *keys; *keys = *keys_alt; *keys_alt = tk;
+        uint32_t *tv = *vals; *vals = *vals_alt; *vals_alt = tv;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace sa

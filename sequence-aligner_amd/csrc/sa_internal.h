@@ -1,0 +1,132 @@
+// sa_internal.h -- device-side data layout and kernel launchers of the
+// MI355X hash-overlap stage.  Host orchestration lives in host/pipeline.cpp;
+// kernels live in kernels/*.hip.  See DESIGN.md for the HBM layout.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sa {
+
+// ---- packed reads --------------------------------------------------------
+// Read r (0-based; reference id r+1) occupies words [woff[r], woff[r+1]) of
+// `codes`; base p sits in word woff[r] + p/16 at bits 30-2*(p%16) (MSB first),
+// 2-bit HOXD order A0 C1 G2 T3 (BioLibs.scala:144-149).  Non-ACGT -> 0 and
+// `bad[r]` = first such position (else INT32_MAX).
+struct DevReads {
+    uint32_t n = 0;
+    const uint8_t *ascii = nullptr;   // raw bases
+    const uint64_t *boff = nullptr;   // [n+1] byte offsets
+    const uint64_t *woff = nullptr;   // [n+1] word offsets (+1 pad word at the end)
+    const int32_t *len = nullptr;     // [n]
+    uint32_t *codes = nullptr;        // packed 2-bit words
+    int32_t *bad = nullptr;           // [n]
+};
+
+// ---- k-mer emission parameters --------------------------------------------
+struct EmitParams {
+    int32_t k;                 // kmer size
+    int32_t m;                 // min(16, k): hashed window (ObjectStore.scala:52)
+    int32_t lb;                // locrank bits in the sort key
+    const uint64_t *occ_off;   // [n+1] first occurrence index of each read
+    const uint32_t *lbase;     // [maxd+1] offset of denominator d = L-k in lrank
+    const uint32_t *lrank;     // rank of float32 i/d among all distinct locs
+    int32_t maxd;
+};
+
+// bit 0 = st, bit 1 = md, bit 2 = en   (KmerTable.scala:106-115)
+enum : uint8_t { TAG_ST = 1, TAG_MD = 2, TAG_EN = 4 };
+
+// ---- bucket / list tables (after the (hash, locrank) sort) -----------------
+struct Buckets {
+    uint64_t n_occ = 0;
+    uint32_t n_buckets = 0, n_groups = 0, n_md = 0, n_ed = 0;
+    uint32_t *md_list = nullptr;     // read index of each middle occurrence, by (bucket, locrank, g)
+    uint32_t *ed_list = nullptr;     // read index of each edge role (st, en)
+    uint32_t *bkt_mdo = nullptr;     // [nb+1] first md entry of bucket
+    uint32_t *bkt_edo = nullptr;     // [nb+1] first edge entry of bucket
+    uint32_t *bkt_start = nullptr;   // [nb+1] first sorted position of bucket
+    uint32_t *grp_bid = nullptr;     // [ng] bucket of group
+    uint32_t *grp_mds = nullptr;     // [ng] md entries of the bucket before the group (locrank <)
+    uint32_t *grp_ede = nullptr;     // [ng] edge entries of the bucket through the group (locrank <=)
+    uint32_t *occ_gid = nullptr;     // [n_occ] group of occurrence g
+    // strict-mode annotations (reference order replay)
+    uint32_t *md_idx = nullptr;      // [n_md] index of the md entry in the bucket's (id,pos)-ordered md list
+    uint32_t *ed_idx = nullptr;      // [n_ed] (phase<<31) | index in the st (phase 0) / en (phase 1) list
+    uint32_t *occ_idx = nullptr;     // [3*n_occ] own st/md/en list index
+    uint32_t *bkt_nst = nullptr;     // [nb] |st| of bucket
+    uint32_t *bkt_rank = nullptr;    // [nb] KmerData iteration rank (host Trove replay)
+};
+
+struct PairParams {
+    int32_t min_coll, max_coll;
+    int32_t emit_all;      // 1: every distinct pair (PairData); 0: dispatched only
+    int32_t strict;        // compute first-occurrence ranks
+    int32_t split;         // partner residue classes (overflow fallback)
+    uint32_t max_occ;      // max occurrences of one read (LDS sizing)
+};
+
+struct PairOut {
+    uint32_t *fst, *snd, *cnt;   // [cap]
+    uint64_t *rank;              // [cap] (strict)
+    unsigned long long *cursor;  // entries written
+    unsigned long long cap;
+    unsigned long long *role_pairs;
+    unsigned long long *distinct;  // distinct (a, partner) keys counted
+    uint32_t *overflow_list;     // reads whose LDS table overflowed
+    uint32_t *overflow_n;
+};
+
+struct AlignParams {
+    int32_t k, gap_open, gap_extend, min_overlap;
+    float one_minus_minid, min_identity, max_ignore;
+    int32_t cost[16];
+    uint32_t rw;                 // traceback words per column (odd)
+};
+
+struct DevAlignment {            // mirrors sa_alignment
+    int32_t lead, trail, start_i, start_j, end_i, end_j, correct, error, ahg, bhg, flags, reserved;
+};
+
+// ---- launchers (kernels/*.hip) ------------------------------------------
+hipError_t launch_pack_reads(const DevReads &r, hipStream_t s);
+hipError_t launch_kmer_emit(const DevReads &r, const EmitParams &p, uint64_t *keys, uint32_t *vals,
+                            hipStream_t s);
+
+// stable LSD radix sort of (key, val) on key bits [lo, hi); ping-pong buffers,
+// result ends in (*keys, *vals) (pointers may be swapped).  tmp: sized by
+// radix_sort_temp_bytes.
+size_t radix_sort_temp_bytes(uint64_t n);
+hipError_t radix_sort(uint64_t **keys, uint32_t **vals, uint64_t **keys_alt, uint32_t **vals_alt,
+                      uint64_t n, int lo, int hi, void *tmp, hipStream_t s);
+
+// exclusive scan of u32 (in place allowed), returns total in *total_dev
+size_t scan_temp_bytes(uint64_t n);
+hipError_t exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *total_dev,
+                              void *tmp, hipStream_t s);
+
+// bucket/list build from sorted keys; totals written to totals_dev[4] =
+// {buckets, groups, md, ed}
+size_t buckets_temp_bytes(uint64_t n);
+hipError_t build_buckets(const uint64_t *skeys, const uint32_t *svals, uint64_t n, int lb,
+                         const uint8_t *tagtab, const uint64_t *occ_off, uint32_t n_reads,
+                         uint32_t uniform_npr, Buckets &b, uint32_t *totals_dev, void *tmp,
+                         hipStream_t s);
+hipError_t build_strict_index(const uint64_t *skeys, const uint32_t *svals, uint64_t n, int lb,
+                              const uint8_t *tagtab, Buckets &b, hipStream_t s);
+
+hipError_t launch_pair_count(const DevReads &r, const EmitParams &e, const Buckets &b,
+                             const uint8_t *tagtab, const PairParams &p, PairOut &o,
+                             const uint32_t *read_list, uint32_t n_blocks, hipStream_t s);
+
+hipError_t launch_make_order_keys(const uint32_t *fst, const uint32_t *snd, const uint64_t *rank,
+                                  uint64_t n, int by_rank, int idbits, uint64_t *keys, uint32_t *vals,
+                                  hipStream_t s);
+hipError_t launch_gather_pairs(const uint32_t *perm, uint64_t n, const uint32_t *fst, const uint32_t *snd,
+                               const uint32_t *cnt, int32_t *lead, int32_t *trail, int32_t *count,
+                               hipStream_t s);
+
+hipError_t launch_dovetail(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
+                           const AlignParams &p, int group_lanes, DevAlignment *out, int32_t *err,
+                           unsigned long long *cells, hipStream_t s);
+
+}  // namespace sa

@@ -1,0 +1,240 @@
+"""saoverlap -- Python binding of the MI355X hash-overlap stage (ctypes over libsa_overlap.so).
+
+Mirrors the reference's calc-overlaps path (rohit507/Sequence-Aligner,
+src/Project4.scala:56-60) through the C ABI in include/sa_overlap.h:
+
+    ov = Overlapper(kmer_size=15)        # AlignSettings (ObjectStore.scala:17-36)
+    ov.read_fasta("reads.seq")           # BioLibs.readSeq (BioLibs.scala:26-50)
+    ov.build()                           # KmerTable.calcPairData + calcDispatchData
+    lead, trail, count = ov.dispatch()   # DispatchData order (KmerTable.scala:251-271)
+    ov.align()                           # genBlockMTAlign -> generateFastDovetailAlignmentSet
+    ov.ovl()                             # Project4.calcOverlaps bytes
+
+There is no CPU fallback: the HIP library must be built (make -C sequence-aligner_amd)
+and a gfx950 device present, otherwise construction raises.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "libsa_overlap.so")
+
+SA_IDS_AUTO, SA_IDS_STRICT, SA_IDS_WIDE = 0, 1, 2
+SA_OPT_KEEP_PAIRS, SA_OPT_TIMING = 1, 2
+STAGES = ("pack", "emit", "sort", "buckets", "pairs", "order", "align")
+ERRORS = {-1: "SA_E_ARG", -2: "SA_E_INPUT", -3: "SA_E_NON_ACGT", -4: "SA_E_ID_RANGE", -5: "SA_E_SHORT_READ",
+          -6: "SA_E_DEGENERATE", -7: "SA_E_HIP", -8: "SA_E_NOMEM", -9: "SA_E_RCCL", -10: "SA_E_STATE",
+          -11: "SA_E_OVERFLOW"}
+FLAG_DUD, FLAG_VALID, FLAG_OVL_VALID = 1, 2, 4
+
+# exported symbols declared in include/sa_overlap.h
+EXPORTS = ("sa_default_settings", "sa_ctx_create", "sa_ctx_destroy", "sa_last_error", "sa_load_hoxd",
+           "sa_add_reads", "sa_read_fasta", "sa_num_reads", "sa_build_candidates", "sa_get_dispatch",
+           "sa_get_pairs", "sa_align", "sa_get_alignments", "sa_write_ovl", "sa_get_ovl", "sa_set_option",
+           "sa_get_stats", "sa_get_stage_times", "sa_reset_stage_times", "sa_device_build", "sa_device_align",
+           "sa_sync")
+
+
+class Settings(C.Structure):
+    _fields_ = [("kmer_size", C.c_int32), ("min_overlap", C.c_int32), ("max_ignore", C.c_int32),
+                ("gap_open", C.c_int32), ("gap_extend", C.c_int32), ("min_collisions", C.c_int32),
+                ("max_collisions", C.c_int32), ("min_identity", C.c_float), ("kmer_edge", C.c_float),
+                ("kmer_center", C.c_float), ("cost", C.c_int32 * 16), ("id_mode", C.c_int32)]
+
+
+class Stats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("kmers", "buckets", "role_pairs", "pairs", "dispatched", "aligned",
+                                           "ovl_records", "dp_cells")] + [("id_mode", C.c_int32),
+                                                                          ("reserved", C.c_int32)]
+
+
+ALIGN_FIELDS = ("lead", "trail", "start_i", "start_j", "end_i", "end_j", "correct", "error", "ahg", "bhg",
+                "flags", "reserved")
+
+_lib = None
+
+
+def lib():
+    """Load libsa_overlap.so (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("libsa_overlap.so not built: run `make -C %s`" % HERE)
+        L = C.CDLL(LIB_PATH)
+        P = C.POINTER
+        vp = C.c_void_p
+        L.sa_default_settings.argtypes = [P(Settings)]
+        L.sa_default_settings.restype = None
+        L.sa_ctx_create.argtypes = [P(Settings), C.c_int, P(vp)]
+        L.sa_ctx_destroy.argtypes = [vp]
+        L.sa_ctx_destroy.restype = None
+        L.sa_last_error.argtypes = [vp]
+        L.sa_last_error.restype = C.c_char_p
+        L.sa_load_hoxd.argtypes = [P(Settings), C.c_char_p]
+        L.sa_add_reads.argtypes = [vp, C.c_char_p, P(C.c_uint64), C.c_uint32]
+        L.sa_read_fasta.argtypes = [vp, C.c_char_p]
+        L.sa_num_reads.argtypes = [vp]
+        L.sa_num_reads.restype = C.c_uint32
+        for fn in ("sa_build_candidates", "sa_align", "sa_device_build", "sa_device_align", "sa_sync",
+                   "sa_reset_stage_times"):
+            getattr(L, fn).argtypes = [vp]
+        L.sa_get_dispatch.argtypes = [vp, P(P(C.c_int32)), P(P(C.c_int32)), P(P(C.c_int32)), P(C.c_size_t)]
+        L.sa_get_pairs.argtypes = [vp, P(P(C.c_int32)), P(P(C.c_int32)), P(P(C.c_int32)), P(C.c_size_t)]
+        L.sa_get_alignments.argtypes = [vp, P(vp), P(C.c_size_t)]
+        L.sa_write_ovl.argtypes = [vp, C.c_char_p]
+        L.sa_get_ovl.argtypes = [vp, P(C.c_char_p), P(C.c_size_t)]
+        L.sa_set_option.argtypes = [vp, C.c_int, C.c_int64]
+        L.sa_get_stats.argtypes = [vp, P(Stats)]
+        L.sa_get_stage_times.argtypes = [vp, P(C.c_double), P(C.c_uint64), C.c_int]
+        _lib = L
+    return _lib
+
+
+class SAError(RuntimeError):
+    def __init__(self, code, msg=""):
+        super().__init__("%s (%d): %s" % (ERRORS.get(code, "?"), code, msg))
+        self.code = code
+        self.name = ERRORS.get(code, "?")
+
+
+def settings(**kw):
+    """AlignSettings with Project4.readArgs defaults; keyword overrides use the C field names."""
+    s = Settings()
+    lib().sa_default_settings(C.byref(s))
+    for k, v in kw.items():
+        if k == "cost":
+            for i, x in enumerate(np.asarray(v).reshape(16)):
+                s.cost[i] = int(x)
+        elif k == "hoxd_file":
+            rc = lib().sa_load_hoxd(C.byref(s), v.encode())
+            if rc:
+                raise SAError(rc, "cannot read " + v)
+        else:
+            setattr(s, k, v)
+    return s
+
+
+def _arr(ptr, n):
+    if n == 0:
+        return np.zeros(0, dtype=np.int32)
+    return np.ctypeslib.as_array(ptr, shape=(n,)).copy()
+
+
+class Overlapper:
+    """One context = one AlignSettings + one KmerTable on one GPU."""
+
+    def __init__(self, device=0, timing=False, keep_pairs=False, **kw):
+        self.s = settings(**kw)
+        h = C.c_void_p()
+        rc = lib().sa_ctx_create(C.byref(self.s), device, C.byref(h))
+        if rc:
+            raise SAError(rc, "no usable gfx950 device %d" % device)
+        self.h = h
+        if timing:
+            self._chk(lib().sa_set_option(h, SA_OPT_TIMING, 1))
+        if keep_pairs:
+            self._chk(lib().sa_set_option(h, SA_OPT_KEEP_PAIRS, 1))
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().sa_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _chk(self, rc):
+        if rc:
+            raise SAError(rc, (lib().sa_last_error(self.h) or b"").decode())
+        return rc
+
+    # -- input -------------------------------------------------------------
+    def add_reads(self, reads):
+        bs = [r.encode() if isinstance(r, str) else bytes(r) for r in reads]
+        off = np.zeros(len(bs) + 1, dtype=np.uint64)
+        if bs:
+            off[1:] = np.cumsum([len(b) for b in bs])
+        self._chk(lib().sa_add_reads(self.h, b"".join(bs), off.ctypes.data_as(C.POINTER(C.c_uint64)), len(bs)))
+
+    def add_packed(self, bases, offsets):
+        """bases: bytes/uint8 array of all reads back to back; offsets: uint64[n+1]."""
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        b = bases if isinstance(bases, bytes) else np.ascontiguousarray(bases, dtype=np.uint8).tobytes()
+        self._chk(lib().sa_add_reads(self.h, b, off.ctypes.data_as(C.POINTER(C.c_uint64)), len(off) - 1))
+
+    def read_fasta(self, path):
+        self._chk(lib().sa_read_fasta(self.h, path.encode()))
+
+    @property
+    def n_reads(self):
+        return lib().sa_num_reads(self.h)
+
+    # -- the hot path ------------------------------------------------------
+    def build(self):
+        self._chk(lib().sa_build_candidates(self.h))
+
+    def device_build(self):
+        self._chk(lib().sa_device_build(self.h))
+
+    def align(self):
+        self._chk(lib().sa_align(self.h))
+
+    def device_align(self):
+        self._chk(lib().sa_device_align(self.h))
+
+    def sync(self):
+        self._chk(lib().sa_sync(self.h))
+
+    # -- results -----------------------------------------------------------
+    def dispatch(self):
+        a, b, c = C.POINTER(C.c_int32)(), C.POINTER(C.c_int32)(), C.POINTER(C.c_int32)()
+        n = C.c_size_t()
+        self._chk(lib().sa_get_dispatch(self.h, C.byref(a), C.byref(b), C.byref(c), C.byref(n)))
+        return _arr(a, n.value), _arr(b, n.value), _arr(c, n.value)
+
+    def pairs(self):
+        a, b, c = C.POINTER(C.c_int32)(), C.POINTER(C.c_int32)(), C.POINTER(C.c_int32)()
+        n = C.c_size_t()
+        self._chk(lib().sa_get_pairs(self.h, C.byref(a), C.byref(b), C.byref(c), C.byref(n)))
+        return _arr(a, n.value), _arr(b, n.value), _arr(c, n.value)
+
+    def alignments(self):
+        p, n = C.c_void_p(), C.c_size_t()
+        self._chk(lib().sa_get_alignments(self.h, C.byref(p), C.byref(n)))
+        if n.value == 0:
+            return np.zeros((0, len(ALIGN_FIELDS)), dtype=np.int32)
+        raw = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_int32)), shape=(n.value * len(ALIGN_FIELDS),))
+        return raw.reshape(n.value, len(ALIGN_FIELDS)).copy()
+
+    def ovl(self):
+        t, n = C.c_char_p(), C.c_size_t()
+        self._chk(lib().sa_get_ovl(self.h, C.byref(t), C.byref(n)))
+        return C.string_at(t, n.value) if n.value else b""
+
+    def write_ovl(self, path=None):
+        self._chk(lib().sa_write_ovl(self.h, path.encode() if path else None))
+
+    def stats(self):
+        st = Stats()
+        self._chk(lib().sa_get_stats(self.h, C.byref(st)))
+        return {f[0]: getattr(st, f[0]) for f in Stats._fields_ if f[0] != "reserved"}
+
+    def stage_times(self):
+        ms = (C.c_double * len(STAGES))()
+        nl = (C.c_uint64 * len(STAGES))()
+        self._chk(lib().sa_get_stage_times(self.h, ms, nl, len(STAGES)))
+        return {s: (ms[i], nl[i]) for i, s in enumerate(STAGES)}
+
+    def reset_stage_times(self):
+        self._chk(lib().sa_reset_stage_times(self.h))

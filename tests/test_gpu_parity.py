@@ -1,0 +1,269 @@
+"""HIP path vs the oracle, through the C ABI (libsa_overlap.so).  GPU only.
+
+Bar: candidate pairs, dispatch order and the .ovl are bit-exact;
+alignment tuples (start, end, c, e, flags, ahg, bhg) are bit-exact.  STRICT ids
+(< 32,768 reads) reproduce the reference's Trove order; WIDE ids use the
+canonical order (lead descending, trail ascending) defined in DESIGN.md.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import helpers as H
+
+pytestmark = pytest.mark.gpu
+
+sao = pytest.importorskip("saoverlap")
+
+ALIGN_CMP = ("start_i", "start_j", "end_i", "end_j", "correct", "error", "ahg", "bhg")
+
+
+def gpu_run(reads=None, fasta=None, wide=False, keep_pairs=True, **kw):
+    ov = sao.Overlapper(keep_pairs=keep_pairs, id_mode=sao.SA_IDS_WIDE if wide else sao.SA_IDS_STRICT, **kw)
+    if fasta:
+        ov.read_fasta(fasta)
+    else:
+        ov.add_reads(reads)
+    ov.build()
+    ov.align()
+    return ov
+
+
+def oracle_settings(oracle_mod, **kw):
+    return oracle_mod.default_settings(**kw)
+
+
+def compare_with_oracle(oracle_mod, ov, r, wide):
+    lead, trail, count = ov.dispatch()
+    np.testing.assert_array_equal(lead, r.lead)
+    np.testing.assert_array_equal(trail, r.trail)
+    pf, ps, pc = ov.pairs()
+    np.testing.assert_array_equal(pf, r.pair_fst)
+    np.testing.assert_array_equal(ps, r.pair_snd)
+    np.testing.assert_array_equal(pc, r.pair_cnt)
+    al = ov.alignments()
+    for name in ALIGN_CMP:
+        np.testing.assert_array_equal(al[:, sao.ALIGN_FIELDS.index(name)], r.align_field(name), err_msg=name)
+    flags = al[:, sao.ALIGN_FIELDS.index("flags")]
+    np.testing.assert_array_equal((flags & sao.FLAG_DUD) != 0, r.align_field("is_dud") != 0)
+    np.testing.assert_array_equal((flags & sao.FLAG_VALID) != 0, r.align_field("valid") != 0)
+    np.testing.assert_array_equal((flags & sao.FLAG_OVL_VALID) != 0,
+                                  (r.align_field("ovl_valid") != 0) & (r.align_field("valid") != 0))
+    assert ov.ovl() == r.ovl
+
+
+@pytest.mark.parametrize("k", [12, 15])
+def test_crp177_strict_golden(k):
+    """crp177 against the Scala-literal golden vectors: .ovl, PairData and dispatch order."""
+    g = np.load(os.path.join(H.GOLDEN, "crp177_k%d.npz" % k))
+    ov = gpu_run(fasta=H.crp177_path(), kmer_size=k)
+    assert ov.ovl() == open(os.path.join(H.GOLDEN, "crp177_k%d.ovl" % k), "rb").read()
+    lead, trail, _ = ov.dispatch()
+    np.testing.assert_array_equal(lead, g["lead"])
+    np.testing.assert_array_equal(trail, g["trail"])
+    pf, ps, pc = ov.pairs()
+    np.testing.assert_array_equal(pf, g["pair_fst"])
+    np.testing.assert_array_equal(ps, g["pair_snd"])
+    np.testing.assert_array_equal(pc, g["pair_cnt"])
+    st = ov.stats()
+    assert st["id_mode"] == sao.SA_IDS_STRICT
+
+
+@pytest.mark.parametrize("k", [12, 15])
+def test_crp177_wide_matches_oracle(oracle_mod, k):
+    r = oracle_mod.Run(fasta=H.crp177_path(), settings=oracle_settings(oracle_mod, kmer_size=k), wide=True)
+    ov = gpu_run(fasta=H.crp177_path(), kmer_size=k, wide=True)
+    compare_with_oracle(oracle_mod, ov, r, True)
+
+
+@pytest.mark.parametrize("k", [15, 12])
+def test_c_ruddii_strict_bit_exact(oracle_mod, k):
+    """The reference's large data set (32,000 reads rebuilt from the AMOS bank)."""
+    reads = H.c_ruddii_reads()
+    r = oracle_mod.Run(reads=reads, settings=oracle_settings(oracle_mod, kmer_size=k))
+    ov = gpu_run(reads=reads, kmer_size=k)
+    compare_with_oracle(oracle_mod, ov, r, False)
+    st = ov.stats()
+    assert st["kmers"] == 32000 * (100 - k + 1)
+
+
+def test_c_ruddii_wide_matches_oracle(oracle_mod):
+    reads = H.c_ruddii_reads()
+    r = oracle_mod.Run(reads=reads, settings=oracle_settings(oracle_mod, kmer_size=15), wide=True)
+    ov = gpu_run(reads=reads, kmer_size=15, wide=True)
+    compare_with_oracle(oracle_mod, ov, r, True)
+
+
+SYNTH = [
+    # (n, L, genome, gc, seed, mixed, settings)
+    (400, 120, 3000, 0.5, 1, None, dict(kmer_size=12)),
+    (300, 200, 4000, 0.3, 2, (80, 260), dict(kmer_size=15, min_collisions=3)),
+    (250, 150, 2500, 0.17, 3, None, dict(kmer_size=10, min_identity=0.95, min_collisions=5)),
+    (200, 90, 1200, 0.5, 4, (40, 140), dict(kmer_size=16)),
+    (200, 120, 1500, 0.5, 5, None, dict(kmer_size=20, min_identity=0.9)),
+    (300, 100, 2000, 0.45, 6, None, dict(kmer_size=13, kmer_edge=0.45, kmer_center=0.6)),
+    (150, 300, 3000, 0.5, 7, None, dict(kmer_size=14, gap_open=-50, gap_extend=-5, min_overlap=20,
+                                        max_ignore=250)),
+]
+
+
+@pytest.mark.parametrize("case", range(len(SYNTH)))
+@pytest.mark.parametrize("wide", [False, True])
+def test_synthetic_matches_oracle(oracle_mod, case, wide):
+    n, L, G, gc, seed, mixed, st = SYNTH[case]
+    reads = H.synth_reads(n, L, G, gc=gc, seed=seed, mixed=mixed)
+    r = oracle_mod.Run(reads=reads, settings=oracle_settings(oracle_mod, **st), wide=wide)
+    ov = gpu_run(reads=reads, wide=wide, **st)
+    compare_with_oracle(oracle_mod, ov, r, wide)
+
+
+def test_mutated_reads_with_indels(oracle_mod):
+    """Reads with substitutions and indels exercise X/Y gap moves in both DP phases."""
+    rng = np.random.default_rng(11)
+    base = H.synth_reads(300, 150, 3000, gc=0.5, seed=12)
+    reads = []
+    for rd in base:
+        s = list(rd)
+        for _ in range(int(rng.integers(0, 4))):
+            p = int(rng.integers(0, len(s)))
+            op = int(rng.integers(0, 3))
+            if op == 0:
+                s[p] = "ACGT"[int(rng.integers(0, 4))]
+            elif op == 1:
+                del s[p]
+            else:
+                s.insert(p, "ACGT"[int(rng.integers(0, 4))])
+        reads.append("".join(s))
+    st = dict(kmer_size=12, min_identity=0.9, min_collisions=4, gap_open=-60, gap_extend=-10)
+    for wide in (False, True):
+        r = oracle_mod.Run(reads=reads, settings=oracle_settings(oracle_mod, **st), wide=wide)
+        ov = gpu_run(reads=reads, wide=wide, **st)
+        compare_with_oracle(oracle_mod, ov, r, wide)
+
+
+def test_duplicate_reads_loc_ties(oracle_mod):
+    """Identical reads give equal-loc k-mers: the tie rule fst = middle (KmerTable.scala:65-71)."""
+    reads = H.synth_reads(60, 100, 700, seed=21)
+    reads = reads + reads[:20] + [reads[5]] * 3
+    for wide in (False, True):
+        r = oracle_mod.Run(reads=reads, settings=oracle_settings(oracle_mod, kmer_size=11, min_collisions=2,
+                                                                 max_collisions=400), wide=wide)
+        ov = gpu_run(reads=reads, wide=wide, kmer_size=11, min_collisions=2, max_collisions=400)
+        compare_with_oracle(oracle_mod, ov, r, wide)
+
+
+def test_short_and_degenerate_reads(oracle_mod):
+    """Reads shorter than k, exactly k (NaN loc: untagged), lowercase, tiny."""
+    reads = H.synth_reads(80, 100, 600, seed=31)
+    reads[3] = reads[3][:9]            # L < k
+    reads[7] = reads[7][:12]           # L == k -> loc NaN
+    reads[9] = reads[9].lower()        # readSeq upper-cases
+    reads.append("")                   # empty sequence
+    r = oracle_mod.Run(reads=[x.upper() for x in reads], settings=oracle_settings(oracle_mod, kmer_size=12))
+    ov = gpu_run(reads=reads, kmer_size=12)
+    compare_with_oracle(oracle_mod, ov, r, False)
+
+
+def test_repeat_overflow_path(oracle_mod):
+    """A 12-mer repeated in 4,000 reads (2,000 copies in the leading edge, 2,000
+    in the middle) gives every middle-copy read 2,000 partners: more than the
+    LDS pair table holds, so the split-pass fallback must reproduce the counts."""
+    rng = np.random.default_rng(41)
+    motif = "ACGTTGCAACGT"
+    reads = []
+    for i in range(4000):
+        s = "".join("ACGT"[x] for x in rng.integers(0, 4, 100))
+        p = 5 if i % 2 == 0 else 45
+        reads.append(s[:p] + motif + s[p + 12:])
+    reads += H.synth_reads(200, 100, 1500, seed=42)
+    st = dict(kmer_size=12, min_collisions=2)
+    for wide in (False, True):
+        r = oracle_mod.Run(reads=reads, settings=oracle_settings(oracle_mod, **st), wide=wide)
+        ov = gpu_run(reads=reads, wide=wide, **st)
+        compare_with_oracle(oracle_mod, ov, r, wide)
+        assert ov.stats()["pairs"] == len(r.pair_fst)
+
+
+def test_literal_c_ruddii_fasta_is_one_read():
+    """amos/c_ruddii.fasta as-is is a single sequence: every pair is same-read, the .ovl is empty (E7)."""
+    z = np.load(os.path.join(H.GOLDEN, "c_ruddii_layout.npz"))
+    contig = z["contig"].tobytes().decode()
+    ov = gpu_run(reads=[contig], kmer_size=15)
+    assert ov.ovl() == b""
+    assert ov.stats()["dispatched"] == 0
+
+
+def test_non_acgt_errors_like_matcherror(oracle_mod):
+    reads = H.synth_reads(50, 100, 500, seed=51)
+    reads = [r[:50] + "N" + r[51:] for r in reads]
+    with pytest.raises(oracle_mod.OracleError):
+        oracle_mod.Run(reads=reads, settings=oracle_settings(oracle_mod, kmer_size=12))
+    with pytest.raises(sao.SAError) as e:
+        gpu_run(reads=reads, kmer_size=12)
+    assert e.value.name == "SA_E_NON_ACGT"
+
+
+def test_strict_rejects_aliasing_sizes():
+    ov = sao.Overlapper(id_mode=sao.SA_IDS_STRICT)
+    ov.add_reads(["ACGTACGTACGTACGT"] * 65536)
+    with pytest.raises(sao.SAError) as e:
+        ov.build()
+    assert e.value.name == "SA_E_ID_RANGE"
+
+
+def test_device_only_path_matches_readback():
+    reads = H.synth_reads(2000, 200, 20000, seed=61)
+    a = gpu_run(reads=reads, kmer_size=15, wide=True, keep_pairs=False)
+    b = sao.Overlapper(kmer_size=15, id_mode=sao.SA_IDS_WIDE, timing=True)
+    b.add_reads(reads)
+    for _ in range(2):
+        b.device_build()
+        b.device_align()
+    for x, y in zip(a.dispatch(), b.dispatch()):
+        np.testing.assert_array_equal(x, y)
+    np.testing.assert_array_equal(a.alignments(), b.alignments())
+    t = b.stage_times()
+    assert t["pairs"][1] >= 2 and t["align"][1] == 2
+
+
+def test_bench_scale_properties():
+    """Bench-shaped input (wide ids, 20x coverage, 500 bp): determinism and the
+    role-pair count against an independent numpy count over the k-mer buckets."""
+    n, L, G, k = 20000, 500, 500000, 15
+    reads = H.synth_reads(n, L, G, seed=71)
+    ov = sao.Overlapper(kmer_size=k, id_mode=sao.SA_IDS_WIDE)
+    ov.add_reads(reads)
+    ov.build()
+    d1 = ov.dispatch()
+    st = ov.stats()
+    ov.build()
+    d2 = ov.dispatch()
+    for x, y in zip(d1, d2):
+        np.testing.assert_array_equal(x, y)
+    # independent role-pair count: sum over buckets of (|st| + |en|) * |md| (incl. same-read pairs)
+    arr = np.frombuffer("".join(reads).encode(), dtype=np.uint8).reshape(n, L)
+    code = np.zeros(256, dtype=np.uint64)
+    code[ord("C")], code[ord("T")], code[ord("G")] = 1, 2, 3
+    c = code[arr]
+    nk = L - k + 1
+    h = np.zeros((n, nk), dtype=np.uint64)
+    for t in range(k):
+        h = (h << np.uint64(2)) | c[:, t:t + nk]
+    loc = np.arange(nk, dtype=np.float32) / np.float32(L - k)
+    stt = loc <= np.float32(0.4)
+    en = np.float32(0.6) <= loc
+    md = (np.float32(0.3) <= loc) & (loc <= np.float32(0.7))
+    hh = h.reshape(-1)
+    _, inv = np.unique(hh, return_inverse=True)
+    w_edge = np.bincount(inv, weights=np.tile(stt.astype(np.float64) + en, n))
+    w_md = np.bincount(inv, weights=np.tile(md.astype(np.float64), n))
+    assert st["role_pairs"] == int(round(float((w_edge * w_md).sum())))
+    assert st["kmers"] == n * nk
+    assert st["buckets"] == len(w_md)
+    # every dispatched pair has its count inside the collision window
+    assert ((d1[2] >= 7) & (d1[2] <= 222)).all()
+    # canonical order: lead descending, trail ascending within a lead
+    assert (np.diff(d1[0]) <= 0).all()
+    same = np.diff(d1[0]) == 0
+    assert (np.diff(d1[1])[same] > 0).all()
