@@ -1,0 +1,26 @@
+#!/bin/bash
+# One GPU session: tests, bench, profile.  Stops at the first crash/timeout.
+set -u
+mkdir -p gpurun_out
+step() {  # step <name> <seconds> <cmd...>
+    local name=$1 secs=$2; shift 2
+    timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "$name rc=$rc" >> gpurun_out/steps.txt
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+    return 0
+}
+MODE=${1:-all}
+if [ "$MODE" = all ] || [ "$MODE" = tests ]; then
+    step smoke 240 python __graft_entry__.py smoke
+    step gpu_tests 900 python -m pytest tests -m gpu -q
+fi
+if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
+    step bench 600 python bench.py --steps 10 --warmup 2
+fi
+if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
+    cd /tmp && export TMPDIR=/tmp
+    step_dir=$GRAFT_REPO_ROOT/gpurun_out
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $step_dir/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 1 --no-cpu-baseline > $step_dir/prof.log 2>&1
+    echo "prof rc=$?" >> $step_dir/steps.txt
+fi

@@ -146,13 +146,15 @@ __global__ __launch_bounds__(256) void dovetail_kernel(DevReads rd, const int32_
         const uint32_t ac = (aw >> (30 - 2 * ((i - 1) & 15))) & 3u;
         const int32_t c = sext8(cb, ac);
         const int32_t diag = shr_g<G, 1>(Tp, 0);
-        int32_t M = c + max(diag, 0);
-        int32_t Y = gE + max(max(max(Mp, Xp) + gO, Yp), 0);
+        // lane 0 is the boundary column j = 0: M = X = 0 and Y <= 0 there, so it
+        // must feed 0 (not a computed cell) into the diagonal and the X scan
+        const int32_t M = lane == 0 ? 0 : c + max(diag, 0);
+        const int32_t Y = lane == 0 ? 0 : gE + max(max(max(Mp, Xp) + gO, Yp), 0);
         const int32_t Z = max(M, Y) + gO;
         const int32_t Zs = shr_g<G, 1>(Z, NEG);
-        int32_t V = lane == 0 ? 0 : gE + max(Zs, 0);
+        const int32_t V = lane == 0 ? 0 : gE + max(Zs, 0);
         int32_t X = xscan<G>(V, gE);
-        if (lane == 0) { M = 0; X = 0; Y = 0; }
+        if (lane == 0) X = 0;
         const int32_t T = max(M, max(X, Y));
         const bool row_ok = col_ok && i <= LA;
         if (row_ok && lane >= 1 && T > best) { best = T; brow = i; }

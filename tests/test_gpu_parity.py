@@ -118,9 +118,11 @@ def test_synthetic_matches_oracle(oracle_mod, case, wide):
     compare_with_oracle(oracle_mod, ov, r, wide)
 
 
-def test_mutated_reads_with_indels(oracle_mod):
-    """Reads with substitutions and indels exercise X/Y gap moves in both DP phases."""
-    rng = np.random.default_rng(11)
+@pytest.mark.parametrize("gaps", [(-60, -10, 0.9), (-20, -5, 0.95), (-200, -20, 0.9), (-35, -1, 0.85)])
+def test_mutated_reads_with_indels(oracle_mod, gaps):
+    """Reads with substitutions and indels exercise X/Y gap moves in both DP phases
+    (small gap-open values make gap cells win and move the argmax)."""
+    rng = np.random.default_rng(11 + gaps[1])
     base = H.synth_reads(300, 150, 3000, gc=0.5, seed=12)
     reads = []
     for rd in base:
@@ -135,7 +137,7 @@ def test_mutated_reads_with_indels(oracle_mod):
             else:
                 s.insert(p, "ACGT"[int(rng.integers(0, 4))])
         reads.append("".join(s))
-    st = dict(kmer_size=12, min_identity=0.9, min_collisions=4, gap_open=-60, gap_extend=-10)
+    st = dict(kmer_size=12, min_identity=gaps[2], min_collisions=4, gap_open=gaps[0], gap_extend=gaps[1])
     for wide in (False, True):
         r = oracle_mod.Run(reads=reads, settings=oracle_settings(oracle_mod, **st), wide=wide)
         ov = gpu_run(reads=reads, wide=wide, **st)
