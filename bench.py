@@ -73,7 +73,7 @@ def main():
     ap.add_argument("--gc", type=float, default=0.50)
     ap.add_argument("--coverage", type=float, default=20.0)
     ap.add_argument("--align-steps", type=int, default=None)
-    ap.add_argument("--cpu-sample-reads", type=int, default=10_000)
+    ap.add_argument("--cpu-sample-reads", type=int, default=100_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 

@@ -641,11 +641,12 @@ int device_align(sa_ctx *c, bool readback) {
     const float omm = 1.0f - c->set.min_identity;
     const float prod = (float)c->maxL * omm;
     const int32_t wmax = std::max(c->set.kmer_size, (int32_t)floor((double)prod) + 1);
-    int G = wmax <= 15 ? 16 : (wmax <= 31 ? 32 : (wmax <= 63 ? 64 : 0));
-    if (!G) return fail(c, SA_E_OVERFLOW, "band width above 63 (min-identity too low for the read length)");
-    uint32_t rw = (uint32_t)((c->maxL + 1 + 15) / 16) | 1u;
-    if ((size_t)256 * rw * 4 > 160 * 1024)
-        return fail(c, SA_E_OVERFLOW, "reads too long for the LDS traceback (max ~2,500 bp this build)");
+    // Lane groups and LDS traceback are sized for the longest read; a pair whose
+    // band (w > 63) or lead (> ~2,500 bp) exceeds what this build holds fails in
+    // the kernel with SA_E_OVERFLOW -- only if such a pair is actually dispatched.
+    const int G = wmax <= 15 ? 16 : (wmax <= 31 ? 32 : 64);
+    const uint32_t rw_fit = (160u * 1024u / (256u * 4u) - 1u) | 1u;
+    const uint32_t rw = std::min<uint32_t>((uint32_t)((c->maxL + 1 + 15) / 16) | 1u, rw_fit);
     AlignParams P;
     P.k = c->set.kmer_size;
     P.gap_open = c->set.gap_open;

@@ -122,7 +122,7 @@ def test_synthetic_matches_oracle(oracle_mod, case, wide):
 def test_mutated_reads_with_indels(oracle_mod, gaps):
     """Reads with substitutions and indels exercise X/Y gap moves in both DP phases
     (small gap-open values make gap cells win and move the argmax)."""
-    rng = np.random.default_rng(11 + gaps[1])
+    rng = np.random.default_rng(11 + abs(gaps[1]))
     base = H.synth_reads(300, 150, 3000, gc=0.5, seed=12)
     reads = []
     for rd in base:
