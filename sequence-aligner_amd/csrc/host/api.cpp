@@ -52,6 +52,9 @@ struct Counters {                    // device-resident scalars, one memset per 
     uint32_t overflow_n;
     int32_t err;
     uint32_t totals[4];
+    uint32_t big_n;
+    uint32_t pad_;
+    unsigned long long bkt_counts[2];
 };
 
 }  // namespace
@@ -80,12 +83,13 @@ struct sa_ctx {
     DBuf d_keys, d_vals, d_keys2, d_vals2, d_sorttmp;
     DBuf d_md, d_ed, d_bmdo, d_bedo, d_bstart, d_gbid, d_gmds, d_gede, d_ogid, d_bkttmp;
     DBuf d_mdidx, d_edidx, d_occidx, d_bnst, d_brank, d_bhash, d_bfirst;
+    DBuf d_pstart, d_biglist, d_rec, d_srec, d_bnmd, d_ishead, d_bnst2;
+    uint32_t *bkt_rank_dev = nullptr;
     DBuf d_pf, d_ps, d_pc, d_pr, d_ovl, d_cnt;
     DBuf d_okeys, d_ovals, d_okeys2, d_ovals2, d_osort;
     DBuf d_lead, d_trail, d_count, d_aln;
     uint64_t pair_cap = 0;
     uint64_t n_disp = 0;
-    Buckets bk{};
     // options / state
     bool keep_pairs = false, timing = false;
     bool built = false, aligned = false;
@@ -382,71 +386,143 @@ int device_build(sa_ctx *c, bool readback) {
         StageScope st(c, SA_STAGE_EMIT);
         HIPCHK(launch_kmer_emit(R, E, keys, vals, c->stream));
     }
+    // ---- partition by the top P bits of mix(seqHash): whole buckets per partition
+    int PB = 1;
+    while (PB < 16 && ((uint64_t)700 << PB) < n) ++PB;
+    const uint32_t nparts = 1u << PB;
+    const int kbits = 32 + c->lb;
     {
         StageScope st(c, SA_STAGE_SORT);
-        HIPCHK(radix_sort(&keys, &vals, &keys2, &vals2, n, 0, c->lb + 2 * c->m, stmp, c->stream));
+        HIPCHK(radix_sort(&keys, &vals, &keys2, &vals2, n, kbits - PB, kbits, stmp, c->stream));
     }
-    Buckets &B = c->bk;
-    B.n_occ = n;
-    ENSURE(c->d_md, n, &B.md_list);
-    ENSURE(c->d_ed, 2 * n, &B.ed_list);
-    ENSURE(c->d_bmdo, n + 2, &B.bkt_mdo);
-    ENSURE(c->d_bedo, n + 2, &B.bkt_edo);
-    ENSURE(c->d_bstart, n + 2, &B.bkt_start);
-    ENSURE(c->d_gbid, n + 1, &B.grp_bid);
-    ENSURE(c->d_gmds, n + 1, &B.grp_mds);
-    ENSURE(c->d_gede, n + 1, &B.grp_ede);
-    ENSURE(c->d_ogid, n + 1, &B.occ_gid);
-    const uint8_t *tagtab = (const uint8_t *)c->d_tagtab.p;
+    uint32_t *pstart, *biglist;
+    ENSURE(c->d_pstart, nparts + 1, &pstart);
+    ENSURE(c->d_biglist, nparts + 1, &biglist);
+    PartArgs PA{};
+    PA.sk = keys; PA.sv = vals; PA.start = pstart; PA.np = nparts; PA.lb = c->lb;
+    PA.tagtab = (const uint8_t *)c->d_tagtab.p;
+    PA.occ_off = (const uint64_t *)c->d_occ_off.p;
+    PA.n_reads = nr; PA.npr = c->uniform_npr;
+    ENSURE(c->d_md, n + 1, &PA.md_list);
+    ENSURE(c->d_ed, 2 * n + 2, &PA.ed_list);
+    ENSURE(c->d_rec, n + 1, &PA.rec);
+    PA.big_list = biglist; PA.big_n = &cnt->big_n;
+    PA.counts = cnt->bkt_counts;
+    if (strict) {
+        ENSURE(c->d_mdidx, n + 1, &PA.md_idx);
+        ENSURE(c->d_edidx, 2 * n + 2, &PA.ed_idx);
+        ENSURE(c->d_srec, n + 1, &PA.srec);
+        ENSURE(c->d_bnst, n + 1, &PA.bkt_nst);
+        ENSURE(c->d_bnmd, n + 1, &PA.bkt_nmd);
+        ENSURE(c->d_bfirst, n + 1, &PA.bkt_first);
+        ENSURE(c->d_ishead, n + 1, &PA.is_head);
+        ENSURE(c->d_brank, n + 1, &c->bkt_rank_dev);
+        HIPCHK(hipMemsetAsync(PA.is_head, 0, n + 1, c->stream));
+    }
+    const uint8_t *tagtab = PA.tagtab;
+    uint32_t big_n = 0;
     {
         StageScope st(c, SA_STAGE_BUCKETS);
-        HIPCHK(build_buckets(keys, vals, n, c->lb, tagtab, (const uint64_t *)c->d_occ_off.p, nr, c->uniform_npr, B,
-                             cnt->totals, stmp, c->stream));
-        if (strict) {
-            ENSURE(c->d_mdidx, n + 1, &B.md_idx);
-            ENSURE(c->d_edidx, 2 * n + 1, &B.ed_idx);
-            ENSURE(c->d_occidx, 3 * n + 3, &B.occ_idx);
-            ENSURE(c->d_bnst, n + 1, &B.bkt_nst);
-            ENSURE(c->d_brank, n + 1, &B.bkt_rank);
-            HIPCHK(build_strict_index(keys, vals, n, c->lb, tagtab, B, c->stream));
-        }
+        HIPCHK(launch_part_starts(keys, n, c->lb + 32 - PB, pstart, nparts, c->stream));
+        HIPCHK(launch_part_build(PA, strict, c->stream));
     }
-    uint32_t totals[4] = {0, 0, 0, 0};
-    if (strict || readback) {
-        HIPCHK(hipMemcpyAsync(totals, cnt->totals, sizeof(totals), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
-        B.n_buckets = totals[0]; B.n_groups = totals[1]; B.n_md = totals[2]; B.n_ed = totals[3];
+    HIPCHK(hipMemcpyAsync(&big_n, &cnt->big_n, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    unsigned long long big_buckets = 0, big_groups = 0;
+    if (big_n) {
+        // partitions too large for LDS (high-copy repeats): sort the rest of the
+        // key in place, then the global scan build of buckets.hip on the range
+        std::vector<uint32_t> bl(big_n), starts(nparts + 1);
+        HIPCHK(hipMemcpy(bl.data(), biglist, big_n * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(starts.data(), pstart, (nparts + 1) * 4, hipMemcpyDeviceToHost));
+        std::sort(bl.begin(), bl.end());
+        uint32_t maxn = 0;
+        for (uint32_t p : bl) maxn = std::max(maxn, starts[p + 1] - starts[p]);
+        Buckets B{};
+        ENSURE(c->d_bmdo, maxn + 2, &B.bkt_mdo);
+        ENSURE(c->d_bedo, maxn + 2, &B.bkt_edo);
+        ENSURE(c->d_bstart, maxn + 2, &B.bkt_start);
+        ENSURE(c->d_gbid, maxn + 1, &B.grp_bid);
+        ENSURE(c->d_gmds, maxn + 1, &B.grp_mds);
+        ENSURE(c->d_gede, maxn + 1, &B.grp_ede);
+        ENSURE(c->d_ogid, n + 1, &B.occ_gid);
+        uint8_t *btmp;
+        ENSURE(c->d_bkttmp, std::max(radix_sort_temp_bytes(maxn), buckets_temp_bytes(maxn)), &btmp);
+        if (strict) {
+            ENSURE(c->d_occidx, 3 * n + 3, &B.occ_idx);
+            ENSURE(c->d_bnst2, maxn + 1, &B.bkt_nst);
+        }
+        StageScope st(c, SA_STAGE_BUCKETS);
+        for (uint32_t p : bl) {
+            const uint32_t ps = starts[p], pn = starts[p + 1] - starts[p];
+            uint64_t *k0 = keys + ps, *k1 = keys2 + ps;
+            uint32_t *v0 = vals + ps, *v1 = vals2 + ps;
+            HIPCHK(radix_sort(&k0, &v0, &k1, &v1, pn, 0, kbits - PB, btmp, c->stream));
+            if (k0 != keys + ps) {  // odd number of passes: copy the sorted range back
+                HIPCHK(hipMemcpyAsync(keys + ps, k0, (size_t)pn * 8, hipMemcpyDeviceToDevice, c->stream));
+                HIPCHK(hipMemcpyAsync(vals + ps, v0, (size_t)pn * 4, hipMemcpyDeviceToDevice, c->stream));
+            }
+            B.n_occ = pn;
+            B.md_list = PA.md_list + ps;
+            B.ed_list = PA.ed_list + 2ull * ps;
+            if (strict) { B.md_idx = PA.md_idx + ps; B.ed_idx = PA.ed_idx + 2ull * ps; }
+            HIPCHK(build_buckets(keys + ps, vals + ps, pn, c->lb, tagtab, PA.occ_off, nr, c->uniform_npr, B,
+                                 cnt->totals, btmp, c->stream));
+            if (strict) HIPCHK(build_strict_index(keys + ps, vals + ps, pn, c->lb, tagtab, B, c->stream));
+            HIPCHK(launch_records_from_tables(keys, vals, ps, pn, c->lb, tagtab, B, PA.rec, strict ? 1 : 0, PA.srec,
+                                              PA.bkt_nst, PA.bkt_nmd, PA.bkt_first, PA.is_head, c->stream));
+            uint32_t tot[4];
+            HIPCHK(hipMemcpyAsync(tot, cnt->totals, 16, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            big_buckets += tot[0];
+            big_groups += tot[1];
+        }
     }
     if (strict) {
         // KmerData iteration rank of every bucket: replay its Trove layout over the
-        // distinct hashes in first-occurrence order (KmerTable.scala:45-50)
-        uint32_t *bh, *bf;
-        ENSURE(c->d_bhash, B.n_buckets + 1, &bh);
-        ENSURE(c->d_bfirst, B.n_buckets + 1, &bf);
-        HIPCHK(launch_bucket_first(keys, vals, B, c->lb, bh, bf, c->stream));
-        std::vector<uint32_t> hh(B.n_buckets), ff(B.n_buckets);
-        if (B.n_buckets) {
-            HIPCHK(hipMemcpyAsync(hh.data(), bh, B.n_buckets * 4, hipMemcpyDeviceToHost, c->stream));
-            HIPCHK(hipMemcpyAsync(ff.data(), bf, B.n_buckets * 4, hipMemcpyDeviceToHost, c->stream));
+        // distinct hashes in first-occurrence order (KmerTable.scala:45-50).  A
+        // bucket is named by the sorted position of its head record.
+        std::vector<uint8_t> head(n);
+        std::vector<uint32_t> first(n);
+        if (n) {
+            HIPCHK(hipMemcpy(head.data(), PA.is_head, n, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(first.data(), PA.bkt_first, n * 4, hipMemcpyDeviceToHost));
         }
-        HIPCHK(hipStreamSynchronize(c->stream));
-        std::vector<uint32_t> order(B.n_buckets);
-        for (uint32_t i = 0; i < B.n_buckets; ++i) order[i] = i;
-        std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return ff[x] < ff[y]; });
+        std::vector<std::pair<uint32_t, uint32_t>> fh;  // (first g, head pos)
+        for (uint64_t i = 0; i < n; ++i)
+            if (head[i]) fh.push_back({first[i], (uint32_t)i});
+        std::sort(fh.begin(), fh.end());
         TroveLayout kd;
-        for (uint32_t i : order) kd.insert((int32_t)hh[i]);
-        // bucket ids are ascending unsigned hash order
-        std::vector<uint32_t> rank(B.n_buckets);
+        std::unordered_map<int32_t, uint32_t> pos_of;
+        pos_of.reserve(fh.size() * 2);
+        const int k = c->set.kmer_size, mm = c->m;
+        for (auto &x : fh) {
+            const uint32_t g = x.first;
+            const uint32_t r = (uint32_t)(std::upper_bound(c->occ_off.begin(), c->occ_off.end(), (uint64_t)g) -
+                                          c->occ_off.begin()) - 1;
+            const char *sq = c->bases.data() + c->boff[r] + (g - c->occ_off[r]);
+            uint32_t h = 0;  // Kmer.seqHash (ObjectStore.scala:48-67)
+            for (int q = 0; q < mm; ++q) {
+                char ch = sq[q];
+                if (ch >= 'a' && ch <= 'z') ch = (char)(ch - 32);
+                h <<= 2;
+                h ^= ch == 'C' ? 1u : ch == 'T' ? 2u : ch == 'G' ? 3u : 0u;
+            }
+            (void)k;
+            kd.insert((int32_t)h);
+            pos_of[(int32_t)h] = x.second;
+        }
+        std::vector<uint32_t> rank(n, 0);
         uint32_t rk = 0;
-        std::vector<std::pair<uint32_t, uint32_t>> hid(B.n_buckets);
-        for (uint32_t i = 0; i < B.n_buckets; ++i) hid[i] = {hh[i], i};
-        std::sort(hid.begin(), hid.end());
-        kd.for_each([&](int32_t key) {
-            auto it = std::lower_bound(hid.begin(), hid.end(), std::make_pair((uint32_t)key, 0u));
-            rank[it->second] = rk++;
-        });
+        kd.for_each([&](int32_t key) { rank[pos_of[key]] = rk++; });
         if (rk >= (1u << 26)) return fail(c, SA_E_OVERFLOW, "strict ids: more than 2^26 distinct k-mers");
-        if (B.n_buckets) HIPCHK(hipMemcpyAsync(B.bkt_rank, rank.data(), B.n_buckets * 4, hipMemcpyHostToDevice, c->stream));
+        if (n) HIPCHK(hipMemcpy(c->bkt_rank_dev, rank.data(), n * 4, hipMemcpyHostToDevice));
+    }
+    PairIn PI{};
+    PI.rec = PA.rec; PI.md_list = PA.md_list; PI.ed_list = PA.ed_list;
+    if (strict) {
+        PI.srec = PA.srec; PI.md_idx = PA.md_idx; PI.ed_idx = PA.ed_idx;
+        PI.bkt_nst = PA.bkt_nst; PI.bkt_nmd = PA.bkt_nmd; PI.bkt_rank = c->bkt_rank_dev;
     }
 
     // ---- pair counting -------------------------------------------------
@@ -467,7 +543,7 @@ int device_build(sa_ctx *c, bool readback) {
         ENSURE(c->d_pc, c->pair_cap, &O.cnt);
         O.rank = nullptr;
         if (strict) ENSURE(c->d_pr, c->pair_cap, &O.rank);
-        ENSURE(c->d_ovl, nr + 1, &O.overflow_list);
+        ENSURE(c->d_ovl, 2 * nr + 2, &O.overflow_list);
         O.cursor = &cnt->cursor;
         O.cap = c->pair_cap;
         O.role_pairs = &cnt->role_pairs;
@@ -477,39 +553,29 @@ int device_build(sa_ctx *c, bool readback) {
         HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(uint32_t), c->stream));
         {
             StageScope st(c, SA_STAGE_PAIRS);
-            HIPCHK(launch_pair_count(R, E, B, tagtab, P, O, nullptr, nr, c->stream));
+            HIPCHK(launch_pair_count(E, PI, P, O, nullptr, nr, c->stream));
         }
         HIPCHK(hipMemcpyAsync(&cursor, &cnt->cursor, 8, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipMemcpyAsync(&ovn, &cnt->overflow_n, 4, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
-        // split passes for reads whose LDS table overflowed (rare; high-copy repeats)
-        uint32_t split = 8;
-        uint32_t *ovl_list = O.overflow_list;
-        while (ovn > 0 && cursor <= c->pair_cap) {
-            if (split > (1u << 16)) return fail(c, SA_E_OVERFLOW, "pair table overflow beyond 65536-way split");
-            std::vector<uint32_t> lst(ovn);
-            HIPCHK(hipMemcpyAsync(lst.data(), ovl_list, ovn * 4, hipMemcpyDeviceToHost, c->stream));
-            HIPCHK(hipStreamSynchronize(c->stream));
-            uint32_t *dl;
-            ENSURE(c->d_bfirst, ovn + 1, &dl);  // reuse as read list (strict bucket_first data already consumed)
-            HIPCHK(hipMemcpyAsync(dl, lst.data(), ovn * 4, hipMemcpyHostToDevice, c->stream));
+        // reads whose LDS table overflowed (> 1,536 partners: high-copy repeats) are
+        // recounted in 64 partner-residue passes; each pass holds up to 1,536 partners
+        if (ovn > 0 && cursor <= c->pair_cap) {
+            const uint32_t split = 64;
             PairParams P2 = P;
             P2.split = (int32_t)split;
             PairOut O2 = O;
             O2.role_pairs = &cnt->role_pairs_dummy;
+            O2.overflow_list = O.overflow_list + ovn;  // keep the read list intact
             HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(uint32_t), c->stream));
             {
                 StageScope st(c, SA_STAGE_PAIRS);
-                HIPCHK(launch_pair_count(R, E, B, tagtab, P2, O2, dl, ovn * split, c->stream));
+                HIPCHK(launch_pair_count(E, PI, P2, O2, O.overflow_list, ovn * split, c->stream));
             }
             HIPCHK(hipMemcpyAsync(&cursor, &cnt->cursor, 8, hipMemcpyDeviceToHost, c->stream));
             HIPCHK(hipMemcpyAsync(&ovn, &cnt->overflow_n, 4, hipMemcpyDeviceToHost, c->stream));
             HIPCHK(hipStreamSynchronize(c->stream));
-            if (ovn) {
-                // the split pass itself overflowed: rerun the whole read set at the next split
-                return fail(c, SA_E_OVERFLOW, "pair table overflow in split pass");
-            }
-            split *= 8;
+            if (ovn) return fail(c, SA_E_OVERFLOW, "a read has more than 98,304 distinct partners");
         }
         if (cursor <= c->pair_cap) break;
         c->pair_cap = cursor + cursor / 4 + 1024;  // grow and recount
@@ -542,10 +608,9 @@ int device_build(sa_ctx *c, bool readback) {
     HIPCHK(hipMemcpyAsync(&hc, cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     resolve_timing(c);
-    B.n_buckets = hc.totals[0]; B.n_groups = hc.totals[1]; B.n_md = hc.totals[2]; B.n_ed = hc.totals[3];
     c->stats = sa_stats{};
     c->stats.kmers = n;
-    c->stats.buckets = B.n_buckets;
+    c->stats.buckets = hc.bkt_counts[0] + big_buckets;
     c->stats.role_pairs = hc.role_pairs;
     c->stats.pairs = hc.distinct;
     c->stats.id_mode = c->mode;
@@ -758,7 +823,8 @@ void sa_ctx_destroy(sa_ctx *c) {
                     &c->d_gmds, &c->d_gede, &c->d_ogid, &c->d_bkttmp, &c->d_mdidx, &c->d_edidx, &c->d_occidx,
                     &c->d_bnst, &c->d_brank, &c->d_bhash, &c->d_bfirst, &c->d_pf, &c->d_ps, &c->d_pc, &c->d_pr,
                     &c->d_ovl, &c->d_cnt, &c->d_okeys, &c->d_ovals, &c->d_okeys2, &c->d_ovals2, &c->d_osort,
-                    &c->d_lead, &c->d_trail, &c->d_count, &c->d_aln};
+                    &c->d_lead, &c->d_trail, &c->d_count, &c->d_aln, &c->d_pstart, &c->d_biglist, &c->d_rec,
+                    &c->d_srec, &c->d_bnmd, &c->d_ishead, &c->d_bnst2};
     for (DBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto &p : c->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }

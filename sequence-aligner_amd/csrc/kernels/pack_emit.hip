@@ -66,7 +66,7 @@ __device__ __forceinline__ uint32_t window16(const uint32_t *w, int32_t p) {
     return (a << (2 * s)) | (b >> (32 - 2 * s));
 }
 
-// One wave per read, lane = position.  key = seqHash << lb | locrank, val = g.
+// One wave per read, lane = position.  key = mix32(seqHash) << lb | locrank, val = g.
 __global__ __launch_bounds__(256) void kmer_emit_kernel(DevReads r, EmitParams e, uint64_t *keys,
                                                         uint32_t *vals) {
     const uint32_t lane = threadIdx.x & 63;
@@ -86,7 +86,7 @@ __global__ __launch_bounds__(256) void kmer_emit_kernel(DevReads r, EmitParams e
             x = shift == 32 ? 0u : (x >> shift);
             // HOXD order (A0 C1 G2 T3) -> seqHash order (A0 C1 T2 G3): c ^ (c >> 1)
             x ^= (x >> 1) & 0x55555555u;
-            keys[g0 + i] = ((uint64_t)x << e.lb) | (uint64_t)lr[i];
+            keys[g0 + i] = ((uint64_t)mix32(x) << e.lb) | (uint64_t)lr[i];
             vals[g0 + i] = (uint32_t)(g0 + i);
         }
     }

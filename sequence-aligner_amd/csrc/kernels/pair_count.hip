@@ -12,8 +12,10 @@
 // collision filter is applied on chip.  Strict mode also tracks each key's
 // first-occurrence rank in calcPairData's traversal order, from which the host
 // replays GNU Trove's PairData layout.
-// Work is load-balanced inside the workgroup over the prefix sum of per-k-mer
-// partner counts.  Bound: gather latency / LDS atomics; HBM bytes are small.
+// Each k-mer's partner ranges arrive as one coalesced 16-byte record
+// (partition.hip).  Work is load-balanced inside the workgroup over the prefix
+// sum of per-k-mer partner counts; partner ids are gathered PC_BATCH at a time.
+// Bound: gather latency / LDS atomics; HBM bytes are small.
 #include "../sa_internal.h"
 
 namespace sa {
@@ -21,7 +23,8 @@ namespace sa {
 constexpr int PC_THREADS = 256;
 constexpr int PC_TAB = 2048;             // LDS hash slots per read
 constexpr int PC_FILL_MAX = PC_TAB * 3 / 4;
-constexpr int PC_CHUNK = 1024;           // occurrences per pass over a read
+constexpr int PC_CHUNK = 512;            // occurrences per pass over a read
+constexpr int PC_BATCH = 8;              // partner loads in flight per thread
 constexpr uint32_t PC_EMPTY = 0xFFFFFFFFu;
 
 __device__ __forceinline__ uint32_t pc_hash(uint32_t p) { return (p * 0x9E3779B1u) >> (32 - 11); }
@@ -30,17 +33,13 @@ struct PcShared {
     uint32_t key[PC_TAB];
     uint32_t cnt[PC_TAB];
     uint32_t pref[PC_CHUNK + 1];
-    uint32_t e0[PC_CHUNK];     // first md-list entry of the bucket (edge role partners)
-    uint32_t d0[PC_CHUNK];     // first edge-list entry of the bucket (middle role partners)
-    uint32_t ne[PC_CHUNK];     // number of edge-role partners; bits 30-31 = edge multiplicity
+    uint4 rec[PC_CHUNK];       // per-occurrence partner ranges (partition.hip)
     uint32_t lds4[4];
-    uint32_t fill, overflow, total, out_base;
+    uint32_t fill, overflow, out_base;
 };
 struct PcSharedStrict {
     unsigned long long rank[PC_TAB];
-    uint32_t bid[PC_CHUNK];
-    uint32_t own_e[PC_CHUNK];  // (phase<<31) | own st/en index
-    uint32_t own_m[PC_CHUNK];  // own md index
+    uint4 srec[PC_CHUNK];      // {bucket head pos, own_e, own_m, 0}
 };
 
 __device__ __forceinline__ uint32_t pc_block_excl_scan(uint32_t v, uint32_t *lds4, uint32_t *total) {
@@ -66,8 +65,24 @@ __device__ __forceinline__ uint32_t pc_block_excl_scan(uint32_t v, uint32_t *lds
 }
 
 template <bool STRICT>
-__global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(DevReads r, EmitParams e, Buckets b,
-                                                                const uint8_t *tagtab, PairParams p, PairOut o,
+__device__ __forceinline__ void pc_insert(PcShared &S, PcSharedStrict &X, uint32_t partner, uint32_t w,
+                                          unsigned long long rank) {
+    uint32_t slot = pc_hash(partner);
+    for (int probe = 0; probe < PC_TAB; ++probe) {
+        const uint32_t old = atomicCAS(&S.key[slot], PC_EMPTY, partner);
+        if (old == PC_EMPTY || old == partner) {
+            if (old == PC_EMPTY && atomicAdd(&S.fill, 1u) >= (uint32_t)PC_FILL_MAX) S.overflow = 1;
+            atomicAdd(&S.cnt[slot], w);
+            if constexpr (STRICT) atomicMin(&X.rank[slot], rank);
+            return;
+        }
+        slot = (slot + 1) & (PC_TAB - 1);
+    }
+    S.overflow = 1;
+}
+
+template <bool STRICT>
+__global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, PairIn in, PairParams p, PairOut o,
                                                                 const uint32_t *read_list) {
     extern __shared__ __align__(16) uint8_t smem[];
     PcShared &S = *reinterpret_cast<PcShared *>(smem);
@@ -87,57 +102,43 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(DevReads r, Emit
 
     const uint64_t g0 = e.occ_off[a];
     const uint32_t nocc = (uint32_t)(e.occ_off[a + 1] - g0);
-    const int32_t L = r.len[a];
-    const uint32_t *lr = nocc ? e.lrank + e.lbase[L - e.k] : nullptr;
-    const uint64_t lbm = (1ull << e.lb) - 1;
     unsigned long long role_pairs = 0;
     __syncthreads();
 
     for (uint32_t c0 = 0; c0 < nocc; c0 += PC_CHUNK) {
         const uint32_t cn = min((uint32_t)PC_CHUNK, nocc - c0);
-        // --- per-occurrence partner ranges -------------------------------
-        uint32_t mytot[PC_CHUNK / PC_THREADS];
+        // --- per-occurrence partner ranges: one coalesced 16-byte record each
+        constexpr int PER = PC_CHUNK / PC_THREADS;
+        uint32_t mytot[PER];
 #pragma unroll
-        for (int j = 0; j < PC_CHUNK / PC_THREADS; ++j) {
-            const uint32_t oi = tid * (PC_CHUNK / PC_THREADS) + j;  // thread-contiguous
+        for (int j = 0; j < PER; ++j) {
+            const uint32_t oi = tid * PER + j;  // thread-contiguous
             uint32_t tot = 0;
             if (oi < cn) {
-                const uint64_t g = g0 + c0 + oi;
-                const uint32_t t = tagtab[lr[c0 + oi] & lbm];
-                const uint32_t gid = b.occ_gid[g];
-                const uint32_t bid = b.grp_bid[gid];
-                const uint32_t me = ((t & TAG_ST) ? 1u : 0u) + ((t & TAG_EN) ? 1u : 0u);
-                const uint32_t mdo = b.bkt_mdo[bid], edo = b.bkt_edo[bid];
-                const uint32_t nE = me ? (b.grp_mds[gid] - mdo) : 0u;
-                const uint32_t nD = (t & TAG_MD) ? (b.grp_ede[gid] - edo) : 0u;
-                S.e0[oi] = mdo;
-                S.d0[oi] = edo;
-                S.ne[oi] = nE | (me << 30);
-                tot = nE + nD;
-                if constexpr (STRICT) {
-                    X.bid[oi] = bid;
-                    X.own_e[oi] = (t & TAG_ST) ? b.occ_idx[3 * g + 0] : ((1u << 31) | b.occ_idx[3 * g + 2]);
-                    X.own_m[oi] = b.occ_idx[3 * g + 1];
-                }
+                const uint4 rc = in.rec[g0 + c0 + oi];
+                S.rec[oi] = rc;
+                tot = (rc.y & 0x3FFFFFFFu) + rc.w;
+                if constexpr (STRICT) X.srec[oi] = in.srec[g0 + c0 + oi];
             }
             mytot[j] = tot;
         }
         uint32_t s = 0;
 #pragma unroll
-        for (int j = 0; j < PC_CHUNK / PC_THREADS; ++j) s += mytot[j];
+        for (int j = 0; j < PER; ++j) s += mytot[j];
         uint32_t total;
         uint32_t ex = pc_block_excl_scan(s, S.lds4, &total);
 #pragma unroll
-        for (int j = 0; j < PC_CHUNK / PC_THREADS; ++j) {
-            const uint32_t oi = tid * (PC_CHUNK / PC_THREADS) + j;
-            if (oi <= cn) S.pref[oi] = ex;   // pref[cn] = total (exclusive prefix of padding = total)
+        for (int j = 0; j < PER; ++j) {
+            const uint32_t oi = tid * PER + j;
+            if (oi <= cn) S.pref[oi] = ex;
             ex += mytot[j];
         }
         if (tid == PC_THREADS - 1 && cn == PC_CHUNK) S.pref[PC_CHUNK] = total;
         role_pairs += total;
         __syncthreads();
 
-        // --- load-balanced enumeration: thread takes a contiguous chunk ------
+        // --- load-balanced enumeration: each thread a contiguous slice, partner
+        //     ids fetched PC_BATCH at a time so the gathers overlap
         const uint32_t per = (total + PC_THREADS - 1) / PC_THREADS;
         const uint32_t t0 = min(total, tid * per), t1 = min(total, t0 + per);
         if (t0 < t1) {
@@ -147,57 +148,59 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(DevReads r, Emit
                 if (S.pref[mid] <= t0) lo = mid; else hi = mid;
             }
             uint32_t oi = lo;
-            uint32_t nxt = S.pref[oi + 1];
-            for (uint32_t t = t0; t < t1; ++t) {
-                while (t >= nxt) { ++oi; nxt = S.pref[oi + 1]; }
-                const uint32_t off = t - S.pref[oi];
-                const uint32_t nev = S.ne[oi];
-                const uint32_t nE = nev & 0x3FFFFFFFu;
-                uint32_t partner, w;
-                unsigned long long rank = 0;
-                if (off < nE) {
-                    const uint32_t q = S.e0[oi] + off;
-                    partner = b.md_list[q];
-                    w = nev >> 30;
-                    if constexpr (STRICT) {
-                        const uint32_t bid = X.bid[oi];
-                        const uint32_t nmd = b.bkt_mdo[bid + 1] - b.bkt_mdo[bid];
-                        const uint32_t nst = b.bkt_nst[bid];
-                        const uint32_t oe = X.own_e[oi];
-                        const unsigned long long within =
-                            (unsigned long long)(oe >> 31) * nst * nmd +
-                            (unsigned long long)(oe & 0x7FFFFFFFu) * nmd + b.md_idx[q];
-                        rank = ((unsigned long long)b.bkt_rank[bid] << 37) | within;
-                    }
-                } else {
-                    const uint32_t q = S.d0[oi] + (off - nE);
-                    partner = b.ed_list[q];
-                    w = 1;
-                    if constexpr (STRICT) {
-                        const uint32_t bid = X.bid[oi];
-                        const uint32_t nmd = b.bkt_mdo[bid + 1] - b.bkt_mdo[bid];
-                        const uint32_t nst = b.bkt_nst[bid];
-                        const uint32_t pe = b.ed_idx[q];
-                        const unsigned long long within =
-                            (unsigned long long)(pe >> 31) * nst * nmd +
-                            (unsigned long long)(pe & 0x7FFFFFFFu) * nmd + X.own_m[oi];
-                        rank = ((unsigned long long)b.bkt_rank[bid] << 37) | within;
+            uint32_t base = S.pref[oi], nxt = S.pref[oi + 1];
+            for (uint32_t t = t0; t < t1; t += PC_BATCH) {
+                uint32_t part[PC_BATCH], wv[PC_BATCH];
+                unsigned long long rk[PC_BATCH];
+#pragma unroll
+                for (int bb = 0; bb < PC_BATCH; ++bb) {
+                    part[bb] = a;  // "same read" = skip
+                    wv[bb] = 0;
+                    rk[bb] = 0;
+                    const uint32_t tt = t + bb;
+                    if (tt < t1) {
+                        while (tt >= nxt) { ++oi; base = nxt; nxt = S.pref[oi + 1]; }
+                        const uint32_t off = tt - base;
+                        const uint4 rc = S.rec[oi];
+                        const uint32_t nE = rc.y & 0x3FFFFFFFu;
+                        if (off < nE) {
+                            const uint32_t q = rc.x + off;
+                            part[bb] = in.md_list[q];
+                            wv[bb] = rc.y >> 30;
+                            if constexpr (STRICT) {
+                                const uint4 sr = X.srec[oi];
+                                const uint32_t bid = sr.x;
+                                const uint32_t nmd = in.bkt_nmd[bid], nst = in.bkt_nst[bid];
+                                const unsigned long long within =
+                                    (unsigned long long)(sr.y >> 31) * nst * nmd +
+                                    (unsigned long long)(sr.y & 0x7FFFFFFFu) * nmd + in.md_idx[q];
+                                rk[bb] = ((unsigned long long)in.bkt_rank[bid] << 37) | within;
+                            }
+                        } else {
+                            const uint32_t q = rc.z + (off - nE);
+                            part[bb] = in.ed_list[q];
+                            wv[bb] = 1;
+                            if constexpr (STRICT) {
+                                const uint4 sr = X.srec[oi];
+                                const uint32_t bid = sr.x;
+                                const uint32_t nmd = in.bkt_nmd[bid], nst = in.bkt_nst[bid];
+                                const uint32_t pe = in.ed_idx[q];
+                                const unsigned long long within =
+                                    (unsigned long long)(pe >> 31) * nst * nmd +
+                                    (unsigned long long)(pe & 0x7FFFFFFFu) * nmd + sr.z;
+                                rk[bb] = ((unsigned long long)in.bkt_rank[bid] << 37) | within;
+                            }
+                        }
                     }
                 }
-                if (partner == a) continue;                 // same read (KmerTable.scala:61-63)
-                if (split > 1 && (partner % split) != residue) continue;
+#pragma unroll
+                for (int bb = 0; bb < PC_BATCH; ++bb) {
+                    const uint32_t partner = part[bb];
+                    if (partner == a) continue;                 // same read (KmerTable.scala:61-63)
+                    if (split > 1 && (partner % split) != residue) continue;
+                    pc_insert<STRICT>(S, X, partner, wv[bb], rk[bb]);
+                }
                 if (S.overflow) break;
-                uint32_t slot = pc_hash(partner);
-                for (int probe = 0; probe < PC_TAB; ++probe) {
-                    const uint32_t old = atomicCAS(&S.key[slot], PC_EMPTY, partner);
-                    if (old == PC_EMPTY || old == partner) {
-                        if (old == PC_EMPTY && atomicAdd(&S.fill, 1u) >= (uint32_t)PC_FILL_MAX) S.overflow = 1;
-                        atomicAdd(&S.cnt[slot], w);
-                        if constexpr (STRICT) atomicMin(&X.rank[slot], rank);
-                        break;
-                    }
-                    slot = (slot + 1) & (PC_TAB - 1);
-                }
             }
         }
         __syncthreads();
@@ -249,19 +252,18 @@ size_t pair_count_lds_bytes(bool strict) {
     return s;
 }
 
-hipError_t launch_pair_count(const DevReads &r, const EmitParams &e, const Buckets &b, const uint8_t *tagtab,
-                             const PairParams &p, PairOut &o, const uint32_t *read_list, uint32_t n_blocks,
-                             hipStream_t s) {
+hipError_t launch_pair_count(const EmitParams &e, const PairIn &in, const PairParams &p, PairOut &o,
+                             const uint32_t *read_list, uint32_t n_blocks, hipStream_t s) {
     if (n_blocks == 0) return hipSuccess;
     const size_t lds = pair_count_lds_bytes(p.strict != 0);
     if (p.strict) {
-        (void)hipFuncSetAttribute((const void *)pair_count_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(pair_count_kernel<true>, dim3(n_blocks), dim3(PC_THREADS), lds, s, r, e, b, tagtab, p, o,
-                           read_list);
+        (void)hipFuncSetAttribute((const void *)pair_count_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        hipLaunchKernelGGL(pair_count_kernel<true>, dim3(n_blocks), dim3(PC_THREADS), lds, s, e, in, p, o, read_list);
     } else {
-        (void)hipFuncSetAttribute((const void *)pair_count_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(pair_count_kernel<false>, dim3(n_blocks), dim3(PC_THREADS), lds, s, r, e, b, tagtab, p,
-                           o, read_list);
+        (void)hipFuncSetAttribute((const void *)pair_count_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        hipLaunchKernelGGL(pair_count_kernel<false>, dim3(n_blocks), dim3(PC_THREADS), lds, s, e, in, p, o, read_list);
     }
     return hipGetLastError();
 }

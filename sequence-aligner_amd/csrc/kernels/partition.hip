@@ -1,0 +1,355 @@
+// partition.hip -- bucket build by hash partition, finished in LDS (gfx950).
+//
+// After two stable radix passes on the top P bits of mix(seqHash) the k-mer
+// records form 2^P partitions, each holding whole buckets (a bucket = one
+// distinct hash = one KmerData entry, KmerTable.scala:41-53) in (read, pos)
+// order.  One 256-thread workgroup per partition then, entirely in LDS:
+//   1. bitonic-sorts its records by (key = mix << lb | locrank, g),
+//   2. finds bucket heads (new hash) and group heads (new hash or loc),
+//   3. scans middle flags / edge-role counts, last bucket/group head, next group head,
+//   4. writes the middle and edge lists (read index per entry) into the
+//      partition's slice of the list arrays (md at ps + i, edge at 2 ps + i: no
+//      global scan needed), and one 16-byte record per k-mer, scattered to its
+//      occurrence index g:
+//        {md_lo, nE | me << 30, ed_lo, nD}
+//      edge role partners  = md entries of the bucket with loc <  own: [md_lo, md_lo + nE)
+//      middle role partners = edge entries of the bucket with loc <= own: [ed_lo, ed_lo + nD)
+//      (addKmerPair's orientation rule, KmerTable.scala:65-71: fst = larger loc, tie -> middle)
+// Strict mode also writes the (read,pos)-order list indices calcPairData's
+// traversal order is built from, per-bucket |st|, |md| and first occurrence.
+// Partitions larger than the LDS capacity take the global scan path
+// (buckets.hip) and records_from_tables_kernel below.  Bound: HBM / LDS.
+#include "../sa_internal.h"
+
+namespace sa {
+
+__device__ __forceinline__ uint32_t read_of_g(uint32_t g, const uint64_t *occ_off, uint32_t n_reads, uint32_t npr) {
+    if (npr) return g / npr;
+    uint32_t lo = 0, hi = n_reads;  // largest r with occ_off[r] <= g
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (occ_off[mid] <= g) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+// ---------------------------------------------------------------------------
+// partition starts: start[p] = first sorted index of partition p (empty -> next)
+// ---------------------------------------------------------------------------
+__global__ void part_mark_kernel(const uint64_t *sk, uint64_t n, int shift, uint32_t *start) {
+    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    const uint32_t p = (uint32_t)(sk[s] >> shift);
+    if (s == 0 || (uint32_t)(sk[s - 1] >> shift) != p) start[p] = (uint32_t)s;
+}
+
+// suffix min over start[0..np] (np+1 entries, start[np] = n) in one block
+__global__ __launch_bounds__(1024) void part_fill_kernel(uint32_t *start, uint32_t np, uint32_t n) {
+    __shared__ uint32_t tmin[1024];
+    if (threadIdx.x == 0) start[np] = n;
+    __syncthreads();
+    const uint32_t per = (np + 1 + 1023) / 1024;
+    const uint32_t b = threadIdx.x * per, e = min(np + 1, b + per);
+    uint32_t m = 0xFFFFFFFFu;
+    for (uint32_t i = e; i-- > b;) m = min(m, start[i]);
+    tmin[threadIdx.x] = m;
+    __syncthreads();
+    // exclusive suffix min over threads (threads after me)
+    uint32_t carry = 0xFFFFFFFFu;
+    for (uint32_t t = threadIdx.x + 1; t < 1024; ++t) carry = min(carry, tmin[t]);
+    for (uint32_t i = e; i-- > b;) {
+        carry = min(carry, start[i]);
+        start[i] = carry;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// the LDS partition builder
+// ---------------------------------------------------------------------------
+constexpr int PB_THREADS = 256;
+
+
+// ---- block (256-thread) scans: wave shuffles + one LDS slot per wave ------
+__device__ __forceinline__ uint32_t blk_excl_sum(uint32_t v, uint32_t *lds) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += t;
+    }
+    if (lane == 63) lds[w] = inc;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (int i = 0; i < w; ++i) pre += lds[i];
+    __syncthreads();
+    return pre + inc - v;
+}
+__device__ __forceinline__ uint32_t blk_excl_max(uint32_t v, uint32_t *lds) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = __shfl_up(inc, off, 64);
+        if (lane >= off) inc = max(inc, t);
+    }
+    uint32_t ex = __shfl_up(inc, 1, 64);
+    if (lane == 0) ex = 0;
+    if (lane == 63) lds[w] = inc;
+    __syncthreads();
+    for (int i = 0; i < w; ++i) ex = max(ex, lds[i]);
+    __syncthreads();
+    return ex;
+}
+__device__ __forceinline__ uint32_t blk_excl_suffix_min(uint32_t v, uint32_t *lds) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = __shfl_down(inc, off, 64);
+        if (lane + off < 64) inc = min(inc, t);
+    }
+    uint32_t ex = __shfl_down(inc, 1, 64);
+    if (lane == 63) ex = 0xFFFFFFFFu;
+    if (lane == 0) lds[w] = inc;
+    __syncthreads();
+    for (int i = w + 1; i < PB_THREADS / 64; ++i) ex = min(ex, lds[i]);
+    __syncthreads();
+    return ex;
+}
+
+template <int CAP>
+struct PartShared {
+    unsigned long long key[CAP];
+    uint32_t g[CAP];
+    uint32_t mdx[CAP + 1];   // exclusive md count (partition-local)
+    uint32_t edx[CAP + 1];   // exclusive edge-role count
+    uint32_t red[3][4];
+    uint32_t lbh[4], lgh[4];
+};
+
+template <int CAP, bool STRICT>
+__global__ __launch_bounds__(PB_THREADS) void part_build_kernel(PartArgs A, uint32_t lo_cap) {
+    extern __shared__ __align__(16) uint8_t smem_raw[];
+    PartShared<CAP> &S = *reinterpret_cast<PartShared<CAP> *>(smem_raw);
+    constexpr int IT = CAP / PB_THREADS;
+    const int tid = threadIdx.x;
+    const uint32_t p = blockIdx.x;
+    const uint32_t ps = A.start[p], pe = A.start[p + 1];
+    const uint32_t n = pe - ps;
+    if (n == 0 || n <= lo_cap) return;
+    if (n > (uint32_t)CAP) {
+        if (CAP >= 4096 && tid == 0) A.big_list[atomicAdd(A.big_n, 1u)] = p;
+        return;
+    }
+    // ---- load + bitonic sort of (key, g) over the next power of two ----------
+    uint32_t np2 = 1;
+    while (np2 < n) np2 <<= 1;
+    for (uint32_t i = tid; i < np2; i += PB_THREADS) {
+        if (i < n) { S.key[i] = A.sk[ps + i]; S.g[i] = A.sv[ps + i]; }
+        else { S.key[i] = ~0ull; S.g[i] = 0xFFFFFFFFu; }
+    }
+    __syncthreads();
+    for (uint32_t k = 2; k <= np2; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = tid; i < np2; i += PB_THREADS) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const unsigned long long ki = S.key[i], kl = S.key[l];
+                    const uint32_t gi = S.g[i], gl = S.g[l];
+                    const bool gt = ki > kl || (ki == kl && gi > gl);
+                    const bool up = (i & k) == 0;
+                    if (gt == up) { S.key[i] = kl; S.key[l] = ki; S.g[i] = gl; S.g[l] = gi; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // ---- per-thread contiguous items: flags and local aggregates -----------
+    const int lb = A.lb;
+    const unsigned long long lbm = (1ull << lb) - 1;
+    const uint32_t b0 = tid * IT;
+    uint32_t md_c = 0, ed_c = 0, last_bh = 0, last_gh = 0, first_gh = 0xFFFFFFFFu;
+    bool any_bh = false, any_gh = false;
+    uint32_t tagv[IT];
+#pragma unroll
+    for (int j = 0; j < IT; ++j) {
+        const uint32_t s = b0 + j;
+        tagv[j] = 0;
+        if (s < n) {
+            const unsigned long long k = S.key[s];
+            const uint32_t t = A.tagtab[k & lbm];
+            tagv[j] = t;
+            const bool bh = s == 0 || (S.key[s - 1] >> lb) != (k >> lb);
+            const bool gh = s == 0 || S.key[s - 1] != k;
+            md_c += (t & TAG_MD) ? 1u : 0u;
+            ed_c += ((t & TAG_ST) ? 1u : 0u) + ((t & TAG_EN) ? 1u : 0u);
+            if (bh) { last_bh = s; any_bh = true; }
+            if (gh) { last_gh = s; any_gh = true; if (first_gh == 0xFFFFFFFFu) first_gh = s; }
+        }
+    }
+    // block-wide exclusive prefix sums / prefix max and suffix min (wave shuffles + LDS)
+    const uint32_t md_ex = blk_excl_sum(md_c, S.red[0]);
+    const uint32_t ed_ex = blk_excl_sum(ed_c, S.red[1]);
+    const uint32_t bh_in = blk_excl_max(any_bh ? last_bh : 0u, S.red[2]);  // element 0 is always a head
+    const uint32_t gh_in = blk_excl_max(any_gh ? last_gh : 0u, S.lbh);
+    const uint32_t gh_next = min(blk_excl_suffix_min(first_gh, S.lgh), n);
+    // per-item exclusive counts into LDS
+    {
+        uint32_t m = md_ex, e = ed_ex;
+#pragma unroll
+        for (int j = 0; j < IT; ++j) {
+            const uint32_t s = b0 + j;
+            if (s <= n) { S.mdx[s] = m; S.edx[s] = e; }
+            const uint32_t t = tagv[j];
+            m += (t & TAG_MD) ? 1u : 0u;
+            e += ((t & TAG_ST) ? 1u : 0u) + ((t & TAG_EN) ? 1u : 0u);
+        }
+        if (b0 + IT == (uint32_t)CAP && n == (uint32_t)CAP) { S.mdx[CAP] = m; S.edx[CAP] = e; }
+    }
+    __syncthreads();
+    // next group head per item (suffix within the thread, then gh_next)
+    uint32_t nextg[IT];
+    {
+        uint32_t nx = gh_next;
+#pragma unroll
+        for (int j = IT - 1; j >= 0; --j) {
+            const uint32_t s = b0 + j;
+            nextg[j] = nx;
+            if (s < n && (s == 0 || S.key[s - 1] != S.key[s])) nx = s;
+        }
+    }
+    // ---- outputs --------------------------------------------------------
+    uint32_t nb = 0, ng = 0;
+    uint32_t bh = bh_in, gh = gh_in;
+#pragma unroll
+    for (int j = 0; j < IT; ++j) {
+        const uint32_t s = b0 + j;
+        if (s >= n) break;
+        const unsigned long long k = S.key[s];
+        const bool isb = s == 0 || (S.key[s - 1] >> lb) != (k >> lb);
+        const bool isg = s == 0 || S.key[s - 1] != k;
+        if (isb) { bh = s; ++nb; }
+        if (isg) { gh = s; ++ng; }
+        const uint32_t t = tagv[j];
+        const uint32_t g = S.g[s];
+        const uint32_t r = read_of_g(g, A.occ_off, A.n_reads, A.npr);
+        const uint32_t st = (t & TAG_ST) ? 1u : 0u, en = (t & TAG_EN) ? 1u : 0u, md = (t & TAG_MD) ? 1u : 0u;
+        const uint32_t mpos = ps + S.mdx[s], epos = 2 * ps + S.edx[s];
+        if (md) A.md_list[mpos] = r;
+        if (st) A.ed_list[epos] = r;
+        if (en) A.ed_list[epos + st] = r;
+        const uint32_t me = st + en;
+        const uint32_t nE = me ? (S.mdx[gh] - S.mdx[bh]) : 0u;
+        const uint32_t nD = md ? (S.edx[nextg[j]] - S.edx[bh]) : 0u;
+        A.rec[g] = make_uint4(ps + S.mdx[bh], nE | (me << 30), 2 * ps + S.edx[bh], nD);
+        if constexpr (STRICT) {
+            // bucket extent [bh, be)
+            uint32_t be = s + 1;
+            while (be < n && (S.key[be] >> lb) == (k >> lb)) ++be;
+            uint32_t nst = 0, nmd = 0, nen = 0, st_tot = 0, md_tot = 0, gmin = 0xFFFFFFFFu;
+            for (uint32_t q = bh; q < be; ++q) {
+                const uint32_t tq = A.tagtab[S.key[q] & lbm];
+                const uint32_t gq = S.g[q];
+                st_tot += (tq & TAG_ST) ? 1u : 0u;
+                md_tot += (tq & TAG_MD) ? 1u : 0u;
+                gmin = min(gmin, gq);
+                if (gq < g) {
+                    nst += (tq & TAG_ST) ? 1u : 0u;
+                    nmd += (tq & TAG_MD) ? 1u : 0u;
+                    nen += (tq & TAG_EN) ? 1u : 0u;
+                }
+            }
+            if (md) A.md_idx[mpos] = nmd;
+            if (st) A.ed_idx[epos] = nst;
+            if (en) A.ed_idx[epos + st] = (1u << 31) | nen;
+            A.srec[g] = make_uint4(ps + bh, st ? nst : ((1u << 31) | nen), nmd, 0u);
+            if (isb) {
+                A.bkt_nst[ps + s] = st_tot;
+                A.bkt_nmd[ps + s] = md_tot;
+                A.bkt_first[ps + s] = gmin;
+                A.is_head[ps + s] = 1;
+            }
+        }
+    }
+    // bucket / group counts for statistics
+    if (nb) atomicAdd(&A.counts[0], (unsigned long long)nb);
+    if (ng) atomicAdd(&A.counts[1], (unsigned long long)ng);
+}
+
+template <int CAP>
+static size_t part_lds() { return sizeof(PartShared<CAP>); }
+
+// ---------------------------------------------------------------------------
+// big partitions: records from the global scan tables (buckets.hip) of one range
+// ---------------------------------------------------------------------------
+__global__ void records_from_tables_kernel(const uint64_t *sk, const uint32_t *sv, uint32_t ps, uint32_t n, int lb,
+                                           const uint8_t *tagtab, Buckets b, uint4 *rec, int strict, uint4 *srec,
+                                           uint32_t *bkt_nst, uint32_t *bkt_nmd, uint32_t *bkt_first,
+                                           uint8_t *is_head) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    const uint64_t lbm = (1ull << lb) - 1;
+    const uint32_t g = sv[ps + s];
+    const uint32_t t = tagtab[sk[ps + s] & lbm];
+    const uint32_t gid = b.occ_gid[g];
+    const uint32_t bid = b.grp_bid[gid];
+    const uint32_t st = (t & TAG_ST) ? 1u : 0u, en = (t & TAG_EN) ? 1u : 0u, md = (t & TAG_MD) ? 1u : 0u;
+    const uint32_t me = st + en;
+    const uint32_t mdo = b.bkt_mdo[bid], edo = b.bkt_edo[bid];
+    const uint32_t nE = me ? (b.grp_mds[gid] - mdo) : 0u;
+    const uint32_t nD = md ? (b.grp_ede[gid] - edo) : 0u;
+    rec[g] = make_uint4(ps + mdo, nE | (me << 30), 2 * ps + edo, nD);
+    if (strict) {
+        const uint32_t s0 = b.bkt_start[bid];
+        srec[g] = make_uint4(ps + s0, st ? b.occ_idx[3ull * g] : ((1u << 31) | b.occ_idx[3ull * g + 2]),
+                             b.occ_idx[3ull * g + 1], 0u);
+        if (s == s0) {
+            const uint32_t s1 = b.bkt_start[bid + 1];
+            uint32_t gmin = 0xFFFFFFFFu;
+            for (uint32_t q = s0; q < s1; ++q) gmin = min(gmin, sv[ps + q]);
+            bkt_nst[ps + s] = b.bkt_nst[bid];
+            bkt_nmd[ps + s] = b.bkt_mdo[bid + 1] - mdo;
+            bkt_first[ps + s] = gmin;
+            is_head[ps + s] = 1;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+hipError_t launch_part_starts(const uint64_t *sk, uint64_t n, int shift, uint32_t *start, uint32_t np,
+                              hipStream_t s) {
+    hipError_t e = hipMemsetAsync(start, 0xFF, (size_t)(np + 1) * sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    if (n) hipLaunchKernelGGL(part_mark_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, sk, n, shift, start);
+    hipLaunchKernelGGL(part_fill_kernel, dim3(1), dim3(1024), 0, s, start, np, (uint32_t)n);
+    return hipGetLastError();
+}
+
+hipError_t launch_part_build(const PartArgs &a, bool strict, hipStream_t s) {
+    if (!a.np) return hipSuccess;
+#define PB_LAUNCH(CAPV, LO, ST)                                                                          \
+    do {                                                                                                 \
+        const size_t lds = part_lds<CAPV>();                                                             \
+        (void)hipFuncSetAttribute((const void *)part_build_kernel<CAPV, ST>,                             \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                 \
+        hipLaunchKernelGGL((part_build_kernel<CAPV, ST>), dim3(a.np), dim3(PB_THREADS), lds, s, a,       \
+                           (uint32_t)(LO));                                                              \
+    } while (0)
+    if (strict) { PB_LAUNCH(1024, 0, true); PB_LAUNCH(4096, 1024, true); }
+    else { PB_LAUNCH(1024, 0, false); PB_LAUNCH(4096, 1024, false); }
+#undef PB_LAUNCH
+    return hipGetLastError();
+}
+
+hipError_t launch_records_from_tables(const uint64_t *sk, const uint32_t *sv, uint32_t ps, uint32_t n, int lb,
+                                      const uint8_t *tagtab, const Buckets &b, uint4 *rec, int strict, uint4 *srec,
+                                      uint32_t *bkt_nst, uint32_t *bkt_nmd, uint32_t *bkt_first, uint8_t *is_head,
+                                      hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(records_from_tables_kernel, dim3((n + 255) / 256), dim3(256), 0, s, sk, sv, ps, n, lb, tagtab, b,
+                       rec, strict, srec, bkt_nst, bkt_nmd, bkt_first, is_head);
+    return hipGetLastError();
+}
+
+}  // namespace sa

@@ -33,6 +33,15 @@ struct EmitParams {
     int32_t maxd;
 };
 
+// bijective 32-bit mix of the seqHash: equal mix <=> equal hash, so a bucket
+// stays contiguous after sorting, while partitions by the top bits are balanced
+__device__ __forceinline__ uint32_t mix32(uint32_t h) {
+    h ^= h >> 16; h *= 0x7feb352du;
+    h ^= h >> 15; h *= 0x846ca68bu;
+    h ^= h >> 16;
+    return h;
+}
+
 // bit 0 = st, bit 1 = md, bit 2 = en   (KmerTable.scala:106-115)
 enum : uint8_t { TAG_ST = 1, TAG_MD = 2, TAG_EN = 4 };
 
@@ -55,6 +64,17 @@ struct Buckets {
     uint32_t *occ_idx = nullptr;     // [3*n_occ] own st/md/en list index
     uint32_t *bkt_nst = nullptr;     // [nb] |st| of bucket
     uint32_t *bkt_rank = nullptr;    // [nb] KmerData iteration rank (host Trove replay)
+};
+
+// Inputs of the pair counter: one 16-byte record per k-mer occurrence g
+// {md_lo, nE | me << 30, ed_lo, nD} (partition.hip) and the two partner lists.
+struct PairIn {
+    const uint4 *rec;
+    const uint32_t *md_list, *ed_list;
+    // strict mode
+    const uint4 *srec;          // {bucket head position, own_e, own_m, 0}
+    const uint32_t *md_idx, *ed_idx;
+    const uint32_t *bkt_nst, *bkt_nmd, *bkt_rank;  // indexed by bucket head position
 };
 
 struct PairParams {
@@ -114,9 +134,36 @@ hipError_t build_buckets(const uint64_t *skeys, const uint32_t *svals, uint64_t 
 hipError_t build_strict_index(const uint64_t *skeys, const uint32_t *svals, uint64_t n, int lb,
                               const uint8_t *tagtab, Buckets &b, hipStream_t s);
 
-hipError_t launch_pair_count(const DevReads &r, const EmitParams &e, const Buckets &b,
-                             const uint8_t *tagtab, const PairParams &p, PairOut &o,
+hipError_t launch_pair_count(const EmitParams &e, const PairIn &in, const PairParams &p, PairOut &o,
                              const uint32_t *read_list, uint32_t n_blocks, hipStream_t s);
+
+// ---- partition bucket build (partition.hip) ------------------------------
+struct PartArgs {
+    const uint64_t *sk;
+    const uint32_t *sv;
+    const uint32_t *start;       // [np+1]
+    uint32_t np;
+    int lb;
+    const uint8_t *tagtab;
+    const uint64_t *occ_off;
+    uint32_t n_reads, npr;
+    uint32_t *md_list, *ed_list;
+    uint4 *rec;                  // [n_occ] by g
+    uint32_t *big_list, *big_n;
+    unsigned long long *counts;  // [2]: buckets, groups
+    // strict
+    uint32_t *md_idx, *ed_idx;   // parallel to lists
+    uint4 *srec;                 // [n_occ] by g
+    uint32_t *bkt_nst, *bkt_nmd, *bkt_first;  // at bucket head sorted positions
+    uint8_t *is_head;            // [n] head flags
+};
+hipError_t launch_part_starts(const uint64_t *sk, uint64_t n, int shift, uint32_t *start, uint32_t np,
+                              hipStream_t s);
+hipError_t launch_part_build(const PartArgs &a, bool strict, hipStream_t s);
+hipError_t launch_records_from_tables(const uint64_t *sk, const uint32_t *sv, uint32_t ps, uint32_t n, int lb,
+                                      const uint8_t *tagtab, const Buckets &b, uint4 *rec, int strict, uint4 *srec,
+                                      uint32_t *bkt_nst, uint32_t *bkt_nmd, uint32_t *bkt_first, uint8_t *is_head,
+                                      hipStream_t s);
 
 hipError_t launch_make_order_keys(const uint32_t *fst, const uint32_t *snd, const uint64_t *rank,
                                   uint64_t n, int by_rank, int idbits, uint64_t *keys, uint32_t *vals,
