@@ -399,7 +399,7 @@ int device_build(sa_ctx *c, bool readback) {
     ENSURE(c->d_pstart, nparts + 1, &pstart);
     ENSURE(c->d_biglist, nparts + 1, &biglist);
     PartArgs PA{};
-    PA.sk = keys; PA.sv = vals; PA.start = pstart; PA.np = nparts; PA.lb = c->lb;
+    PA.sk = keys; PA.sv = vals; PA.start = pstart; PA.np = nparts; PA.lb = c->lb; PA.sort_bits = kbits - PB;
     PA.tagtab = (const uint8_t *)c->d_tagtab.p;
     PA.occ_off = (const uint64_t *)c->d_occ_off.p;
     PA.n_reads = nr; PA.npr = c->uniform_npr;

@@ -126,7 +126,74 @@ struct PartShared {
     uint32_t edx[CAP + 1];   // exclusive edge-role count
     uint32_t red[3][4];
     uint32_t lbh[4], lgh[4];
+    uint32_t cnt[4][256];    // LDS radix sort: per-wave digit counts / bases
 };
+
+// Stable LSD radix sort of the partition's (key, g) in LDS over key bits
+// [0, bits): wave w owns elements [w*CAP/4, (w+1)*CAP/4) (slices of 64), ranks
+// come from a 64-lane ballot multisplit + wave-private counts, elements are held
+// in registers across the scatter, so one LDS buffer and 3 barriers per pass.
+template <int CAP, class SH>
+__device__ __forceinline__ void lds_radix_sort(SH &S, uint32_t n, int bits) {
+    constexpr int SUB = CAP / 4, SL = SUB / 64;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int shift = 0; shift < bits; shift += 8) {
+        for (int q = lane; q < 256; q += 64) S.cnt[w][q] = 0;
+        unsigned long long k[SL];
+        uint32_t gv[SL], rk[SL];
+#pragma unroll
+        for (int j = 0; j < SL; ++j) {
+            const uint32_t i = w * SUB + j * 64 + lane;
+            k[j] = i < n ? S.key[i] : 0ull;
+            gv[j] = i < n ? S.g[i] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < SL; ++j) {
+            const uint32_t i = w * SUB + j * 64 + lane;
+            const bool valid = i < n;
+            const uint32_t d = (uint32_t)(k[j] >> shift) & 255u;
+            uint64_t peer = __ballot(valid);
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                const bool bit = (d >> b) & 1u;
+                const uint64_t bb = __ballot(bit);
+                peer &= bit ? bb : ~bb;
+            }
+            const uint32_t before = valid ? S.cnt[w][d] : 0u;
+            rk[j] = before + __popcll(peer & lt_mask);
+            __builtin_amdgcn_wave_barrier();
+            if (valid && (peer & lt_mask) == 0) S.cnt[w][d] = before + __popcll(peer);
+            __builtin_amdgcn_wave_barrier();
+        }
+        __syncthreads();
+        {   // digit tid: exclusive scan over digits, then per-wave bases in place
+            uint32_t tot = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) tot += S.cnt[q][tid];
+            const uint32_t lo = blk_excl_sum(tot, S.red[0]);
+            uint32_t acc = lo;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t c = S.cnt[q][tid];
+                S.cnt[q][tid] = acc;
+                acc += c;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < SL; ++j) {
+            const uint32_t i = w * SUB + j * 64 + lane;
+            if (i < n) {
+                const uint32_t d = (uint32_t)(k[j] >> shift) & 255u;
+                const uint32_t pos = S.cnt[w][d] + rk[j];
+                S.key[pos] = k[j];
+                S.g[pos] = gv[j];
+            }
+        }
+        __syncthreads();
+    }
+}
 
 template <int CAP, bool STRICT>
 __global__ __launch_bounds__(PB_THREADS) void part_build_kernel(PartArgs A, uint32_t lo_cap) {
@@ -142,29 +209,10 @@ __global__ __launch_bounds__(PB_THREADS) void part_build_kernel(PartArgs A, uint
         if (CAP >= 4096 && tid == 0) A.big_list[atomicAdd(A.big_n, 1u)] = p;
         return;
     }
-    // ---- load + bitonic sort of (key, g) over the next power of two ----------
-    uint32_t np2 = 1;
-    while (np2 < n) np2 <<= 1;
-    for (uint32_t i = tid; i < np2; i += PB_THREADS) {
-        if (i < n) { S.key[i] = A.sk[ps + i]; S.g[i] = A.sv[ps + i]; }
-        else { S.key[i] = ~0ull; S.g[i] = 0xFFFFFFFFu; }
-    }
+    // ---- load, then stable LDS radix sort on the key bits below the partition id
+    for (uint32_t i = tid; i < n; i += PB_THREADS) { S.key[i] = A.sk[ps + i]; S.g[i] = A.sv[ps + i]; }
     __syncthreads();
-    for (uint32_t k = 2; k <= np2; k <<= 1) {
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t i = tid; i < np2; i += PB_THREADS) {
-                const uint32_t l = i ^ j;
-                if (l > i) {
-                    const unsigned long long ki = S.key[i], kl = S.key[l];
-                    const uint32_t gi = S.g[i], gl = S.g[l];
-                    const bool gt = ki > kl || (ki == kl && gi > gl);
-                    const bool up = (i & k) == 0;
-                    if (gt == up) { S.key[i] = kl; S.key[l] = ki; S.g[i] = gl; S.g[l] = gi; }
-                }
-            }
-            __syncthreads();
-        }
-    }
+    lds_radix_sort<CAP>(S, n, A.sort_bits);
     // ---- per-thread contiguous items: flags and local aggregates -----------
     const int lb = A.lb;
     const unsigned long long lbm = (1ull << lb) - 1;

@@ -145,54 +145,116 @@ __global__ __launch_bounds__(RS_THREADS) void rs_upsweep_kernel(const uint64_t *
     hist[(uint64_t)threadIdx.x * nblocks + blockIdx.x] = cnt[threadIdx.x];
 }
 
-// Stable scatter: elements keep tile order (slice j, then thread) inside each digit.
+// Stable scatter.  Wave w owns the contiguous sub-tile [base + w*1024, +1024),
+// read as 16 coalesced slices of 64; each element's rank among equal digits of
+// its wave comes from a 64-lane ballot multisplit (8 ballots -> peer mask) plus
+// a wave-private running count in LDS, so the only barriers are per tile.  The
+// tile is then staged in LDS in digit order and written out in digit-contiguous
+// runs (coalesced), at hist[digit][block] + run offset.
+constexpr int RS_WAVES = RS_THREADS / 64;
+constexpr int RS_SUB = RS_TILE / RS_WAVES;   // 1024 elements per wave
+constexpr int RS_SLICES = RS_SUB / 64;       // 16
+
+struct RsShared {
+    unsigned long long key[RS_TILE];
+    uint32_t val[RS_TILE];
+    uint32_t cnt[RS_WAVES][256];   // per-wave digit counts
+    uint32_t lofs[256];            // tile-local start of each digit run
+    uint32_t gofs[256];            // global start of each digit run
+};
+
+__device__ __forceinline__ uint64_t wave_peers(uint32_t d, bool valid) {
+    uint64_t peer = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        const bool bit = (d >> b) & 1u;
+        const uint64_t bb = __ballot(bit);
+        peer &= bit ? bb : ~bb;
+    }
+    return peer;
+}
+
 __global__ __launch_bounds__(RS_THREADS) void rs_downsweep_kernel(const uint64_t *kin, const uint32_t *vin,
                                                                   uint64_t *kout, uint32_t *vout, uint64_t n,
                                                                   int shift, const uint32_t *hist,
                                                                   uint32_t nblocks) {
-    __shared__ uint32_t run[256];     // next output position of each digit for this block
-    __shared__ uint32_t wcnt[4][256]; // per-wave digit counts of the current slice
+    extern __shared__ __align__(16) uint8_t rs_smem[];
+    RsShared &S = *reinterpret_cast<RsShared *>(rs_smem);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    run[tid] = hist[(uint64_t)tid * nblocks + blockIdx.x];
-    const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (int j = 0; j < RS_ITEMS; ++j) {
-        const uint64_t i = base + (uint64_t)j * RS_THREADS + tid;
+    const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+    for (int q = lane; q < 256; q += 64) S.cnt[w][q] = 0;
+    // no barrier needed: each wave only touches its own counters until the block barrier
+    unsigned long long k[RS_SLICES];
+    uint32_t v[RS_SLICES], rk[RS_SLICES];
+    const uint64_t sub = base + (uint64_t)w * RS_SUB;
+#pragma unroll
+    for (int j = 0; j < RS_SLICES; ++j) {
+        const uint64_t i = sub + (uint64_t)j * 64 + lane;
+        k[j] = i < n ? kin[i] : ~0ull;
+        v[j] = i < n ? vin[i] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < RS_SLICES; ++j) {
+        const uint64_t i = sub + (uint64_t)j * 64 + lane;
         const bool valid = i < n;
-        const uint64_t key = valid ? kin[i] : 0ull;
-        const uint32_t val = valid ? vin[i] : 0u;
-        const uint32_t d = (uint32_t)(key >> shift) & 255u;
-        uint64_t peer = __ballot(valid);
+        const uint32_t d = (uint32_t)(k[j] >> shift) & 255u;
+        const uint64_t peer = wave_peers(d, valid);
+        const uint32_t before = valid ? S.cnt[w][d] : 0u;
+        rk[j] = before + __popcll(peer & lt_mask);
+        __builtin_amdgcn_wave_barrier();
+        if (valid && (peer & lt_mask) == 0) S.cnt[w][d] = before + __popcll(peer);
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    // digit tid: tile total, tile-local run start (exclusive scan over digits), global start
+    {
+        uint32_t tot = 0;
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            const bool bit = (d >> b) & 1u;
-            const uint64_t bb = __ballot(bit);
-            peer &= bit ? bb : ~bb;
-        }
-        const uint32_t rank_w = __popcll(peer & lt_mask);
-        const uint32_t cnt_w = __popcll(peer);
+        for (int q = 0; q < RS_WAVES; ++q) tot += S.cnt[q][tid];
+        // block exclusive scan of tot over the 256 digits
+        uint32_t inc = tot;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) wcnt[w][lane * 4 + q] = 0;
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t t = __shfl_up(inc, off, 64);
+            if (lane >= off) inc += t;
+        }
+        if (lane == 63) S.lofs[w] = inc;  // temporarily: wave sums
         __syncthreads();
-        if (valid && rank_w == 0) wcnt[w][d] = cnt_w;
+        uint32_t pre = 0;
+        for (int q = 0; q < w; ++q) pre += S.lofs[q];
         __syncthreads();
-        {   // digit tid: exclusive prefix across the 4 waves, in place
-            uint32_t acc = run[tid];
+        const uint32_t lo = pre + inc - tot;
+        S.lofs[tid] = lo;
+        S.gofs[tid] = hist[(uint64_t)tid * nblocks + blockIdx.x];
+        // per-wave bases inside the tile, in place of the counts
+        uint32_t acc = lo;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t c = wcnt[q][tid];
-                wcnt[q][tid] = acc;
-                acc += c;
-            }
-            run[tid] = acc;
+        for (int q = 0; q < RS_WAVES; ++q) {
+            const uint32_t c = S.cnt[q][tid];
+            S.cnt[q][tid] = acc;
+            acc += c;
         }
-        __syncthreads();
-        if (valid) {
-            const uint32_t pos = wcnt[w][d] + rank_w;
-            kout[pos] = key;
-            vout[pos] = val;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RS_SLICES; ++j) {
+        const uint64_t i = sub + (uint64_t)j * 64 + lane;
+        if (i < n) {
+            const uint32_t d = (uint32_t)(k[j] >> shift) & 255u;
+            const uint32_t pos = S.cnt[w][d] + rk[j];
+            S.key[pos] = k[j];
+            S.val[pos] = v[j];
         }
-        __syncthreads();
+    }
+    __syncthreads();
+    const uint32_t nt = (uint32_t)min((uint64_t)RS_TILE, n - base);
+    for (uint32_t i = tid; i < nt; i += RS_THREADS) {
+        const unsigned long long kk = S.key[i];
+        const uint32_t d = (uint32_t)(kk >> shift) & 255u;
+        const uint32_t pos = S.gofs[d] + (i - S.lofs[d]);
+        kout[pos] = kk;
+        vout[pos] = S.val[i];
     }
 }
 
@@ -206,6 +268,12 @@ hipError_t radix_sort(uint64_t **keys, uint32_t **vals, uint64_t **keys_alt, uin
                       uint64_t n, int lo, int hi, void *tmp, hipStream_t s) {
     if (n <= 1 || hi <= lo) return hipSuccess;
     const uint64_t nb = (n + RS_TILE - 1) / RS_TILE;
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void *)rs_downsweep_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)sizeof(RsShared));
+        attr_set = true;
+    }
     uint32_t *hist = (uint32_t *)tmp;
     void *stmp = (void *)(hist + 256 * nb);
     for (int shift = lo; shift < hi; shift += 8) {
@@ -213,8 +281,8 @@ hipError_t radix_sort(uint64_t **keys, uint32_t **vals, uint64_t **keys_alt, uin
                            (uint32_t)nb);
         hipError_t e = exclusive_scan_u32(hist, hist, 256 * nb, nullptr, stmp, s);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(rs_downsweep_kernel, dim3((uint32_t)nb), dim3(RS_THREADS), 0, s, *keys, *vals,
-                           *keys_alt, *vals_alt, n, shift, (const uint32_t *)hist, (uint32_t)nb);
+        hipLaunchKernelGGL(rs_downsweep_kernel, dim3((uint32_t)nb), dim3(RS_THREADS), sizeof(RsShared), s, *keys,
+                           *vals, *keys_alt, *vals_alt, n, shift, (const uint32_t *)hist, (uint32_t)nb);
         uint64_t *tk = *keys; *keys = *keys_alt; *keys_alt = tk;
         uint32_t *tv = *vals; *vals = *vals_alt; *vals_alt = tv;
     }

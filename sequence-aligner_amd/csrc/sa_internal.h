@@ -144,6 +144,7 @@ struct PartArgs {
     const uint32_t *start;       // [np+1]
     uint32_t np;
     int lb;
+    int sort_bits;               // key bits below the partition id (sorted in LDS)
     const uint8_t *tagtab;
     const uint64_t *occ_off;
     uint32_t n_reads, npr;
