@@ -43,19 +43,28 @@ struct DBuf {
     size_t bytes = 0;
 };
 
-struct Counters {                    // device-resident scalars, one memset per build
-    unsigned long long cursor;
-    unsigned long long role_pairs;
-    unsigned long long role_pairs_dummy;
-    unsigned long long distinct;
-    unsigned long long cells;
+// device-resident counters, one memset per build; the hot ones are NSHARD-way
+// sharded (see sa_internal.h) and summed here
+struct Counters {
+    unsigned long long cursor[NSHARD];
+    unsigned long long role_pairs[NSHARD];
+    unsigned long long role_pairs_dummy[NSHARD];
+    unsigned long long distinct[NSHARD];
+    unsigned long long cells[NSHARD];
+    unsigned long long bkt_counts[2 * NSHARD];
     uint32_t overflow_n;
     int32_t err;
     uint32_t totals[4];
     uint32_t big_n;
     uint32_t pad_;
-    unsigned long long bkt_counts[2];
+    uint32_t shard_off[NSHARD + 2];
 };
+
+unsigned long long shard_sum(const unsigned long long *v) {
+    unsigned long long t = 0;
+    for (int i = 0; i < NSHARD; ++i) t += v[i];
+    return t;
+}
 
 }  // namespace
 
@@ -92,6 +101,7 @@ struct sa_ctx {
     uint64_t n_disp = 0;
     // options / state
     bool keep_pairs = false, timing = false;
+    int ablate = 0;  // profiling only: SA_ABLATE env (results are wrong when set)
     bool built = false, aligned = false;
     // results (host)
     std::vector<int32_t> lead, trail, count;
@@ -400,6 +410,7 @@ int device_build(sa_ctx *c, bool readback) {
     ENSURE(c->d_biglist, nparts + 1, &biglist);
     PartArgs PA{};
     PA.sk = keys; PA.sv = vals; PA.start = pstart; PA.np = nparts; PA.lb = c->lb; PA.sort_bits = kbits - PB;
+    PA.ablate = c->ablate;
     PA.tagtab = (const uint8_t *)c->d_tagtab.p;
     PA.occ_off = (const uint64_t *)c->d_occ_off.p;
     PA.n_reads = nr; PA.npr = c->uniform_npr;
@@ -533,55 +544,62 @@ int device_build(sa_ctx *c, bool readback) {
     P.strict = strict ? 1 : 0;
     P.split = 1;
     P.max_occ = c->max_occ;
+    P.ablate = c->ablate;
     if (c->pair_cap == 0) c->pair_cap = std::max<uint64_t>(1 << 16, (uint64_t)nr * (P.emit_all ? 64 : 24));
-    unsigned long long cursor = 0;
+    // output regions: NSHARD x cap_s entries (a block appends to region blockIdx % NSHARD)
+    unsigned long long cur[NSHARD];
+    auto cur_max = [&]() { unsigned long long m = 0; for (auto v : cur) m = std::max(m, v); return m; };
     uint32_t ovn = 0;
+    uint64_t cap_s = (c->pair_cap + NSHARD - 1) / NSHARD;
     for (int attempt = 0; attempt < 4; ++attempt) {
         PairOut O;
-        ENSURE(c->d_pf, c->pair_cap, &O.fst);
-        ENSURE(c->d_ps, c->pair_cap, &O.snd);
-        ENSURE(c->d_pc, c->pair_cap, &O.cnt);
+        const uint64_t tot_cap = cap_s * NSHARD;
+        ENSURE(c->d_pf, tot_cap, &O.fst);
+        ENSURE(c->d_ps, tot_cap, &O.snd);
+        ENSURE(c->d_pc, tot_cap, &O.cnt);
         O.rank = nullptr;
-        if (strict) ENSURE(c->d_pr, c->pair_cap, &O.rank);
+        if (strict) ENSURE(c->d_pr, tot_cap, &O.rank);
         ENSURE(c->d_ovl, 2 * nr + 2, &O.overflow_list);
-        O.cursor = &cnt->cursor;
-        O.cap = c->pair_cap;
-        O.role_pairs = &cnt->role_pairs;
+        O.cursor = cnt->cursor;
+        O.cap_s = cap_s;
+        O.role_pairs = cnt->role_pairs;
         O.overflow_n = &cnt->overflow_n;
-        O.distinct = &cnt->distinct;
-        HIPCHK(hipMemsetAsync(&cnt->cursor, 0, 4 * sizeof(unsigned long long), c->stream));
+        O.distinct = cnt->distinct;
+        HIPCHK(hipMemsetAsync(cnt->cursor, 0, 4 * NSHARD * sizeof(unsigned long long), c->stream));
         HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(uint32_t), c->stream));
         {
             StageScope st(c, SA_STAGE_PAIRS);
             HIPCHK(launch_pair_count(E, PI, P, O, nullptr, nr, c->stream));
         }
-        HIPCHK(hipMemcpyAsync(&cursor, &cnt->cursor, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(cur, cnt->cursor, sizeof(cur), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipMemcpyAsync(&ovn, &cnt->overflow_n, 4, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         // reads whose LDS table overflowed (> 1,536 partners: high-copy repeats) are
         // recounted in 64 partner-residue passes; each pass holds up to 1,536 partners
-        if (ovn > 0 && cursor <= c->pair_cap) {
+        if (ovn > 0 && cur_max() <= cap_s) {
             const uint32_t split = 64;
             PairParams P2 = P;
             P2.split = (int32_t)split;
             PairOut O2 = O;
-            O2.role_pairs = &cnt->role_pairs_dummy;
+            O2.role_pairs = cnt->role_pairs_dummy;
             O2.overflow_list = O.overflow_list + ovn;  // keep the read list intact
             HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(uint32_t), c->stream));
             {
                 StageScope st(c, SA_STAGE_PAIRS);
                 HIPCHK(launch_pair_count(E, PI, P2, O2, O.overflow_list, ovn * split, c->stream));
             }
-            HIPCHK(hipMemcpyAsync(&cursor, &cnt->cursor, 8, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipMemcpyAsync(cur, cnt->cursor, sizeof(cur), hipMemcpyDeviceToHost, c->stream));
             HIPCHK(hipMemcpyAsync(&ovn, &cnt->overflow_n, 4, hipMemcpyDeviceToHost, c->stream));
             HIPCHK(hipStreamSynchronize(c->stream));
             if (ovn) return fail(c, SA_E_OVERFLOW, "a read has more than 98,304 distinct partners");
         }
-        if (cursor <= c->pair_cap) break;
-        c->pair_cap = cursor + cursor / 4 + 1024;  // grow and recount
+        if (cur_max() <= cap_s) break;
+        cap_s = cur_max() + cur_max() / 4 + 1024;  // grow and recount
+        c->pair_cap = cap_s * NSHARD;
         if (attempt == 3) return fail(c, SA_E_OVERFLOW, "pair output did not fit");
     }
-    const uint64_t np = cursor;
+    uint64_t np = 0;
+    for (auto v : cur) np += v;
 
     // ---- ordering --------------------------------------------------------
     uint64_t *ok, *ok2; uint32_t *ov, *ov2; uint8_t *otmp;
@@ -598,7 +616,8 @@ int device_build(sa_ctx *c, bool readback) {
         StageScope st(c, SA_STAGE_ORDER);
         const int idb = bits_for(nr ? nr - 1 : 0);
         HIPCHK(launch_make_order_keys((const uint32_t *)c->d_pf.p, (const uint32_t *)c->d_ps.p,
-                                      (const uint64_t *)c->d_pr.p, np, strict ? 1 : 0, idb, ok, ov, c->stream));
+                                      (const uint64_t *)c->d_pr.p, cnt->cursor, cap_s, strict ? 1 : 0, idb, ok, ov,
+                                      cnt->shard_off, c->stream));
         const int hi = strict ? 64 : 2 * idb;
         HIPCHK(radix_sort(&ok, &ov, &ok2, &ov2, np, 0, hi, otmp, c->stream));
         HIPCHK(launch_gather_pairs(ov, np, (const uint32_t *)c->d_pf.p, (const uint32_t *)c->d_ps.p,
@@ -610,9 +629,9 @@ int device_build(sa_ctx *c, bool readback) {
     resolve_timing(c);
     c->stats = sa_stats{};
     c->stats.kmers = n;
-    c->stats.buckets = hc.bkt_counts[0] + big_buckets;
-    c->stats.role_pairs = hc.role_pairs;
-    c->stats.pairs = hc.distinct;
+    c->stats.buckets = shard_sum(hc.bkt_counts) + big_buckets;
+    c->stats.role_pairs = shard_sum(hc.role_pairs);
+    c->stats.pairs = shard_sum(hc.distinct);
     c->stats.id_mode = c->mode;
 
     c->lead.clear(); c->trail.clear(); c->count.clear();
@@ -726,20 +745,20 @@ int device_align(sa_ctx *c, bool readback) {
     DevAlignment *out;
     ENSURE(c->d_aln, nd, &out);
     HIPCHK(hipMemsetAsync(&cnt->err, 0, 4, c->stream));
-    HIPCHK(hipMemsetAsync(&cnt->cells, 0, 8, c->stream));
+    HIPCHK(hipMemsetAsync(cnt->cells, 0, sizeof(cnt->cells), c->stream));
     {
         StageScope st(c, SA_STAGE_ALIGN);
         HIPCHK(launch_dovetail(dev_reads(c), (const int32_t *)c->d_lead.p, (const int32_t *)c->d_trail.p, nd, P, G,
-                               out, &cnt->err, &cnt->cells, c->stream));
+                               out, &cnt->err, cnt->cells, c->stream));
     }
     int32_t err = 0;
-    unsigned long long cells = 0;
+    unsigned long long cells_s[NSHARD];
     HIPCHK(hipMemcpyAsync(&err, &cnt->err, 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(&cells, &cnt->cells, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(cells_s, cnt->cells, sizeof(cells_s), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     resolve_timing(c);
     c->stats.aligned = nd;
-    c->stats.dp_cells = cells;
+    c->stats.dp_cells = shard_sum(cells_s);
     if (err) {
         const char *msg = err == SA_E_NON_ACGT ? "non-ACGT base in an aligned region (HOXD MatchError)"
                         : err == SA_E_SHORT_READ ? "trail shorter than the band width (StringIndexOutOfBounds)"
@@ -805,6 +824,7 @@ int sa_ctx_create(const sa_settings *s, int device, sa_ctx **out) {
     sa_ctx *c = new sa_ctx();
     c->set = *s;
     c->device = device;
+    if (const char *ab = getenv("SA_ABLATE")) c->ablate = atoi(ab);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return SA_E_HIP;

@@ -317,10 +317,18 @@ __global__ __launch_bounds__(256) void dovetail_kernel(DevReads rd, const int32_
             out[pair] = o;
         }
     }
-    if (lane == 0 && have && ok) {
-        unsigned long long cells = (unsigned long long)LA * w;
-        if (status == 0) cells += (unsigned long long)(dL + 1) * (w + 1);
-        atomicAdd(cells_total, cells);
+    // DP cells for statistics: block-reduced, one sharded atomic per block
+    {
+        __shared__ unsigned long long cell_sum;
+        if (threadIdx.x == 0) cell_sum = 0;
+        __syncthreads();
+        if (lane == 0 && have && ok) {
+            unsigned long long cells = (unsigned long long)LA * w;
+            if (status == 0) cells += (unsigned long long)(dL + 1) * (w + 1);
+            atomicAdd(&cell_sum, cells);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0 && cell_sum) atomicAdd(&cells_total[blockIdx.x % NSHARD], cell_sum);
     }
 }
 

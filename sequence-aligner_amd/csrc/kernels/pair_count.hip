@@ -198,6 +198,7 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
                     const uint32_t partner = part[bb];
                     if (partner == a) continue;                 // same read (KmerTable.scala:61-63)
                     if (split > 1 && (partner % split) != residue) continue;
+                    if (p.ablate & 16) { if (partner == 0xFFFFFFF0u) S.fill = 0; continue; }
                     pc_insert<STRICT>(S, X, partner, wv[bb], rk[bb]);
                 }
                 if (S.overflow) break;
@@ -206,8 +207,9 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
         __syncthreads();
     }
 
-    if (tid == 0 && residue == 0 && role_pairs) atomicAdd(o.role_pairs, role_pairs);
-    if (tid == 0 && !S.overflow) atomicAdd(o.distinct, (unsigned long long)S.fill);
+    const uint32_t shard = blockIdx.x % NSHARD;
+    if (tid == 0 && residue == 0 && role_pairs) atomicAdd(&o.role_pairs[shard], role_pairs);
+    if (tid == 0 && !S.overflow) atomicAdd(&o.distinct[shard], (unsigned long long)S.fill);
     if (S.overflow) {
         if (tid == 0 && residue == 0) {
             const uint32_t at = atomicAdd(o.overflow_n, 1u);
@@ -216,6 +218,7 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
         return;
     }
     // --- emit (a, partner, count[, rank]) --------------------------------
+    if (p.ablate & 32) return;
     constexpr int PER = PC_TAB / PC_THREADS;
     uint32_t keep = 0;
 #pragma unroll
@@ -228,16 +231,18 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
     uint32_t total;
     uint32_t ex = pc_block_excl_scan(__popc(keep), S.lds4, &total);
     if (total == 0) return;
-    if (tid == 0) S.out_base = (uint32_t)atomicAdd(o.cursor, (unsigned long long)total);
+    if (tid == 0) S.out_base = (uint32_t)atomicAdd(&o.cursor[shard], (unsigned long long)total);
     __syncthreads();
     const unsigned long long base = (unsigned long long)S.out_base + ex;
+    const unsigned long long region = (unsigned long long)shard * o.cap_s;
     uint32_t k = 0;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
         if (!(keep & (1u << j))) continue;
         const uint32_t sl = tid * PER + j;
-        const unsigned long long at = base + k++;
-        if (at < o.cap) {
+        const unsigned long long lat = base + k++;
+        const unsigned long long at = region + lat;
+        if (lat < o.cap_s) {
             o.fst[at] = a;
             o.snd[at] = S.key[sl];
             o.cnt[at] = S.cnt[sl];
@@ -271,21 +276,41 @@ hipError_t launch_pair_count(const EmitParams &e, const PairIn &in, const PairPa
 // ---------------------------------------------------------------------------
 // output ordering helpers
 // ---------------------------------------------------------------------------
-__global__ void make_order_keys_kernel(const uint32_t *fst, const uint32_t *snd, const uint64_t *rank, uint64_t n,
-                                       int by_rank, int idbits, uint64_t *keys, uint32_t *vals) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    // wide: lead descending then trail ascending; strict: first-occurrence rank
-    const uint64_t top = (1ull << idbits) - 1;
-    keys[i] = by_rank ? rank[i] : (((top - fst[i]) << idbits) | snd[i]);
-    vals[i] = (uint32_t)i;
+// exclusive prefix of the NSHARD region counts (one tiny block)
+__global__ void shard_offsets_kernel(const unsigned long long *cursor, unsigned long long cap_s, uint32_t *off) {
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int i = 0; i < NSHARD; ++i) {
+            off[i] = acc;
+            acc += (uint32_t)min(cursor[i], cap_s);
+        }
+        off[NSHARD] = acc;
+    }
 }
 
-hipError_t launch_make_order_keys(const uint32_t *fst, const uint32_t *snd, const uint64_t *rank, uint64_t n,
-                                  int by_rank, int idbits, uint64_t *keys, uint32_t *vals, hipStream_t s) {
-    if (!n) return hipSuccess;
-    hipLaunchKernelGGL(make_order_keys_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, fst, snd, rank, n,
-                       by_rank, idbits, keys, vals);
+__global__ void make_order_keys_kernel(const uint32_t *fst, const uint32_t *snd, const uint64_t *rank,
+                                       const unsigned long long *cursor, unsigned long long cap_s, int by_rank,
+                                       int idbits, uint64_t *keys, uint32_t *vals, const uint32_t *off) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // region-space index
+    const uint32_t shard = (uint32_t)(i / cap_s);
+    if (shard >= NSHARD) return;
+    const uint64_t j = i - (uint64_t)shard * cap_s;
+    if (j >= cursor[shard]) return;
+    const uint32_t pos = off[shard] + (uint32_t)j;
+    // wide: lead descending then trail ascending; strict: first-occurrence rank
+    const uint64_t top = (1ull << idbits) - 1;
+    keys[pos] = by_rank ? rank[i] : (((top - fst[i]) << idbits) | snd[i]);
+    vals[pos] = (uint32_t)i;
+}
+
+hipError_t launch_make_order_keys(const uint32_t *fst, const uint32_t *snd, const uint64_t *rank,
+                                  const unsigned long long *cursor, unsigned long long cap_s, int by_rank,
+                                  int idbits, uint64_t *keys, uint32_t *vals, uint32_t *shard_off,
+                                  hipStream_t s) {
+    hipLaunchKernelGGL(shard_offsets_kernel, dim3(1), dim3(64), 0, s, cursor, cap_s, shard_off);
+    const uint64_t tot = (uint64_t)NSHARD * cap_s;
+    hipLaunchKernelGGL(make_order_keys_kernel, dim3((uint32_t)((tot + 255) / 256)), dim3(256), 0, s, fst, snd, rank,
+                       cursor, cap_s, by_rank, idbits, keys, vals, (const uint32_t *)shard_off);
     return hipGetLastError();
 }
 

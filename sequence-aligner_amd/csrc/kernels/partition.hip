@@ -212,7 +212,7 @@ __global__ __launch_bounds__(PB_THREADS) void part_build_kernel(PartArgs A, uint
     // ---- load, then stable LDS radix sort on the key bits below the partition id
     for (uint32_t i = tid; i < n; i += PB_THREADS) { S.key[i] = A.sk[ps + i]; S.g[i] = A.sv[ps + i]; }
     __syncthreads();
-    lds_radix_sort<CAP>(S, n, A.sort_bits);
+    if (!(A.ablate & 1)) lds_radix_sort<CAP>(S, n, A.sort_bits);
     // ---- per-thread contiguous items: flags and local aggregates -----------
     const int lb = A.lb;
     const unsigned long long lbm = (1ull << lb) - 1;
@@ -284,13 +284,15 @@ __global__ __launch_bounds__(PB_THREADS) void part_build_kernel(PartArgs A, uint
         const uint32_t r = read_of_g(g, A.occ_off, A.n_reads, A.npr);
         const uint32_t st = (t & TAG_ST) ? 1u : 0u, en = (t & TAG_EN) ? 1u : 0u, md = (t & TAG_MD) ? 1u : 0u;
         const uint32_t mpos = ps + S.mdx[s], epos = 2 * ps + S.edx[s];
-        if (md) A.md_list[mpos] = r;
-        if (st) A.ed_list[epos] = r;
-        if (en) A.ed_list[epos + st] = r;
+        if (!(A.ablate & 4)) {
+            if (md) A.md_list[mpos] = r;
+            if (st) A.ed_list[epos] = r;
+            if (en) A.ed_list[epos + st] = r;
+        }
         const uint32_t me = st + en;
         const uint32_t nE = me ? (S.mdx[gh] - S.mdx[bh]) : 0u;
         const uint32_t nD = md ? (S.edx[nextg[j]] - S.edx[bh]) : 0u;
-        A.rec[g] = make_uint4(ps + S.mdx[bh], nE | (me << 30), 2 * ps + S.edx[bh], nD);
+        if (!(A.ablate & 2)) A.rec[g] = make_uint4(ps + S.mdx[bh], nE | (me << 30), 2 * ps + S.edx[bh], nD);
         if constexpr (STRICT) {
             // bucket extent [bh, be)
             uint32_t be = s + 1;
@@ -320,9 +322,13 @@ __global__ __launch_bounds__(PB_THREADS) void part_build_kernel(PartArgs A, uint
             }
         }
     }
-    // bucket / group counts for statistics
-    if (nb) atomicAdd(&A.counts[0], (unsigned long long)nb);
-    if (ng) atomicAdd(&A.counts[1], (unsigned long long)ng);
+    // bucket / group counts for statistics: block-reduced, sharded
+    const uint32_t nb_blk = blk_excl_sum(nb, S.red[0]) + nb;  // inclusive for the last thread
+    const uint32_t ng_blk = blk_excl_sum(ng, S.red[1]) + ng;
+    if (tid == PB_THREADS - 1) {
+        atomicAdd(&A.counts[p % NSHARD], (unsigned long long)nb_blk);
+        atomicAdd(&A.counts[NSHARD + p % NSHARD], (unsigned long long)ng_blk);
+    }
 }
 
 template <int CAP>

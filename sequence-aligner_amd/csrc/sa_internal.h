@@ -83,15 +83,23 @@ struct PairParams {
     int32_t strict;        // compute first-occurrence ranks
     int32_t split;         // partner residue classes (overflow fallback)
     uint32_t max_occ;      // max occurrences of one read (LDS sizing)
+    int32_t ablate;        // profiling only (env SA_ABLATE): 16 skip inserts, 32 skip emission
 };
 
+// Device-wide counters are sharded NSHARD ways (shard = blockIdx % NSHARD) and
+// block-reduced first: same-address device atomics from every block serialise
+// at one L2 channel (MI355X_MICROARCH.md, fan-in row).
+constexpr int NSHARD = 64;
+
+// Output of the pair counter: NSHARD regions of cap_s entries each; block b
+// appends to region b % NSHARD.
 struct PairOut {
-    uint32_t *fst, *snd, *cnt;   // [cap]
-    uint64_t *rank;              // [cap] (strict)
-    unsigned long long *cursor;  // entries written
-    unsigned long long cap;
-    unsigned long long *role_pairs;
-    unsigned long long *distinct;  // distinct (a, partner) keys counted
+    uint32_t *fst, *snd, *cnt;   // [NSHARD * cap_s]
+    uint64_t *rank;              // [NSHARD * cap_s] (strict)
+    unsigned long long *cursor;  // [NSHARD] entries written per region
+    unsigned long long cap_s;
+    unsigned long long *role_pairs;  // [NSHARD]
+    unsigned long long *distinct;    // [NSHARD] distinct (a, partner) keys counted
     uint32_t *overflow_list;     // reads whose LDS table overflowed
     uint32_t *overflow_n;
 };
@@ -145,13 +153,14 @@ struct PartArgs {
     uint32_t np;
     int lb;
     int sort_bits;               // key bits below the partition id (sorted in LDS)
+    int ablate;                  // profiling only (env SA_ABLATE): 1 skip sort, 2 skip record scatter, 4 skip lists
     const uint8_t *tagtab;
     const uint64_t *occ_off;
     uint32_t n_reads, npr;
     uint32_t *md_list, *ed_list;
     uint4 *rec;                  // [n_occ] by g
     uint32_t *big_list, *big_n;
-    unsigned long long *counts;  // [2]: buckets, groups
+    unsigned long long *counts;  // [2][NSHARD]: buckets, groups
     // strict
     uint32_t *md_idx, *ed_idx;   // parallel to lists
     uint4 *srec;                 // [n_occ] by g
@@ -166,8 +175,10 @@ hipError_t launch_records_from_tables(const uint64_t *sk, const uint32_t *sv, ui
                                       uint32_t *bkt_nst, uint32_t *bkt_nmd, uint32_t *bkt_first, uint8_t *is_head,
                                       hipStream_t s);
 
+// compact the NSHARD output regions into sort keys (vals = region-space index)
 hipError_t launch_make_order_keys(const uint32_t *fst, const uint32_t *snd, const uint64_t *rank,
-                                  uint64_t n, int by_rank, int idbits, uint64_t *keys, uint32_t *vals,
+                                  const unsigned long long *cursor, unsigned long long cap_s, int by_rank,
+                                  int idbits, uint64_t *keys, uint32_t *vals, uint32_t *shard_off,
                                   hipStream_t s);
 hipError_t launch_gather_pairs(const uint32_t *perm, uint64_t n, const uint32_t *fst, const uint32_t *snd,
                                const uint32_t *cnt, int32_t *lead, int32_t *trail, int32_t *count,
