@@ -82,7 +82,7 @@ struct sa_ctx {
     std::vector<uint64_t> woff, occ_off;
     std::vector<uint32_t> lbase, lrank;
     std::vector<uint8_t> tagtab;
-    int lb = 1, m = 0, maxd = 0, maxL = 0;
+    int lb = 1, m = 0, maxd = 0, maxL = 0, minL = 0;
     uint32_t uniform_npr = 0;
     uint64_t n_occ = 0, n_words = 0;
     uint32_t max_occ = 0;
@@ -101,6 +101,7 @@ struct sa_ctx {
     uint64_t n_disp = 0;
     // options / state
     bool keep_pairs = false, timing = false;
+    int align_kernel = 0;  // SA_OPT_ALIGN_KERNEL
     int ablate = 0;  // profiling only: SA_ABLATE env (results are wrong when set)
     bool built = false, aligned = false;
     // results (host)
@@ -216,6 +217,7 @@ int prepare_reads(sa_ctx *c) {
     c->woff[0] = 0;
     c->occ_off[0] = 0;
     c->maxL = 0;
+    c->minL = n ? INT32_MAX : 0;
     c->max_occ = 0;
     std::vector<char> has_d;
     int maxd = -1;
@@ -227,6 +229,7 @@ int prepare_reads(sa_ctx *c) {
         const int32_t L = (int32_t)L64;
         c->len[r] = L;
         c->maxL = std::max(c->maxL, L);
+        c->minL = std::min(c->minL, L);
         c->woff[r + 1] = c->woff[r] + (uint64_t)((L + 15) / 16);
         const int32_t nk = L - k + 1 > 0 ? L - k + 1 : 0;
         c->occ_off[r + 1] = c->occ_off[r] + (uint64_t)nk;
@@ -731,6 +734,17 @@ int device_align(sa_ctx *c, bool readback) {
     const int G = wmax <= 15 ? 16 : (wmax <= 31 ? 32 : 64);
     const uint32_t rw_fit = (160u * 1024u / (256u * 4u) - 1u) | 1u;
     const uint32_t rw = std::min<uint32_t>((uint32_t)((c->maxL + 1 + 15) / 16) | 1u, rw_fit);
+    // both kernels hold the cost matrix as int8 bytes (HOXD70 spans -125..100)
+    for (int x = 0; x < 16; ++x)
+        if (c->set.cost[x] < -128 || c->set.cost[x] > 127)
+            return fail(c, SA_E_ARG, "cost matrix entries must lie in [-128, 127]");
+    // lane-per-pair kernel: band <= 15 columns, reads <= 30,000 bp (c << 16 | e packing)
+    const bool lane_fits = wmax <= 15 && c->maxL <= 30000;
+    if (c->align_kernel == 2 && !lane_fits)
+        return fail(c, SA_E_ARG, "SA_OPT_ALIGN_KERNEL=2 but a band or read exceeds the lane kernel");
+    const bool use_lane = c->align_kernel == 2 || (c->align_kernel == 0 && lane_fits);
+    const int32_t wmin = std::max(c->set.kmer_size, (int32_t)floor((double)((float)c->minL * omm)) + 1);
+    const bool exact = wmin == 15 && wmax == 15;  // every band exactly 16 cells wide
     AlignParams P;
     P.k = c->set.kmer_size;
     P.gap_open = c->set.gap_open;
@@ -748,8 +762,12 @@ int device_align(sa_ctx *c, bool readback) {
     HIPCHK(hipMemsetAsync(cnt->cells, 0, sizeof(cnt->cells), c->stream));
     {
         StageScope st(c, SA_STAGE_ALIGN);
-        HIPCHK(launch_dovetail(dev_reads(c), (const int32_t *)c->d_lead.p, (const int32_t *)c->d_trail.p, nd, P, G,
-                               out, &cnt->err, cnt->cells, c->stream));
+        if (use_lane)
+            HIPCHK(launch_dovetail_lane(dev_reads(c), (const int32_t *)c->d_lead.p, (const int32_t *)c->d_trail.p, nd,
+                                        P, exact, out, &cnt->err, cnt->cells, c->stream));
+        else
+            HIPCHK(launch_dovetail(dev_reads(c), (const int32_t *)c->d_lead.p, (const int32_t *)c->d_trail.p, nd, P,
+                                   G, out, &cnt->err, cnt->cells, c->stream));
     }
     int32_t err = 0;
     unsigned long long cells_s[NSHARD];
@@ -966,6 +984,10 @@ int sa_set_option(sa_ctx *c, int option, int64_t value) {
     switch (option) {
     case SA_OPT_KEEP_PAIRS: c->keep_pairs = value != 0; return SA_OK;
     case SA_OPT_TIMING: c->timing = value != 0; return SA_OK;
+    case SA_OPT_ALIGN_KERNEL:
+        if (value < 0 || value > 2) return fail(c, SA_E_ARG, "SA_OPT_ALIGN_KERNEL must be 0, 1 or 2");
+        c->align_kernel = (int)value;
+        return SA_OK;
     default: return fail(c, SA_E_ARG, "unknown option");
     }
 }

@@ -187,5 +187,9 @@ hipError_t launch_gather_pairs(const uint32_t *perm, uint64_t n, const uint32_t 
 hipError_t launch_dovetail(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
                            const AlignParams &p, int group_lanes, DevAlignment *out, int32_t *err,
                            unsigned long long *cells, hipStream_t s);
+// one pair per lane, w <= 15, |A| <= 30000 (dovetail_lane.hip); exact: w == 15 for every pair
+hipError_t launch_dovetail_lane(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
+                                const AlignParams &p, bool exact, DevAlignment *out, int32_t *err, unsigned long long *cells,
+                                hipStream_t s);
 
 }  // namespace sa

@@ -22,7 +22,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "build", "libsa_overlap.so")
 
 SA_IDS_AUTO, SA_IDS_STRICT, SA_IDS_WIDE = 0, 1, 2
-SA_OPT_KEEP_PAIRS, SA_OPT_TIMING = 1, 2
+SA_OPT_KEEP_PAIRS, SA_OPT_TIMING, SA_OPT_ALIGN_KERNEL = 1, 2, 3
+ALIGN_AUTO, ALIGN_GROUP, ALIGN_LANE = 0, 1, 2
 STAGES = ("pack", "emit", "sort", "buckets", "pairs", "order", "align")
 ERRORS = {-1: "SA_E_ARG", -2: "SA_E_INPUT", -3: "SA_E_NON_ACGT", -4: "SA_E_ID_RANGE", -5: "SA_E_SHORT_READ",
           -6: "SA_E_DEGENERATE", -7: "SA_E_HIP", -8: "SA_E_NOMEM", -9: "SA_E_RCCL", -10: "SA_E_STATE",
@@ -125,7 +126,7 @@ def _arr(ptr, n):
 class Overlapper:
     """One context = one AlignSettings + one KmerTable on one GPU."""
 
-    def __init__(self, device=0, timing=False, keep_pairs=False, **kw):
+    def __init__(self, device=0, timing=False, keep_pairs=False, align_kernel=ALIGN_AUTO, **kw):
         self.s = settings(**kw)
         h = C.c_void_p()
         rc = lib().sa_ctx_create(C.byref(self.s), device, C.byref(h))
@@ -136,6 +137,8 @@ class Overlapper:
             self._chk(lib().sa_set_option(h, SA_OPT_TIMING, 1))
         if keep_pairs:
             self._chk(lib().sa_set_option(h, SA_OPT_KEEP_PAIRS, 1))
+        if align_kernel != ALIGN_AUTO:
+            self._chk(lib().sa_set_option(h, SA_OPT_ALIGN_KERNEL, align_kernel))
 
     def close(self):
         if getattr(self, "h", None):

@@ -144,6 +144,55 @@ def test_mutated_reads_with_indels(oracle_mod, gaps):
         compare_with_oracle(oracle_mod, ov, r, wide)
 
 
+def mutate(reads, rng, max_ops):
+    out = []
+    for rd in reads:
+        s = list(rd)
+        for _ in range(int(rng.integers(0, max_ops + 1))):
+            p = int(rng.integers(0, len(s)))
+            op = int(rng.integers(0, 3))
+            if op == 0:
+                s[p] = "ACGT"[int(rng.integers(0, 4))]
+            elif op == 1:
+                del s[p]
+            else:
+                s.insert(p, "ACGT"[int(rng.integers(0, 4))])
+        out.append("".join(s))
+    return out
+
+
+@pytest.mark.parametrize("gaps", [(-400, -30, 0.98), (-60, -10, 0.98), (-35, -1, 0.98)])
+def test_full_width_band_500bp(oracle_mod, gaps):
+    """k = 15 on 500-560 bp reads: every band is exactly 16 cells wide, the
+    bench's shape (the lane kernel's EXACT variant), with substitutions and
+    indels so gap moves, duds and invalid overlaps all occur."""
+    rng = np.random.default_rng(abs(gaps[0]) + abs(gaps[1]))
+    reads = mutate(H.synth_reads(500, 500, 25000, gc=0.5, seed=51), rng, 6)
+    st = dict(kmer_size=15, min_identity=gaps[2], gap_open=gaps[0], gap_extend=gaps[1])
+    r = oracle_mod.Run(reads=reads, settings=oracle_settings(oracle_mod, **st), wide=True)
+    ov = gpu_run(reads=reads, wide=True, **st)
+    assert ov.stats()["dispatched"] > 1000
+    compare_with_oracle(oracle_mod, ov, r, True)
+
+
+@pytest.mark.parametrize("k,L,minid", [(15, 500, 0.98), (12, 150, 0.92), (12, 300, 0.96), (9, 120, 0.9)])
+def test_align_kernels_agree(k, L, minid):
+    """The lane-per-pair kernel and the lane-group kernel give identical
+    alignment tuples on the same dispatch (both are also checked against the
+    oracle elsewhere)."""
+    rng = np.random.default_rng(k * 1000 + L)
+    reads = mutate(H.synth_reads(400, L, 20 * L, gc=0.5, seed=k + L), rng, 5)
+    st = dict(kmer_size=k, min_identity=minid, min_collisions=3, gap_open=-60, gap_extend=-10)
+    res = []
+    for kern in (sao.ALIGN_GROUP, sao.ALIGN_LANE):
+        ov = gpu_run(reads=reads, wide=True, align_kernel=kern, **st)
+        res.append((ov.alignments(), ov.ovl(), ov.stats()["dp_cells"]))
+    assert len(res[0][0]) > 100
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    assert res[0][1] == res[1][1]
+    assert res[0][2] == res[1][2]
+
+
 def test_duplicate_reads_loc_ties(oracle_mod):
     """Identical reads give equal-loc k-mers: the tie rule fst = middle (KmerTable.scala:65-71)."""
     reads = H.synth_reads(60, 100, 700, seed=21)
