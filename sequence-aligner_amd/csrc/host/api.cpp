@@ -96,7 +96,7 @@ struct sa_ctx {
     uint32_t *bkt_rank_dev = nullptr;
     DBuf d_pf, d_ps, d_pc, d_pr, d_ovl, d_cnt;
     DBuf d_okeys, d_ovals, d_okeys2, d_ovals2, d_osort;
-    DBuf d_lead, d_trail, d_count, d_aln;
+    DBuf d_lead, d_trail, d_count, d_aln, d_p1;
     uint64_t pair_cap = 0;
     uint64_t n_disp = 0;
     // options / state
@@ -762,10 +762,21 @@ int device_align(sa_ctx *c, bool readback) {
     HIPCHK(hipMemsetAsync(cnt->cells, 0, sizeof(cnt->cells), c->stream));
     {
         StageScope st(c, SA_STAGE_ALIGN);
-        if (use_lane)
-            HIPCHK(launch_dovetail_lane(dev_reads(c), (const int32_t *)c->d_lead.p, (const int32_t *)c->d_trail.p, nd,
-                                        P, exact, out, &cnt->err, cnt->cells, c->stream));
-        else
+        if (use_lane) {
+            // phase 1, then pairs grouped by phase-2 row count, then phase 2
+            int32_t *p1; uint64_t *k0, *k1; uint32_t *v0, *v1; uint8_t *tmp;
+            ENSURE(c->d_p1, nd, &p1);
+            ENSURE(c->d_okeys, nd, &k0);
+            ENSURE(c->d_okeys2, nd, &k1);
+            ENSURE(c->d_ovals, nd, &v0);
+            ENSURE(c->d_ovals2, nd, &v1);
+            ENSURE(c->d_osort, radix_sort_temp_bytes(nd), &tmp);
+            const int32_t *dl = (const int32_t *)c->d_lead.p, *dt = (const int32_t *)c->d_trail.p;
+            HIPCHK(launch_dovetail_p1(dev_reads(c), dl, dt, nd, P, exact, p1, k0, v0, &cnt->err, cnt->cells,
+                                      c->stream));
+            HIPCHK(radix_sort(&k0, &v0, &k1, &v1, nd, 0, bits_for((uint64_t)c->maxL), tmp, c->stream));
+            HIPCHK(launch_dovetail_p2(dev_reads(c), dl, dt, nd, P, exact, p1, v0, out, &cnt->err, c->stream));
+        } else
             HIPCHK(launch_dovetail(dev_reads(c), (const int32_t *)c->d_lead.p, (const int32_t *)c->d_trail.p, nd, P,
                                    G, out, &cnt->err, cnt->cells, c->stream));
     }
@@ -861,7 +872,7 @@ void sa_ctx_destroy(sa_ctx *c) {
                     &c->d_gmds, &c->d_gede, &c->d_ogid, &c->d_bkttmp, &c->d_mdidx, &c->d_edidx, &c->d_occidx,
                     &c->d_bnst, &c->d_brank, &c->d_bhash, &c->d_bfirst, &c->d_pf, &c->d_ps, &c->d_pc, &c->d_pr,
                     &c->d_ovl, &c->d_cnt, &c->d_okeys, &c->d_ovals, &c->d_okeys2, &c->d_ovals2, &c->d_osort,
-                    &c->d_lead, &c->d_trail, &c->d_count, &c->d_aln, &c->d_pstart, &c->d_biglist, &c->d_rec,
+                    &c->d_lead, &c->d_trail, &c->d_count, &c->d_aln, &c->d_p1, &c->d_pstart, &c->d_biglist, &c->d_rec,
                     &c->d_srec, &c->d_bnmd, &c->d_ishead, &c->d_bnst2};
     for (DBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);

@@ -35,20 +35,29 @@ __device__ __forceinline__ uint32_t code_of(const uint32_t *w, int32_t p) {
 
 __device__ __forceinline__ void set_err(int32_t *err, int32_t code) { atomicCAS(err, 0, code); }
 
+// Phase-2 lane state: the band row in registers plus the A / B read windows.
+struct Band {
+    uint32_t b8[LW];                            // 8 * B[k - zr + u - 1] for the current row u (0 outside B)
+    int32_t Tk[LW], Qk[LW], Pk[LW], Ck[LW];     // max(T,0), max(Q,0), stop cell (u << 6 | k), (c << 16 | e)
+    int32_t best, bpos, bstop, bce;             // first row-major argmax and its path summary
+    int32_t ap, bp;                             // A position of the next row; B position entering column LW-1
+    uint32_t awd, bw;                           // packed words holding A[ap], B[bp]
+};
+
 // One phase-2 cell (u, k) of the band (BioLibs.scala:725-764) plus the forward
 // summary of the greedy backtrack out of it (:768-809): stop cell and
 // (matches << 16 | errors).  MASKED rows test 1 <= j <= |B| per cell; EXACT
 // launches have w == LW - 1 for every pair (no per-lane column tests).
+// Q = max(max(M, X) + gO, Y) is kept clamped at 0: the next row's Y is gE + Q.
 template <bool MASKED, bool EXACT>
-__device__ __forceinline__ void band_cell(const int k, const int32_t u6, const int32_t jb, const int32_t LB,
-                                          const int32_t w, const uint32_t cp, const uint32_t a8, const int32_t gO,
-                                          const int32_t gE, const uint32_t (&b8)[LW], int32_t (&Tk)[LW],
-                                          int32_t (&Qk)[LW], int32_t (&Pk)[LW], int32_t (&Ck)[LW], int32_t &Zl,
-                                          int32_t &Xl, int32_t &Pl, int32_t &Cl, int32_t &best, int32_t &bpos,
-                                          int32_t &bstop, int32_t &bce) {
+__device__ __forceinline__ void band_cell(Band &S, const int k, const int32_t u6, const int32_t jb, const int32_t LB,
+                                          const int32_t w, const uint32_t cp, const uint32_t eqsh, const int32_t gO,
+                                          const int32_t gE, const bool act, int32_t &Zl, int32_t &Xl, int32_t &Pl,
+                                          int32_t &Cl) {
     const bool last = EXACT ? (k == LW - 1) : (k == LW - 1 || k == w);  // Y = 0 at k == width
-    int32_t M = bfe_s8(cp, b8[k]) + Tk[k];
-    int32_t Y = last ? 0 : gE + max(Qk[k < LW - 1 ? k + 1 : k], 0);
+    const int kn = k < LW - 1 ? k + 1 : k;
+    int32_t M = bfe_s8(cp, S.b8[k]) + S.Tk[k];
+    int32_t Y = last ? 0 : gE + S.Qk[kn];
     int32_t X = k == 0 ? 0 : gE + max(max(Zl, Xl), 0);
     if (MASKED) {
         const bool valid = (uint32_t)(jb + k) < (uint32_t)LB;
@@ -58,64 +67,118 @@ __device__ __forceinline__ void band_cell(const int k, const int32_t u6, const i
     }
     const int32_t T = max(max(M, X), Y);
     const bool isM = M == T, isX = X == T, pos = T > 0;
-    const int32_t Pu = k == LW - 1 ? 0 : Pk[k < LW - 1 ? k + 1 : k];
-    const int32_t Cu = k == LW - 1 ? 0 : Ck[k < LW - 1 ? k + 1 : k];
+    const int32_t Pu = k == LW - 1 ? 0 : S.Pk[kn];
+    const int32_t Cu = k == LW - 1 ? 0 : S.Ck[kn];
     const int32_t pxy = isX ? Pl : Pu;
     const int32_t cxy = (isX ? Cl : Cu) + 1;
-    const int32_t cm = Ck[k] + (b8[k] == a8 ? 0x10000 : 1);
+    // + (1 << 16) on a match, + 1 on a mismatch: byte b of eqsh is 16 iff b == A[i-1]
+    const int32_t cm = (int32_t)((1u << __builtin_amdgcn_ubfe(eqsh, S.b8[k], 8)) + (uint32_t)S.Ck[k]);
     const int32_t self = u6 | k;
-    const int32_t pn = pos ? (isM ? Pk[k] : pxy) : self;
+    const int32_t pn = pos ? (isM ? S.Pk[k] : pxy) : self;
     const int32_t cn = pos ? (isM ? cm : cxy) : 0;
-    Tk[k] = max(T, 0);
-    Qk[k] = max(max(M, X) + gO, Y);
-    Pk[k] = pn;
-    Ck[k] = cn;
-    const bool nb = T > best && (EXACT || k <= w);
-    best = nb ? T : best;
-    bpos = nb ? self : bpos;
-    bstop = nb ? pn : bstop;
-    bce = nb ? cn : bce;
+    S.Tk[k] = max(T, 0);
+    S.Qk[k] = max(max(max(M, X) + gO, Y), 0);
+    S.Pk[k] = pn;
+    S.Ck[k] = cn;
+    const bool nb = T > S.best && act && (EXACT || k <= w);
+    S.best = nb ? T : S.best;
+    S.bpos = nb ? self : S.bpos;
+    S.bstop = nb ? pn : S.bstop;
+    S.bce = nb ? cn : S.bce;
     Zl = max(M, Y) + gO;
     Xl = X;
     Pl = pn;
     Cl = cn;
 }
 
-}  // namespace
+// One phase-2 row u, then advance the A / B windows one base.  Branch-free:
+// lanes past their last row (u > rows2) keep computing but no longer update the
+// argmax, and the window loads are unconditional (clamped to the read).
+template <bool MASKED, bool EXACT>
+__device__ __forceinline__ void band_row(Band &S, const int32_t u, const int32_t rows2, const int32_t zr,
+                                         const int32_t LB, const int32_t w, const uint32_t (&cpa)[4],
+                                         const int32_t gO, const int32_t gE, const uint32_t *Aw, const int32_t awl,
+                                         const uint32_t *Bw, const int32_t bwl) {
+    const uint32_t a8 = ((S.awd >> (30 - 2 * (S.ap & 15))) & 3u) << 3;
+    const uint32_t c01 = (a8 & 8) ? cpa[1] : cpa[0], c23 = (a8 & 8) ? cpa[3] : cpa[2];
+    const uint32_t cp = (a8 & 16) ? c23 : c01;
+    const uint32_t eqsh = 16u << a8;
+    const int32_t u6 = u << 6;
+    const int32_t jb = u - zr - 1;  // j - 1 of column 0
+    const bool act = u <= rows2;
+    int32_t Zl = 0, Xl = 0, Pl = 0, Cl = 0;
+#pragma unroll
+    for (int k = 0; k < LW; ++k) band_cell<MASKED, EXACT>(S, k, u6, jb, LB, w, cp, eqsh, gO, gE, act, Zl, Xl, Pl, Cl);
+    ++S.ap;
+    S.awd = Aw[min(S.ap >> 4, awl)];
+#pragma unroll
+    for (int k = 0; k < LW - 1; ++k) S.b8[k] = S.b8[k + 1];
+    S.b8[LW - 1] = S.bp < LB ? ((S.bw >> (30 - 2 * (S.bp & 15))) & 3u) << 3 : 0u;
+    ++S.bp;
+    S.bw = Bw[min(S.bp >> 4, bwl)];
+}
+
+// Pair setup shared by both phases: ids, lengths, band width, input checks.
+struct LanePair {
+    int32_t a, b, LA, LB, w, status;
+    const uint32_t *Aw, *Bw;
+};
 
 template <bool EXACT>
-__global__ __launch_bounds__(256) void dovetail_lane_kernel(DevReads rd, const int32_t *lead, const int32_t *trail,
-                                                            uint64_t npairs, AlignParams P, DevAlignment *out,
-                                                            int32_t *err, unsigned long long *cells_total) {
+__device__ __forceinline__ LanePair lane_pair(const DevReads &rd, const int32_t *lead, const int32_t *trail,
+                                              uint64_t pair, const AlignParams &P) {
+    LanePair q;
+    q.a = lead[pair] - 1;
+    q.b = trail[pair] - 1;
+    q.LA = rd.len[q.a];
+    q.LB = rd.len[q.b];
+    q.Aw = rd.codes + rd.woff[q.a];
+    q.Bw = rd.codes + rd.woff[q.b];
+    // width = max(k, floor(|A| * (1 - minId)).toInt + 1)   (BioLibs.scala:619-620)
+    const float prod = (float)q.LA * P.one_minus_minid;
+    q.w = max(P.k, (int32_t)floorf(prod) + 1);
+    q.status = 0;
+    if (q.w > LW - 1 || (EXACT && q.w != LW - 1) || q.LA > 30000) q.status = -11;  // (c << 16 | e) packing
+    else if (q.LB < q.w) q.status = -5;
+    else if (rd.bad[q.a] < q.LA || rd.bad[q.b] < q.w) q.status = -3;
+    return q;
+}
+
+__device__ __forceinline__ void add_cells(unsigned long long cells, unsigned long long *cells_total) {
+    // block-reduced, one sharded atomic per block
+    __shared__ unsigned long long cell_sum;
+    if (threadIdx.x == 0) cell_sum = 0;
+    __syncthreads();
+    if (cells) atomicAdd(&cell_sum, cells);
+    __syncthreads();
+    if (threadIdx.x == 0 && cell_sum) atomicAdd(&cells_total[blockIdx.x % NSHARD], cell_sum);
+}
+
+}  // namespace
+
+// Phase 1 (BioLibs.scala:644-689): per pair the start row ds of the phase-1
+// backtrack and the dud test.  p1[pair] = (ds << 1 | dud) or a negative error;
+// rows2[pair] = phase-2 row count (0 when phase 2 does not run) -- the key the
+// host sorts by so each wave of the phase-2 kernel gets pairs of similar length.
+template <bool EXACT>
+__global__ __launch_bounds__(256) void dovetail_p1_kernel(DevReads rd, const int32_t *lead, const int32_t *trail,
+                                                          uint64_t npairs, AlignParams P, int32_t *p1,
+                                                          uint64_t *rows2_key, uint32_t *order, int32_t *err,
+                                                          unsigned long long *cells_total) {
     const uint64_t pair = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool have = pair < npairs;
     const int32_t gO = P.gap_open, gE = P.gap_extend;
-
-    int32_t a = 0, b = 0, LA = 0, LB = 0, w = 0;
-    const uint32_t *Aw = rd.codes, *Bw = rd.codes;
-    int32_t status = have ? 0 : -100;  // 0 ok, 1 dud, < 0 error / no pair
+    LanePair q{0, 0, 0, 0, 0, -100, rd.codes, rd.codes};
     if (have) {
-        a = lead[pair] - 1;
-        b = trail[pair] - 1;
-        LA = rd.len[a];
-        LB = rd.len[b];
-        Aw = rd.codes + rd.woff[a];
-        Bw = rd.codes + rd.woff[b];
-        // width = max(k, floor(|A| * (1 - minId)).toInt + 1)   (BioLibs.scala:619-620)
-        const float prod = (float)LA * P.one_minus_minid;
-        w = max(P.k, (int32_t)floorf(prod) + 1);
-        if (w > LW - 1 || (EXACT && w != LW - 1) || LA > 30000) status = -11;  // (c << 16 | e) packing
-        else if (LB < w) status = -5;
-        else if (rd.bad[a] < LA || rd.bad[b] < w) status = -3;
-        if (status < 0) set_err(err, status);
+        q = lane_pair<EXACT>(rd, lead, trail, pair, P);
+        if (q.status < 0) set_err(err, q.status);
     }
-
-    // ---------------- phase 1: A vs B[0 .. w)   (BioLibs.scala:644-668) ------
+    const int32_t w = q.w;
     // column j (1..w) costs for A base x = 0..3 against B[j-1], as int8 bytes
     uint32_t cb[LW - 1];
 #pragma unroll
     for (int j = 1; j < LW; ++j) {
-        const uint32_t bj = (status == 0 && j <= w) ? code_of(Bw, j - 1) : 0u;
+        const uint32_t bj = (q.status == 0 && j <= w) ? code_of(q.Bw, j - 1) : 0u;
         uint32_t v = 0;
 #pragma unroll
         for (int x = 0; x < 4; ++x) v |= ((uint32_t)(uint8_t)(int8_t)P.cost[x * 4 + bj]) << (8 * x);
@@ -127,14 +190,14 @@ __global__ __launch_bounds__(256) void dovetail_lane_kernel(DevReads rd, const i
 #pragma unroll
     for (int j = 0; j < LW - 1; ++j) { Tc[j] = 0; Q[j] = Q0; O[j] = 1; }  // origin (row 0, col != 0)
     int32_t best = 0, borg = 0;
-    const int32_t rows1 = status == 0 ? LA : 0;
+    const int32_t rows1 = q.status == 0 ? q.LA : 0;
     int32_t rmax = rows1;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) rmax = max(rmax, __shfl_xor(rmax, off, 64));
     rmax = __builtin_amdgcn_readfirstlane(rmax);  // wave-uniform loop bound
     uint32_t aw = 0;
     for (int32_t i = 1; i <= rmax; ++i) {
-        if (((i - 1) & 15) == 0) aw = (i <= rows1) ? Aw[(i - 1) >> 4] : 0u;
+        if (((i - 1) & 15) == 0) aw = (i <= rows1) ? q.Aw[(i - 1) >> 4] : 0u;
         if (i > rows1) continue;
         const uint32_t a8 = ((aw >> (30 - 2 * ((i - 1) & 15))) & 3u) << 3;
         // origin = (stop row << 1) | (stop col != 0); column 0 cells stop with col 0
@@ -144,7 +207,7 @@ __global__ __launch_bounds__(256) void dovetail_lane_kernel(DevReads rd, const i
 #pragma unroll
         for (int j = 0; j < LW - 1; ++j) {
             const int32_t M = bfe_s8(cb[j], a8) + Tdiag;
-            const int32_t Y = gE + max(Q[j], 0);
+            const int32_t Y = gE + Q[j];
             const int32_t X = gE + max(max(Zl, Xl), 0);
             const int32_t T = max(max(M, X), Y);
             const int32_t Oup = O[j];
@@ -152,7 +215,7 @@ __global__ __launch_bounds__(256) void dovetail_lane_kernel(DevReads rd, const i
             Tdiag = Tc[j];
             Odiag = Oup;
             Tc[j] = max(T, 0);
-            Q[j] = max(max(M, X) + gO, Y);
+            Q[j] = max(max(max(M, X) + gO, Y), 0);  // clamped: next row's Y = gE + Q
             O[j] = on;
             // first strict '>' in row-major order; columns > w never win
             const bool nb = T > best && (EXACT || j < w);
@@ -163,27 +226,57 @@ __global__ __launch_bounds__(256) void dovetail_lane_kernel(DevReads rd, const i
             Ol = on;
         }
     }
-    int32_t ds = 0;
-    const bool p1ok = status == 0;
-    if (status == 0) {
-        if (best <= 0) { status = -6; set_err(err, -6); }  // reference walks off (0,0)
-        else { ds = borg >> 1; status = (borg & 1) ? 1 : 0; }
+    unsigned long long cells = 0;
+    if (have) {
+        int32_t r = q.status, rows2 = 0;
+        if (r == 0) {
+            cells = (unsigned long long)q.LA * w;
+            if (best <= 0) { r = -6; set_err(err, -6); }  // the reference walks off (0,0)
+            else {
+                r = borg;  // (ds << 1) | dud
+                if (!(borg & 1)) {
+                    const int32_t ds = borg >> 1, zr = w / 2, dL = q.LA - ds;
+                    cells += (unsigned long long)(dL + 1) * (w + 1);
+                    // every B base touched by phase 2 must be ACGT (MatchError otherwise)
+                    const int32_t touched = max(w, min(q.LB, dL - zr + w));
+                    if (rd.bad[q.b] < touched) { r = -3; set_err(err, -3); }
+                    else rows2 = dL;
+                }
+            }
+        }
+        p1[pair] = r;
+        rows2_key[pair] = (uint64_t)rows2;
+        order[pair] = (uint32_t)pair;
     }
+    add_cells(cells, cells_total);
+}
 
-    // ---------------- phase 2: band (u, k), i = u + ds, j = k - zr + u (:696-764)
-    const int32_t st1 = status;
-    const int32_t zr = w / 2;
-    const int32_t dL = LA - ds;
-    if (status == 0) {
-        // every B base touched by phase 2 must be ACGT (MatchError otherwise)
-        const int32_t touched = max(w, min(LB, dL - zr + w));
-        if (rd.bad[b] < touched) { status = -3; set_err(err, -3); }
+// Phase 2 (BioLibs.scala:691-819) + Alignment/Overlap validity, one pair per
+// lane, pairs taken in the order `order` (grouped by phase-2 row count).
+template <bool EXACT>
+__global__ __launch_bounds__(256) void dovetail_p2_kernel(DevReads rd, const int32_t *lead, const int32_t *trail,
+                                                          uint64_t npairs, AlignParams P, const int32_t *p1,
+                                                          const uint32_t *order, DevAlignment *out, int32_t *err) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool have = t < npairs;
+    const uint64_t pair = have ? order[t] : 0;
+    const int32_t gO = P.gap_open, gE = P.gap_extend;
+    LanePair q{0, 0, 0, 0, 0, -100, rd.codes, rd.codes};
+    int32_t r1 = -100;
+    if (have) {
+        q = lane_pair<EXACT>(rd, lead, trail, pair, P);
+        r1 = p1[pair];
     }
-    const bool p2 = status == 0;
+    const int32_t w = q.w;
+    const bool p2 = r1 >= 0 && !(r1 & 1);
+    const int32_t ds = r1 >= 0 ? r1 >> 1 : 0;
+    const int32_t zr = w / 2;
+    const int32_t dL = q.LA - ds;
+    const int32_t LB = q.LB;
     const int32_t rows2 = p2 ? dL : 0;
     // rows where every cell k <= w is inside B (1 <= j <= LB) run without masks
     int32_t lo = p2 ? zr + 1 : 0, hi = p2 ? LB + zr - w : 0x7fffffff;
-    rmax = rows2;
+    int32_t rmax = rows2;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         rmax = max(rmax, __shfl_xor(rmax, off, 64));
@@ -193,77 +286,41 @@ __global__ __launch_bounds__(256) void dovetail_lane_kernel(DevReads rd, const i
     rmax = __builtin_amdgcn_readfirstlane(rmax);
     lo = __builtin_amdgcn_readfirstlane(lo);
     hi = __builtin_amdgcn_readfirstlane(hi);
-    const uint32_t cpa[4] = {
-        (uint32_t)(uint8_t)(int8_t)P.cost[0] | ((uint32_t)(uint8_t)(int8_t)P.cost[1] << 8) |
-            ((uint32_t)(uint8_t)(int8_t)P.cost[2] << 16) | ((uint32_t)(uint8_t)(int8_t)P.cost[3] << 24),
-        (uint32_t)(uint8_t)(int8_t)P.cost[4] | ((uint32_t)(uint8_t)(int8_t)P.cost[5] << 8) |
-            ((uint32_t)(uint8_t)(int8_t)P.cost[6] << 16) | ((uint32_t)(uint8_t)(int8_t)P.cost[7] << 24),
-        (uint32_t)(uint8_t)(int8_t)P.cost[8] | ((uint32_t)(uint8_t)(int8_t)P.cost[9] << 8) |
-            ((uint32_t)(uint8_t)(int8_t)P.cost[10] << 16) | ((uint32_t)(uint8_t)(int8_t)P.cost[11] << 24),
-        (uint32_t)(uint8_t)(int8_t)P.cost[12] | ((uint32_t)(uint8_t)(int8_t)P.cost[13] << 8) |
-            ((uint32_t)(uint8_t)(int8_t)P.cost[14] << 16) | ((uint32_t)(uint8_t)(int8_t)P.cost[15] << 24)};
-    // b8[k] = 8 * B[k - zr + u - 1] for the current row u (0 outside B)
-    uint32_t b8[LW];
+    uint32_t cpa[4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+        cpa[x] = (uint32_t)(uint8_t)(int8_t)P.cost[x * 4] | ((uint32_t)(uint8_t)(int8_t)P.cost[x * 4 + 1] << 8) |
+                 ((uint32_t)(uint8_t)(int8_t)P.cost[x * 4 + 2] << 16) |
+                 ((uint32_t)(uint8_t)(int8_t)P.cost[x * 4 + 3] << 24);
+    Band S;
 #pragma unroll
     for (int k = 0; k < LW; ++k) {
         const int32_t p = k - zr;
-        b8[k] = (p2 && p >= 0 && p < LB) ? code_of(Bw, p) << 3 : 0u;
+        S.b8[k] = (p2 && p >= 0 && p < LB) ? code_of(q.Bw, p) << 3 : 0u;
     }
-    int32_t Tk[LW], Qk[LW], Pk[LW], Ck[LW];  // clamped max, Q, stop cell (u << 6 | k), (c << 16 | e)
+    const int32_t Q0 = max(gO, 0);
 #pragma unroll
-    for (int k = 0; k < LW; ++k) { Tk[k] = 0; Qk[k] = Q0; Pk[k] = k; Ck[k] = 0; }
-    int32_t best2 = 0, bpos = 0, bstop = 0, bce = 0;
-    int32_t bp = LW - zr;           // B position entering column LW-1 at the next row
-    uint32_t bw = (p2 && bp < LB) ? Bw[bp >> 4] : 0u;
-    int32_t ap = ds;                 // A position of row u + 1
-    uint32_t awd = p2 ? Aw[ap >> 4] : 0u;
-    for (int32_t u = 1; u <= rmax; ++u) {
-        if (u > rows2) continue;
-        const uint32_t a8 = ((awd >> (30 - 2 * (ap & 15))) & 3u) << 3;
-        const uint32_t c01 = (a8 & 8) ? cpa[1] : cpa[0], c23 = (a8 & 8) ? cpa[3] : cpa[2];
-        const uint32_t cp = (a8 & 16) ? c23 : c01;
-        const int32_t u6 = u << 6;
-        int32_t Zl = 0, Xl = 0, Pl = 0, Cl = 0;
-        if (u >= lo && u <= hi) {
-#pragma unroll
-            for (int k = 0; k < LW; ++k)
-                band_cell<false, EXACT>(k, u6, 0, LB, w, cp, a8, gO, gE, b8, Tk, Qk, Pk, Ck, Zl, Xl, Pl, Cl, best2,
-                                        bpos, bstop, bce);
-        } else {
-            const int32_t jb = u - zr - 1;  // j - 1 of column 0
-#pragma unroll
-            for (int k = 0; k < LW; ++k)
-                band_cell<true, EXACT>(k, u6, jb, LB, w, cp, a8, gO, gE, b8, Tk, Qk, Pk, Ck, Zl, Xl, Pl, Cl, best2,
-                                       bpos, bstop, bce);
-        }
-        // advance the A and B windows one base
-        ++ap;
-        if ((ap & 15) == 0 && u < rows2) awd = Aw[ap >> 4];
-#pragma unroll
-        for (int k = 0; k < LW - 1; ++k) b8[k] = b8[k + 1];
-        b8[LW - 1] = bp < LB ? ((bw >> (30 - 2 * (bp & 15))) & 3u) << 3 : 0u;
-        ++bp;
-        if ((bp & 15) == 0 && bp < LB) bw = Bw[bp >> 4];
-    }
-
-    // DP cells for statistics (same count as dovetail.hip): block-reduced, sharded
-    {
-        __shared__ unsigned long long cell_sum;
-        if (threadIdx.x == 0) cell_sum = 0;
-        __syncthreads();
-        if (p1ok) {
-            unsigned long long cells = (unsigned long long)LA * w;
-            if (st1 == 0) cells += (unsigned long long)(dL + 1) * (w + 1);
-            atomicAdd(&cell_sum, cells);
-        }
-        __syncthreads();
-        if (threadIdx.x == 0 && cell_sum) atomicAdd(&cells_total[blockIdx.x % NSHARD], cell_sum);
-    }
+    for (int k = 0; k < LW; ++k) { S.Tk[k] = 0; S.Qk[k] = Q0; S.Pk[k] = k; S.Ck[k] = 0; }
+    S.best = 0; S.bpos = 0; S.bstop = 0; S.bce = 0;
+    S.bp = LW - zr;
+    S.bw = (p2 && S.bp < LB) ? q.Bw[S.bp >> 4] : 0u;
+    S.ap = ds;
+    S.awd = p2 ? q.Aw[S.ap >> 4] : 0u;
+    // rows [lo, hi] run unmasked; the first zr rows and the rows past the end
+    // of some lane's B test every cell (separate loops keep each body one block)
+    const int32_t awl = max((q.LA + 15) / 16 - 1, 0), bwl = max((LB + 15) / 16 - 1, 0);
+    int32_t u = 1;
+    const int32_t e1 = min(lo - 1, rmax), e2 = min(hi, rmax);
+    for (; u <= e1; ++u) band_row<true, EXACT>(S, u, rows2, zr, LB, w, cpa, gO, gE, q.Aw, awl, q.Bw, bwl);
+    for (; u <= e2; ++u) band_row<false, EXACT>(S, u, rows2, zr, LB, w, cpa, gO, gE, q.Aw, awl, q.Bw, bwl);
+    for (; u <= rmax; ++u) band_row<true, EXACT>(S, u, rows2, zr, LB, w, cpa, gO, gE, q.Aw, awl, q.Bw, bwl);
+    const int32_t best2 = S.best, bpos = S.bpos, bstop = S.bstop, bce = S.bce;
     if (!have) return;
+    int32_t status = r1 < 0 ? r1 : (r1 & 1);
     if (p2 && best2 <= 0) { status = -6; set_err(err, -6); }
 
     DevAlignment o;
-    o.lead = a + 1; o.trail = b + 1;
+    o.lead = q.a + 1; o.trail = q.b + 1;
     o.reserved = 0;
     if (status < 0) {
         o.start_i = o.start_j = o.end_i = o.end_j = 0; o.correct = 0; o.error = 0;
@@ -279,7 +336,7 @@ __global__ __launch_bounds__(256) void dovetail_lane_kernel(DevReads rd, const i
         si = su + ds; sj = sk - zr + su;
         ei = eu + ds; ej = ek - zr + eu;
         c = bce >> 16; e = bce & 0xFFFF;
-        la = LA; lb = LB;
+        la = q.LA; lb = LB;
         alen = c + e;
     }
     // Alignment.valid / Overlap.valid (ObjectStore.scala:99-141)
@@ -295,15 +352,29 @@ __global__ __launch_bounds__(256) void dovetail_lane_kernel(DevReads rd, const i
     out[pair] = o;
 }
 
-hipError_t launch_dovetail_lane(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
-                                const AlignParams &p, bool exact, DevAlignment *out, int32_t *err,
-                                unsigned long long *cells, hipStream_t s) {
+hipError_t launch_dovetail_p1(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
+                              const AlignParams &p, bool exact, int32_t *p1, uint64_t *rows2_key, uint32_t *order,
+                              int32_t *err, unsigned long long *cells, hipStream_t s) {
     if (!n) return hipSuccess;
     const dim3 grid((uint32_t)((n + 255) / 256));
     if (exact)
-        hipLaunchKernelGGL(dovetail_lane_kernel<true>, grid, dim3(256), 0, s, r, lead, trail, n, p, out, err, cells);
+        hipLaunchKernelGGL(dovetail_p1_kernel<true>, grid, dim3(256), 0, s, r, lead, trail, n, p, p1, rows2_key, order,
+                           err, cells);
     else
-        hipLaunchKernelGGL(dovetail_lane_kernel<false>, grid, dim3(256), 0, s, r, lead, trail, n, p, out, err, cells);
+        hipLaunchKernelGGL(dovetail_p1_kernel<false>, grid, dim3(256), 0, s, r, lead, trail, n, p, p1, rows2_key, order,
+                           err, cells);
+    return hipGetLastError();
+}
+
+hipError_t launch_dovetail_p2(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
+                              const AlignParams &p, bool exact, const int32_t *p1, const uint32_t *order,
+                              DevAlignment *out, int32_t *err, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const dim3 grid((uint32_t)((n + 255) / 256));
+    if (exact)
+        hipLaunchKernelGGL(dovetail_p2_kernel<true>, grid, dim3(256), 0, s, r, lead, trail, n, p, p1, order, out, err);
+    else
+        hipLaunchKernelGGL(dovetail_p2_kernel<false>, grid, dim3(256), 0, s, r, lead, trail, n, p, p1, order, out, err);
     return hipGetLastError();
 }
 

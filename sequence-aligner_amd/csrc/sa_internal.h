@@ -187,9 +187,14 @@ hipError_t launch_gather_pairs(const uint32_t *perm, uint64_t n, const uint32_t 
 hipError_t launch_dovetail(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
                            const AlignParams &p, int group_lanes, DevAlignment *out, int32_t *err,
                            unsigned long long *cells, hipStream_t s);
-// one pair per lane, w <= 15, |A| <= 30000 (dovetail_lane.hip); exact: w == 15 for every pair
-hipError_t launch_dovetail_lane(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
-                                const AlignParams &p, bool exact, DevAlignment *out, int32_t *err, unsigned long long *cells,
-                                hipStream_t s);
+// one pair per lane, w <= 15, |A| <= 30000 (dovetail_lane.hip); exact: w == 15
+// for every pair.  Phase 1 writes p1 / rows2_key / order (identity); the host
+// sorts (rows2_key, order) and phase 2 takes pairs in that order.
+hipError_t launch_dovetail_p1(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
+                              const AlignParams &p, bool exact, int32_t *p1, uint64_t *rows2_key, uint32_t *order,
+                              int32_t *err, unsigned long long *cells, hipStream_t s);
+hipError_t launch_dovetail_p2(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
+                              const AlignParams &p, bool exact, const int32_t *p1, const uint32_t *order,
+                              DevAlignment *out, int32_t *err, hipStream_t s);
 
 }  // namespace sa
