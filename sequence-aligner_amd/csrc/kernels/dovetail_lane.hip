@@ -29,11 +29,13 @@ __device__ __forceinline__ int32_t bfe_s8(uint32_t packed, uint32_t shift) {
     return __builtin_amdgcn_sbfe((int32_t)packed, shift, 8);
 }
 
-__device__ __forceinline__ uint32_t code_of(const uint32_t *w, int32_t p) {
-    return (w[p >> 4] >> (30 - 2 * (p & 15))) & 3u;
-}
-
 __device__ __forceinline__ void set_err(int32_t *err, int32_t code) { atomicCAS(err, 0, code); }
+
+// read-window loads through the global address space (plain pointers held in
+// structs otherwise lower to flat loads, which also count against lgkmcnt)
+__device__ __forceinline__ uint32_t gld(const uint32_t *p, int32_t i) {
+    return ((const __attribute__((address_space(1))) uint32_t *)p)[i];
+}
 
 // Phase-2 lane state: the band row in registers plus the A / B read windows.
 struct Band {
@@ -42,6 +44,7 @@ struct Band {
     int32_t best, bpos, bstop, bce;             // first row-major argmax and its path summary
     int32_t ap, bp;                             // A position of the next row; B position entering column LW-1
     uint32_t awd, bw;                           // packed words holding A[ap], B[bp]
+    uint32_t awn, bwn;                          // the words after them (loaded a row ahead of use)
 };
 
 // One phase-2 cell (u, k) of the band (BioLibs.scala:725-764) plus the forward
@@ -96,11 +99,12 @@ __device__ __forceinline__ void band_cell(Band &S, const int k, const int32_t u6
 // argmax, and the window loads are unconditional (clamped to the read).
 template <bool MASKED, bool EXACT>
 __device__ __forceinline__ void band_row(Band &S, const int32_t u, const int32_t rows2, const int32_t zr,
-                                         const int32_t LB, const int32_t w, const uint32_t (&cpa)[4],
+                                         const int32_t LB, const int32_t w, const uint32_t c0, const uint32_t c1,
+                                         const uint32_t c2, const uint32_t c3,
                                          const int32_t gO, const int32_t gE, const uint32_t *Aw, const int32_t awl,
                                          const uint32_t *Bw, const int32_t bwl) {
     const uint32_t a8 = ((S.awd >> (30 - 2 * (S.ap & 15))) & 3u) << 3;
-    const uint32_t c01 = (a8 & 8) ? cpa[1] : cpa[0], c23 = (a8 & 8) ? cpa[3] : cpa[2];
+    const uint32_t c01 = (a8 & 8) ? c1 : c0, c23 = (a8 & 8) ? c3 : c2;
     const uint32_t cp = (a8 & 16) ? c23 : c01;
     const uint32_t eqsh = 16u << a8;
     const int32_t u6 = u << 6;
@@ -109,13 +113,17 @@ __device__ __forceinline__ void band_row(Band &S, const int32_t u, const int32_t
     int32_t Zl = 0, Xl = 0, Pl = 0, Cl = 0;
 #pragma unroll
     for (int k = 0; k < LW; ++k) band_cell<MASKED, EXACT>(S, k, u6, jb, LB, w, cp, eqsh, gO, gE, act, Zl, Xl, Pl, Cl);
+    // two-word windows: the word after the current one was loaded at least one
+    // row earlier, so the loads issued here are not waited on until next row
     ++S.ap;
-    S.awd = Aw[min(S.ap >> 4, awl)];
+    S.awd = (S.ap & 15) == 0 ? S.awn : S.awd;
+    S.awn = gld(Aw, min((S.ap >> 4) + 1, awl));
 #pragma unroll
     for (int k = 0; k < LW - 1; ++k) S.b8[k] = S.b8[k + 1];
     S.b8[LW - 1] = S.bp < LB ? ((S.bw >> (30 - 2 * (S.bp & 15))) & 3u) << 3 : 0u;
     ++S.bp;
-    S.bw = Bw[min(S.bp >> 4, bwl)];
+    S.bw = (S.bp & 15) == 0 ? S.bwn : S.bw;
+    S.bwn = gld(Bw, min((S.bp >> 4) + 1, bwl));
 }
 
 // Pair setup shared by both phases: ids, lengths, band width, input checks.
@@ -175,14 +183,22 @@ __global__ __launch_bounds__(256) void dovetail_p1_kernel(DevReads rd, const int
     }
     const int32_t w = q.w;
     // column j (1..w) costs for A base x = 0..3 against B[j-1], as int8 bytes
+    // column packs (byte x = cost(x, b)) as four scalars: selects over an array
+    // index would be lowered to an LDS table
+    auto colpack = [&](int bb) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int x = 0; x < 4; ++x) v |= ((uint32_t)(uint8_t)(int8_t)P.cost[x * 4 + bb]) << (8 * x);
+        return v;
+    };
+    const uint32_t cq0 = colpack(0), cq1 = colpack(1), cq2 = colpack(2), cq3 = colpack(3);
+    const uint32_t bw0 = q.status == 0 ? gld(q.Bw, 0) : 0u;  // B[0 .. 16) covers every j <= w <= 15
     uint32_t cb[LW - 1];
 #pragma unroll
     for (int j = 1; j < LW; ++j) {
-        const uint32_t bj = (q.status == 0 && j <= w) ? code_of(q.Bw, j - 1) : 0u;
-        uint32_t v = 0;
-#pragma unroll
-        for (int x = 0; x < 4; ++x) v |= ((uint32_t)(uint8_t)(int8_t)P.cost[x * 4 + bj]) << (8 * x);
-        cb[j - 1] = v;
+        const uint32_t bj = (bw0 >> (30 - 2 * (j - 1))) & 3u;
+        const uint32_t c01 = (bj & 1) ? cq1 : cq0, c23 = (bj & 1) ? cq3 : cq2;
+        cb[j - 1] = (bj & 2) ? c23 : c01;
     }
     // row-0 state: every cell 0; Q = max(max(M, X) + gO, Y) feeds the next row's Y
     const int32_t Q0 = max(gO, 0);
@@ -195,10 +211,14 @@ __global__ __launch_bounds__(256) void dovetail_p1_kernel(DevReads rd, const int
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) rmax = max(rmax, __shfl_xor(rmax, off, 64));
     rmax = __builtin_amdgcn_readfirstlane(rmax);  // wave-uniform loop bound
-    uint32_t aw = 0;
+    // A window: current word + the next one, loaded a row ahead of use;
+    // branch-free rows (lanes past their last row stop updating the argmax)
+    const int32_t awl = max((q.LA + 15) / 16 - 1, 0);
+    uint32_t aw = q.Aw[0], awn = q.Aw[min(1, awl)];
+    __builtin_amdgcn_s_waitcnt(0);  // (see phase 2)
+#pragma unroll 2
     for (int32_t i = 1; i <= rmax; ++i) {
-        if (((i - 1) & 15) == 0) aw = (i <= rows1) ? q.Aw[(i - 1) >> 4] : 0u;
-        if (i > rows1) continue;
+        const bool act = i <= rows1;
         const uint32_t a8 = ((aw >> (30 - 2 * ((i - 1) & 15))) & 3u) << 3;
         // origin = (stop row << 1) | (stop col != 0); column 0 cells stop with col 0
         int32_t Tdiag = 0, Odiag = (i - 1) << 1;
@@ -218,13 +238,15 @@ __global__ __launch_bounds__(256) void dovetail_p1_kernel(DevReads rd, const int
             Q[j] = max(max(max(M, X) + gO, Y), 0);  // clamped: next row's Y = gE + Q
             O[j] = on;
             // first strict '>' in row-major order; columns > w never win
-            const bool nb = T > best && (EXACT || j < w);
+            const bool nb = T > best && act && (EXACT || j < w);
             best = nb ? T : best;
             borg = nb ? on : borg;
             Zl = max(M, Y) + gO;
             Xl = X;
             Ol = on;
         }
+        aw = (i & 15) == 0 ? awn : aw;
+        awn = gld(q.Aw, min((i >> 4) + 1, awl));
     }
     unsigned long long cells = 0;
     if (have) {
@@ -293,27 +315,36 @@ __global__ __launch_bounds__(256) void dovetail_p2_kernel(DevReads rd, const int
                  ((uint32_t)(uint8_t)(int8_t)P.cost[x * 4 + 2] << 16) |
                  ((uint32_t)(uint8_t)(int8_t)P.cost[x * 4 + 3] << 24);
     Band S;
+    const uint32_t bw0 = p2 ? gld(q.Bw, 0) : 0u;  // k - zr <= 15: B[0 .. 16)
 #pragma unroll
     for (int k = 0; k < LW; ++k) {
         const int32_t p = k - zr;
-        S.b8[k] = (p2 && p >= 0 && p < LB) ? code_of(q.Bw, p) << 3 : 0u;
+        S.b8[k] = (p >= 0 && p < LB) ? ((bw0 >> (30 - 2 * p)) & 3u) << 3 : 0u;
     }
     const int32_t Q0 = max(gO, 0);
 #pragma unroll
     for (int k = 0; k < LW; ++k) { S.Tk[k] = 0; S.Qk[k] = Q0; S.Pk[k] = k; S.Ck[k] = 0; }
     S.best = 0; S.bpos = 0; S.bstop = 0; S.bce = 0;
     S.bp = LW - zr;
-    S.bw = (p2 && S.bp < LB) ? q.Bw[S.bp >> 4] : 0u;
+    const int32_t awl = max((q.LA + 15) / 16 - 1, 0), bwl = max((LB + 15) / 16 - 1, 0);
+    S.bw = q.Bw[min(S.bp >> 4, bwl)];
+    S.bwn = q.Bw[min((S.bp >> 4) + 1, bwl)];
     S.ap = ds;
-    S.awd = p2 ? q.Aw[S.ap >> 4] : 0u;
+    S.awd = q.Aw[min(S.ap >> 4, awl)];
+    S.awn = q.Aw[min((S.ap >> 4) + 1, awl)];
     // rows [lo, hi] run unmasked; the first zr rows and the rows past the end
     // of some lane's B test every cell (separate loops keep each body one block)
-    const int32_t awl = max((q.LA + 15) / 16 - 1, 0), bwl = max((LB + 15) / 16 - 1, 0);
+    // drain the setup loads here: otherwise the wait the loop needs on entry is
+    // emitted inside it and also waits on each row's fresh prefetch
+    __builtin_amdgcn_s_waitcnt(0);
     int32_t u = 1;
     const int32_t e1 = min(lo - 1, rmax), e2 = min(hi, rmax);
-    for (; u <= e1; ++u) band_row<true, EXACT>(S, u, rows2, zr, LB, w, cpa, gO, gE, q.Aw, awl, q.Bw, bwl);
-    for (; u <= e2; ++u) band_row<false, EXACT>(S, u, rows2, zr, LB, w, cpa, gO, gE, q.Aw, awl, q.Bw, bwl);
-    for (; u <= rmax; ++u) band_row<true, EXACT>(S, u, rows2, zr, LB, w, cpa, gO, gE, q.Aw, awl, q.Bw, bwl);
+    for (; u <= e1; ++u) band_row<true, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl,
+                                                    q.Bw, bwl);
+    for (; u <= e2; ++u) band_row<false, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw,
+                                                     awl, q.Bw, bwl);
+    for (; u <= rmax; ++u) band_row<true, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl,
+                                                    q.Bw, bwl);
     const int32_t best2 = S.best, bpos = S.bpos, bstop = S.bstop, bce = S.bce;
     if (!have) return;
     int32_t status = r1 < 0 ? r1 : (r1 & 1);

@@ -1,0 +1,19 @@
+#!/bin/bash
+# PMC passes over a short bench run (one counter group per pass, as the MI355X
+# guide prescribes: FETCH_SIZE and WRITE_SIZE cannot share a pass).  Outputs
+# under gpurun_out/pmc_*; copy the summaries worth keeping into profiles/.
+set -u
+R=$GRAFT_REPO_ROOT
+mkdir -p $R/gpurun_out
+cd /tmp && export TMPDIR=/tmp
+BENCH="$R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --align-steps 2"
+pass() {  # pass <name> <counters...>
+    local name=$1; shift
+    timeout -k 10 300 rocprofv3 --kernel-trace --pmc "$@" --output-format csv -d $R/gpurun_out/pmc_$name -o pmc -- python3 $BENCH > $R/gpurun_out/pmc_$name.log 2>&1
+    local rc=$?
+    echo "pmc_$name rc=$rc" >> $R/gpurun_out/steps.txt
+    if [ $rc -ne 0 ]; then echo "stopping after pmc_$name (rc=$rc)"; exit $rc; fi
+}
+pass fetch FETCH_SIZE
+pass write WRITE_SIZE
+pass sq SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY
