@@ -31,6 +31,15 @@ __device__ __forceinline__ int32_t bfe_s8(uint32_t packed, uint32_t shift) {
 
 __device__ __forceinline__ void set_err(int32_t *err, int32_t code) { atomicCAS(err, 0, code); }
 
+// A wave-uniform value copied into a VGPR the compiler cannot see through: on
+// gfx950 a VALU add with an SGPR operand issues at half rate (~4.4 cycles per
+// wave64 instruction vs ~2.4 with VGPR / inline operands; tools/valu_rate.hip).
+__device__ __forceinline__ int32_t in_vgpr(int32_t x) {
+    int32_t r;
+    asm("v_mov_b32 %0, %1" : "=v"(r) : "s"(x));
+    return r;
+}
+
 // read-window loads through the global address space (plain pointers held in
 // structs otherwise lower to flat loads, which also count against lgkmcnt)
 __device__ __forceinline__ uint32_t gld(const uint32_t *p, int32_t i) {
@@ -175,7 +184,7 @@ __global__ __launch_bounds__(256) void dovetail_p1_kernel(DevReads rd, const int
                                                           unsigned long long *cells_total) {
     const uint64_t pair = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool have = pair < npairs;
-    const int32_t gO = P.gap_open, gE = P.gap_extend;
+    const int32_t gO = in_vgpr(P.gap_open), gE = in_vgpr(P.gap_extend);
     LanePair q{0, 0, 0, 0, 0, -100, rd.codes, rd.codes};
     if (have) {
         q = lane_pair<EXACT>(rd, lead, trail, pair, P);
@@ -282,7 +291,7 @@ __global__ __launch_bounds__(256) void dovetail_p2_kernel(DevReads rd, const int
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool have = t < npairs;
     const uint64_t pair = have ? order[t] : 0;
-    const int32_t gO = P.gap_open, gE = P.gap_extend;
+    const int32_t gO = in_vgpr(P.gap_open), gE = in_vgpr(P.gap_extend);
     LanePair q{0, 0, 0, 0, 0, -100, rd.codes, rd.codes};
     int32_t r1 = -100;
     if (have) {
