@@ -53,7 +53,7 @@ struct Band {
     int32_t best, bpos, bstop, bce;             // first row-major argmax and its path summary
     int32_t ap, bp;                             // A position of the next row; B position entering column LW-1
     uint32_t awd, bw;                           // packed words holding A[ap], B[bp]
-    uint32_t awn, bwn;                          // the words after them (loaded a row ahead of use)
+    uint32_t pa, pb;                            // next words, fetched the row before a window crosses
 };
 
 // One phase-2 cell (u, k) of the band (BioLibs.scala:725-764) plus the forward
@@ -111,7 +111,7 @@ __device__ __forceinline__ void band_row(Band &S, const int32_t u, const int32_t
                                          const int32_t LB, const int32_t w, const uint32_t c0, const uint32_t c1,
                                          const uint32_t c2, const uint32_t c3,
                                          const int32_t gO, const int32_t gE, const uint32_t *Aw, const int32_t awl,
-                                         const uint32_t *Bw, const int32_t bwl) {
+                                         const uint32_t *Bw, const int32_t bwl, const uint32_t *dummy) {
     const uint32_t a8 = ((S.awd >> (30 - 2 * (S.ap & 15))) & 3u) << 3;
     const uint32_t c01 = (a8 & 8) ? c1 : c0, c23 = (a8 & 8) ? c3 : c2;
     const uint32_t cp = (a8 & 16) ? c23 : c01;
@@ -124,15 +124,19 @@ __device__ __forceinline__ void band_row(Band &S, const int32_t u, const int32_t
     for (int k = 0; k < LW; ++k) band_cell<MASKED, EXACT>(S, k, u6, jb, LB, w, cp, eqsh, gO, gE, act, Zl, Xl, Pl, Cl);
     // two-word windows: the word after the current one was loaded at least one
     // row earlier, so the loads issued here are not waited on until next row
+    // Window words are fetched the row before a window crosses into them, so a
+    // load is consumed one row of compute after it is issued.  The load is
+    // unconditional (no merge copy, which would wait at once) but lanes that are
+    // not about to cross all read `dummy`: one shared line instead of 64.
     ++S.ap;
-    S.awd = (S.ap & 15) == 0 ? S.awn : S.awd;
-    S.awn = gld(Aw, min((S.ap >> 4) + 1, awl));
+    S.awd = (S.ap & 15) == 0 ? S.pa : S.awd;
+    S.pa = gld((((S.ap + 1) & 15) == 0) ? Aw + min((S.ap + 1) >> 4, awl) : dummy, 0);
 #pragma unroll
     for (int k = 0; k < LW - 1; ++k) S.b8[k] = S.b8[k + 1];
     S.b8[LW - 1] = S.bp < LB ? ((S.bw >> (30 - 2 * (S.bp & 15))) & 3u) << 3 : 0u;
     ++S.bp;
-    S.bw = (S.bp & 15) == 0 ? S.bwn : S.bw;
-    S.bwn = gld(Bw, min((S.bp >> 4) + 1, bwl));
+    S.bw = (S.bp & 15) == 0 ? S.pb : S.bw;
+    S.pb = gld((((S.bp + 1) & 15) == 0) ? Bw + min((S.bp + 1) >> 4, bwl) : dummy, 0);
 }
 
 // Pair setup shared by both phases: ids, lengths, band width, input checks.
@@ -337,10 +341,10 @@ __global__ __launch_bounds__(256) void dovetail_p2_kernel(DevReads rd, const int
     S.bp = LW - zr;
     const int32_t awl = max((q.LA + 15) / 16 - 1, 0), bwl = max((LB + 15) / 16 - 1, 0);
     S.bw = q.Bw[min(S.bp >> 4, bwl)];
-    S.bwn = q.Bw[min((S.bp >> 4) + 1, bwl)];
+    S.pb = q.Bw[min((S.bp >> 4) + 1, bwl)];
     S.ap = ds;
     S.awd = q.Aw[min(S.ap >> 4, awl)];
-    S.awn = q.Aw[min((S.ap >> 4) + 1, awl)];
+    S.pa = q.Aw[min((S.ap >> 4) + 1, awl)];
     // rows [lo, hi] run unmasked; the first zr rows and the rows past the end
     // of some lane's B test every cell (separate loops keep each body one block)
     // drain the setup loads here: otherwise the wait the loop needs on entry is
@@ -349,11 +353,12 @@ __global__ __launch_bounds__(256) void dovetail_p2_kernel(DevReads rd, const int
     int32_t u = 1;
     const int32_t e1 = min(lo - 1, rmax), e2 = min(hi, rmax);
     for (; u <= e1; ++u) band_row<true, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl,
-                                                    q.Bw, bwl);
+                                                    q.Bw, bwl, rd.codes);
     for (; u <= e2; ++u) band_row<false, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw,
-                                                     awl, q.Bw, bwl);
+                                                     awl, q.Bw, bwl, rd.codes);
     for (; u <= rmax; ++u) band_row<true, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl,
-                                                    q.Bw, bwl);
+                                                    q.Bw, bwl, rd.codes);
+
     const int32_t best2 = S.best, bpos = S.bpos, bstop = S.bstop, bce = S.bce;
     if (!have) return;
     int32_t status = r1 < 0 ? r1 : (r1 & 1);
