@@ -97,6 +97,7 @@ struct sa_ctx {
     DBuf d_pf, d_ps, d_pc, d_pr, d_ovl, d_cnt;
     DBuf d_okeys, d_ovals, d_okeys2, d_ovals2, d_osort;
     DBuf d_lead, d_trail, d_count, d_aln, d_p1;
+    DBuf d_rkey, d_rkey2, d_rord, d_rord2, d_rtmp;
     uint64_t pair_cap = 0;
     uint64_t n_disp = 0;
     // options / state
@@ -343,6 +344,8 @@ EmitParams emit_params(sa_ctx *c) {
     e.lbase = (const uint32_t *)c->d_lbase.p;
     e.lrank = (const uint32_t *)c->d_lrank.p;
     e.maxd = c->maxd;
+    e.rkey = nullptr;
+    e.rord = nullptr;
     return e;
 }
 
@@ -395,10 +398,21 @@ int device_build(sa_ctx *c, bool readback) {
         StageScope st(c, SA_STAGE_PACK);
         HIPCHK(launch_pack_reads(R, c->stream));
     }
+    uint64_t *rk0, *rk1; uint32_t *ro0, *ro1; uint8_t *rtmp;
+    ENSURE(c->d_rkey, nr, &rk0);
+    ENSURE(c->d_rkey2, nr, &rk1);
+    ENSURE(c->d_rord, nr, &ro0);
+    ENSURE(c->d_rord2, nr, &ro1);
+    ENSURE(c->d_rtmp, radix_sort_temp_bytes(nr), &rtmp);
+    E.rkey = rk0;
+    E.rord = ro0;
     {
         StageScope st(c, SA_STAGE_EMIT);
         HIPCHK(launch_kmer_emit(R, E, keys, vals, c->stream));
+        // reads in locality order (overlapping reads adjacent) for pair_count
+        HIPCHK(radix_sort(&rk0, &ro0, &rk1, &ro1, nr, 0, 32, rtmp, c->stream));
     }
+    const uint32_t *read_order = ro0;
     // ---- partition by the top P bits of mix(seqHash): whole buckets per partition
     int PB = 1;
     while (PB < 16 && ((uint64_t)700 << PB) < n) ++PB;
@@ -548,6 +562,8 @@ int device_build(sa_ctx *c, bool readback) {
     P.split = 1;
     P.max_occ = c->max_occ;
     P.ablate = c->ablate;
+    P.n_items = nr;
+    P.xcd_swizzle = 1;
     if (c->pair_cap == 0) c->pair_cap = std::max<uint64_t>(1 << 16, (uint64_t)nr * (P.emit_all ? 64 : 24));
     // output regions: NSHARD x cap_s entries (a block appends to region blockIdx % NSHARD)
     unsigned long long cur[NSHARD];
@@ -572,7 +588,7 @@ int device_build(sa_ctx *c, bool readback) {
         HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(uint32_t), c->stream));
         {
             StageScope st(c, SA_STAGE_PAIRS);
-            HIPCHK(launch_pair_count(E, PI, P, O, nullptr, nr, c->stream));
+            HIPCHK(launch_pair_count(E, PI, P, O, read_order, (nr + 7) & ~7u, c->stream));
         }
         HIPCHK(hipMemcpyAsync(cur, cnt->cursor, sizeof(cur), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipMemcpyAsync(&ovn, &cnt->overflow_n, 4, hipMemcpyDeviceToHost, c->stream));
@@ -583,6 +599,8 @@ int device_build(sa_ctx *c, bool readback) {
             const uint32_t split = 64;
             PairParams P2 = P;
             P2.split = (int32_t)split;
+            P2.n_items = ovn * split;
+            P2.xcd_swizzle = 0;
             PairOut O2 = O;
             O2.role_pairs = cnt->role_pairs_dummy;
             O2.overflow_list = O.overflow_list + ovn;  // keep the read list intact
@@ -872,7 +890,7 @@ void sa_ctx_destroy(sa_ctx *c) {
                     &c->d_gmds, &c->d_gede, &c->d_ogid, &c->d_bkttmp, &c->d_mdidx, &c->d_edidx, &c->d_occidx,
                     &c->d_bnst, &c->d_brank, &c->d_bhash, &c->d_bfirst, &c->d_pf, &c->d_ps, &c->d_pc, &c->d_pr,
                     &c->d_ovl, &c->d_cnt, &c->d_okeys, &c->d_ovals, &c->d_okeys2, &c->d_ovals2, &c->d_osort,
-                    &c->d_lead, &c->d_trail, &c->d_count, &c->d_aln, &c->d_p1, &c->d_pstart, &c->d_biglist, &c->d_rec,
+                    &c->d_lead, &c->d_trail, &c->d_count, &c->d_aln, &c->d_p1, &c->d_rkey, &c->d_rkey2, &c->d_rord, &c->d_rord2, &c->d_rtmp, &c->d_pstart, &c->d_biglist, &c->d_rec,
                     &c->d_srec, &c->d_bnmd, &c->d_ishead, &c->d_bnst2};
     for (DBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);

@@ -76,18 +76,30 @@ __global__ __launch_bounds__(256) void kmer_emit_kernel(DevReads r, EmitParams e
     for (uint32_t rd = wave; rd < r.n; rd += nwaves) {
         const int32_t L = r.len[rd];
         const int32_t nk = L - e.k + 1;
-        if (nk <= 0) continue;
+        if (nk <= 0) {
+            if (e.rkey && lane == 0) { e.rkey[rd] = 0xFFFFFFFFu; e.rord[rd] = rd; }
+            continue;
+        }
         const uint32_t *w = r.codes + r.woff[rd];
         const uint64_t g0 = e.occ_off[rd];
         const int32_t d = L - e.k;
         const uint32_t *lr = e.lrank + e.lbase[d];
+        uint32_t kmin = 0xFFFFFFFFu;
         for (int32_t i = lane; i < nk; i += 64) {
             uint32_t x = window16(w, i);
             x = shift == 32 ? 0u : (x >> shift);
             // HOXD order (A0 C1 G2 T3) -> seqHash order (A0 C1 T2 G3): c ^ (c >> 1)
             x ^= (x >> 1) & 0x55555555u;
-            keys[g0 + i] = ((uint64_t)mix32(x) << e.lb) | (uint64_t)lr[i];
+            const uint32_t h = mix32(x);
+            kmin = min(kmin, h);
+            keys[g0 + i] = ((uint64_t)h << e.lb) | (uint64_t)lr[i];
             vals[g0 + i] = (uint32_t)(g0 + i);
+        }
+        if (e.rkey) {
+            // locality key: reads sharing their minimum k-mer overlap, so sorting
+            // by it puts overlapping reads next to each other (pair_count order)
+            for (int off = 32; off > 0; off >>= 1) kmin = min(kmin, (uint32_t)__shfl_xor(kmin, off, 64));
+            if (lane == 0) { e.rkey[rd] = kmin; e.rord[rd] = rd; }
         }
     }
 }

@@ -89,8 +89,15 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
     PcSharedStrict &X = *reinterpret_cast<PcSharedStrict *>(smem + ((sizeof(PcShared) + 15) & ~size_t(15)));
     const int tid = threadIdx.x;
     const uint32_t split = (uint32_t)p.split;
-    const uint32_t item = blockIdx.x / split;
-    const uint32_t residue = blockIdx.x % split;
+    uint32_t bid = blockIdx.x;
+    if (p.xcd_swizzle) {
+        // blocks are dealt round-robin over the 8 XCDs: give each XCD a contiguous
+        // run of the (locality-sorted) read list so overlapping reads share its L2
+        bid = (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+    }
+    if (bid >= p.n_items) return;  // whole block: before any barrier
+    const uint32_t item = bid / split;
+    const uint32_t residue = bid % split;
     const uint32_t a = read_list ? read_list[item] : item;
 
     for (int i = tid; i < PC_TAB; i += PC_THREADS) {

@@ -31,6 +31,8 @@ struct EmitParams {
     const uint32_t *lbase;     // [maxd+1] offset of denominator d = L-k in lrank
     const uint32_t *lrank;     // rank of float32 i/d among all distinct locs
     int32_t maxd;
+    uint64_t *rkey;            // [n] per-read locality key (min k-mer mix; nullable)
+    uint32_t *rord;            // [n] read ids (sort payload for rkey)
 };
 
 // bijective 32-bit mix of the seqHash: equal mix <=> equal hash, so a bucket
@@ -84,6 +86,8 @@ struct PairParams {
     int32_t split;         // partner residue classes (overflow fallback)
     uint32_t max_occ;      // max occurrences of one read (LDS sizing)
     int32_t ablate;        // profiling only (env SA_ABLATE): 16 skip inserts, 32 skip emission
+    uint32_t n_items;      // reads (x split) to process; blocks beyond it exit
+    int32_t xcd_swizzle;   // 1: XCD-contiguous block -> item map (grid % 8 == 0)
 };
 
 // Device-wide counters are sharded NSHARD ways (shard = blockIdx % NSHARD) and
