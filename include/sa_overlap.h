@@ -166,6 +166,43 @@ int sa_device_build(sa_ctx *ctx);   /* == sa_build_candidates without host readb
 int sa_device_align(sa_ctx *ctx);   /* == sa_align without host readback */
 int sa_sync(sa_ctx *ctx);
 
+/* ---- Sharded hash stage, one process (context) per GPU ----
+ * Rank r holds reads [starts[r], starts[r+1]) of the global read set (0-based,
+ * global id = index + 1), added to its context with sa_add_reads as usual.
+ * The caller moves data between ranks (all-to-all / all-gather, e.g. with
+ * torch.distributed over RCCL); every buffer argument below is a DEVICE
+ * pointer on this context's GPU.  Wide ids only.  The sequence per step is
+ *   sa_dist_emit      -> exchange 1 (k-mer records, grouped by owner rank)
+ *   sa_dist_count     -> sa_dist_partials -> exchange 2 (partial pair counts)
+ *   sa_dist_reduce    (this rank's leads: sum, [min,max] filter, dispatch)
+ * and, for alignment, sa_dist_codes -> all-gather -> sa_dist_set_reads, then
+ * sa_align / sa_device_align / sa_get_ovl over this rank's leads.  No
+ * reference counterpart: the reference is single-process
+ * (KmerTable.scala:41-187 is the semantics each rank restates).
+ */
+/* nranks is a power of two <= 256; starts has nranks + 1 entries;
+ * lengths[i] is the length of global read i (all starts[nranks] reads). */
+int sa_dist_init(sa_ctx *ctx, int rank, int nranks, const uint32_t *starts, const int32_t *lengths);
+/* k-mer occurrences of this rank's reads (the size of the exchange-1 send buffers). */
+int sa_dist_local_kmers(sa_ctx *ctx, uint64_t *n);
+/* Emit this rank's k-mer records into send_keys (u64[n]) / send_vals (u32[n]),
+ * grouped by owner rank; counts[nranks] = records per owner. */
+int sa_dist_emit(sa_ctx *ctx, void *send_keys, void *send_vals, uint64_t *counts);
+/* Records received in exchange 1 (concatenated in source-rank order; the
+ * buffers are consumed and may be overwritten): build this rank's buckets and
+ * count partial pairs for every read; counts[nranks] = partials per lead owner. */
+int sa_dist_count(sa_ctx *ctx, void *recv_keys, void *recv_vals, uint64_t n, uint64_t *counts);
+/* Copy the partials (u32 lead, trail, count; 0-based ids) grouped by lead owner. */
+int sa_dist_partials(sa_ctx *ctx, void *fst, void *snd, void *cnt);
+/* Partials received in exchange 2: sum, filter, dispatch this rank's leads
+ * (wide canonical order: lead descending, trail ascending). */
+int sa_dist_reduce(sa_ctx *ctx, const void *fst, const void *snd, const void *cnt, uint64_t n);
+/* This rank's packed reads (2-bit words, u32[*nwords]) and first-invalid
+ * positions (int32 per read); NULL buffers query *nwords only. */
+int sa_dist_codes(sa_ctx *ctx, void *codes, void *bad, uint64_t *nwords);
+/* All ranks' packed words / bad positions in global read order (all-gathered). */
+int sa_dist_set_reads(sa_ctx *ctx, const void *codes, const void *bad, uint64_t nwords);
+
 #ifdef __cplusplus
 }
 #endif

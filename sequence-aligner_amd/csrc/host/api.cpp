@@ -100,6 +100,18 @@ struct sa_ctx {
     DBuf d_rkey, d_rkey2, d_rord, d_rord2, d_rtmp;
     uint64_t pair_cap = 0;
     uint64_t n_disp = 0;
+    // distributed mode (sa_dist_*): this rank's slice of a global read set
+    bool dist = false, dist_reads = false;
+    int rank = 0, nranks = 1, log_ranks = 0;
+    std::vector<uint32_t> dstarts;   // [nranks+1] first global read of each rank
+    std::vector<int32_t> dlen;       // length of every global read
+    std::vector<uint64_t> gocc;      // global occurrence offsets [N+1]
+    uint32_t gnpr = 0;               // uniform k-mers per read over all reads (0: mixed)
+    int32_t gmaxL = 0, gminL = 0;
+    uint64_t part_np = 0;            // partial pairs after sa_dist_count
+    uint32_t *part_perm = nullptr;   // their ascending-lead order (region-space indices)
+    DBuf d_gocc, d_rid, d_loff, d_starts, d_bounds, d_gcodes, d_gwoff, d_glen, d_gbad, d_psum, d_pkeep, d_ppos;
+    DBuf d_scan;
     // options / state
     bool keep_pairs = false, timing = false;
     int align_kernel = 0;  // SA_OPT_ALIGN_KERNEL
@@ -245,6 +257,18 @@ int prepare_reads(sa_ctx *c) {
     }
     c->n_occ = c->occ_off[n];
     if (c->n_occ >= 0xFFFFFFF0ull) return fail(c, SA_E_OVERFLOW, "more than 2^32 k-mers on one device");
+    if (c->dist) {
+        // loc ranks / tags / sort-key width must agree on every rank: derive
+        // them from the lengths of ALL reads, not just this rank's
+        has_d.clear();
+        maxd = -1;
+        for (int32_t L : c->dlen) {
+            if (L < k) continue;
+            const int d = L - k;
+            if (d > maxd) { maxd = d; has_d.resize(d + 1, 0); }
+            has_d[d] = 1;
+        }
+    }
     c->n_words = c->woff[n] + 2;  // pad: windows read one word past a read
     c->uniform_npr = (uniform && n > 0) ? (uint32_t)(uni - k + 1) : 0;
     c->maxd = maxd < 0 ? 0 : maxd;
@@ -346,6 +370,7 @@ EmitParams emit_params(sa_ctx *c) {
     e.maxd = c->maxd;
     e.rkey = nullptr;
     e.rord = nullptr;
+    e.g_base = 0;
     return e;
 }
 
@@ -363,16 +388,202 @@ int ensure_prepared(sa_ctx *c) {
     const uint32_t n = (uint32_t)(c->boff.size() - 1);
     int mode = c->set.id_mode;
     if (mode == SA_IDS_AUTO) mode = n < 32768 ? SA_IDS_STRICT : SA_IDS_WIDE;
+    if (c->dist) mode = SA_IDS_WIDE;
     if (mode == SA_IDS_STRICT && n >= 65536)
         return fail(c, SA_E_ID_RANGE, "strict ids: >= 65,536 reads alias in the reference's (fst<<16)^snd keys; use wide ids");
     c->mode = mode;
     return SA_OK;
 }
 
+// Bucket build over one device's k-mer records (keys = mix << lb | locrank,
+// vals = occurrence index): partition radix sort on the top PB bits of the
+// mix, then one LDS workgroup per partition (part_build), the global scan path
+// for partitions too large for LDS.  Read ids come from rid[val] when given
+// (distributed mode), else from the occurrence offsets.
+int bucket_stage(sa_ctx *c, uint64_t *&keys, uint32_t *&vals, uint64_t *&keys2, uint32_t *&vals2, uint64_t n,
+                 const uint64_t *occ_off, uint32_t n_reads, uint32_t npr, const uint32_t *rid, bool strict,
+                 void *stmp, Counters *cnt, PartArgs &PA, unsigned long long &big_buckets) {
+    // ---- partition by the top P bits of mix(seqHash): whole buckets per partition
+    int PB = 1;
+    while (PB < 16 && ((uint64_t)700 << PB) < n) ++PB;
+    const uint32_t nparts = 1u << PB;
+    const int kbits = 32 + c->lb;
+    {
+        StageScope st(c, SA_STAGE_SORT);
+        HIPCHK(radix_sort(&keys, &vals, &keys2, &vals2, n, kbits - PB, kbits, stmp, c->stream));
+    }
+    uint32_t *pstart, *biglist;
+    ENSURE(c->d_pstart, nparts + 1, &pstart);
+    ENSURE(c->d_biglist, nparts + 1, &biglist);
+    PA = PartArgs{};
+    PA.sk = keys; PA.sv = vals; PA.start = pstart; PA.np = nparts; PA.lb = c->lb; PA.sort_bits = kbits - PB;
+    PA.ablate = c->ablate;
+    PA.tagtab = (const uint8_t *)c->d_tagtab.p;
+    PA.occ_off = occ_off;
+    PA.n_reads = n_reads; PA.npr = npr; PA.rid = rid;
+    ENSURE(c->d_md, n + 1, &PA.md_list);
+    ENSURE(c->d_ed, 2 * n + 2, &PA.ed_list);
+    ENSURE(c->d_rec, n + 1, &PA.rec);
+    PA.big_list = biglist; PA.big_n = &cnt->big_n;
+    PA.counts = cnt->bkt_counts;
+    if (strict) {
+        ENSURE(c->d_mdidx, n + 1, &PA.md_idx);
+        ENSURE(c->d_edidx, 2 * n + 2, &PA.ed_idx);
+        ENSURE(c->d_srec, n + 1, &PA.srec);
+        ENSURE(c->d_bnst, n + 1, &PA.bkt_nst);
+        ENSURE(c->d_bnmd, n + 1, &PA.bkt_nmd);
+        ENSURE(c->d_bfirst, n + 1, &PA.bkt_first);
+        ENSURE(c->d_ishead, n + 1, &PA.is_head);
+        ENSURE(c->d_brank, n + 1, &c->bkt_rank_dev);
+        HIPCHK(hipMemsetAsync(PA.is_head, 0, n + 1, c->stream));
+    }
+    const uint8_t *tagtab = PA.tagtab;
+    uint32_t big_n = 0;
+    {
+        StageScope st(c, SA_STAGE_BUCKETS);
+        HIPCHK(launch_part_starts(keys, n, c->lb + 32 - PB, pstart, nparts, c->stream));
+        HIPCHK(launch_part_build(PA, strict, c->stream));
+    }
+    HIPCHK(hipMemcpyAsync(&big_n, &cnt->big_n, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    big_buckets = 0;
+    unsigned long long big_groups = 0;
+    if (big_n) {
+        // partitions too large for LDS (high-copy repeats): sort the rest of the
+        // key in place, then the global scan build of buckets.hip on the range
+        std::vector<uint32_t> bl(big_n), starts(nparts + 1);
+        HIPCHK(hipMemcpy(bl.data(), biglist, big_n * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(starts.data(), pstart, (nparts + 1) * 4, hipMemcpyDeviceToHost));
+        std::sort(bl.begin(), bl.end());
+        uint32_t maxn = 0;
+        for (uint32_t p : bl) maxn = std::max(maxn, starts[p + 1] - starts[p]);
+        Buckets B{};
+        ENSURE(c->d_bmdo, maxn + 2, &B.bkt_mdo);
+        ENSURE(c->d_bedo, maxn + 2, &B.bkt_edo);
+        ENSURE(c->d_bstart, maxn + 2, &B.bkt_start);
+        ENSURE(c->d_gbid, maxn + 1, &B.grp_bid);
+        ENSURE(c->d_gmds, maxn + 1, &B.grp_mds);
+        ENSURE(c->d_gede, maxn + 1, &B.grp_ede);
+        ENSURE(c->d_ogid, n + 1, &B.occ_gid);
+        uint8_t *btmp;
+        ENSURE(c->d_bkttmp, std::max(radix_sort_temp_bytes(maxn), buckets_temp_bytes(maxn)), &btmp);
+        if (strict) {
+            ENSURE(c->d_occidx, 3 * n + 3, &B.occ_idx);
+            ENSURE(c->d_bnst2, maxn + 1, &B.bkt_nst);
+        }
+        StageScope st(c, SA_STAGE_BUCKETS);
+        for (uint32_t p : bl) {
+            const uint32_t ps = starts[p], pn = starts[p + 1] - starts[p];
+            uint64_t *k0 = keys + ps, *k1 = keys2 + ps;
+            uint32_t *v0 = vals + ps, *v1 = vals2 + ps;
+            HIPCHK(radix_sort(&k0, &v0, &k1, &v1, pn, 0, kbits - PB, btmp, c->stream));
+            if (k0 != keys + ps) {  // odd number of passes: copy the sorted range back
+                HIPCHK(hipMemcpyAsync(keys + ps, k0, (size_t)pn * 8, hipMemcpyDeviceToDevice, c->stream));
+                HIPCHK(hipMemcpyAsync(vals + ps, v0, (size_t)pn * 4, hipMemcpyDeviceToDevice, c->stream));
+            }
+            B.n_occ = pn;
+            B.md_list = PA.md_list + ps;
+            B.ed_list = PA.ed_list + 2ull * ps;
+            if (strict) { B.md_idx = PA.md_idx + ps; B.ed_idx = PA.ed_idx + 2ull * ps; }
+            HIPCHK(build_buckets(keys + ps, vals + ps, pn, c->lb, tagtab, PA.occ_off, n_reads, npr, rid, B,
+                                 cnt->totals, btmp, c->stream));
+            if (strict) HIPCHK(build_strict_index(keys + ps, vals + ps, pn, c->lb, tagtab, B, c->stream));
+            HIPCHK(launch_records_from_tables(keys, vals, ps, pn, c->lb, tagtab, B, PA.rec, strict ? 1 : 0, PA.srec,
+                                              PA.bkt_nst, PA.bkt_nmd, PA.bkt_first, PA.is_head, c->stream));
+            uint32_t tot[4];
+            HIPCHK(hipMemcpyAsync(tot, cnt->totals, 16, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            big_buckets += tot[0];
+            big_groups += tot[1];
+        }
+    }
+    (void)big_groups;
+    return SA_OK;
+}
+
+// Pair counting (pair_count.hip) with output-capacity growth and the
+// partner-residue split pass for reads whose LDS table overflows.  Leaves np
+// entries in the NSHARD output regions of cap_s_out entries each.
+int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bool emit_all,
+               const uint32_t *read_order, uint32_t n_items, Counters *cnt, uint64_t &np, uint64_t &cap_s_out) {
+    // ---- pair counting -------------------------------------------------
+    PairParams P;
+    P.min_coll = c->set.min_collisions;
+    P.max_coll = c->set.max_collisions;
+    P.emit_all = emit_all ? 1 : 0;
+    P.strict = strict ? 1 : 0;
+    P.split = 1;
+    P.max_occ = c->max_occ;
+    P.ablate = c->ablate;
+    P.n_items = n_items;
+    P.xcd_swizzle = read_order ? 1 : 0;
+    if (c->pair_cap == 0) c->pair_cap = std::max<uint64_t>(1 << 16, (uint64_t)n_items * (P.emit_all ? 64 : 24));
+    // output regions: NSHARD x cap_s entries (a block appends to region blockIdx % NSHARD)
+    unsigned long long cur[NSHARD];
+    auto cur_max = [&]() { unsigned long long m = 0; for (auto v : cur) m = std::max(m, v); return m; };
+    uint32_t ovn = 0;
+    uint64_t cap_s = (c->pair_cap + NSHARD - 1) / NSHARD;
+    for (int attempt = 0; attempt < 4; ++attempt) {
+        PairOut O;
+        const uint64_t tot_cap = cap_s * NSHARD;
+        ENSURE(c->d_pf, tot_cap, &O.fst);
+        ENSURE(c->d_ps, tot_cap, &O.snd);
+        ENSURE(c->d_pc, tot_cap, &O.cnt);
+        O.rank = nullptr;
+        if (strict) ENSURE(c->d_pr, tot_cap, &O.rank);
+        ENSURE(c->d_ovl, 2 * (uint64_t)n_items + 2, &O.overflow_list);
+        O.cursor = cnt->cursor;
+        O.cap_s = cap_s;
+        O.role_pairs = cnt->role_pairs;
+        O.overflow_n = &cnt->overflow_n;
+        O.distinct = cnt->distinct;
+        HIPCHK(hipMemsetAsync(cnt->cursor, 0, 4 * NSHARD * sizeof(unsigned long long), c->stream));
+        HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(uint32_t), c->stream));
+        {
+            StageScope st(c, SA_STAGE_PAIRS);
+            HIPCHK(launch_pair_count(E, PI, P, O, read_order, read_order ? ((n_items + 7) & ~7u) : n_items, c->stream));
+        }
+        HIPCHK(hipMemcpyAsync(cur, cnt->cursor, sizeof(cur), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(&ovn, &cnt->overflow_n, 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        // reads whose LDS table overflowed (> 1,536 partners: high-copy repeats) are
+        // recounted in 64 partner-residue passes; each pass holds up to 1,536 partners
+        if (ovn > 0 && cur_max() <= cap_s) {
+            const uint32_t split = 64;
+            PairParams P2 = P;
+            P2.split = (int32_t)split;
+            P2.n_items = ovn * split;
+            P2.xcd_swizzle = 0;
+            PairOut O2 = O;
+            O2.role_pairs = cnt->role_pairs_dummy;
+            O2.overflow_list = O.overflow_list + ovn;  // keep the read list intact
+            HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(uint32_t), c->stream));
+            {
+                StageScope st(c, SA_STAGE_PAIRS);
+                HIPCHK(launch_pair_count(E, PI, P2, O2, O.overflow_list, ovn * split, c->stream));
+            }
+            HIPCHK(hipMemcpyAsync(cur, cnt->cursor, sizeof(cur), hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipMemcpyAsync(&ovn, &cnt->overflow_n, 4, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            if (ovn) return fail(c, SA_E_OVERFLOW, "a read has more than 98,304 distinct partners");
+        }
+        if (cur_max() <= cap_s) break;
+        cap_s = cur_max() + cur_max() / 4 + 1024;  // grow and recount
+        c->pair_cap = cap_s * NSHARD;
+        if (attempt == 3) return fail(c, SA_E_OVERFLOW, "pair output did not fit");
+    }
+    np = 0;
+    for (auto v : cur) np += v;
+    cap_s_out = cap_s;
+    return SA_OK;
+}
+
+
 // ---------------------------------------------------------------------------
 // candidate build (device), optional host readback
 // ---------------------------------------------------------------------------
 int device_build(sa_ctx *c, bool readback) {
+    if (c->dist) return fail(c, SA_E_STATE, "distributed context: use sa_dist_emit / sa_dist_count / sa_dist_reduce");
     int rc = ensure_prepared(c);
     if (rc) return rc;
     c->built = false;
@@ -413,99 +624,11 @@ int device_build(sa_ctx *c, bool readback) {
         HIPCHK(radix_sort(&rk0, &ro0, &rk1, &ro1, nr, 0, 32, rtmp, c->stream));
     }
     const uint32_t *read_order = ro0;
-    // ---- partition by the top P bits of mix(seqHash): whole buckets per partition
-    int PB = 1;
-    while (PB < 16 && ((uint64_t)700 << PB) < n) ++PB;
-    const uint32_t nparts = 1u << PB;
-    const int kbits = 32 + c->lb;
-    {
-        StageScope st(c, SA_STAGE_SORT);
-        HIPCHK(radix_sort(&keys, &vals, &keys2, &vals2, n, kbits - PB, kbits, stmp, c->stream));
-    }
-    uint32_t *pstart, *biglist;
-    ENSURE(c->d_pstart, nparts + 1, &pstart);
-    ENSURE(c->d_biglist, nparts + 1, &biglist);
     PartArgs PA{};
-    PA.sk = keys; PA.sv = vals; PA.start = pstart; PA.np = nparts; PA.lb = c->lb; PA.sort_bits = kbits - PB;
-    PA.ablate = c->ablate;
-    PA.tagtab = (const uint8_t *)c->d_tagtab.p;
-    PA.occ_off = (const uint64_t *)c->d_occ_off.p;
-    PA.n_reads = nr; PA.npr = c->uniform_npr;
-    ENSURE(c->d_md, n + 1, &PA.md_list);
-    ENSURE(c->d_ed, 2 * n + 2, &PA.ed_list);
-    ENSURE(c->d_rec, n + 1, &PA.rec);
-    PA.big_list = biglist; PA.big_n = &cnt->big_n;
-    PA.counts = cnt->bkt_counts;
-    if (strict) {
-        ENSURE(c->d_mdidx, n + 1, &PA.md_idx);
-        ENSURE(c->d_edidx, 2 * n + 2, &PA.ed_idx);
-        ENSURE(c->d_srec, n + 1, &PA.srec);
-        ENSURE(c->d_bnst, n + 1, &PA.bkt_nst);
-        ENSURE(c->d_bnmd, n + 1, &PA.bkt_nmd);
-        ENSURE(c->d_bfirst, n + 1, &PA.bkt_first);
-        ENSURE(c->d_ishead, n + 1, &PA.is_head);
-        ENSURE(c->d_brank, n + 1, &c->bkt_rank_dev);
-        HIPCHK(hipMemsetAsync(PA.is_head, 0, n + 1, c->stream));
-    }
-    const uint8_t *tagtab = PA.tagtab;
-    uint32_t big_n = 0;
-    {
-        StageScope st(c, SA_STAGE_BUCKETS);
-        HIPCHK(launch_part_starts(keys, n, c->lb + 32 - PB, pstart, nparts, c->stream));
-        HIPCHK(launch_part_build(PA, strict, c->stream));
-    }
-    HIPCHK(hipMemcpyAsync(&big_n, &cnt->big_n, 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    unsigned long long big_buckets = 0, big_groups = 0;
-    if (big_n) {
-        // partitions too large for LDS (high-copy repeats): sort the rest of the
-        // key in place, then the global scan build of buckets.hip on the range
-        std::vector<uint32_t> bl(big_n), starts(nparts + 1);
-        HIPCHK(hipMemcpy(bl.data(), biglist, big_n * 4, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(starts.data(), pstart, (nparts + 1) * 4, hipMemcpyDeviceToHost));
-        std::sort(bl.begin(), bl.end());
-        uint32_t maxn = 0;
-        for (uint32_t p : bl) maxn = std::max(maxn, starts[p + 1] - starts[p]);
-        Buckets B{};
-        ENSURE(c->d_bmdo, maxn + 2, &B.bkt_mdo);
-        ENSURE(c->d_bedo, maxn + 2, &B.bkt_edo);
-        ENSURE(c->d_bstart, maxn + 2, &B.bkt_start);
-        ENSURE(c->d_gbid, maxn + 1, &B.grp_bid);
-        ENSURE(c->d_gmds, maxn + 1, &B.grp_mds);
-        ENSURE(c->d_gede, maxn + 1, &B.grp_ede);
-        ENSURE(c->d_ogid, n + 1, &B.occ_gid);
-        uint8_t *btmp;
-        ENSURE(c->d_bkttmp, std::max(radix_sort_temp_bytes(maxn), buckets_temp_bytes(maxn)), &btmp);
-        if (strict) {
-            ENSURE(c->d_occidx, 3 * n + 3, &B.occ_idx);
-            ENSURE(c->d_bnst2, maxn + 1, &B.bkt_nst);
-        }
-        StageScope st(c, SA_STAGE_BUCKETS);
-        for (uint32_t p : bl) {
-            const uint32_t ps = starts[p], pn = starts[p + 1] - starts[p];
-            uint64_t *k0 = keys + ps, *k1 = keys2 + ps;
-            uint32_t *v0 = vals + ps, *v1 = vals2 + ps;
-            HIPCHK(radix_sort(&k0, &v0, &k1, &v1, pn, 0, kbits - PB, btmp, c->stream));
-            if (k0 != keys + ps) {  // odd number of passes: copy the sorted range back
-                HIPCHK(hipMemcpyAsync(keys + ps, k0, (size_t)pn * 8, hipMemcpyDeviceToDevice, c->stream));
-                HIPCHK(hipMemcpyAsync(vals + ps, v0, (size_t)pn * 4, hipMemcpyDeviceToDevice, c->stream));
-            }
-            B.n_occ = pn;
-            B.md_list = PA.md_list + ps;
-            B.ed_list = PA.ed_list + 2ull * ps;
-            if (strict) { B.md_idx = PA.md_idx + ps; B.ed_idx = PA.ed_idx + 2ull * ps; }
-            HIPCHK(build_buckets(keys + ps, vals + ps, pn, c->lb, tagtab, PA.occ_off, nr, c->uniform_npr, B,
-                                 cnt->totals, btmp, c->stream));
-            if (strict) HIPCHK(build_strict_index(keys + ps, vals + ps, pn, c->lb, tagtab, B, c->stream));
-            HIPCHK(launch_records_from_tables(keys, vals, ps, pn, c->lb, tagtab, B, PA.rec, strict ? 1 : 0, PA.srec,
-                                              PA.bkt_nst, PA.bkt_nmd, PA.bkt_first, PA.is_head, c->stream));
-            uint32_t tot[4];
-            HIPCHK(hipMemcpyAsync(tot, cnt->totals, 16, hipMemcpyDeviceToHost, c->stream));
-            HIPCHK(hipStreamSynchronize(c->stream));
-            big_buckets += tot[0];
-            big_groups += tot[1];
-        }
-    }
+    unsigned long long big_buckets = 0;
+    rc = bucket_stage(c, keys, vals, keys2, vals2, n, (const uint64_t *)c->d_occ_off.p, nr, c->uniform_npr,
+                      nullptr, strict, stmp, cnt, PA, big_buckets);
+    if (rc) return rc;
     if (strict) {
         // KmerData iteration rank of every bucket: replay its Trove layout over the
         // distinct hashes in first-occurrence order (KmerTable.scala:45-50).  A
@@ -553,74 +676,10 @@ int device_build(sa_ctx *c, bool readback) {
         PI.bkt_nst = PA.bkt_nst; PI.bkt_nmd = PA.bkt_nmd; PI.bkt_rank = c->bkt_rank_dev;
     }
 
-    // ---- pair counting -------------------------------------------------
-    PairParams P;
-    P.min_coll = c->set.min_collisions;
-    P.max_coll = c->set.max_collisions;
-    P.emit_all = (strict || c->keep_pairs) ? 1 : 0;
-    P.strict = strict ? 1 : 0;
-    P.split = 1;
-    P.max_occ = c->max_occ;
-    P.ablate = c->ablate;
-    P.n_items = nr;
-    P.xcd_swizzle = 1;
-    if (c->pair_cap == 0) c->pair_cap = std::max<uint64_t>(1 << 16, (uint64_t)nr * (P.emit_all ? 64 : 24));
-    // output regions: NSHARD x cap_s entries (a block appends to region blockIdx % NSHARD)
-    unsigned long long cur[NSHARD];
-    auto cur_max = [&]() { unsigned long long m = 0; for (auto v : cur) m = std::max(m, v); return m; };
-    uint32_t ovn = 0;
-    uint64_t cap_s = (c->pair_cap + NSHARD - 1) / NSHARD;
-    for (int attempt = 0; attempt < 4; ++attempt) {
-        PairOut O;
-        const uint64_t tot_cap = cap_s * NSHARD;
-        ENSURE(c->d_pf, tot_cap, &O.fst);
-        ENSURE(c->d_ps, tot_cap, &O.snd);
-        ENSURE(c->d_pc, tot_cap, &O.cnt);
-        O.rank = nullptr;
-        if (strict) ENSURE(c->d_pr, tot_cap, &O.rank);
-        ENSURE(c->d_ovl, 2 * nr + 2, &O.overflow_list);
-        O.cursor = cnt->cursor;
-        O.cap_s = cap_s;
-        O.role_pairs = cnt->role_pairs;
-        O.overflow_n = &cnt->overflow_n;
-        O.distinct = cnt->distinct;
-        HIPCHK(hipMemsetAsync(cnt->cursor, 0, 4 * NSHARD * sizeof(unsigned long long), c->stream));
-        HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(uint32_t), c->stream));
-        {
-            StageScope st(c, SA_STAGE_PAIRS);
-            HIPCHK(launch_pair_count(E, PI, P, O, read_order, (nr + 7) & ~7u, c->stream));
-        }
-        HIPCHK(hipMemcpyAsync(cur, cnt->cursor, sizeof(cur), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipMemcpyAsync(&ovn, &cnt->overflow_n, 4, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
-        // reads whose LDS table overflowed (> 1,536 partners: high-copy repeats) are
-        // recounted in 64 partner-residue passes; each pass holds up to 1,536 partners
-        if (ovn > 0 && cur_max() <= cap_s) {
-            const uint32_t split = 64;
-            PairParams P2 = P;
-            P2.split = (int32_t)split;
-            P2.n_items = ovn * split;
-            P2.xcd_swizzle = 0;
-            PairOut O2 = O;
-            O2.role_pairs = cnt->role_pairs_dummy;
-            O2.overflow_list = O.overflow_list + ovn;  // keep the read list intact
-            HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(uint32_t), c->stream));
-            {
-                StageScope st(c, SA_STAGE_PAIRS);
-                HIPCHK(launch_pair_count(E, PI, P2, O2, O.overflow_list, ovn * split, c->stream));
-            }
-            HIPCHK(hipMemcpyAsync(cur, cnt->cursor, sizeof(cur), hipMemcpyDeviceToHost, c->stream));
-            HIPCHK(hipMemcpyAsync(&ovn, &cnt->overflow_n, 4, hipMemcpyDeviceToHost, c->stream));
-            HIPCHK(hipStreamSynchronize(c->stream));
-            if (ovn) return fail(c, SA_E_OVERFLOW, "a read has more than 98,304 distinct partners");
-        }
-        if (cur_max() <= cap_s) break;
-        cap_s = cur_max() + cur_max() / 4 + 1024;  // grow and recount
-        c->pair_cap = cap_s * NSHARD;
-        if (attempt == 3) return fail(c, SA_E_OVERFLOW, "pair output did not fit");
-    }
-    uint64_t np = 0;
-    for (auto v : cur) np += v;
+    uint64_t np = 0, cap_s = 0;
+    rc = pair_stage(c, E, PI, strict, strict || c->keep_pairs, read_order, nr, cnt, np, cap_s);
+    if (rc) return rc;
+    const bool emit_all = strict || c->keep_pairs;
 
     // ---- ordering --------------------------------------------------------
     uint64_t *ok, *ok2; uint32_t *ov, *ov2; uint8_t *otmp;
@@ -657,7 +716,7 @@ int device_build(sa_ctx *c, bool readback) {
 
     c->lead.clear(); c->trail.clear(); c->count.clear();
     c->pfst.clear(); c->psnd.clear(); c->pcnt.clear();
-    if (!strict && !P.emit_all) {
+    if (!strict && !emit_all) {
         c->n_disp = np;
         if (readback && np) {
             c->lead.resize(np); c->trail.resize(np); c->count.resize(np);
@@ -743,25 +802,40 @@ int device_build(sa_ctx *c, bool readback) {
 int device_align(sa_ctx *c, bool readback) {
     if (!c->built) return fail(c, SA_E_STATE, "sa_align before sa_build_candidates");
     const uint64_t nd = c->n_disp;
+    // reads the aligner sees: this device's, or (distributed) the all-gathered set
+    DevReads AR = dev_reads(c);
+    int32_t maxL = c->maxL, minL = c->minL;
+    if (c->dist) {
+        if (!c->dist_reads) return fail(c, SA_E_STATE, "distributed align before sa_dist_set_reads");
+        AR.n = (uint32_t)c->dlen.size();
+        AR.ascii = nullptr;
+        AR.boff = nullptr;
+        AR.woff = (const uint64_t *)c->d_gwoff.p;
+        AR.len = (const int32_t *)c->d_glen.p;
+        AR.codes = (uint32_t *)c->d_gcodes.p;
+        AR.bad = (int32_t *)c->d_gbad.p;
+        maxL = c->gmaxL;
+        minL = c->gminL;
+    }
     const float omm = 1.0f - c->set.min_identity;
-    const float prod = (float)c->maxL * omm;
+    const float prod = (float)maxL * omm;
     const int32_t wmax = std::max(c->set.kmer_size, (int32_t)floor((double)prod) + 1);
     // Lane groups and LDS traceback are sized for the longest read; a pair whose
     // band (w > 63) or lead (> ~2,500 bp) exceeds what this build holds fails in
     // the kernel with SA_E_OVERFLOW -- only if such a pair is actually dispatched.
     const int G = wmax <= 15 ? 16 : (wmax <= 31 ? 32 : 64);
     const uint32_t rw_fit = (160u * 1024u / (256u * 4u) - 1u) | 1u;
-    const uint32_t rw = std::min<uint32_t>((uint32_t)((c->maxL + 1 + 15) / 16) | 1u, rw_fit);
+    const uint32_t rw = std::min<uint32_t>((uint32_t)((maxL + 1 + 15) / 16) | 1u, rw_fit);
     // both kernels hold the cost matrix as int8 bytes (HOXD70 spans -125..100)
     for (int x = 0; x < 16; ++x)
         if (c->set.cost[x] < -128 || c->set.cost[x] > 127)
             return fail(c, SA_E_ARG, "cost matrix entries must lie in [-128, 127]");
     // lane-per-pair kernel: band <= 15 columns, reads <= 30,000 bp (c << 16 | e packing)
-    const bool lane_fits = wmax <= 15 && c->maxL <= 30000;
+    const bool lane_fits = wmax <= 15 && maxL <= 30000;
     if (c->align_kernel == 2 && !lane_fits)
         return fail(c, SA_E_ARG, "SA_OPT_ALIGN_KERNEL=2 but a band or read exceeds the lane kernel");
     const bool use_lane = c->align_kernel == 2 || (c->align_kernel == 0 && lane_fits);
-    const int32_t wmin = std::max(c->set.kmer_size, (int32_t)floor((double)((float)c->minL * omm)) + 1);
+    const int32_t wmin = std::max(c->set.kmer_size, (int32_t)floor((double)((float)minL * omm)) + 1);
     const bool exact = wmin == 15 && wmax == 15;  // every band exactly 16 cells wide
     AlignParams P;
     P.k = c->set.kmer_size;
@@ -790,12 +864,12 @@ int device_align(sa_ctx *c, bool readback) {
             ENSURE(c->d_ovals2, nd, &v1);
             ENSURE(c->d_osort, radix_sort_temp_bytes(nd), &tmp);
             const int32_t *dl = (const int32_t *)c->d_lead.p, *dt = (const int32_t *)c->d_trail.p;
-            HIPCHK(launch_dovetail_p1(dev_reads(c), dl, dt, nd, P, exact, p1, k0, v0, &cnt->err, cnt->cells,
+            HIPCHK(launch_dovetail_p1(AR, dl, dt, nd, P, exact, p1, k0, v0, &cnt->err, cnt->cells,
                                       c->stream));
-            HIPCHK(radix_sort(&k0, &v0, &k1, &v1, nd, 0, bits_for((uint64_t)c->maxL), tmp, c->stream));
-            HIPCHK(launch_dovetail_p2(dev_reads(c), dl, dt, nd, P, exact, p1, v0, out, &cnt->err, c->stream));
+            HIPCHK(radix_sort(&k0, &v0, &k1, &v1, nd, 0, bits_for((uint64_t)maxL), tmp, c->stream));
+            HIPCHK(launch_dovetail_p2(AR, dl, dt, nd, P, exact, p1, v0, out, &cnt->err, c->stream));
         } else
-            HIPCHK(launch_dovetail(dev_reads(c), (const int32_t *)c->d_lead.p, (const int32_t *)c->d_trail.p, nd, P,
+            HIPCHK(launch_dovetail(AR, (const int32_t *)c->d_lead.p, (const int32_t *)c->d_trail.p, nd, P,
                                    G, out, &cnt->err, cnt->cells, c->stream));
     }
     int32_t err = 0;
@@ -890,7 +964,7 @@ void sa_ctx_destroy(sa_ctx *c) {
                     &c->d_gmds, &c->d_gede, &c->d_ogid, &c->d_bkttmp, &c->d_mdidx, &c->d_edidx, &c->d_occidx,
                     &c->d_bnst, &c->d_brank, &c->d_bhash, &c->d_bfirst, &c->d_pf, &c->d_ps, &c->d_pc, &c->d_pr,
                     &c->d_ovl, &c->d_cnt, &c->d_okeys, &c->d_ovals, &c->d_okeys2, &c->d_ovals2, &c->d_osort,
-                    &c->d_lead, &c->d_trail, &c->d_count, &c->d_aln, &c->d_p1, &c->d_rkey, &c->d_rkey2, &c->d_rord, &c->d_rord2, &c->d_rtmp, &c->d_pstart, &c->d_biglist, &c->d_rec,
+                    &c->d_lead, &c->d_trail, &c->d_count, &c->d_aln, &c->d_p1, &c->d_rkey, &c->d_rkey2, &c->d_rord, &c->d_rord2, &c->d_rtmp, &c->d_gocc, &c->d_rid, &c->d_loff, &c->d_starts, &c->d_bounds, &c->d_gcodes, &c->d_gwoff, &c->d_glen, &c->d_gbad, &c->d_psum, &c->d_pkeep, &c->d_ppos, &c->d_scan, &c->d_pstart, &c->d_biglist, &c->d_rec,
                     &c->d_srec, &c->d_bnmd, &c->d_ishead, &c->d_bnst2};
     for (DBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
@@ -1045,6 +1119,301 @@ int sa_reset_stage_times(sa_ctx *c) {
 int sa_sync(sa_ctx *c) {
     if (!c) return SA_E_ARG;
     HIPCHK(hipStreamSynchronize(c->stream));
+    return SA_OK;
+}
+
+// ---------------------------------------------------------------------------
+// sharded hash stage; the exchanges are the caller's
+// ---------------------------------------------------------------------------
+int sa_dist_init(sa_ctx *c, int rank, int nranks, const uint32_t *starts, const int32_t *lengths) {
+    if (!c || !starts || !lengths) return SA_E_ARG;
+    if (nranks < 1 || nranks > 256 || (nranks & (nranks - 1)) || rank < 0 || rank >= nranks)
+        return fail(c, SA_E_ARG, "nranks must be a power of two <= 256 and 0 <= rank < nranks");
+    if (c->set.id_mode == SA_IDS_STRICT) return fail(c, SA_E_ARG, "the sharded path runs in wide-id mode only");
+    const uint32_t N = starts[nranks];
+    for (int r = 0; r < nranks; ++r)
+        if (starts[r + 1] < starts[r]) return fail(c, SA_E_ARG, "rank starts must be non-decreasing");
+    const uint32_t nl = (uint32_t)(c->boff.size() - 1);
+    if (starts[0] != 0 || starts[rank + 1] - starts[rank] != nl)
+        return fail(c, SA_E_ARG, "this rank's read count does not match starts[rank+1] - starts[rank]");
+    for (uint32_t i = 0; i < nl; ++i)
+        if ((int64_t)(c->boff[i + 1] - c->boff[i]) != (int64_t)lengths[starts[rank] + i])
+            return fail(c, SA_E_ARG, "lengths[] disagrees with this rank's reads");
+    const int k = c->set.kmer_size;
+    c->dist = true;
+    c->dist_reads = false;
+    c->rank = rank;
+    c->nranks = nranks;
+    c->log_ranks = 0;
+    while ((1 << c->log_ranks) < nranks) ++c->log_ranks;
+    c->dstarts.assign(starts, starts + nranks + 1);
+    c->dlen.assign(lengths, lengths + N);
+    c->gocc.assign((size_t)N + 1, 0);
+    c->gmaxL = 0;
+    c->gminL = N ? INT32_MAX : 0;
+    int32_t uni = -1;
+    bool uniform = N > 0;
+    for (uint32_t i = 0; i < N; ++i) {
+        const int32_t L = lengths[i];
+        if (L < 0) return fail(c, SA_E_ARG, "negative read length");
+        c->gocc[i + 1] = c->gocc[i] + (uint64_t)(L - k + 1 > 0 ? L - k + 1 : 0);
+        c->gmaxL = std::max(c->gmaxL, L);
+        c->gminL = std::min(c->gminL, L);
+        if (uni < 0) uni = L;
+        if (L != uni || L < k) uniform = false;
+    }
+    if (c->gocc[N] >= 0xFFFFFFF0ull) return fail(c, SA_E_OVERFLOW, "more than 2^32 k-mers in the global read set");
+    c->gnpr = uniform ? (uint32_t)(uni - k + 1) : 0;
+    c->reads_dirty = true;  // loc tables come from all lengths now
+    c->built = c->aligned = false;
+    (void)hipSetDevice(c->device);
+    uint64_t *gocc;
+    uint32_t *st;
+    ENSURE(c->d_gocc, (size_t)N + 1, &gocc);
+    ENSURE(c->d_starts, (size_t)nranks + 1, &st);
+    HIPCHK(hipMemcpy(gocc, c->gocc.data(), ((size_t)N + 1) * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(st, c->dstarts.data(), ((size_t)nranks + 1) * 4, hipMemcpyHostToDevice));
+    return SA_OK;
+}
+
+int sa_dist_local_kmers(sa_ctx *c, uint64_t *n) {
+    if (!c || !n) return SA_E_ARG;
+    if (!c->dist) return fail(c, SA_E_STATE, "sa_dist_init first");
+    (void)hipSetDevice(c->device);
+    int rc = ensure_prepared(c);
+    if (rc) return rc;
+    *n = c->n_occ;
+    return SA_OK;
+}
+
+int sa_dist_emit(sa_ctx *c, void *send_keys, void *send_vals, uint64_t *counts) {
+    if (!c || !counts) return SA_E_ARG;
+    if (!c->dist) return fail(c, SA_E_STATE, "sa_dist_init first");
+    (void)hipSetDevice(c->device);
+    int rc = ensure_prepared(c);
+    if (rc) return rc;
+    c->built = c->aligned = false;
+    const uint64_t n = c->n_occ;
+    if (n && (!send_keys || !send_vals)) return SA_E_ARG;
+    DevReads R = dev_reads(c);
+    EmitParams E = emit_params(c);
+    E.g_base = (uint32_t)c->gocc[c->dstarts[c->rank]];
+    uint64_t *keys, *keys2; uint32_t *vals, *vals2; uint8_t *stmp;
+    ENSURE(c->d_keys, n, &keys);
+    ENSURE(c->d_vals, n, &vals);
+    ENSURE(c->d_sorttmp, std::max(radix_sort_temp_bytes(n), buckets_temp_bytes(n)), &stmp);
+    {
+        StageScope st(c, SA_STAGE_PACK);
+        HIPCHK(launch_pack_reads(R, c->stream));
+    }
+    {
+        StageScope st(c, SA_STAGE_EMIT);
+        HIPCHK(launch_kmer_emit(R, E, keys, vals, c->stream));
+    }
+    // owner = top log2(P) bits of the mixed hash: one stable radix pass groups
+    // the records by owner and keeps them in occurrence order within each
+    const int kbits = 32 + c->lb;
+    keys2 = (uint64_t *)send_keys;
+    vals2 = (uint32_t *)send_vals;
+    {
+        StageScope st(c, SA_STAGE_SORT);
+        if (c->log_ranks > 0) HIPCHK(radix_sort(&keys, &vals, &keys2, &vals2, n, kbits - c->log_ranks, kbits, stmp,
+                                                c->stream));
+        if (keys != (uint64_t *)send_keys && n) {
+            HIPCHK(hipMemcpyAsync(send_keys, keys, n * 8, hipMemcpyDeviceToDevice, c->stream));
+            HIPCHK(hipMemcpyAsync(send_vals, vals, n * 4, hipMemcpyDeviceToDevice, c->stream));
+        }
+    }
+    uint64_t *bounds;
+    ENSURE(c->d_bounds, (size_t)c->nranks + 1, &bounds);
+    std::vector<uint64_t> b((size_t)c->nranks + 1, 0);
+    if (n) {
+        HIPCHK(launch_owner_bounds((const uint64_t *)send_keys, n, kbits - c->log_ranks, (uint32_t)c->nranks, bounds,
+                                   c->stream));
+        HIPCHK(hipMemcpyAsync(b.data(), bounds, b.size() * 8, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPCHK(hipStreamSynchronize(c->stream));
+    b[c->nranks] = n;
+    for (int o = 0; o < c->nranks; ++o) counts[o] = b[o + 1] - b[o];
+    c->stats = sa_stats{};
+    c->stats.kmers = n;
+    c->stats.id_mode = SA_IDS_WIDE;
+    return SA_OK;
+}
+
+int sa_dist_count(sa_ctx *c, void *recv_keys, void *recv_vals, uint64_t n, uint64_t *counts) {
+    if (!c || !counts || (n && (!recv_keys || !recv_vals))) return SA_E_ARG;
+    if (!c->dist) return fail(c, SA_E_STATE, "sa_dist_init first");
+    (void)hipSetDevice(c->device);
+    int rc = ensure_prepared(c);
+    if (rc) return rc;
+    const uint32_t N = (uint32_t)c->dlen.size();
+    Counters *cnt;
+    ENSURE(c->d_cnt, 1, &cnt);
+    HIPCHK(hipMemsetAsync(cnt, 0, sizeof(Counters), c->stream));
+    // received records are in global occurrence order (sources in rank order,
+    // each in occurrence order): local index i <-> i-th owned occurrence
+    uint32_t *rid, *vals, *vals2; uint64_t *loff, *keys2; uint8_t *stmp;
+    ENSURE(c->d_rid, n, &rid);
+    ENSURE(c->d_loff, (size_t)N + 1, &loff);
+    ENSURE(c->d_vals, n, &vals);
+    ENSURE(c->d_vals2, n, &vals2);
+    ENSURE(c->d_keys2, n, &keys2);
+    ENSURE(c->d_sorttmp, std::max(radix_sort_temp_bytes(n), buckets_temp_bytes(n)), &stmp);
+    uint64_t *keys = (uint64_t *)recv_keys;
+    {
+        StageScope st(c, SA_STAGE_EMIT);
+        HIPCHK(launch_read_ids((const uint32_t *)recv_vals, n, (const uint64_t *)c->d_gocc.p, N, c->gnpr, rid,
+                               c->stream));
+        HIPCHK(launch_local_offsets(rid, n, N, loff, c->stream));
+        HIPCHK(launch_iota(vals, n, c->stream));
+    }
+    PartArgs PA{};
+    unsigned long long big_buckets = 0;
+    rc = bucket_stage(c, keys, vals, keys2, vals2, n, loff, N, 0, rid, false, stmp, cnt, PA, big_buckets);
+    if (rc) return rc;
+    PairIn PI{};
+    PI.rec = PA.rec; PI.md_list = PA.md_list; PI.ed_list = PA.ed_list;
+    EmitParams E = emit_params(c);
+    E.occ_off = loff;  // occurrences of read a on this rank: [loff[a], loff[a+1])
+    uint64_t np = 0, cap_s = 0;
+    rc = pair_stage(c, E, PI, false, true, nullptr, N, cnt, np, cap_s);
+    if (rc) return rc;
+    // partials grouped by the rank owning their lead: ascending (lead, trail)
+    uint64_t *ok, *ok2; uint32_t *ov, *ov2; uint8_t *otmp; uint64_t *bounds;
+    ENSURE(c->d_okeys, np, &ok);
+    ENSURE(c->d_okeys2, np, &ok2);
+    ENSURE(c->d_ovals, np, &ov);
+    ENSURE(c->d_ovals2, np, &ov2);
+    ENSURE(c->d_osort, radix_sort_temp_bytes(np), &otmp);
+    ENSURE(c->d_bounds, (size_t)c->nranks + 1, &bounds);
+    const int idb = bits_for(N ? N - 1 : 0);
+    std::vector<uint64_t> b((size_t)c->nranks + 1, 0);
+    {
+        StageScope st(c, SA_STAGE_ORDER);
+        HIPCHK(launch_make_order_keys((const uint32_t *)c->d_pf.p, (const uint32_t *)c->d_ps.p, nullptr, cnt->cursor,
+                                      cap_s, 2, idb, ok, ov, cnt->shard_off, c->stream));
+        HIPCHK(radix_sort(&ok, &ov, &ok2, &ov2, np, 0, 2 * idb, otmp, c->stream));
+        if (np) HIPCHK(launch_lead_bounds(ok, np, idb, (const uint32_t *)c->d_starts.p, (uint32_t)c->nranks, bounds,
+                                          c->stream));
+    }
+    Counters hc;
+    HIPCHK(hipMemcpyAsync(&hc, cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+    if (np) HIPCHK(hipMemcpyAsync(b.data(), bounds, b.size() * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    resolve_timing(c);
+    b[c->nranks] = np;
+    for (int o = 0; o < c->nranks; ++o) counts[o] = b[o + 1] - b[o];
+    c->part_np = np;
+    c->part_perm = ov;
+    c->stats.buckets = shard_sum(hc.bkt_counts) + big_buckets;
+    c->stats.role_pairs = shard_sum(hc.role_pairs);
+    return SA_OK;
+}
+
+int sa_dist_partials(sa_ctx *c, void *fst, void *snd, void *cnt_out) {
+    if (!c) return SA_E_ARG;
+    if (!c->dist) return fail(c, SA_E_STATE, "sa_dist_init first");
+    if (c->part_np && (!fst || !snd || !cnt_out)) return SA_E_ARG;
+    (void)hipSetDevice(c->device);
+    HIPCHK(launch_gather_partials(c->part_perm, c->part_np, (const uint32_t *)c->d_pf.p, (const uint32_t *)c->d_ps.p,
+                                  (const uint32_t *)c->d_pc.p, (uint32_t *)fst, (uint32_t *)snd, (uint32_t *)cnt_out,
+                                  c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return SA_OK;
+}
+
+int sa_dist_reduce(sa_ctx *c, const void *fst, const void *snd, const void *cnt_in, uint64_t n) {
+    if (!c || (n && (!fst || !snd || !cnt_in))) return SA_E_ARG;
+    if (!c->dist) return fail(c, SA_E_STATE, "sa_dist_init first");
+    (void)hipSetDevice(c->device);
+    const uint32_t N = (uint32_t)c->dlen.size();
+    const int idb = bits_for(N ? N - 1 : 0);
+    Counters *cnt;
+    ENSURE(c->d_cnt, 1, &cnt);
+    uint64_t *ok, *ok2; uint32_t *ov, *ov2, *sum, *keep, *pos; uint8_t *otmp, *scan;
+    ENSURE(c->d_okeys, n, &ok);
+    ENSURE(c->d_okeys2, n, &ok2);
+    ENSURE(c->d_ovals, n, &ov);
+    ENSURE(c->d_ovals2, n, &ov2);
+    ENSURE(c->d_osort, radix_sort_temp_bytes(n), &otmp);
+    ENSURE(c->d_psum, n, &sum);
+    ENSURE(c->d_pkeep, n, &keep);
+    ENSURE(c->d_ppos, n, &pos);
+    ENSURE(c->d_scan, scan_temp_bytes(n), &scan);
+    HIPCHK(hipMemsetAsync(cnt->distinct, 0, sizeof(cnt->distinct), c->stream));
+    HIPCHK(hipMemsetAsync(cnt->totals, 0, sizeof(cnt->totals), c->stream));
+    {
+        StageScope st(c, SA_STAGE_ORDER);
+        HIPCHK(launch_reduce_keys((const uint32_t *)fst, (const uint32_t *)snd, n, idb, ok, ov, c->stream));
+        HIPCHK(radix_sort(&ok, &ov, &ok2, &ov2, n, 0, 2 * idb, otmp, c->stream));
+        HIPCHK(launch_reduce_heads(ok, ov, n, (const uint32_t *)cnt_in, c->set.min_collisions, c->set.max_collisions,
+                                   sum, keep, cnt->distinct, c->stream));
+        if (n) HIPCHK(exclusive_scan_u32(keep, pos, n, &cnt->totals[0], scan, c->stream));
+    }
+    uint32_t nd = 0;
+    HIPCHK(hipMemcpyAsync(&nd, &cnt->totals[0], 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    int32_t *dlead, *dtrail, *dcount;
+    ENSURE(c->d_lead, nd, &dlead);
+    ENSURE(c->d_trail, nd, &dtrail);
+    ENSURE(c->d_count, nd, &dcount);
+    HIPCHK(launch_reduce_compact(ok, n, idb, sum, keep, pos, dlead, dtrail, dcount, c->stream));
+    Counters hc;
+    HIPCHK(hipMemcpyAsync(&hc, cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    resolve_timing(c);
+    c->n_disp = nd;
+    c->lead.clear(); c->trail.clear(); c->count.clear();
+    c->pfst.clear(); c->psnd.clear(); c->pcnt.clear();
+    c->stats.pairs = shard_sum(hc.distinct);
+    c->stats.dispatched = nd;
+    c->stats.id_mode = SA_IDS_WIDE;
+    c->mode = SA_IDS_WIDE;
+    c->built = true;
+    c->aligned = false;
+    return SA_OK;
+}
+
+int sa_dist_codes(sa_ctx *c, void *codes, void *bad, uint64_t *nwords) {
+    if (!c || !nwords) return SA_E_ARG;
+    if (!c->dist) return fail(c, SA_E_STATE, "sa_dist_init first");
+    (void)hipSetDevice(c->device);
+    int rc = ensure_prepared(c);
+    if (rc) return rc;
+    const uint32_t nl = (uint32_t)(c->boff.size() - 1);
+    const uint64_t nw = c->woff[nl];
+    *nwords = nw;
+    if (!codes && !bad) return SA_OK;
+    DevReads R = dev_reads(c);
+    HIPCHK(launch_pack_reads(R, c->stream));  // idempotent; the codes may not exist yet
+    if (codes && nw) HIPCHK(hipMemcpyAsync(codes, c->d_codes.p, nw * 4, hipMemcpyDeviceToDevice, c->stream));
+    if (bad && nl) HIPCHK(hipMemcpyAsync(bad, c->d_bad.p, (size_t)nl * 4, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return SA_OK;
+}
+
+int sa_dist_set_reads(sa_ctx *c, const void *codes, const void *bad, uint64_t nwords) {
+    if (!c) return SA_E_ARG;
+    if (!c->dist) return fail(c, SA_E_STATE, "sa_dist_init first");
+    (void)hipSetDevice(c->device);
+    const uint32_t N = (uint32_t)c->dlen.size();
+    std::vector<uint64_t> gw((size_t)N + 1, 0);
+    for (uint32_t i = 0; i < N; ++i) gw[i + 1] = gw[i] + (uint64_t)((c->dlen[i] + 15) / 16);
+    if (gw[N] != nwords) return fail(c, SA_E_ARG, "word count does not match the global read lengths");
+    if ((nwords && !codes) || (N && !bad)) return SA_E_ARG;
+    uint32_t *gcodes; uint64_t *gwoff; int32_t *glen, *gbad;
+    ENSURE(c->d_gcodes, nwords + 2, &gcodes);  // pad: windows read past a read's last word
+    ENSURE(c->d_gwoff, (size_t)N + 1, &gwoff);
+    ENSURE(c->d_glen, (size_t)N + 1, &glen);
+    ENSURE(c->d_gbad, (size_t)N + 1, &gbad);
+    HIPCHK(hipMemsetAsync(gcodes + nwords, 0, 8, c->stream));
+    if (nwords) HIPCHK(hipMemcpyAsync(gcodes, codes, nwords * 4, hipMemcpyDeviceToDevice, c->stream));
+    if (N) HIPCHK(hipMemcpyAsync(gbad, bad, (size_t)N * 4, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(gwoff, gw.data(), gw.size() * 8, hipMemcpyHostToDevice, c->stream));
+    if (N) HIPCHK(hipMemcpyAsync(glen, c->dlen.data(), (size_t)N * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->dist_reads = true;
     return SA_OK;
 }
 

@@ -93,7 +93,7 @@ __global__ __launch_bounds__(256) void kmer_emit_kernel(DevReads r, EmitParams e
             const uint32_t h = mix32(x);
             kmin = min(kmin, h);
             keys[g0 + i] = ((uint64_t)h << e.lb) | (uint64_t)lr[i];
-            vals[g0 + i] = (uint32_t)(g0 + i);
+            vals[g0 + i] = (uint32_t)(g0 + i) + e.g_base;
         }
         if (e.rkey) {
             // locality key: reads sharing their minimum k-mer overlap, so sorting

@@ -306,7 +306,11 @@ __global__ void make_order_keys_kernel(const uint32_t *fst, const uint32_t *snd,
     const uint32_t pos = off[shard] + (uint32_t)j;
     // wide: lead descending then trail ascending; strict: first-occurrence rank
     const uint64_t top = (1ull << idbits) - 1;
-    keys[pos] = by_rank ? rank[i] : (((top - fst[i]) << idbits) | snd[i]);
+    // by_rank 0: lead descending, trail ascending (wide canonical order);
+    // 1: first-occurrence rank (strict); 2: lead ascending (distributed send side)
+    keys[pos] = by_rank == 1 ? rank[i]
+              : by_rank == 2 ? (((uint64_t)fst[i] << idbits) | snd[i])
+                             : (((top - fst[i]) << idbits) | snd[i]);
     vals[pos] = (uint32_t)i;
 }
 

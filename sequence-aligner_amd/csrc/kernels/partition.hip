@@ -23,7 +23,9 @@
 
 namespace sa {
 
-__device__ __forceinline__ uint32_t read_of_g(uint32_t g, const uint64_t *occ_off, uint32_t n_reads, uint32_t npr) {
+__device__ __forceinline__ uint32_t read_of_g(uint32_t g, const uint64_t *occ_off, uint32_t n_reads, uint32_t npr,
+                                              const uint32_t *rid) {
+    if (rid) return rid[g];  // distributed mode: occurrence index -> global read id
     if (npr) return g / npr;
     uint32_t lo = 0, hi = n_reads;  // largest r with occ_off[r] <= g
     while (hi - lo > 1) {
@@ -281,7 +283,7 @@ __global__ __launch_bounds__(PB_THREADS) void part_build_kernel(PartArgs A, uint
         if (isg) { gh = s; ++ng; }
         const uint32_t t = tagv[j];
         const uint32_t g = S.g[s];
-        const uint32_t r = read_of_g(g, A.occ_off, A.n_reads, A.npr);
+        const uint32_t r = read_of_g(g, A.occ_off, A.n_reads, A.npr, A.rid);
         const uint32_t st = (t & TAG_ST) ? 1u : 0u, en = (t & TAG_EN) ? 1u : 0u, md = (t & TAG_MD) ? 1u : 0u;
         const uint32_t mpos = ps + S.mdx[s], epos = 2 * ps + S.edx[s];
         if (!(A.ablate & 4)) {

@@ -33,6 +33,7 @@ struct EmitParams {
     int32_t maxd;
     uint64_t *rkey;            // [n] per-read locality key (min k-mer mix; nullable)
     uint32_t *rord;            // [n] read ids (sort payload for rkey)
+    uint32_t g_base;           // occurrence index of this device's first k-mer (distributed mode)
 };
 
 // bijective 32-bit mix of the seqHash: equal mix <=> equal hash, so a bucket
@@ -141,8 +142,8 @@ hipError_t exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, uin
 size_t buckets_temp_bytes(uint64_t n);
 hipError_t build_buckets(const uint64_t *skeys, const uint32_t *svals, uint64_t n, int lb,
                          const uint8_t *tagtab, const uint64_t *occ_off, uint32_t n_reads,
-                         uint32_t uniform_npr, Buckets &b, uint32_t *totals_dev, void *tmp,
-                         hipStream_t s);
+                         uint32_t uniform_npr, const uint32_t *rid, Buckets &b, uint32_t *totals_dev,
+                         void *tmp, hipStream_t s);
 hipError_t build_strict_index(const uint64_t *skeys, const uint32_t *svals, uint64_t n, int lb,
                               const uint8_t *tagtab, Buckets &b, hipStream_t s);
 
@@ -161,6 +162,7 @@ struct PartArgs {
     const uint8_t *tagtab;
     const uint64_t *occ_off;
     uint32_t n_reads, npr;
+    const uint32_t *rid;         // read id by occurrence index (distributed mode) or null
     uint32_t *md_list, *ed_list;
     uint4 *rec;                  // [n_occ] by g
     uint32_t *big_list, *big_n;
@@ -200,5 +202,24 @@ hipError_t launch_dovetail_p1(const DevReads &r, const int32_t *lead, const int3
 hipError_t launch_dovetail_p2(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
                               const AlignParams &p, bool exact, const int32_t *p1, const uint32_t *order,
                               DevAlignment *out, int32_t *err, hipStream_t s);
+
+// distributed (multi-GPU) glue, dist.hip
+hipError_t launch_iota(uint32_t *v, uint64_t n, hipStream_t s);
+hipError_t launch_read_ids(const uint32_t *g, uint64_t n, const uint64_t *occ_off, uint32_t n_reads, uint32_t npr,
+                           uint32_t *rid, hipStream_t s);
+hipError_t launch_local_offsets(const uint32_t *rid, uint64_t n, uint32_t n_reads, uint64_t *loff, hipStream_t s);
+hipError_t launch_owner_bounds(const uint64_t *keys, uint64_t n, int shift, uint32_t P, uint64_t *bounds,
+                               hipStream_t s);
+hipError_t launch_lead_bounds(const uint64_t *keys, uint64_t n, int idb, const uint32_t *starts, uint32_t P,
+                              uint64_t *bounds, hipStream_t s);
+hipError_t launch_gather_partials(const uint32_t *perm, uint64_t n, const uint32_t *fst, const uint32_t *snd,
+                                  const uint32_t *cnt, uint32_t *of, uint32_t *os, uint32_t *oc, hipStream_t s);
+hipError_t launch_reduce_keys(const uint32_t *fst, const uint32_t *snd, uint64_t n, int idb, uint64_t *keys,
+                              uint32_t *vals, hipStream_t s);
+hipError_t launch_reduce_heads(const uint64_t *skeys, const uint32_t *sidx, uint64_t n, const uint32_t *cnt,
+                               int32_t min_c, int32_t max_c, uint32_t *sum, uint32_t *keep,
+                               unsigned long long *distinct, hipStream_t s);
+hipError_t launch_reduce_compact(const uint64_t *skeys, uint64_t n, int idb, const uint32_t *sum, const uint32_t *keep,
+                                 const uint32_t *pos, int32_t *lead, int32_t *trail, int32_t *count, hipStream_t s);
 
 }  // namespace sa

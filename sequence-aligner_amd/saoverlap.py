@@ -35,7 +35,8 @@ EXPORTS = ("sa_default_settings", "sa_ctx_create", "sa_ctx_destroy", "sa_last_er
            "sa_add_reads", "sa_read_fasta", "sa_num_reads", "sa_build_candidates", "sa_get_dispatch",
            "sa_get_pairs", "sa_align", "sa_get_alignments", "sa_write_ovl", "sa_get_ovl", "sa_set_option",
            "sa_get_stats", "sa_get_stage_times", "sa_reset_stage_times", "sa_device_build", "sa_device_align",
-           "sa_sync")
+           "sa_sync", "sa_dist_init", "sa_dist_local_kmers", "sa_dist_emit", "sa_dist_count", "sa_dist_partials",
+           "sa_dist_reduce", "sa_dist_codes", "sa_dist_set_reads")
 
 
 class Settings(C.Structure):
@@ -89,6 +90,14 @@ def lib():
         L.sa_set_option.argtypes = [vp, C.c_int, C.c_int64]
         L.sa_get_stats.argtypes = [vp, P(Stats)]
         L.sa_get_stage_times.argtypes = [vp, P(C.c_double), P(C.c_uint64), C.c_int]
+        L.sa_dist_init.argtypes = [vp, C.c_int, C.c_int, P(C.c_uint32), P(C.c_int32)]
+        L.sa_dist_local_kmers.argtypes = [vp, P(C.c_uint64)]
+        L.sa_dist_emit.argtypes = [vp, vp, vp, P(C.c_uint64)]
+        L.sa_dist_count.argtypes = [vp, vp, vp, C.c_uint64, P(C.c_uint64)]
+        L.sa_dist_partials.argtypes = [vp, vp, vp, vp]
+        L.sa_dist_reduce.argtypes = [vp, vp, vp, vp, C.c_uint64]
+        L.sa_dist_codes.argtypes = [vp, vp, vp, P(C.c_uint64)]
+        L.sa_dist_set_reads.argtypes = [vp, vp, vp, C.c_uint64]
         _lib = L
     return _lib
 
@@ -241,3 +250,45 @@ class Overlapper:
 
     def reset_stage_times(self):
         self._chk(lib().sa_reset_stage_times(self.h))
+
+    # ---- sharded hash stage (include/sa_overlap.h, sa_dist_*); buffers are
+    # device pointers (ints), e.g. torch_tensor.data_ptr() on this context's GPU
+    def dist_init(self, rank, nranks, starts, lengths):
+        st = np.ascontiguousarray(starts, dtype=np.uint32)
+        ln = np.ascontiguousarray(lengths, dtype=np.int32)
+        self._chk(lib().sa_dist_init(self.h, rank, nranks, st.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                     ln.ctypes.data_as(C.POINTER(C.c_int32))))
+        self.nranks = nranks
+
+    def dist_local_kmers(self):
+        n = C.c_uint64()
+        self._chk(lib().sa_dist_local_kmers(self.h, C.byref(n)))
+        return n.value
+
+    def _counts(self):
+        return (C.c_uint64 * self.nranks)()
+
+    def dist_emit(self, send_keys, send_vals):
+        cnt = self._counts()
+        self._chk(lib().sa_dist_emit(self.h, send_keys, send_vals, cnt))
+        return np.array(cnt[:], dtype=np.int64)
+
+    def dist_count(self, recv_keys, recv_vals, n):
+        cnt = self._counts()
+        self._chk(lib().sa_dist_count(self.h, recv_keys, recv_vals, n, cnt))
+        return np.array(cnt[:], dtype=np.int64)
+
+    def dist_partials(self, fst, snd, cnt):
+        self._chk(lib().sa_dist_partials(self.h, fst, snd, cnt))
+
+    def dist_reduce(self, fst, snd, cnt, n):
+        self._chk(lib().sa_dist_reduce(self.h, fst, snd, cnt, n))
+
+    def dist_codes(self, codes=None, bad=None):
+        nw = C.c_uint64()
+        self._chk(lib().sa_dist_codes(self.h, codes, bad, C.byref(nw)))
+        return nw.value
+
+    def dist_set_reads(self, codes, bad, nwords):
+        self._chk(lib().sa_dist_set_reads(self.h, codes, bad, nwords))
+

@@ -1,0 +1,142 @@
+"""dist_model.py -- a numpy model of one rank of the sharded hash stage, with the
+same worker interface as sharded.HipWorker (test infrastructure only).
+
+It restates the reference semantics the sharded protocol has to preserve:
+seqHash over min(16, k) chars (ObjectStore.scala:48-67), float32 loc = i/(L-k)
+and the st / md / en tags (BioLibs.scala:56-58, KmerTable.scala:106-115),
+role pairs st x md and en x md per bucket with fst = the larger loc, ties to
+the md occurrence, same-read pairs skipped (KmerTable.scala:57-80, :118-128),
+and the [min, max] collision filter (:155-187), in wide-id form.  Records are
+owned by a hash of the bucket; the orchestrator moves them between ranks.
+"""
+import numpy as np
+
+CODE = {"A": 0, "C": 1, "T": 2, "G": 3}
+
+
+def seq_hash(s):
+    h = 0
+    for ch in s:
+        h = ((h << 2) ^ CODE.get(ch, 0)) & 0xFFFFFFFF
+    return h
+
+
+class NumpyWorker:
+    device_kind = "cpu"
+
+    def __init__(self, reads, k=15, edge=0.4, center=0.4, min_c=7, max_c=222):
+        self.reads = [r.upper() for r in reads]
+        self.k, self.m = k, min(16, k)
+        f32 = np.float32
+        self.head, self.tail = f32(edge), f32(1.0) - f32(edge)
+        half = f32(center) * f32(0.5)
+        self.mid_lo, self.mid_hi = f32(0.5) - half, f32(0.5) + half
+        self.min_c, self.max_c = min_c, max_c
+        self.lead = self.trail = self.dcount = np.zeros(0, dtype=np.int32)
+        self.role_pairs = 0
+
+    def init(self, rank, nranks, starts, lengths):
+        self.rank, self.P = rank, nranks
+        self.starts = np.asarray(starts, dtype=np.int64)
+        lengths = np.asarray(lengths, dtype=np.int64)
+        self.gocc = np.concatenate([[0], np.cumsum(np.maximum(lengths - self.k + 1, 0))]).astype(np.int64)
+        self.logp = int(nranks).bit_length() - 1
+
+    def _owner(self, h):
+        return 0 if self.logp == 0 else ((h * 0x9E3779B1) & 0xFFFFFFFF) >> (32 - self.logp)
+
+    def local_kmers(self):
+        return int(sum(max(len(r) - self.k + 1, 0) for r in self.reads))
+
+    def emit(self, send_keys, send_vals):
+        recs = []
+        g = int(self.gocc[self.starts[self.rank]])
+        for r in self.reads:
+            d = len(r) - self.k
+            for i in range(d + 1):
+                h = seq_hash(r[i:i + self.m])
+                loc = np.float32(i) / np.float32(d) if d > 0 else np.float32("nan")
+                key = (h << 32) | int(np.array(loc, dtype=np.float32).view(np.uint32))
+                recs.append((self._owner(h), g, key))
+                g += 1
+        recs.sort(key=lambda x: x[0])  # stable: occurrence order within an owner
+        n = len(recs)
+        if n:
+            send_keys[:n].copy_(_t(np.array([x[2] for x in recs], dtype=np.uint64).view(np.int64)))
+            send_vals[:n].copy_(_t(np.array([x[1] for x in recs], dtype=np.uint32).view(np.int32)))
+        counts = np.zeros(self.P, dtype=np.int64)
+        for o, _, _ in recs:
+            counts[o] += 1
+        return counts
+
+    def _tags(self, loc):
+        st = loc <= self.head
+        md = (self.mid_lo <= loc) and (loc <= self.mid_hi)
+        en = self.tail <= loc
+        return st, md, en
+
+    def count(self, recv_keys, recv_vals, n):
+        keys = recv_keys[:n].numpy().view(np.uint64)
+        g = recv_vals[:n].numpy().view(np.uint32).astype(np.int64)
+        rid = np.searchsorted(self.gocc, g, side="right") - 1
+        buckets = {}
+        for key, r in zip(keys.tolist(), rid.tolist()):
+            h = key >> 32
+            loc = np.array(key & 0xFFFFFFFF, dtype=np.uint32).view(np.float32)[()]
+            buckets.setdefault(h, []).append((r, loc))
+        pairs = {}
+        rp = 0
+        for occ in buckets.values():
+            st, md, en = [], [], []
+            for r, loc in occ:
+                if np.isnan(loc):
+                    continue
+                s_, m_, e_ = self._tags(loc)
+                if s_:
+                    st.append((r, loc))
+                if m_:
+                    md.append((r, loc))
+                if e_:
+                    en.append((r, loc))
+            for edge_list in (st, en):
+                for ra, la in edge_list:
+                    for rb, lb in md:
+                        rp += 1
+                        if ra == rb:
+                            continue
+                        fst, snd = (ra, rb) if la > lb else (rb, ra)  # tie: md occurrence first
+                        pairs[(fst, snd)] = pairs.get((fst, snd), 0) + 1
+        self.role_pairs = rp
+        items = sorted(pairs.items())
+        self._pf = np.array([a for (a, _), _ in items], dtype=np.int32)
+        self._ps = np.array([b for (_, b), _ in items], dtype=np.int32)
+        self._pc = np.array([c for _, c in items], dtype=np.int32)
+        owner = np.searchsorted(self.starts, self._pf, side="right") - 1
+        return np.bincount(owner, minlength=self.P).astype(np.int64)
+
+    def partials(self, fst, snd, cnt):
+        n = len(self._pf)
+        if n:
+            fst[:n].copy_(_t(self._pf))
+            snd[:n].copy_(_t(self._ps))
+            cnt[:n].copy_(_t(self._pc))
+
+    def reduce(self, fst, snd, cnt, n):
+        f, s, c = fst[:n].numpy(), snd[:n].numpy(), cnt[:n].numpy()
+        tot = {}
+        for a, b, x in zip(f.tolist(), s.tolist(), c.tolist()):
+            tot[(a, b)] = tot.get((a, b), 0) + x
+        keep = sorted(((a, b, x) for (a, b), x in tot.items() if self.min_c <= x <= self.max_c),
+                      key=lambda t: (-t[0], t[1]))
+        self.lead = np.array([a + 1 for a, _, _ in keep], dtype=np.int32)
+        self.trail = np.array([b + 1 for _, b, _ in keep], dtype=np.int32)
+        self.dcount = np.array([x for _, _, x in keep], dtype=np.int32)
+        self.distinct = len(tot)
+
+    def stats(self):
+        return {"role_pairs": self.role_pairs, "dispatched": len(self.lead)}
+
+
+def _t(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a))

@@ -318,3 +318,60 @@ def test_bench_scale_properties():
     assert (np.diff(d1[0]) <= 0).all()
     same = np.diff(d1[0]) == 0
     assert (np.diff(d1[1])[same] > 0).all()
+
+
+def _hip_rank_main(rank, P, port, reads, starts, st, outdir):
+    import torch
+    import torch.distributed as dist
+
+    import saoverlap as sao_
+    from sharded import HipWorker, ShardedOverlapper
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=P)
+    try:
+        torch.cuda.set_device(0)
+        ov = sao_.Overlapper(id_mode=sao_.SA_IDS_WIDE, **st)
+        ov.add_reads(reads[starts[rank]:starts[rank + 1]])
+        so = ShardedOverlapper(HipWorker(ov), rank, P, starts, [len(r) for r in reads], "cuda:0")
+        so.build()
+        so.build()  # buffers reused
+        lead, trail, count = ov.dispatch()
+        so.gather_reads()
+        ov.align()
+        s = ov.stats()
+        np.savez(os.path.join(outdir, "h%d.npz" % rank), lead=lead, trail=trail, count=count, al=ov.alignments(),
+                 ovl=np.frombuffer(ov.ovl(), dtype=np.uint8), rp=np.int64(s["role_pairs"]))
+        ov.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("P", [2, 4])
+def test_sharded_hip_matches_single_gpu(P, tmp_path):
+    """P processes share the GPU (gloo, host-staged exchanges) and run the
+    sharded stage on the HIP path: the ranks' dispatch, alignments and .ovl in
+    descending rank order equal the single-context wide-id run exactly."""
+    import socket
+
+    import torch.multiprocessing as mp
+    rng = np.random.default_rng(70 + P)
+    reads = mutate(H.synth_reads(1200, 300, 18000, gc=0.5, seed=71 + P, mixed=(250, 340)), rng, 3)
+    st = dict(kmer_size=15, min_collisions=5)
+    cut = [0] + [int(len(reads) * f) for f in np.linspace(0.2, 0.75, P - 1)] + [len(reads)]
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_hip_rank_main, args=(P, port, reads, cut, st, str(tmp_path)), nprocs=P)
+    res = [np.load(os.path.join(str(tmp_path), "h%d.npz" % r)) for r in range(P)]
+    order = list(range(P - 1, -1, -1))
+    ref = gpu_run(reads=reads, wide=True, keep_pairs=False, **st)
+    lead, trail, count = ref.dispatch()
+    assert len(lead) > 1000
+    np.testing.assert_array_equal(np.concatenate([res[r]["lead"] for r in order]), lead)
+    np.testing.assert_array_equal(np.concatenate([res[r]["trail"] for r in order]), trail)
+    np.testing.assert_array_equal(np.concatenate([res[r]["count"] for r in order]), count)
+    np.testing.assert_array_equal(np.concatenate([res[r]["al"] for r in order]), ref.alignments())
+    assert b"".join(res[r]["ovl"].tobytes() for r in order) == ref.ovl()
+    assert sum(int(x["rp"]) for x in res) == ref.stats()["role_pairs"]
