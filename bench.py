@@ -1,8 +1,8 @@
 """bench.py -- MI355X hash-overlap stage benchmark (BASELINE.json configs[1] and [2]).
 
 Workload: a synthetic splitmix64 genome of
-2.5 Mbp per GPU (GC 0.50, seed 1 + rank), 100,000 error-free forward reads of
-500 bp per GPU (20x coverage), k = 15, reference defaults otherwise, wide ids
+2.5 Mbp per GPU (GC 0.50, seed 1), 100,000 error-free forward reads of 500 bp
+per GPU (20x coverage), k = 15, reference defaults otherwise, wide ids
 (N >= 32,768 is outside the reference's 16-bit id domain).
 
 A step = one pass of the hash stage over the device-resident reads:
@@ -13,9 +13,16 @@ pairs per second summed over ranks.  The end-to-end config (banded HOXD
 dovetail alignment of every dispatched pair) is timed in a second loop and
 reported as aligned_read_pairs_per_s.
 
-Multi-GPU: one process per GPU (torchrun); each rank owns its own read shard
-and genome (weak scaling, no data-path collective: "replicas" until the
-RCCL-sharded exchange lands), barrier + max-over-ranks timing.
+Multi-GPU: one process per GPU (torchrun), backend "nccl"
+(RCCL over xGMI).  Weak scaling: the genome grows with the GPU count (20x
+coverage kept), each rank holds 100,000 reads of it (global ids by rank), and
+a step is the SHARDED hash stage -- local k-mer emit, all-to-all of the
+records to the rank owning their hash range, bucket build + partial pair
+counts there, all-to-all of the partials to the rank owning the lead,
+reduce + collision filter (sharded.py).  Reads are all-gathered once for the
+alignment of each rank's own leads.  Barrier + max-over-ranks timing;
+`value` sums the role pairs over all ranks.  `--replicas` runs independent
+per-rank datasets instead (no exchange), for comparison.
 """
 import argparse
 import json
@@ -39,16 +46,19 @@ def splitmix64(seed, n):
     return z ^ (z >> np.uint64(31))
 
 
-def synth_workload(n_reads, read_len, genome_len, gc, seed):
+def synth_workload(n_reads, read_len, genome_len, gc, seed, shard=0):
     """Genome: base i from splitmix64(seed) (GC with probability gc); reads start
-    uniformly in [0, G-L] (splitmix64(seed ^ 0xABCDEF)), forward strand, error-free."""
+    uniformly in [0, G-L] (splitmix64((seed ^ 0xABCDEF) + 7919 * shard): shard
+    r of a multi-GPU run samples its own reads of the same genome), forward
+    strand, error-free."""
     with np.errstate(over="ignore"):
         z = splitmix64(seed, genome_len)
         u = (z >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
         bit = (z & np.uint64(1)).astype(np.uint8)
         genome = np.where(u < gc, np.where(bit == 1, ord("G"), ord("C")),
                           np.where(bit == 1, ord("T"), ord("A"))).astype(np.uint8)
-        starts = (splitmix64(seed ^ 0xABCDEF, n_reads) % np.uint64(genome_len - read_len + 1)).astype(np.int64)
+        rs = (seed ^ 0xABCDEF) + 7919 * shard
+        starts = (splitmix64(rs, n_reads) % np.uint64(genome_len - read_len + 1)).astype(np.int64)
     idx = starts[:, None] + np.arange(read_len, dtype=np.int64)[None, :]
     bases = genome[idx].reshape(-1)
     offsets = np.arange(n_reads + 1, dtype=np.uint64) * np.uint64(read_len)
@@ -75,24 +85,45 @@ def main():
     ap.add_argument("--align-steps", type=int, default=None)
     ap.add_argument("--cpu-sample-reads", type=int, default=100_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--replicas", action="store_true", help="N>1: independent per-rank datasets, no exchange")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) or gloo (host-staged, testing)")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
     dist = None
+    sharded = ws > 1 and not args.replicas
     if ws > 1:
         import torch
         import torch.distributed as dist_
         dist = dist_
+        ndev = torch.cuda.device_count()
+        local = local % max(ndev, 1)  # (gloo tests may run several ranks on one GPU)
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
 
     import saoverlap as sao
 
     G = int(args.reads * args.len / args.coverage)
-    bases, offsets = synth_workload(args.reads, args.len, G, args.gc, seed=1 + rank)
+    if sharded:
+        # one genome for all ranks (G per GPU, weak scaling), rank r's reads are
+        # global ids r*reads+1 .. (r+1)*reads
+        bases, offsets = synth_workload(args.reads, args.len, G * ws, args.gc, seed=1, shard=rank)
+    else:
+        bases, offsets = synth_workload(args.reads, args.len, G, args.gc, seed=1 + rank)
     ov = sao.Overlapper(device=local if ws > 1 else 0, timing=True, kmer_size=args.k,
                         id_mode=sao.SA_IDS_WIDE)
     ov.add_packed(bases.tobytes(), offsets)
+    so = None
+    if sharded:
+        from sharded import HipWorker, ShardedOverlapper
+        starts = np.arange(ws + 1, dtype=np.int64) * args.reads
+        lengths = np.full(args.reads * ws, args.len, dtype=np.int32)
+        so = ShardedOverlapper(HipWorker(ov), rank, ws, starts, lengths, "cuda:%d" % local)
+    build_step = so.build if so is not None else ov.device_build
+    red_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
 
     def barrier():
         if dist is not None:
@@ -104,7 +135,7 @@ def main():
         if dist is None:
             return x
         import torch
-        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        t = torch.tensor([x], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -112,20 +143,21 @@ def main():
         if dist is None:
             return x
         import torch
-        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        t = torch.tensor([x], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return float(t.item())
 
     # ---- hash stage (configs[1]) ------------------------------------------
-    ov.device_build()  # allocations happen here, outside the timed region
+    build_step()  # allocations happen here, outside the timed region
     for _ in range(args.warmup):
-        ov.device_build()
+        build_step()
     ov.reset_stage_times()
+    xb0 = so.exchanged_bytes if so is not None else 0
     barrier()
     ov.sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        ov.device_build()
+        build_step()
     ov.sync()
     barrier()
     t_build = max_over_ranks(time.perf_counter() - t0)
@@ -136,6 +168,15 @@ def main():
 
     # ---- end-to-end incl. banded HOXD alignment (configs[2]) --------------
     asteps = args.align_steps if args.align_steps is not None else max(1, args.steps // 2)
+    xbytes = (so.exchanged_bytes - xb0) / max(args.steps, 1) if so is not None else 0
+    t_gather = None
+    if so is not None:  # the reads every rank needs to align its own leads
+        barrier()
+        t0 = time.perf_counter()
+        so.gather_reads()
+        ov.sync()
+        barrier()
+        t_gather = max_over_ranks(time.perf_counter() - t0)
     ov.device_align()
     ov.reset_stage_times()
     barrier()
@@ -205,7 +246,8 @@ def main():
                                    "edge/middle pair filter" % (args.reads // 1000, args.len, args.k),
                        "reads_per_gpu": args.reads, "read_len": args.len, "k": args.k,
                        "genome_bp_per_gpu": G, "ids": "wide",
-                       "parallelism": "replicas" if ws > 1 else "single"},
+                       "parallelism": ("sharded-a2a-%s" % args.dist_backend if sharded else
+                                       "replicas" if ws > 1 else "single")},
             "aligned_read_pairs_per_s": round(aligned_total / t_align, 1),
             "ms_per_align_step": round(t_align / asteps * 1e3, 3),
             "per_gpu": {k: int(v) for k, v in st.items() if k not in ("aligned", "ovl_records", "dp_cells")},
@@ -213,6 +255,8 @@ def main():
             "stage_ms_per_step": {k: round(v[0] / max(args.steps, 1), 4) for k, v in stages.items() if v[1]},
             "align_kernel_ms": round(astages["align"][0] / max(astages["align"][1], 1), 4),
             "roofline": roofline,
+            "exchange_bytes_per_step_rank0": int(xbytes) if sharded else None,
+            "read_allgather_ms": round(t_gather * 1e3, 3) if t_gather is not None else None,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -402,7 +402,9 @@ int ensure_prepared(sa_ctx *c) {
 // (distributed mode), else from the occurrence offsets.
 int bucket_stage(sa_ctx *c, uint64_t *&keys, uint32_t *&vals, uint64_t *&keys2, uint32_t *&vals2, uint64_t n,
                  const uint64_t *occ_off, uint32_t n_reads, uint32_t npr, const uint32_t *rid, bool strict,
-                 void *stmp, Counters *cnt, PartArgs &PA, unsigned long long &big_buckets) {
+                 void *stmp, Counters *cnt, PartArgs &PA, unsigned long long &big_buckets, int skip_bits = 0) {
+    // skip_bits: top bits of the mix every key here shares (the owner rank's
+    // bits in distributed mode); partitions use the PB bits below them
     // ---- partition by the top P bits of mix(seqHash): whole buckets per partition
     int PB = 1;
     while (PB < 16 && ((uint64_t)700 << PB) < n) ++PB;
@@ -410,13 +412,13 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint32_t *&vals, uint64_t *&keys2, 
     const int kbits = 32 + c->lb;
     {
         StageScope st(c, SA_STAGE_SORT);
-        HIPCHK(radix_sort(&keys, &vals, &keys2, &vals2, n, kbits - PB, kbits, stmp, c->stream));
+        HIPCHK(radix_sort(&keys, &vals, &keys2, &vals2, n, kbits - skip_bits - PB, kbits - skip_bits, stmp, c->stream));
     }
     uint32_t *pstart, *biglist;
     ENSURE(c->d_pstart, nparts + 1, &pstart);
     ENSURE(c->d_biglist, nparts + 1, &biglist);
     PA = PartArgs{};
-    PA.sk = keys; PA.sv = vals; PA.start = pstart; PA.np = nparts; PA.lb = c->lb; PA.sort_bits = kbits - PB;
+    PA.sk = keys; PA.sv = vals; PA.start = pstart; PA.np = nparts; PA.lb = c->lb; PA.sort_bits = kbits - skip_bits - PB;
     PA.ablate = c->ablate;
     PA.tagtab = (const uint8_t *)c->d_tagtab.p;
     PA.occ_off = occ_off;
@@ -441,7 +443,7 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint32_t *&vals, uint64_t *&keys2, 
     uint32_t big_n = 0;
     {
         StageScope st(c, SA_STAGE_BUCKETS);
-        HIPCHK(launch_part_starts(keys, n, c->lb + 32 - PB, pstart, nparts, c->stream));
+        HIPCHK(launch_part_starts(keys, n, c->lb + 32 - skip_bits - PB, pstart, nparts, c->stream));
         HIPCHK(launch_part_build(PA, strict, c->stream));
     }
     HIPCHK(hipMemcpyAsync(&big_n, &cnt->big_n, 4, hipMemcpyDeviceToHost, c->stream));
@@ -476,7 +478,7 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint32_t *&vals, uint64_t *&keys2, 
             const uint32_t ps = starts[p], pn = starts[p + 1] - starts[p];
             uint64_t *k0 = keys + ps, *k1 = keys2 + ps;
             uint32_t *v0 = vals + ps, *v1 = vals2 + ps;
-            HIPCHK(radix_sort(&k0, &v0, &k1, &v1, pn, 0, kbits - PB, btmp, c->stream));
+            HIPCHK(radix_sort(&k0, &v0, &k1, &v1, pn, 0, kbits - skip_bits - PB, btmp, c->stream));
             if (k0 != keys + ps) {  // odd number of passes: copy the sorted range back
                 HIPCHK(hipMemcpyAsync(keys + ps, k0, (size_t)pn * 8, hipMemcpyDeviceToDevice, c->stream));
                 HIPCHK(hipMemcpyAsync(vals + ps, v0, (size_t)pn * 4, hipMemcpyDeviceToDevice, c->stream));
@@ -1270,7 +1272,8 @@ int sa_dist_count(sa_ctx *c, void *recv_keys, void *recv_vals, uint64_t n, uint6
     }
     PartArgs PA{};
     unsigned long long big_buckets = 0;
-    rc = bucket_stage(c, keys, vals, keys2, vals2, n, loff, N, 0, rid, false, stmp, cnt, PA, big_buckets);
+    rc = bucket_stage(c, keys, vals, keys2, vals2, n, loff, N, 0, rid, false, stmp, cnt, PA, big_buckets,
+                      c->log_ranks);
     if (rc) return rc;
     PairIn PI{};
     PI.rec = PA.rec; PI.md_list = PA.md_list; PI.ed_list = PA.ed_list;

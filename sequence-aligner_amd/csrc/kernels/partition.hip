@@ -38,11 +38,13 @@ __device__ __forceinline__ uint32_t read_of_g(uint32_t g, const uint64_t *occ_of
 // ---------------------------------------------------------------------------
 // partition starts: start[p] = first sorted index of partition p (empty -> next)
 // ---------------------------------------------------------------------------
-__global__ void part_mark_kernel(const uint64_t *sk, uint64_t n, int shift, uint32_t *start) {
+// (bits above the partition id -- the owner rank's in distributed mode -- are
+// the same for every key and masked off)
+__global__ void part_mark_kernel(const uint64_t *sk, uint64_t n, int shift, uint32_t mask, uint32_t *start) {
     const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n) return;
-    const uint32_t p = (uint32_t)(sk[s] >> shift);
-    if (s == 0 || (uint32_t)(sk[s - 1] >> shift) != p) start[p] = (uint32_t)s;
+    const uint32_t p = (uint32_t)(sk[s] >> shift) & mask;
+    if (s == 0 || ((uint32_t)(sk[s - 1] >> shift) & mask) != p) start[p] = (uint32_t)s;
 }
 
 // suffix min over start[0..np] (np+1 entries, start[np] = n) in one block
@@ -377,7 +379,9 @@ hipError_t launch_part_starts(const uint64_t *sk, uint64_t n, int shift, uint32_
                               hipStream_t s) {
     hipError_t e = hipMemsetAsync(start, 0xFF, (size_t)(np + 1) * sizeof(uint32_t), s);
     if (e != hipSuccess) return e;
-    if (n) hipLaunchKernelGGL(part_mark_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, sk, n, shift, start);
+    if (n)
+        hipLaunchKernelGGL(part_mark_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, sk, n, shift, np - 1,
+                           start);
     hipLaunchKernelGGL(part_fill_kernel, dim3(1), dim3(1024), 0, s, start, np, (uint32_t)n);
     return hipGetLastError();
 }
