@@ -65,6 +65,23 @@ def synth_workload(n_reads, read_len, genome_len, gc, seed, shard=0):
     return bases, offsets
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/*/pmc_summary_*.csv, written from separate rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes of this bench by tools_profile.sh):
+    (FETCH_SIZE + WRITE_SIZE) KiB x 1024, uncorrected."""
+    import csv
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary_*.csv")))
+    for path in reversed(files):
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                if kernel in row["kernel"] and row.get("FETCH_SIZE_avg") and row.get("WRITE_SIZE_avg"):
+                    b = (float(row["FETCH_SIZE_avg"]) + float(row["WRITE_SIZE_avg"])) * 1024.0
+                    return int(b), os.path.relpath(path, ROOT)
+    return None, None
+
+
 def dist_env():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -199,10 +216,11 @@ def main():
     pc_avg_ms = pc_ms / max(pc_n, 1)
     alg_bytes = 8.0 * st["kmers"] + 4.0 * st["role_pairs"] + 12.0 * st["dispatched"]
     achieved = alg_bytes / (pc_avg_ms * 1e-3) / 1e9 if pc_avg_ms > 0 else 0.0
+    traffic, tsrc = pmc_traffic("pair_count_kernel<false>")
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "kernel": "pair_count_kernel<false>", "launch_ms": round(pc_avg_ms, 4),
-                "algorithmic_bytes_per_launch": int(alg_bytes)}
+                "algorithmic_bytes_per_launch": int(alg_bytes), "traffic_source": tsrc}
 
     # ---- CPU baseline: the C oracle (port of the reference), 1 thread -----
     cpu = None

@@ -17,3 +17,4 @@ pass() {  # pass <name> <counters...>
 pass fetch FETCH_SIZE
 pass write WRITE_SIZE
 pass sq SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY
+python3 $R/tools/pmc_summary.py $R/gpurun_out $R/gpurun_out/pmc_summary.csv
