@@ -130,10 +130,11 @@ int sa_get_ovl(sa_ctx *ctx, const char **text, size_t *len);
 enum sa_option {
     SA_OPT_KEEP_PAIRS = 1,   /* also materialise PairData for sa_get_pairs */
     SA_OPT_TIMING = 2,       /* record HIP events per stage (sa_get_stage_times) */
-    SA_OPT_ALIGN_KERNEL = 3  /* 0 auto (default): lane-per-pair kernel when every band
+    SA_OPT_ALIGN_KERNEL = 3  /* 0 auto (default): lane-per-pair kernels when every band
                                 fits 15 columns, else lane-group kernel; 1 force the
                                 lane-group kernel; 2 force lane-per-pair (SA_E_ARG if
-                                a band or read does not fit it) */
+                                a band or read does not fit it); 3 lane-per-pair with
+                                per-cell path summaries instead of stored codes */
 };
 int sa_set_option(sa_ctx *ctx, int option, int64_t value);
 

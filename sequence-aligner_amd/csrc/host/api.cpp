@@ -96,7 +96,7 @@ struct sa_ctx {
     uint32_t *bkt_rank_dev = nullptr;
     DBuf d_pf, d_ps, d_pc, d_pr, d_ovl, d_cnt;
     DBuf d_okeys, d_ovals, d_okeys2, d_ovals2, d_osort;
-    DBuf d_lead, d_trail, d_count, d_aln, d_p1;
+    DBuf d_lead, d_trail, d_count, d_aln, d_p1, d_tb;
     DBuf d_rkey, d_rkey2, d_rord, d_rord2, d_rtmp;
     uint64_t pair_cap = 0;
     uint64_t n_disp = 0;
@@ -519,6 +519,7 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
     P.ablate = c->ablate;
     P.n_items = n_items;
     P.xcd_swizzle = read_order ? 1 : 0;
+    P.table = 256;
     if (c->pair_cap == 0) c->pair_cap = std::max<uint64_t>(1 << 16, (uint64_t)n_items * (P.emit_all ? 64 : 24));
     // output regions: NSHARD x cap_s entries (a block appends to region blockIdx % NSHARD)
     unsigned long long cur[NSHARD];
@@ -533,7 +534,7 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
         ENSURE(c->d_pc, tot_cap, &O.cnt);
         O.rank = nullptr;
         if (strict) ENSURE(c->d_pr, tot_cap, &O.rank);
-        ENSURE(c->d_ovl, 2 * (uint64_t)n_items + 2, &O.overflow_list);
+        ENSURE(c->d_ovl, 3 * (uint64_t)n_items + 3, &O.overflow_list);
         O.cursor = cnt->cursor;
         O.cap_s = cap_s;
         O.role_pairs = cnt->role_pairs;
@@ -548,21 +549,42 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
         HIPCHK(hipMemcpyAsync(cur, cnt->cursor, sizeof(cur), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipMemcpyAsync(&ovn, &cnt->overflow_n, 4, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
-        // reads whose LDS table overflowed (> 1,536 partners: high-copy repeats) are
-        // recounted in 64 partner-residue passes; each pass holds up to 1,536 partners
+        // reads whose 256-slot table overflowed (> 192 partners) are recounted
+        // with 2,048 slots; those that fill that too (> 1,536 partners: high-copy
+        // repeats) in 64 partner-residue passes of up to 1,536 partners each
+        uint32_t *list = O.overflow_list;
+        if (ovn > 0 && cur_max() <= cap_s) {
+            PairParams P1 = P;
+            P1.table = 2048;
+            P1.n_items = ovn;
+            P1.xcd_swizzle = 0;
+            PairOut O1 = O;
+            O1.role_pairs = cnt->role_pairs_dummy;
+            O1.overflow_list = list + ovn;  // keep the read list intact
+            HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(uint32_t), c->stream));
+            {
+                StageScope st(c, SA_STAGE_PAIRS);
+                HIPCHK(launch_pair_count(E, PI, P1, O1, list, ovn, c->stream));
+            }
+            HIPCHK(hipMemcpyAsync(cur, cnt->cursor, sizeof(cur), hipMemcpyDeviceToHost, c->stream));
+            list += ovn;
+            HIPCHK(hipMemcpyAsync(&ovn, &cnt->overflow_n, 4, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+        }
         if (ovn > 0 && cur_max() <= cap_s) {
             const uint32_t split = 64;
             PairParams P2 = P;
+            P2.table = 2048;
             P2.split = (int32_t)split;
             P2.n_items = ovn * split;
             P2.xcd_swizzle = 0;
             PairOut O2 = O;
             O2.role_pairs = cnt->role_pairs_dummy;
-            O2.overflow_list = O.overflow_list + ovn;  // keep the read list intact
+            O2.overflow_list = list + ovn;
             HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(uint32_t), c->stream));
             {
                 StageScope st(c, SA_STAGE_PAIRS);
-                HIPCHK(launch_pair_count(E, PI, P2, O2, O.overflow_list, ovn * split, c->stream));
+                HIPCHK(launch_pair_count(E, PI, P2, O2, list, ovn * split, c->stream));
             }
             HIPCHK(hipMemcpyAsync(cur, cnt->cursor, sizeof(cur), hipMemcpyDeviceToHost, c->stream));
             HIPCHK(hipMemcpyAsync(&ovn, &cnt->overflow_n, 4, hipMemcpyDeviceToHost, c->stream));
@@ -836,7 +858,9 @@ int device_align(sa_ctx *c, bool readback) {
     const bool lane_fits = wmax <= 15 && maxL <= 30000;
     if (c->align_kernel == 2 && !lane_fits)
         return fail(c, SA_E_ARG, "SA_OPT_ALIGN_KERNEL=2 but a band or read exceeds the lane kernel");
-    const bool use_lane = c->align_kernel == 2 || (c->align_kernel == 0 && lane_fits);
+    if (c->align_kernel == 3 && !lane_fits)
+        return fail(c, SA_E_ARG, "SA_OPT_ALIGN_KERNEL=3 but a band or read exceeds the lane kernel");
+    const bool use_lane = c->align_kernel >= 2 || (c->align_kernel == 0 && lane_fits);
     const int32_t wmin = std::max(c->set.kmer_size, (int32_t)floor((double)((float)minL * omm)) + 1);
     const bool exact = wmin == 15 && wmax == 15;  // every band exactly 16 cells wide
     AlignParams P;
@@ -868,8 +892,19 @@ int device_align(sa_ctx *c, bool readback) {
             const int32_t *dl = (const int32_t *)c->d_lead.p, *dt = (const int32_t *)c->d_trail.p;
             HIPCHK(launch_dovetail_p1(AR, dl, dt, nd, P, exact, p1, k0, v0, &cnt->err, cnt->cells,
                                       c->stream));
-            HIPCHK(radix_sort(&k0, &v0, &k1, &v1, nd, 0, bits_for((uint64_t)maxL), tmp, c->stream));
-            HIPCHK(launch_dovetail_p2(AR, dl, dt, nd, P, exact, p1, v0, out, &cnt->err, c->stream));
+            HIPCHK(radix_sort(&k0, &v0, &k1, &v1, nd, 0, 20, tmp, c->stream));
+            if (c->align_kernel == 3) {  // path summaries forwarded per cell
+                HIPCHK(launch_dovetail_p2(AR, dl, dt, nd, P, exact, p1, v0, out, &cnt->err, c->stream));
+            } else {  // 2-bit traceback codes in HBM + per-lane walk, in launches of <= 4 GiB of codes
+                const uint64_t per_lane = dovetail_tb_words(1, maxL);
+                uint64_t chunk = std::max<uint64_t>(256, ((1ull << 30) / per_lane) & ~255ull);
+                chunk = std::min<uint64_t>(chunk, (nd + 255) & ~255ull);
+                uint32_t *tb;
+                ENSURE(c->d_tb, dovetail_tb_words(chunk, maxL), &tb);
+                for (uint64_t t0 = 0; t0 < nd; t0 += chunk)
+                    HIPCHK(launch_dovetail_p2tb(AR, dl, dt, nd, t0, chunk, P, exact, p1, v0, out, &cnt->err, tb,
+                                                c->stream));
+            }
         } else
             HIPCHK(launch_dovetail(AR, (const int32_t *)c->d_lead.p, (const int32_t *)c->d_trail.p, nd, P,
                                    G, out, &cnt->err, cnt->cells, c->stream));
@@ -966,7 +1001,7 @@ void sa_ctx_destroy(sa_ctx *c) {
                     &c->d_gmds, &c->d_gede, &c->d_ogid, &c->d_bkttmp, &c->d_mdidx, &c->d_edidx, &c->d_occidx,
                     &c->d_bnst, &c->d_brank, &c->d_bhash, &c->d_bfirst, &c->d_pf, &c->d_ps, &c->d_pc, &c->d_pr,
                     &c->d_ovl, &c->d_cnt, &c->d_okeys, &c->d_ovals, &c->d_okeys2, &c->d_ovals2, &c->d_osort,
-                    &c->d_lead, &c->d_trail, &c->d_count, &c->d_aln, &c->d_p1, &c->d_rkey, &c->d_rkey2, &c->d_rord, &c->d_rord2, &c->d_rtmp, &c->d_gocc, &c->d_rid, &c->d_loff, &c->d_starts, &c->d_bounds, &c->d_gcodes, &c->d_gwoff, &c->d_glen, &c->d_gbad, &c->d_psum, &c->d_pkeep, &c->d_ppos, &c->d_scan, &c->d_pstart, &c->d_biglist, &c->d_rec,
+                    &c->d_lead, &c->d_trail, &c->d_count, &c->d_aln, &c->d_p1, &c->d_tb, &c->d_rkey, &c->d_rkey2, &c->d_rord, &c->d_rord2, &c->d_rtmp, &c->d_gocc, &c->d_rid, &c->d_loff, &c->d_starts, &c->d_bounds, &c->d_gcodes, &c->d_gwoff, &c->d_glen, &c->d_gbad, &c->d_psum, &c->d_pkeep, &c->d_ppos, &c->d_scan, &c->d_pstart, &c->d_biglist, &c->d_rec,
                     &c->d_srec, &c->d_bnmd, &c->d_ishead, &c->d_bnst2};
     for (DBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
@@ -1090,7 +1125,7 @@ int sa_set_option(sa_ctx *c, int option, int64_t value) {
     case SA_OPT_KEEP_PAIRS: c->keep_pairs = value != 0; return SA_OK;
     case SA_OPT_TIMING: c->timing = value != 0; return SA_OK;
     case SA_OPT_ALIGN_KERNEL:
-        if (value < 0 || value > 2) return fail(c, SA_E_ARG, "SA_OPT_ALIGN_KERNEL must be 0, 1 or 2");
+        if (value < 0 || value > 3) return fail(c, SA_E_ARG, "SA_OPT_ALIGN_KERNEL must be 0..3");
         c->align_kernel = (int)value;
         return SA_OK;
     default: return fail(c, SA_E_ARG, "unknown option");

@@ -175,6 +175,135 @@ __device__ __forceinline__ void add_cells(unsigned long long cells, unsigned lon
     if (threadIdx.x == 0 && cell_sum) atomicAdd(&cells_total[blockIdx.x % NSHARD], cell_sum);
 }
 
+// Alignment record from the phase-2 argmax and its path summary (stop cell
+// (u << 6 | k), matches << 16 | errors), with Alignment / Overlap validity
+// (ObjectStore.scala:99-141).  r1 = phase-1 result ((ds << 1) | dud or error).
+__device__ __forceinline__ void finish_alignment(const AlignParams &P, const LanePair &q, int32_t r1, int32_t ds,
+                                                 int32_t zr, int32_t best2, int32_t bpos, int32_t bstop, int32_t bce,
+                                                 DevAlignment *out, int32_t *err) {
+    const bool p2 = r1 >= 0 && !(r1 & 1);
+    int32_t status = r1 < 0 ? r1 : (r1 & 1);
+    if (p2 && best2 <= 0) { status = -6; set_err(err, -6); }
+    DevAlignment o;
+    o.lead = q.a + 1; o.trail = q.b + 1;
+    o.reserved = 0;
+    if (status < 0) {
+        o.start_i = o.start_j = o.end_i = o.end_j = 0; o.correct = 0; o.error = 0;
+        o.ahg = o.bhg = 0; o.flags = 0x100;  // error marker
+        *out = o;
+        return;
+    }
+    int32_t si = 0, sj = 0, ei = 0, ej = 0, c = 0, e = 1, la = 0, lb = 0, alen = 0;
+    const bool dud = status == 1;
+    if (!dud) {
+        const int32_t su = bstop >> 6, sk = bstop & 63;
+        const int32_t eu = bpos >> 6, ek = bpos & 63;
+        si = su + ds; sj = sk - zr + su;
+        ei = eu + ds; ej = ek - zr + eu;
+        c = bce >> 16; e = bce & 0xFFFF;
+        la = q.LA; lb = q.LB;
+        alen = c + e;
+    }
+    const float ratio = __fdiv_rn((float)c, (float)c + (float)e);
+    const bool valid = (ratio >= P.min_identity) && (alen >= P.min_overlap) &&
+                       ((si == 0 && lb == ej) || (sj == 0 && la == ei));
+    const int32_t ahg = si - sj;
+    const int32_t bhg = lb - la + ahg;
+    const bool ovl = valid && ((float)abs(ahg) < P.max_ignore) && ((float)abs(bhg) < P.max_ignore);
+    o.start_i = si; o.start_j = sj; o.end_i = ei; o.end_j = ej;
+    o.correct = c; o.error = e; o.ahg = ahg; o.bhg = bhg;
+    o.flags = (dud ? 1 : 0) | (valid ? 2 : 0) | (ovl ? 4 : 0);
+    *out = o;
+}
+
+// ---- phase 2 with stored traceback codes (the cheaper variant) ------------
+// Per cell only the DP, a 2-bit code (0: cell max <= 0, 1: M, 2: X, 3: Y --
+// what the reference's greedy walk reads, BioLibs.scala:780-809) OR-ed into a
+// per-column word of 16 rows, and the argmax; every 16 rows the 16 words go
+// to HBM lane-interleaved (one coalesced 256-B store per column).  The walk
+// then runs per lane from the argmax over those words, 16 diagonal steps per
+// word load, counting matches with a 2-bit XOR / popcount.
+struct BandTb {
+    uint32_t b8[LW];
+    int32_t Tk[LW], Qk[LW];
+    uint32_t acc[LW];
+    int32_t best, bpos;
+    int32_t ap, bp;
+    uint32_t awd, bw, pa, pb;
+};
+
+template <bool MASKED, bool EXACT>
+__device__ __forceinline__ void band_cell_tb(BandTb &S, const int k, const int32_t u6, const int32_t jb,
+                                             const int32_t LB, const int32_t w, const uint32_t cp, const int32_t gO,
+                                             const int32_t gE, const bool act, const uint32_t c1, const uint32_t c2,
+                                             const uint32_t c3, int32_t &Zl, int32_t &Xl) {
+    const bool last = EXACT ? (k == LW - 1) : (k == LW - 1 || k == w);
+    const int kn = k < LW - 1 ? k + 1 : k;
+    int32_t M = bfe_s8(cp, S.b8[k]) + S.Tk[k];
+    int32_t Y = last ? 0 : gE + S.Qk[kn];
+    int32_t X = k == 0 ? 0 : gE + max(max(Zl, Xl), 0);
+    if (MASKED) {
+        const bool valid = (uint32_t)(jb + k) < (uint32_t)LB;
+        M = valid ? M : 0;
+        X = valid ? X : 0;
+        Y = valid ? Y : 0;
+    }
+    const int32_t T = max(max(M, X), Y);
+    const uint32_t code = T > 0 ? (M == T ? c1 : (X == T ? c2 : c3)) : 0u;
+    S.acc[k] |= code;
+    S.Tk[k] = max(T, 0);
+    S.Qk[k] = max(max(max(M, X) + gO, Y), 0);
+    const bool nb = T > S.best && act && (EXACT || k <= w);
+    S.best = nb ? T : S.best;
+    S.bpos = nb ? (u6 | k) : S.bpos;
+    Zl = max(M, Y) + gO;
+    Xl = X;
+}
+
+template <bool MASKED, bool EXACT>
+__device__ __forceinline__ void band_row_tb(BandTb &S, const int32_t u, const int32_t rows2, const int32_t zr,
+                                            const int32_t LB, const int32_t w, const uint32_t c0, const uint32_t cq1,
+                                            const uint32_t cq2, const uint32_t cq3, const int32_t gO, const int32_t gE,
+                                            const uint32_t *Aw, const int32_t awl, const uint32_t *Bw,
+                                            const int32_t bwl, const uint32_t *dummy, uint32_t *tb, uint64_t nt) {
+    const uint32_t a8 = ((S.awd >> (30 - 2 * (S.ap & 15))) & 3u) << 3;
+    const uint32_t c01 = (a8 & 8) ? cq1 : c0, c23 = (a8 & 8) ? cq3 : cq2;
+    const uint32_t cp = (a8 & 16) ? c23 : c01;
+    const int32_t u6 = u << 6;
+    const int32_t jb = u - zr - 1;
+    const bool act = u <= rows2;
+    const int sh = 2 * (u & 15);
+    const uint32_t k1 = in_vgpr((int32_t)(1u << sh)), k2 = in_vgpr((int32_t)(2u << sh)),
+                   k3 = in_vgpr((int32_t)(3u << sh));
+    int32_t Zl = 0, Xl = 0;
+#pragma unroll
+    for (int k = 0; k < LW; ++k) band_cell_tb<MASKED, EXACT>(S, k, u6, jb, LB, w, cp, gO, gE, act, k1, k2, k3, Zl, Xl);
+    if ((u & 15) == 15) {  // a full 16-row word per column: out, lane-interleaved
+        uint32_t *base = tb + (uint64_t)(u >> 4) * LW * nt;
+#pragma unroll
+        for (int k = 0; k < LW; ++k) {
+            base[(uint64_t)k * nt] = S.acc[k];
+            S.acc[k] = 0;
+        }
+    }
+    ++S.ap;
+    S.awd = (S.ap & 15) == 0 ? S.pa : S.awd;
+    S.pa = gld((((S.ap + 1) & 15) == 0) ? Aw + min((S.ap + 1) >> 4, awl) : dummy, 0);
+#pragma unroll
+    for (int k = 0; k < LW - 1; ++k) S.b8[k] = S.b8[k + 1];
+    S.b8[LW - 1] = S.bp < LB ? ((S.bw >> (30 - 2 * (S.bp & 15))) & 3u) << 3 : 0u;
+    ++S.bp;
+    S.bw = (S.bp & 15) == 0 ? S.pb : S.bw;
+    S.pb = gld((((S.bp + 1) & 15) == 0) ? Bw + min((S.bp + 1) >> 4, bwl) : dummy, 0);
+}
+
+__device__ __forceinline__ uint32_t win16_g(const uint32_t *w, int32_t p) {
+    const uint32_t a = gld(w, p >> 4);
+    const int s = p & 15;
+    if (s == 0) return a;
+    return (a << (2 * s)) | (gld(w, (p >> 4) + 1) >> (32 - 2 * s));
+}
+
 }  // namespace
 
 // Phase 1 (BioLibs.scala:644-689): per pair the start row ds of the phase-1
@@ -280,7 +409,9 @@ __global__ __launch_bounds__(256) void dovetail_p1_kernel(DevReads rd, const int
             }
         }
         p1[pair] = r;
-        rows2_key[pair] = (uint64_t)rows2;
+        // descending row count: the longest waves launch first, so the grid's
+        // tail is made of short ones (longest-processing-time-first)
+        rows2_key[pair] = (uint64_t)(0xFFFFFu - (uint32_t)min(rows2, 0xFFFFF));
         order[pair] = (uint32_t)pair;
     }
     add_cells(cells, cells_total);
@@ -359,42 +490,126 @@ __global__ __launch_bounds__(256) void dovetail_p2_kernel(DevReads rd, const int
     for (; u <= rmax; ++u) band_row<true, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl,
                                                     q.Bw, bwl, rd.codes);
 
-    const int32_t best2 = S.best, bpos = S.bpos, bstop = S.bstop, bce = S.bce;
     if (!have) return;
-    int32_t status = r1 < 0 ? r1 : (r1 & 1);
-    if (p2 && best2 <= 0) { status = -6; set_err(err, -6); }
+    finish_alignment(P, q, r1, ds, zr, S.best, S.bpos, S.bstop, S.bce, out + pair, err);
+}
 
-    DevAlignment o;
-    o.lead = q.a + 1; o.trail = q.b + 1;
-    o.reserved = 0;
-    if (status < 0) {
-        o.start_i = o.start_j = o.end_i = o.end_j = 0; o.correct = 0; o.error = 0;
-        o.ahg = o.bhg = 0; o.flags = 0x100;  // error marker
-        out[pair] = o;
-        return;
+// Phase 2 with stored traceback codes: same contract as dovetail_p2_kernel;
+// tb holds 16 columns x rw words for each of the nt lanes of this launch,
+// which covers pairs order[t0 .. t0 + nt).
+template <bool EXACT>
+__global__ __launch_bounds__(256) void dovetail_p2tb_kernel(DevReads rd, const int32_t *lead, const int32_t *trail,
+                                                            uint64_t npairs, uint64_t t0, uint64_t nt, AlignParams P,
+                                                            const int32_t *p1, const uint32_t *order,
+                                                            DevAlignment *out, int32_t *err, uint32_t *tbbuf) {
+    const uint64_t tl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // lane within this launch
+    const uint64_t t = t0 + tl;
+    const bool have = tl < nt && t < npairs;
+    const uint64_t pair = have ? order[t] : 0;
+    const int32_t gO = in_vgpr(P.gap_open), gE = in_vgpr(P.gap_extend);
+    LanePair q{0, 0, 0, 0, 0, -100, rd.codes, rd.codes};
+    int32_t r1 = -100;
+    if (have) {
+        q = lane_pair<EXACT>(rd, lead, trail, pair, P);
+        r1 = p1[pair];
     }
-    int32_t si = 0, sj = 0, ei = 0, ej = 0, c = 0, e = 1, la = 0, lb = 0, alen = 0;
-    const bool dud = status == 1;
-    if (!dud) {
-        const int32_t su = bstop >> 6, sk = bstop & 63;
-        const int32_t eu = bpos >> 6, ek = bpos & 63;
-        si = su + ds; sj = sk - zr + su;
-        ei = eu + ds; ej = ek - zr + eu;
-        c = bce >> 16; e = bce & 0xFFFF;
-        la = q.LA; lb = LB;
-        alen = c + e;
+    const int32_t w = q.w;
+    const bool p2 = r1 >= 0 && !(r1 & 1);
+    const int32_t ds = r1 >= 0 ? r1 >> 1 : 0;
+    const int32_t zr = w / 2;
+    const int32_t dL = q.LA - ds;
+    const int32_t LB = q.LB;
+    const int32_t rows2 = p2 ? dL : 0;
+    int32_t lo = p2 ? zr + 1 : 0, hi = p2 ? LB + zr - w : 0x7fffffff;
+    int32_t rmax = rows2;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        rmax = max(rmax, __shfl_xor(rmax, off, 64));
+        lo = max(lo, __shfl_xor(lo, off, 64));
+        hi = min(hi, __shfl_xor(hi, off, 64));
     }
-    // Alignment.valid / Overlap.valid (ObjectStore.scala:99-141)
-    const float ratio = __fdiv_rn((float)c, (float)c + (float)e);
-    const bool valid = (ratio >= P.min_identity) && (alen >= P.min_overlap) &&
-                       ((si == 0 && lb == ej) || (sj == 0 && la == ei));
-    const int32_t ahg = si - sj;
-    const int32_t bhg = lb - la + ahg;
-    const bool ovl = valid && ((float)abs(ahg) < P.max_ignore) && ((float)abs(bhg) < P.max_ignore);
-    o.start_i = si; o.start_j = sj; o.end_i = ei; o.end_j = ej;
-    o.correct = c; o.error = e; o.ahg = ahg; o.bhg = bhg;
-    o.flags = (dud ? 1 : 0) | (valid ? 2 : 0) | (ovl ? 4 : 0);
-    out[pair] = o;
+    rmax = __builtin_amdgcn_readfirstlane(rmax);
+    lo = __builtin_amdgcn_readfirstlane(lo);
+    hi = __builtin_amdgcn_readfirstlane(hi);
+    uint32_t cpa[4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+        cpa[x] = (uint32_t)(uint8_t)(int8_t)P.cost[x * 4] | ((uint32_t)(uint8_t)(int8_t)P.cost[x * 4 + 1] << 8) |
+                 ((uint32_t)(uint8_t)(int8_t)P.cost[x * 4 + 2] << 16) |
+                 ((uint32_t)(uint8_t)(int8_t)P.cost[x * 4 + 3] << 24);
+    BandTb S;
+    const uint32_t bw0 = p2 ? gld(q.Bw, 0) : 0u;
+#pragma unroll
+    for (int k = 0; k < LW; ++k) {
+        const int32_t p = k - zr;
+        S.b8[k] = (p >= 0 && p < LB) ? ((bw0 >> (30 - 2 * p)) & 3u) << 3 : 0u;
+    }
+    const int32_t Q0 = max(gO, 0);
+#pragma unroll
+    for (int k = 0; k < LW; ++k) { S.Tk[k] = 0; S.Qk[k] = Q0; S.acc[k] = 0; }
+    S.best = 0; S.bpos = 0;
+    S.bp = LW - zr;
+    const int32_t awl = max((q.LA + 15) / 16 - 1, 0), bwl = max((LB + 15) / 16 - 1, 0);
+    S.bw = q.Bw[min(S.bp >> 4, bwl)];
+    S.pb = q.Bw[min((S.bp >> 4) + 1, bwl)];
+    S.ap = ds;
+    S.awd = q.Aw[min(S.ap >> 4, awl)];
+    S.pa = q.Aw[min((S.ap >> 4) + 1, awl)];
+    uint32_t *tb = tbbuf + tl;  // lane column; word (row block rb, column k) at (rb * LW + k) * nt
+    __builtin_amdgcn_s_waitcnt(0);
+    int32_t u = 1;
+    const int32_t e1 = min(lo - 1, rmax), e2 = min(hi, rmax);
+    for (; u <= e1; ++u)
+        band_row_tb<true, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl, q.Bw,
+                                 bwl, rd.codes, tb, nt);
+    for (; u <= e2; ++u)
+        band_row_tb<false, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl, q.Bw,
+                                  bwl, rd.codes, tb, nt);
+    for (; u <= rmax; ++u)
+        band_row_tb<true, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl, q.Bw,
+                                 bwl, rd.codes, tb, nt);
+    if ((rmax & 15) != 15) {  // the last, partial row block
+        uint32_t *base = tb + (uint64_t)(rmax >> 4) * LW * nt;
+#pragma unroll
+        for (int k = 0; k < LW; ++k) base[(uint64_t)k * nt] = S.acc[k];
+    }
+    if (!have) return;
+    // ---- greedy walk from the argmax (BioLibs.scala:768-809) ---------------
+    int32_t bstop = 0, bce = 0;
+    if (p2 && S.best > 0) {
+        int32_t uu = S.bpos >> 6, k = S.bpos & 63;
+        int32_t c = 0, e = 0;
+        uint32_t word = tb[((uint64_t)(uu >> 4) * LW + k) * nt];
+        uint32_t code = (word >> (2 * (uu & 15))) & 3u;
+        while (code != 0) {
+            if (code == 1) {
+                // run of M codes in column k from row uu down, inside this word
+                const int r = uu & 15;
+                uint32_t x = word ^ 0x55555555u;
+                x &= (r == 15) ? 0xFFFFFFFFu : ((1u << (2 * r + 2)) - 1u);
+                const int32_t n = x == 0 ? r + 1 : r - ((31 - __clz(x)) >> 1);
+                const int32_t i = uu + ds, j = k - zr + uu;
+                // compare A[i-n .. i) with B[j-n .. j)
+                const uint32_t sh = 32 - 2 * n;
+                const uint32_t xa = win16_g(q.Aw, i - n), xb = win16_g(q.Bw, j - n);
+                uint32_t d = (sh == 0) ? (xa ^ xb) : ((xa ^ xb) >> sh);
+                d = (d | (d >> 1)) & 0x55555555u;
+                const int32_t mism = __popc(d);
+                c += n - mism;
+                e += mism;
+                uu -= n;
+            } else if (code == 2) {
+                ++e; --k;
+            } else {
+                ++e; --uu; ++k;
+            }
+            word = tb[((uint64_t)(uu >> 4) * LW + k) * nt];
+            code = (word >> (2 * (uu & 15))) & 3u;
+        }
+        bstop = (uu << 6) | k;
+        bce = (c << 16) | e;
+    }
+    finish_alignment(P, q, r1, ds, zr, S.best, S.bpos, bstop, bce, out + pair, err);
 }
 
 hipError_t launch_dovetail_p1(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
@@ -420,6 +635,26 @@ hipError_t launch_dovetail_p2(const DevReads &r, const int32_t *lead, const int3
         hipLaunchKernelGGL(dovetail_p2_kernel<true>, grid, dim3(256), 0, s, r, lead, trail, n, p, p1, order, out, err);
     else
         hipLaunchKernelGGL(dovetail_p2_kernel<false>, grid, dim3(256), 0, s, r, lead, trail, n, p, p1, order, out, err);
+    return hipGetLastError();
+}
+
+size_t dovetail_tb_words(uint64_t nt, int32_t max_len) {
+    const uint64_t rw = (uint64_t)(max_len + 1 + 15) / 16 + 1;
+    return rw * LW * nt;
+}
+
+hipError_t launch_dovetail_p2tb(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
+                                uint64_t t0, uint64_t nt, const AlignParams &p, bool exact, const int32_t *p1,
+                                const uint32_t *order, DevAlignment *out, int32_t *err, uint32_t *tb,
+                                hipStream_t s) {
+    if (!n || !nt) return hipSuccess;
+    const dim3 grid((uint32_t)((nt + 255) / 256));
+    if (exact)
+        hipLaunchKernelGGL(dovetail_p2tb_kernel<true>, grid, dim3(256), 0, s, r, lead, trail, n, t0, nt, p, p1, order,
+                           out, err, tb);
+    else
+        hipLaunchKernelGGL(dovetail_p2tb_kernel<false>, grid, dim3(256), 0, s, r, lead, trail, n, t0, nt, p, p1,
+                           order, out, err, tb);
     return hipGetLastError();
 }
 

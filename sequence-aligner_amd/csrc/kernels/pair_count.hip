@@ -20,25 +20,36 @@
 
 namespace sa {
 
-constexpr int PC_THREADS = 256;
-constexpr int PC_TAB = 2048;             // LDS hash slots per read
-constexpr int PC_FILL_MAX = PC_TAB * 3 / 4;
+#ifndef SA_PC_THREADS
+#define SA_PC_THREADS 256
+#endif
+constexpr int PC_THREADS = SA_PC_THREADS;
+// LDS hash slots per read: a read has ~20-60 distinct partners at 20x coverage,
+// so the first pass runs a 256-slot table (small LDS -> 8 workgroups per CU);
+// reads that fill it (repeats) are re-run with 2,048 slots, then split
+constexpr int PC_TAB_SMALL = 256;
+constexpr int PC_TAB_BIG = 2048;
 constexpr int PC_CHUNK = 512;            // occurrences per pass over a read
 constexpr int PC_BATCH = 8;              // partner loads in flight per thread
 constexpr uint32_t PC_EMPTY = 0xFFFFFFFFu;
 
-__device__ __forceinline__ uint32_t pc_hash(uint32_t p) { return (p * 0x9E3779B1u) >> (32 - 11); }
+template <int TAB>
+__device__ __forceinline__ uint32_t pc_hash(uint32_t p) {
+    return (p * 0x9E3779B1u) >> (32 - __builtin_ctz((unsigned)TAB));
+}
 
+template <int TAB>
 struct PcShared {
-    uint32_t key[PC_TAB];
-    uint32_t cnt[PC_TAB];
+    uint32_t key[TAB];
+    uint32_t cnt[TAB];
     uint32_t pref[PC_CHUNK + 1];
     uint4 rec[PC_CHUNK];       // per-occurrence partner ranges (partition.hip)
-    uint32_t lds4[4];
+    uint32_t lds4[PC_THREADS / 64];
     uint32_t fill, overflow, out_base;
 };
+template <int TAB>
 struct PcSharedStrict {
-    unsigned long long rank[PC_TAB];
+    unsigned long long rank[TAB];
     uint4 srec[PC_CHUNK];      // {bucket head pos, own_e, own_m, 0}
 };
 
@@ -64,29 +75,31 @@ __device__ __forceinline__ uint32_t pc_block_excl_scan(uint32_t v, uint32_t *lds
     return off + inc - v;
 }
 
-template <bool STRICT>
-__device__ __forceinline__ void pc_insert(PcShared &S, PcSharedStrict &X, uint32_t partner, uint32_t w,
+template <bool STRICT, int TAB>
+__device__ __forceinline__ void pc_insert(PcShared<TAB> &S, PcSharedStrict<TAB> &X, uint32_t partner, uint32_t w,
                                           unsigned long long rank) {
-    uint32_t slot = pc_hash(partner);
-    for (int probe = 0; probe < PC_TAB; ++probe) {
+    constexpr uint32_t FILL_MAX = TAB * 3 / 4;
+    uint32_t slot = pc_hash<TAB>(partner);
+    for (int probe = 0; probe < TAB; ++probe) {
         const uint32_t old = atomicCAS(&S.key[slot], PC_EMPTY, partner);
         if (old == PC_EMPTY || old == partner) {
-            if (old == PC_EMPTY && atomicAdd(&S.fill, 1u) >= (uint32_t)PC_FILL_MAX) S.overflow = 1;
+            if (old == PC_EMPTY && atomicAdd(&S.fill, 1u) >= FILL_MAX) S.overflow = 1;
             atomicAdd(&S.cnt[slot], w);
             if constexpr (STRICT) atomicMin(&X.rank[slot], rank);
             return;
         }
-        slot = (slot + 1) & (PC_TAB - 1);
+        slot = (slot + 1) & (TAB - 1);
     }
     S.overflow = 1;
 }
 
-template <bool STRICT>
+template <bool STRICT, int TAB>
 __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, PairIn in, PairParams p, PairOut o,
                                                                 const uint32_t *read_list) {
     extern __shared__ __align__(16) uint8_t smem[];
-    PcShared &S = *reinterpret_cast<PcShared *>(smem);
-    PcSharedStrict &X = *reinterpret_cast<PcSharedStrict *>(smem + ((sizeof(PcShared) + 15) & ~size_t(15)));
+    PcShared<TAB> &S = *reinterpret_cast<PcShared<TAB> *>(smem);
+    PcSharedStrict<TAB> &X =
+        *reinterpret_cast<PcSharedStrict<TAB> *>(smem + ((sizeof(PcShared<TAB>) + 15) & ~size_t(15)));
     const int tid = threadIdx.x;
     const uint32_t split = (uint32_t)p.split;
     uint32_t bid = blockIdx.x;
@@ -100,7 +113,7 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
     const uint32_t residue = bid % split;
     const uint32_t a = read_list ? read_list[item] : item;
 
-    for (int i = tid; i < PC_TAB; i += PC_THREADS) {
+    for (int i = tid; i < TAB; i += PC_THREADS) {
         S.key[i] = PC_EMPTY;
         S.cnt[i] = 0;
         if constexpr (STRICT) X.rank[i] = ~0ull;
@@ -206,7 +219,7 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
                     if (partner == a) continue;                 // same read (KmerTable.scala:61-63)
                     if (split > 1 && (partner % split) != residue) continue;
                     if (p.ablate & 16) { if (partner == 0xFFFFFFF0u) S.fill = 0; continue; }
-                    pc_insert<STRICT>(S, X, partner, wv[bb], rk[bb]);
+                    pc_insert<STRICT, TAB>(S, X, partner, wv[bb], rk[bb]);
                 }
                 if (S.overflow) break;
             }
@@ -226,7 +239,7 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
     }
     // --- emit (a, partner, count[, rank]) --------------------------------
     if (p.ablate & 32) return;
-    constexpr int PER = PC_TAB / PC_THREADS;
+    constexpr int PER = TAB / PC_THREADS;
     uint32_t keep = 0;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
@@ -258,24 +271,35 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
     }
 }
 
-size_t pair_count_lds_bytes(bool strict) {
-    size_t s = (sizeof(PcShared) + 15) & ~size_t(15);
-    if (strict) s += sizeof(PcSharedStrict);
+template <int TAB>
+static size_t pc_lds_bytes(bool strict) {
+    size_t s = (sizeof(PcShared<TAB>) + 15) & ~size_t(15);
+    if (strict) s += sizeof(PcSharedStrict<TAB>);
     return s;
+}
+
+size_t pair_count_lds_bytes(bool strict) { return pc_lds_bytes<PC_TAB_BIG>(strict); }
+
+template <bool STRICT, int TAB>
+static void pc_launch(const EmitParams &e, const PairIn &in, const PairParams &p, PairOut &o,
+                      const uint32_t *read_list, uint32_t n_blocks, hipStream_t s) {
+    const size_t lds = pc_lds_bytes<TAB>(STRICT);
+    (void)hipFuncSetAttribute((const void *)pair_count_kernel<STRICT, TAB>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((pair_count_kernel<STRICT, TAB>), dim3(n_blocks), dim3(PC_THREADS), lds, s, e, in, p, o,
+                       read_list);
 }
 
 hipError_t launch_pair_count(const EmitParams &e, const PairIn &in, const PairParams &p, PairOut &o,
                              const uint32_t *read_list, uint32_t n_blocks, hipStream_t s) {
     if (n_blocks == 0) return hipSuccess;
-    const size_t lds = pair_count_lds_bytes(p.strict != 0);
+    const bool big = p.table != PC_TAB_SMALL;
     if (p.strict) {
-        (void)hipFuncSetAttribute((const void *)pair_count_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds);
-        hipLaunchKernelGGL(pair_count_kernel<true>, dim3(n_blocks), dim3(PC_THREADS), lds, s, e, in, p, o, read_list);
+        if (big) pc_launch<true, PC_TAB_BIG>(e, in, p, o, read_list, n_blocks, s);
+        else pc_launch<true, PC_TAB_SMALL>(e, in, p, o, read_list, n_blocks, s);
     } else {
-        (void)hipFuncSetAttribute((const void *)pair_count_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds);
-        hipLaunchKernelGGL(pair_count_kernel<false>, dim3(n_blocks), dim3(PC_THREADS), lds, s, e, in, p, o, read_list);
+        if (big) pc_launch<false, PC_TAB_BIG>(e, in, p, o, read_list, n_blocks, s);
+        else pc_launch<false, PC_TAB_SMALL>(e, in, p, o, read_list, n_blocks, s);
     }
     return hipGetLastError();
 }

@@ -89,6 +89,7 @@ struct PairParams {
     int32_t ablate;        // profiling only (env SA_ABLATE): 16 skip inserts, 32 skip emission
     uint32_t n_items;      // reads (x split) to process; blocks beyond it exit
     int32_t xcd_swizzle;   // 1: XCD-contiguous block -> item map (grid % 8 == 0)
+    int32_t table;         // LDS hash slots per read: 256 (first pass) or 2048
 };
 
 // Device-wide counters are sharded NSHARD ways (shard = blockIdx % NSHARD) and
@@ -202,6 +203,13 @@ hipError_t launch_dovetail_p1(const DevReads &r, const int32_t *lead, const int3
 hipError_t launch_dovetail_p2(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
                               const AlignParams &p, bool exact, const int32_t *p1, const uint32_t *order,
                               DevAlignment *out, int32_t *err, hipStream_t s);
+// phase 2 with traceback codes in HBM: lanes t0 .. t0+nt of the order, nt
+// rounded up to 64; tb = dovetail_tb_words(nt, longest lead) u32 words
+size_t dovetail_tb_words(uint64_t nt, int32_t max_len);
+hipError_t launch_dovetail_p2tb(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
+                                uint64_t t0, uint64_t nt, const AlignParams &p, bool exact, const int32_t *p1,
+                                const uint32_t *order, DevAlignment *out, int32_t *err, uint32_t *tb,
+                                hipStream_t s);
 
 // distributed (multi-GPU) glue, dist.hip
 hipError_t launch_iota(uint32_t *v, uint64_t n, hipStream_t s);

@@ -177,20 +177,21 @@ def test_full_width_band_500bp(oracle_mod, gaps):
 
 @pytest.mark.parametrize("k,L,minid", [(15, 500, 0.98), (12, 150, 0.92), (12, 300, 0.96), (9, 120, 0.9)])
 def test_align_kernels_agree(k, L, minid):
-    """The lane-per-pair kernel and the lane-group kernel give identical
-    alignment tuples on the same dispatch (both are also checked against the
-    oracle elsewhere)."""
+    """The lane-per-pair kernels (stored codes + walk, and forwarded path
+    summaries) and the lane-group kernel give identical alignment tuples on the
+    same dispatch (the default is also checked against the oracle elsewhere)."""
     rng = np.random.default_rng(k * 1000 + L)
     reads = mutate(H.synth_reads(400, L, 20 * L, gc=0.5, seed=k + L), rng, 5)
     st = dict(kmer_size=k, min_identity=minid, min_collisions=3, gap_open=-60, gap_extend=-10)
     res = []
-    for kern in (sao.ALIGN_GROUP, sao.ALIGN_LANE):
+    for kern in (sao.ALIGN_GROUP, sao.ALIGN_LANE, sao.ALIGN_LANE_SUMMARY):
         ov = gpu_run(reads=reads, wide=True, align_kernel=kern, **st)
         res.append((ov.alignments(), ov.ovl(), ov.stats()["dp_cells"]))
     assert len(res[0][0]) > 100
-    np.testing.assert_array_equal(res[0][0], res[1][0])
-    assert res[0][1] == res[1][1]
-    assert res[0][2] == res[1][2]
+    for r in res[1:]:
+        np.testing.assert_array_equal(res[0][0], r[0])
+        assert res[0][1] == r[1]
+        assert res[0][2] == r[2]
 
 
 def test_duplicate_reads_loc_ties(oracle_mod):
@@ -216,14 +217,16 @@ def test_short_and_degenerate_reads(oracle_mod):
     compare_with_oracle(oracle_mod, ov, r, False)
 
 
-def test_repeat_overflow_path(oracle_mod):
-    """A 12-mer repeated in 4,000 reads (2,000 copies in the leading edge, 2,000
-    in the middle) gives every middle-copy read 2,000 partners: more than the
-    LDS pair table holds, so the split-pass fallback must reproduce the counts."""
+@pytest.mark.parametrize("copies", [4000, 600])
+def test_repeat_overflow_path(oracle_mod, copies):
+    """A 12-mer repeated in `copies` reads (half in the leading edge, half in the
+    middle) gives every middle-copy read copies/2 partners: 4,000 copies exceed
+    both LDS pair tables (256 and 2,048 slots -> 64-way split pass), 600 only
+    the first-pass table (-> the 2,048-slot re-run); counts must not change."""
     rng = np.random.default_rng(41)
     motif = "ACGTTGCAACGT"
     reads = []
-    for i in range(4000):
+    for i in range(copies):
         s = "".join("ACGT"[x] for x in rng.integers(0, 4, 100))
         p = 5 if i % 2 == 0 else 45
         reads.append(s[:p] + motif + s[p + 12:])
