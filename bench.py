@@ -65,20 +65,27 @@ def synth_workload(n_reads, read_len, genome_len, gc, seed, shard=0):
     return bases, offsets
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary
-    (profiles/*/pmc_summary_*.csv, written from separate rocprofv3 --pmc
-    FETCH_SIZE / WRITE_SIZE passes of this bench by tools_profile.sh):
-    (FETCH_SIZE + WRITE_SIZE) KiB x 1024, uncorrected."""
+def pmc_traffic(kernels):
+    """HBM bytes per step of the named kernels (substrings) from the newest
+    committed PMC summary (profiles/*/pmc_summary_*.csv, written from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench by
+    tools_profile.sh): sum of (FETCH_SIZE + WRITE_SIZE) KiB x 1024 per
+    dispatch, uncorrected."""
     import csv
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary_*.csv")))
     for path in reversed(files):
         with open(path) as f:
-            for row in csv.DictReader(f):
-                if kernel in row["kernel"] and row.get("FETCH_SIZE_avg") and row.get("WRITE_SIZE_avg"):
-                    b = (float(row["FETCH_SIZE_avg"]) + float(row["WRITE_SIZE_avg"])) * 1024.0
-                    return int(b), os.path.relpath(path, ROOT)
+            rows = list(csv.DictReader(f))
+        tot, found = 0.0, 0
+        for kname in kernels:
+            for row in rows:
+                if kname in row["kernel"] and row.get("FETCH_SIZE_avg") and row.get("WRITE_SIZE_avg"):
+                    tot += (float(row["FETCH_SIZE_avg"]) + float(row["WRITE_SIZE_avg"])) * 1024.0
+                    found += 1
+                    break
+        if found == len(kernels):
+            return int(tot), os.path.relpath(path, ROOT)
     return None, None
 
 
@@ -209,18 +216,40 @@ def main():
     aligned_total = sum_over_ranks(float(ast["aligned"])) * asteps
 
     # ---- roofline of the dominant hash-stage kernel ----------------------
-    # pair_count is one launch per step; algorithmic HBM bytes per launch
-    # ("pair_count"): per k-mer 8 B (group id + partner range) + per
-    # candidate (role) pair 4 B (partner id) + per distinct pair 12 B written.
+    # By time the bucket build dominates the step: part_mark + part_build<1024>
+    # + part_build<4096> (the "buckets" stage, one HIP-event scope).  Algorithmic
+    # HBM bytes per step: per k-mer 8 B (partition-start scan) +
+    # 12 B (record load) + 16 B (partner record store), + 4 B per partner-list
+    # entry (st/md/en tags of every position: E2 cut table for the workload).
+    d = args.len - args.k
+    npos = d + 1
+    loc = np.arange(npos, dtype=np.float32) / np.float32(d)
+    f32 = np.float32
+    edge, center = f32(0.4), f32(0.4)
+    tags = ((loc <= edge).astype(np.int64) + ((f32(0.5) - center * f32(0.5) <= loc) &
+            (loc <= f32(0.5) + center * f32(0.5))).astype(np.int64) + (f32(1.0) - edge <= loc).astype(np.int64))
+    list_entries = st["kmers"] * float(tags.sum()) / npos
+    bk_ms, bk_n = stages["buckets"]
+    bk_avg_ms = bk_ms / max(bk_n, 1)
+    bk_bytes = 36.0 * st["kmers"] + 4.0 * list_entries
+    bk_ach = bk_bytes / (bk_avg_ms * 1e-3) / 1e9 if bk_avg_ms > 0 else 0.0
+    bk_traffic, bk_src = pmc_traffic(("part_mark_kernel", "part_build_kernel<1024", "part_build_kernel<4096"))
+    roofline = {"bound": "hbm", "achieved": round(bk_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(bk_ach / HBM_PEAK_GBS, 4), "traffic": bk_traffic,
+                "kernel": "bucket build: part_mark + part_build<1024> + part_build<4096>",
+                "launch_ms": round(bk_avg_ms, 4), "algorithmic_bytes_per_launch": int(bk_bytes),
+                "traffic_source": bk_src}
+    # the candidate counter itself (the metric's unit is its work):
+    # per k-mer 8 B (record) + 4 B per role pair (partner id) + 12 B per dispatched pair
     pc_ms, pc_n = stages["pairs"]
     pc_avg_ms = pc_ms / max(pc_n, 1)
     alg_bytes = 8.0 * st["kmers"] + 4.0 * st["role_pairs"] + 12.0 * st["dispatched"]
     achieved = alg_bytes / (pc_avg_ms * 1e-3) / 1e9 if pc_avg_ms > 0 else 0.0
-    traffic, tsrc = pmc_traffic("pair_count_kernel<false>")
-    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "pair_count_kernel<false>", "launch_ms": round(pc_avg_ms, 4),
-                "algorithmic_bytes_per_launch": int(alg_bytes), "traffic_source": tsrc}
+    traffic, tsrc = pmc_traffic(("pair_count_kernel<false",))
+    roofline_pc = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                   "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                   "kernel": "pair_count_kernel<false, 256>", "launch_ms": round(pc_avg_ms, 4),
+                   "algorithmic_bytes_per_launch": int(alg_bytes), "traffic_source": tsrc}
 
     # ---- CPU baseline: the C oracle (port of the reference), 1 thread -----
     cpu = None
@@ -273,6 +302,7 @@ def main():
             "stage_ms_per_step": {k: round(v[0] / max(args.steps, 1), 4) for k, v in stages.items() if v[1]},
             "align_kernel_ms": round(astages["align"][0] / max(astages["align"][1], 1), 4),
             "roofline": roofline,
+            "roofline_pair_count": roofline_pc,
             "exchange_bytes_per_step_rank0": int(xbytes) if sharded else None,
             "read_allgather_ms": round(t_gather * 1e3, 3) if t_gather is not None else None,
             "cpu_baseline": cpu,

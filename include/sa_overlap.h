@@ -173,7 +173,7 @@ int sa_sync(sa_ctx *ctx);
  * The caller moves data between ranks (all-to-all / all-gather, e.g. with
  * torch.distributed over RCCL); every buffer argument below is a DEVICE
  * pointer on this context's GPU.  Wide ids only.  The sequence per step is
- *   sa_dist_emit      -> exchange 1 (k-mer records, grouped by owner rank)
+ *   sa_dist_emit      -> exchange 1 (8-byte k-mer records, grouped by owner rank)
  *   sa_dist_count     -> sa_dist_partials -> exchange 2 (partial pair counts)
  *   sa_dist_reduce    (this rank's leads: sum, [min,max] filter, dispatch)
  * and, for alignment, sa_dist_codes -> all-gather -> sa_dist_set_reads, then
@@ -186,13 +186,13 @@ int sa_sync(sa_ctx *ctx);
 int sa_dist_init(sa_ctx *ctx, int rank, int nranks, const uint32_t *starts, const int32_t *lengths);
 /* k-mer occurrences of this rank's reads (the size of the exchange-1 send buffers). */
 int sa_dist_local_kmers(sa_ctx *ctx, uint64_t *n);
-/* Emit this rank's k-mer records into send_keys (u64[n]) / send_vals (u32[n]),
- * grouped by owner rank; counts[nranks] = records per owner. */
-int sa_dist_emit(sa_ctx *ctx, void *send_keys, void *send_vals, uint64_t *counts);
+/* Emit this rank's k-mer records (u64[n]: mixed hash << 32 | global occurrence
+ * index) into send_recs, grouped by owner rank; counts[nranks] = records per owner. */
+int sa_dist_emit(sa_ctx *ctx, void *send_recs, uint64_t *counts);
 /* Records received in exchange 1 (concatenated in source-rank order; the
- * buffers are consumed and may be overwritten): build this rank's buckets and
- * count partial pairs for every read; counts[nranks] = partials per lead owner. */
-int sa_dist_count(sa_ctx *ctx, void *recv_keys, void *recv_vals, uint64_t n, uint64_t *counts);
+ * buffer is consumed and overwritten): build this rank's buckets and count
+ * partial pairs for every read; counts[nranks] = partials per lead owner. */
+int sa_dist_count(sa_ctx *ctx, void *recv_recs, uint64_t n, uint64_t *counts);
 /* Copy the partials (u32 lead, trail, count; 0-based ids) grouped by lead owner. */
 int sa_dist_partials(sa_ctx *ctx, void *fst, void *snd, void *cnt);
 /* Partials received in exchange 2: sum, filter, dispatch this rank's leads

@@ -111,7 +111,7 @@ struct sa_ctx {
     uint64_t part_np = 0;            // partial pairs after sa_dist_count
     uint32_t *part_perm = nullptr;   // their ascending-lead order (region-space indices)
     DBuf d_gocc, d_rid, d_loff, d_starts, d_bounds, d_gcodes, d_gwoff, d_glen, d_gbad, d_psum, d_pkeep, d_ppos;
-    DBuf d_scan;
+    DBuf d_scan, d_lr;
     // options / state
     bool keep_pairs = false, timing = false;
     int align_kernel = 0;  // SA_OPT_ALIGN_KERNEL
@@ -400,29 +400,38 @@ int ensure_prepared(sa_ctx *c) {
 // mix, then one LDS workgroup per partition (part_build), the global scan path
 // for partitions too large for LDS.  Read ids come from rid[val] when given
 // (distributed mode), else from the occurrence offsets.
-int bucket_stage(sa_ctx *c, uint64_t *&keys, uint32_t *&vals, uint64_t *&keys2, uint32_t *&vals2, uint64_t n,
-                 const uint64_t *occ_off, uint32_t n_reads, uint32_t npr, const uint32_t *rid, bool strict,
-                 void *stmp, Counters *cnt, PartArgs &PA, unsigned long long &big_buckets, int skip_bits = 0) {
-    // skip_bits: top bits of the mix every key here shares (the owner rank's
-    // bits in distributed mode); partitions use the PB bits below them
+int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, uint32_t *vals2, uint64_t n,
+                 const uint64_t *occ_off, uint32_t n_reads, uint32_t npr, const uint32_t *rid, const uint32_t *lr,
+                 const int32_t *len, bool strict, void *stmp, Counters *cnt, PartArgs &PA,
+                 unsigned long long &big_buckets, int skip_bits = 0) {
+    // keys: 8-byte records (mix32 << 32 | occurrence index); vals / vals2: u32
+    // scratch for the big-partition path.  skip_bits: top bits of the mix every
+    // record here shares (the owner rank's bits in distributed mode);
+    // partitions use the PB bits below them
     // ---- partition by the top P bits of mix(seqHash): whole buckets per partition
     int PB = 1;
     while (PB < 16 && ((uint64_t)700 << PB) < n) ++PB;
     const uint32_t nparts = 1u << PB;
-    const int kbits = 32 + c->lb;
+    const int kbits = 32 + c->lb;  // LDS sort key: mix << lb | loc rank
     {
         StageScope st(c, SA_STAGE_SORT);
-        HIPCHK(radix_sort(&keys, &vals, &keys2, &vals2, n, kbits - skip_bits - PB, kbits - skip_bits, stmp, c->stream));
+        uint32_t *nv = nullptr, *nv2 = nullptr;  // key-only: the payload rides in the record
+        HIPCHK(radix_sort(&keys, &nv, &keys2, &nv2, n, 64 - skip_bits - PB, 64 - skip_bits, stmp, c->stream));
     }
     uint32_t *pstart, *biglist;
     ENSURE(c->d_pstart, nparts + 1, &pstart);
     ENSURE(c->d_biglist, nparts + 1, &biglist);
     PA = PartArgs{};
-    PA.sk = keys; PA.sv = vals; PA.start = pstart; PA.np = nparts; PA.lb = c->lb; PA.sort_bits = kbits - skip_bits - PB;
+    PA.sk = keys; PA.sv = nullptr; PA.start = pstart; PA.np = nparts; PA.lb = c->lb; PA.sort_bits = kbits - skip_bits - PB;
     PA.ablate = c->ablate;
     PA.tagtab = (const uint8_t *)c->d_tagtab.p;
     PA.occ_off = occ_off;
     PA.n_reads = n_reads; PA.npr = npr; PA.rid = rid;
+    PA.lr = lr;
+    PA.len = len;
+    PA.lbase = (const uint32_t *)c->d_lbase.p;
+    PA.lrank = (const uint32_t *)c->d_lrank.p;
+    PA.k = c->set.kmer_size;
     ENSURE(c->d_md, n + 1, &PA.md_list);
     ENSURE(c->d_ed, 2 * n + 2, &PA.ed_list);
     ENSURE(c->d_rec, n + 1, &PA.rec);
@@ -443,7 +452,7 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint32_t *&vals, uint64_t *&keys2, 
     uint32_t big_n = 0;
     {
         StageScope st(c, SA_STAGE_BUCKETS);
-        HIPCHK(launch_part_starts(keys, n, c->lb + 32 - skip_bits - PB, pstart, nparts, c->stream));
+        HIPCHK(launch_part_starts(keys, n, 64 - skip_bits - PB, pstart, nparts, c->stream));
         HIPCHK(launch_part_build(PA, strict, c->stream));
     }
     HIPCHK(hipMemcpyAsync(&big_n, &cnt->big_n, 4, hipMemcpyDeviceToHost, c->stream));
@@ -476,21 +485,24 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint32_t *&vals, uint64_t *&keys2, 
         StageScope st(c, SA_STAGE_BUCKETS);
         for (uint32_t p : bl) {
             const uint32_t ps = starts[p], pn = starts[p + 1] - starts[p];
-            uint64_t *k0 = keys + ps, *k1 = keys2 + ps;
+            // (mix << lb | loc rank, g) pairs of the range into keys2 / vals, then
+            // sort the bits below the partition id (the records in keys are spent)
+            HIPCHK(launch_convert_records(keys + ps, pn, PA, keys2 + ps, vals + ps, c->stream));
+            uint64_t *k0 = keys2 + ps, *k1 = keys + ps;
             uint32_t *v0 = vals + ps, *v1 = vals2 + ps;
             HIPCHK(radix_sort(&k0, &v0, &k1, &v1, pn, 0, kbits - skip_bits - PB, btmp, c->stream));
-            if (k0 != keys + ps) {  // odd number of passes: copy the sorted range back
-                HIPCHK(hipMemcpyAsync(keys + ps, k0, (size_t)pn * 8, hipMemcpyDeviceToDevice, c->stream));
+            if (k0 != keys2 + ps) {  // odd number of passes: copy the sorted range back
+                HIPCHK(hipMemcpyAsync(keys2 + ps, k0, (size_t)pn * 8, hipMemcpyDeviceToDevice, c->stream));
                 HIPCHK(hipMemcpyAsync(vals + ps, v0, (size_t)pn * 4, hipMemcpyDeviceToDevice, c->stream));
             }
             B.n_occ = pn;
             B.md_list = PA.md_list + ps;
             B.ed_list = PA.ed_list + 2ull * ps;
             if (strict) { B.md_idx = PA.md_idx + ps; B.ed_idx = PA.ed_idx + 2ull * ps; }
-            HIPCHK(build_buckets(keys + ps, vals + ps, pn, c->lb, tagtab, PA.occ_off, n_reads, npr, rid, B,
+            HIPCHK(build_buckets(keys2 + ps, vals + ps, pn, c->lb, tagtab, PA.occ_off, n_reads, npr, rid, B,
                                  cnt->totals, btmp, c->stream));
-            if (strict) HIPCHK(build_strict_index(keys + ps, vals + ps, pn, c->lb, tagtab, B, c->stream));
-            HIPCHK(launch_records_from_tables(keys, vals, ps, pn, c->lb, tagtab, B, PA.rec, strict ? 1 : 0, PA.srec,
+            if (strict) HIPCHK(build_strict_index(keys2 + ps, vals + ps, pn, c->lb, tagtab, B, c->stream));
+            HIPCHK(launch_records_from_tables(keys2, vals, ps, pn, c->lb, tagtab, B, PA.rec, strict ? 1 : 0, PA.srec,
                                               PA.bkt_nst, PA.bkt_nmd, PA.bkt_first, PA.is_head, c->stream));
             uint32_t tot[4];
             HIPCHK(hipMemcpyAsync(tot, cnt->totals, 16, hipMemcpyDeviceToHost, c->stream));
@@ -650,8 +662,8 @@ int device_build(sa_ctx *c, bool readback) {
     const uint32_t *read_order = ro0;
     PartArgs PA{};
     unsigned long long big_buckets = 0;
-    rc = bucket_stage(c, keys, vals, keys2, vals2, n, (const uint64_t *)c->d_occ_off.p, nr, c->uniform_npr,
-                      nullptr, strict, stmp, cnt, PA, big_buckets);
+    rc = bucket_stage(c, keys, keys2, vals, vals2, n, (const uint64_t *)c->d_occ_off.p, nr, c->uniform_npr,
+                      nullptr, nullptr, (const int32_t *)c->d_len.p, strict, stmp, cnt, PA, big_buckets);
     if (rc) return rc;
     if (strict) {
         // KmerData iteration rank of every bucket: replay its Trove layout over the
@@ -1001,7 +1013,7 @@ void sa_ctx_destroy(sa_ctx *c) {
                     &c->d_gmds, &c->d_gede, &c->d_ogid, &c->d_bkttmp, &c->d_mdidx, &c->d_edidx, &c->d_occidx,
                     &c->d_bnst, &c->d_brank, &c->d_bhash, &c->d_bfirst, &c->d_pf, &c->d_ps, &c->d_pc, &c->d_pr,
                     &c->d_ovl, &c->d_cnt, &c->d_okeys, &c->d_ovals, &c->d_okeys2, &c->d_ovals2, &c->d_osort,
-                    &c->d_lead, &c->d_trail, &c->d_count, &c->d_aln, &c->d_p1, &c->d_tb, &c->d_rkey, &c->d_rkey2, &c->d_rord, &c->d_rord2, &c->d_rtmp, &c->d_gocc, &c->d_rid, &c->d_loff, &c->d_starts, &c->d_bounds, &c->d_gcodes, &c->d_gwoff, &c->d_glen, &c->d_gbad, &c->d_psum, &c->d_pkeep, &c->d_ppos, &c->d_scan, &c->d_pstart, &c->d_biglist, &c->d_rec,
+                    &c->d_lead, &c->d_trail, &c->d_count, &c->d_aln, &c->d_p1, &c->d_tb, &c->d_rkey, &c->d_rkey2, &c->d_rord, &c->d_rord2, &c->d_rtmp, &c->d_gocc, &c->d_rid, &c->d_loff, &c->d_starts, &c->d_bounds, &c->d_gcodes, &c->d_gwoff, &c->d_glen, &c->d_gbad, &c->d_psum, &c->d_pkeep, &c->d_ppos, &c->d_scan, &c->d_lr, &c->d_pstart, &c->d_biglist, &c->d_rec,
                     &c->d_srec, &c->d_bnmd, &c->d_ishead, &c->d_bnst2};
     for (DBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
@@ -1206,9 +1218,12 @@ int sa_dist_init(sa_ctx *c, int rank, int nranks, const uint32_t *starts, const 
     (void)hipSetDevice(c->device);
     uint64_t *gocc;
     uint32_t *st;
+    int32_t *glen;
     ENSURE(c->d_gocc, (size_t)N + 1, &gocc);
     ENSURE(c->d_starts, (size_t)nranks + 1, &st);
+    ENSURE(c->d_glen, (size_t)N + 1, &glen);
     HIPCHK(hipMemcpy(gocc, c->gocc.data(), ((size_t)N + 1) * 8, hipMemcpyHostToDevice));
+    if (N) HIPCHK(hipMemcpy(glen, lengths, (size_t)N * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(st, c->dstarts.data(), ((size_t)nranks + 1) * 4, hipMemcpyHostToDevice));
     return SA_OK;
 }
@@ -1223,7 +1238,7 @@ int sa_dist_local_kmers(sa_ctx *c, uint64_t *n) {
     return SA_OK;
 }
 
-int sa_dist_emit(sa_ctx *c, void *send_keys, void *send_vals, uint64_t *counts) {
+int sa_dist_emit(sa_ctx *c, void *send_recs, uint64_t *counts) {
     if (!c || !counts) return SA_E_ARG;
     if (!c->dist) return fail(c, SA_E_STATE, "sa_dist_init first");
     (void)hipSetDevice(c->device);
@@ -1231,13 +1246,12 @@ int sa_dist_emit(sa_ctx *c, void *send_keys, void *send_vals, uint64_t *counts) 
     if (rc) return rc;
     c->built = c->aligned = false;
     const uint64_t n = c->n_occ;
-    if (n && (!send_keys || !send_vals)) return SA_E_ARG;
+    if (n && !send_recs) return SA_E_ARG;
     DevReads R = dev_reads(c);
     EmitParams E = emit_params(c);
     E.g_base = (uint32_t)c->gocc[c->dstarts[c->rank]];
-    uint64_t *keys, *keys2; uint32_t *vals, *vals2; uint8_t *stmp;
+    uint64_t *keys, *keys2; uint8_t *stmp;
     ENSURE(c->d_keys, n, &keys);
-    ENSURE(c->d_vals, n, &vals);
     ENSURE(c->d_sorttmp, std::max(radix_sort_temp_bytes(n), buckets_temp_bytes(n)), &stmp);
     {
         StageScope st(c, SA_STAGE_PACK);
@@ -1245,27 +1259,23 @@ int sa_dist_emit(sa_ctx *c, void *send_keys, void *send_vals, uint64_t *counts) 
     }
     {
         StageScope st(c, SA_STAGE_EMIT);
-        HIPCHK(launch_kmer_emit(R, E, keys, vals, c->stream));
+        HIPCHK(launch_kmer_emit(R, E, keys, nullptr, c->stream));
     }
     // owner = top log2(P) bits of the mixed hash: one stable radix pass groups
-    // the records by owner and keeps them in occurrence order within each
-    const int kbits = 32 + c->lb;
-    keys2 = (uint64_t *)send_keys;
-    vals2 = (uint32_t *)send_vals;
+    // the 8-byte records by owner and keeps them in occurrence order within each
+    keys2 = (uint64_t *)send_recs;
     {
         StageScope st(c, SA_STAGE_SORT);
-        if (c->log_ranks > 0) HIPCHK(radix_sort(&keys, &vals, &keys2, &vals2, n, kbits - c->log_ranks, kbits, stmp,
-                                                c->stream));
-        if (keys != (uint64_t *)send_keys && n) {
-            HIPCHK(hipMemcpyAsync(send_keys, keys, n * 8, hipMemcpyDeviceToDevice, c->stream));
-            HIPCHK(hipMemcpyAsync(send_vals, vals, n * 4, hipMemcpyDeviceToDevice, c->stream));
-        }
+        uint32_t *nv = nullptr, *nv2 = nullptr;
+        if (c->log_ranks > 0) HIPCHK(radix_sort(&keys, &nv, &keys2, &nv2, n, 64 - c->log_ranks, 64, stmp, c->stream));
+        if (keys != (uint64_t *)send_recs && n)
+            HIPCHK(hipMemcpyAsync(send_recs, keys, n * 8, hipMemcpyDeviceToDevice, c->stream));
     }
     uint64_t *bounds;
     ENSURE(c->d_bounds, (size_t)c->nranks + 1, &bounds);
     std::vector<uint64_t> b((size_t)c->nranks + 1, 0);
     if (n) {
-        HIPCHK(launch_owner_bounds((const uint64_t *)send_keys, n, kbits - c->log_ranks, (uint32_t)c->nranks, bounds,
+        HIPCHK(launch_owner_bounds((const uint64_t *)send_recs, n, 64 - c->log_ranks, (uint32_t)c->nranks, bounds,
                                    c->stream));
         HIPCHK(hipMemcpyAsync(b.data(), bounds, b.size() * 8, hipMemcpyDeviceToHost, c->stream));
     }
@@ -1278,8 +1288,8 @@ int sa_dist_emit(sa_ctx *c, void *send_keys, void *send_vals, uint64_t *counts) 
     return SA_OK;
 }
 
-int sa_dist_count(sa_ctx *c, void *recv_keys, void *recv_vals, uint64_t n, uint64_t *counts) {
-    if (!c || !counts || (n && (!recv_keys || !recv_vals))) return SA_E_ARG;
+int sa_dist_count(sa_ctx *c, void *recv_recs, uint64_t n, uint64_t *counts) {
+    if (!c || !counts || (n && !recv_recs)) return SA_E_ARG;
     if (!c->dist) return fail(c, SA_E_STATE, "sa_dist_init first");
     (void)hipSetDevice(c->device);
     int rc = ensure_prepared(c);
@@ -1290,25 +1300,28 @@ int sa_dist_count(sa_ctx *c, void *recv_keys, void *recv_vals, uint64_t n, uint6
     HIPCHK(hipMemsetAsync(cnt, 0, sizeof(Counters), c->stream));
     // received records are in global occurrence order (sources in rank order,
     // each in occurrence order): local index i <-> i-th owned occurrence
-    uint32_t *rid, *vals, *vals2; uint64_t *loff, *keys2; uint8_t *stmp;
+    uint32_t *rid, *lr, *vals, *vals2; uint64_t *loff, *keys2; uint8_t *stmp;
     ENSURE(c->d_rid, n, &rid);
+    ENSURE(c->d_lr, n, &lr);
     ENSURE(c->d_loff, (size_t)N + 1, &loff);
     ENSURE(c->d_vals, n, &vals);
     ENSURE(c->d_vals2, n, &vals2);
     ENSURE(c->d_keys2, n, &keys2);
     ENSURE(c->d_sorttmp, std::max(radix_sort_temp_bytes(n), buckets_temp_bytes(n)), &stmp);
-    uint64_t *keys = (uint64_t *)recv_keys;
+    uint64_t *keys = (uint64_t *)recv_recs;
     {
         StageScope st(c, SA_STAGE_EMIT);
-        HIPCHK(launch_read_ids((const uint32_t *)recv_vals, n, (const uint64_t *)c->d_gocc.p, N, c->gnpr, rid,
-                               c->stream));
+        // read id and loc rank of every received occurrence; the record's low
+        // word becomes its local index (record i of this rank)
+        HIPCHK(launch_prepare_received(keys, n, (const uint64_t *)c->d_gocc.p, N, c->gnpr,
+                                       (const int32_t *)c->d_glen.p, (const uint32_t *)c->d_lbase.p,
+                                       (const uint32_t *)c->d_lrank.p, c->set.kmer_size, rid, lr, c->stream));
         HIPCHK(launch_local_offsets(rid, n, N, loff, c->stream));
-        HIPCHK(launch_iota(vals, n, c->stream));
     }
     PartArgs PA{};
     unsigned long long big_buckets = 0;
-    rc = bucket_stage(c, keys, vals, keys2, vals2, n, loff, N, 0, rid, false, stmp, cnt, PA, big_buckets,
-                      c->log_ranks);
+    rc = bucket_stage(c, keys, keys2, vals, vals2, n, loff, N, 0, rid, lr, nullptr, false, stmp, cnt, PA,
+                      big_buckets, c->log_ranks);
     if (rc) return rc;
     PairIn PI{};
     PI.rec = PA.rec; PI.md_list = PA.md_list; PI.ed_list = PA.ed_list;

@@ -37,6 +37,22 @@ __global__ void iota_kernel(uint32_t *v, uint64_t n) {
     if (i < n) v[i] = (uint32_t)i;
 }
 
+// received 8-byte records (mix << 32 | global occurrence g): rid[i] = read of
+// g, lr[i] = its loc rank (lrank[lbase[L - k] + pos]); the low word becomes i
+__global__ void prepare_received_kernel(uint64_t *recs, uint64_t n, const uint64_t *occ_off, uint32_t n_reads,
+                                        uint32_t npr, const int32_t *len, const uint32_t *lbase,
+                                        const uint32_t *lrank, int32_t k, uint32_t *rid, uint32_t *lr) {
+    const uint64_t i = (uint64_t)blockIdx.x * DT + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t rec = recs[i];
+    const uint32_t g = (uint32_t)rec;
+    const uint32_t r = read_of_occ(g, occ_off, n_reads, npr);
+    const uint32_t pos = g - (uint32_t)occ_off[r];
+    rid[i] = r;
+    lr[i] = lrank[lbase[len[r] - k] + pos];
+    recs[i] = (rec & 0xFFFFFFFF00000000ull) | (uint32_t)i;
+}
+
 // rid[i] = global read of global occurrence g[i]
 __global__ void read_ids_kernel(const uint32_t *g, uint64_t n, const uint64_t *occ_off, uint32_t n_reads,
                                 uint32_t npr, uint32_t *rid) {
@@ -149,6 +165,15 @@ __global__ void reduce_compact_kernel(const uint64_t *skeys, uint64_t n, int idb
 hipError_t launch_iota(uint32_t *v, uint64_t n, hipStream_t s) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(iota_kernel, grid_for(n), dim3(DT), 0, s, v, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_prepare_received(uint64_t *recs, uint64_t n, const uint64_t *occ_off, uint32_t n_reads,
+                                   uint32_t npr, const int32_t *len, const uint32_t *lbase, const uint32_t *lrank,
+                                   int32_t k, uint32_t *rid, uint32_t *lr, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(prepare_received_kernel, grid_for(n), dim3(DT), 0, s, recs, n, occ_off, n_reads, npr, len,
+                       lbase, lrank, k, rid, lr);
     return hipGetLastError();
 }
 

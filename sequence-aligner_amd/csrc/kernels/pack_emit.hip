@@ -66,7 +66,7 @@ __device__ __forceinline__ uint32_t window16(const uint32_t *w, int32_t p) {
     return (a << (2 * s)) | (b >> (32 - 2 * s));
 }
 
-// One wave per read, lane = position.  key = mix32(seqHash) << lb | locrank, val = g.
+// One wave per read, lane = position.  record = mix32(seqHash) << 32 | g.
 __global__ __launch_bounds__(256) void kmer_emit_kernel(DevReads r, EmitParams e, uint64_t *keys,
                                                         uint32_t *vals) {
     const uint32_t lane = threadIdx.x & 63;
@@ -82,8 +82,6 @@ __global__ __launch_bounds__(256) void kmer_emit_kernel(DevReads r, EmitParams e
         }
         const uint32_t *w = r.codes + r.woff[rd];
         const uint64_t g0 = e.occ_off[rd];
-        const int32_t d = L - e.k;
-        const uint32_t *lr = e.lrank + e.lbase[d];
         uint32_t kmin = 0xFFFFFFFFu;
         for (int32_t i = lane; i < nk; i += 64) {
             uint32_t x = window16(w, i);
@@ -92,8 +90,9 @@ __global__ __launch_bounds__(256) void kmer_emit_kernel(DevReads r, EmitParams e
             x ^= (x >> 1) & 0x55555555u;
             const uint32_t h = mix32(x);
             kmin = min(kmin, h);
-            keys[g0 + i] = ((uint64_t)h << e.lb) | (uint64_t)lr[i];
-            vals[g0 + i] = (uint32_t)(g0 + i) + e.g_base;
+            // 8-byte record: mixed hash | occurrence index (the loc rank is
+            // re-derived from the index where it is needed, partition.hip)
+            keys[g0 + i] = ((uint64_t)h << 32) | (uint64_t)((uint32_t)(g0 + i) + e.g_base);
         }
         if (e.rkey) {
             // locality key: reads sharing their minimum k-mer overlap, so sorting

@@ -35,6 +35,21 @@ __device__ __forceinline__ uint32_t read_of_g(uint32_t g, const uint64_t *occ_of
     return lo;
 }
 
+// sort key (mix << lb | loc rank) and occurrence index of an 8-byte record
+__device__ __forceinline__ unsigned long long record_key(uint64_t rec, const PartArgs &A, uint32_t &g) {
+    g = (uint32_t)rec;
+    uint32_t lr;
+    if (A.lr) {
+        lr = A.lr[g];
+    } else {
+        const uint32_t r = read_of_g(g, A.occ_off, A.n_reads, A.npr, nullptr);
+        const uint32_t pos = A.npr ? g - r * A.npr : g - (uint32_t)A.occ_off[r];
+        const int32_t d = A.npr ? (int32_t)A.npr - 1 : A.len[r] - A.k;
+        lr = A.lrank[A.lbase[d] + pos];
+    }
+    return ((rec >> 32) << A.lb) | lr;
+}
+
 // ---------------------------------------------------------------------------
 // partition starts: start[p] = first sorted index of partition p (empty -> next)
 // ---------------------------------------------------------------------------
@@ -214,7 +229,11 @@ __global__ __launch_bounds__(PB_THREADS) void part_build_kernel(PartArgs A, uint
         return;
     }
     // ---- load, then stable LDS radix sort on the key bits below the partition id
-    for (uint32_t i = tid; i < n; i += PB_THREADS) { S.key[i] = A.sk[ps + i]; S.g[i] = A.sv[ps + i]; }
+    for (uint32_t i = tid; i < n; i += PB_THREADS) {
+        uint32_t g;
+        S.key[i] = record_key(A.sk[ps + i], A, g);
+        S.g[i] = g;
+    }
     __syncthreads();
     if (!(A.ablate & 1)) lds_radix_sort<CAP>(S, n, A.sort_bits);
     // ---- per-thread contiguous items: flags and local aggregates -----------
@@ -399,6 +418,22 @@ hipError_t launch_part_build(const PartArgs &a, bool strict, hipStream_t s) {
     if (strict) { PB_LAUNCH(1024, 0, true); PB_LAUNCH(4096, 1024, true); }
     else { PB_LAUNCH(1024, 0, false); PB_LAUNCH(4096, 1024, false); }
 #undef PB_LAUNCH
+    return hipGetLastError();
+}
+
+__global__ void convert_records_kernel(const uint64_t *rec8, uint32_t n, PartArgs A, uint64_t *okeys,
+                                       uint32_t *ovals) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t g;
+    okeys[i] = record_key(rec8[i], A, g);
+    ovals[i] = g;
+}
+
+hipError_t launch_convert_records(const uint64_t *rec8, uint32_t n, const PartArgs &a, uint64_t *okeys,
+                                  uint32_t *ovals, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(convert_records_kernel, dim3((n + 255) / 256), dim3(256), 0, s, rec8, n, a, okeys, ovals);
     return hipGetLastError();
 }
 

@@ -155,9 +155,10 @@ constexpr int RS_WAVES = RS_THREADS / 64;
 constexpr int RS_SUB = RS_TILE / RS_WAVES;   // 1024 elements per wave
 constexpr int RS_SLICES = RS_SUB / 64;       // 16
 
+template <bool VALS>
 struct RsShared {
     unsigned long long key[RS_TILE];
-    uint32_t val[RS_TILE];
+    uint32_t val[VALS ? RS_TILE : 1];
     uint32_t cnt[RS_WAVES][256];   // per-wave digit counts
     uint32_t lofs[256];            // tile-local start of each digit run
     uint32_t gofs[256];            // global start of each digit run
@@ -174,12 +175,14 @@ __device__ __forceinline__ uint64_t wave_peers(uint32_t d, bool valid) {
     return peer;
 }
 
+// VALS = false: key-only sort (records that carry their payload in the key)
+template <bool VALS>
 __global__ __launch_bounds__(RS_THREADS) void rs_downsweep_kernel(const uint64_t *kin, const uint32_t *vin,
                                                                   uint64_t *kout, uint32_t *vout, uint64_t n,
                                                                   int shift, const uint32_t *hist,
                                                                   uint32_t nblocks) {
     extern __shared__ __align__(16) uint8_t rs_smem[];
-    RsShared &S = *reinterpret_cast<RsShared *>(rs_smem);
+    RsShared<VALS> &S = *reinterpret_cast<RsShared<VALS> *>(rs_smem);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
@@ -192,7 +195,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep_kernel(const uint64_t
     for (int j = 0; j < RS_SLICES; ++j) {
         const uint64_t i = sub + (uint64_t)j * 64 + lane;
         k[j] = i < n ? kin[i] : ~0ull;
-        v[j] = i < n ? vin[i] : 0u;
+        v[j] = (VALS && i < n) ? vin[i] : 0u;
     }
 #pragma unroll
     for (int j = 0; j < RS_SLICES; ++j) {
@@ -244,7 +247,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep_kernel(const uint64_t
             const uint32_t d = (uint32_t)(k[j] >> shift) & 255u;
             const uint32_t pos = S.cnt[w][d] + rk[j];
             S.key[pos] = k[j];
-            S.val[pos] = v[j];
+            if constexpr (VALS) S.val[pos] = v[j];
         }
     }
     __syncthreads();
@@ -254,7 +257,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep_kernel(const uint64_t
         const uint32_t d = (uint32_t)(kk >> shift) & 255u;
         const uint32_t pos = S.gofs[d] + (i - S.lofs[d]);
         kout[pos] = kk;
-        vout[pos] = S.val[i];
+        if constexpr (VALS) vout[pos] = S.val[i];
     }
 }
 
@@ -270,10 +273,13 @@ hipError_t radix_sort(uint64_t **keys, uint32_t **vals, uint64_t **keys_alt, uin
     const uint64_t nb = (n + RS_TILE - 1) / RS_TILE;
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void *)rs_downsweep_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)sizeof(RsShared));
+        (void)hipFuncSetAttribute((const void *)rs_downsweep_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)sizeof(RsShared<true>));
+        (void)hipFuncSetAttribute((const void *)rs_downsweep_kernel<false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(RsShared<false>));
         attr_set = true;
     }
+    const bool with_vals = vals != nullptr && *vals != nullptr;
     uint32_t *hist = (uint32_t *)tmp;
     void *stmp = (void *)(hist + 256 * nb);
     for (int shift = lo; shift < hi; shift += 8) {
@@ -281,10 +287,16 @@ hipError_t radix_sort(uint64_t **keys, uint32_t **vals, uint64_t **keys_alt, uin
                            (uint32_t)nb);
         hipError_t e = exclusive_scan_u32(hist, hist, 256 * nb, nullptr, stmp, s);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(rs_downsweep_kernel, dim3((uint32_t)nb), dim3(RS_THREADS), sizeof(RsShared), s, *keys,
-                           *vals, *keys_alt, *vals_alt, n, shift, (const uint32_t *)hist, (uint32_t)nb);
+        if (with_vals) {
+            hipLaunchKernelGGL(rs_downsweep_kernel<true>, dim3((uint32_t)nb), dim3(RS_THREADS), sizeof(RsShared<true>),
+                               s, *keys, *vals, *keys_alt, *vals_alt, n, shift, (const uint32_t *)hist, (uint32_t)nb);
+            uint32_t *tv = *vals; *vals = *vals_alt; *vals_alt = tv;
+        } else {
+            hipLaunchKernelGGL(rs_downsweep_kernel<false>, dim3((uint32_t)nb), dim3(RS_THREADS),
+                               sizeof(RsShared<false>), s, *keys, nullptr, *keys_alt, nullptr, n, shift,
+                               (const uint32_t *)hist, (uint32_t)nb);
+        }
         uint64_t *tk = *keys; *keys = *keys_alt; *keys_alt = tk;
-        uint32_t *tv = *vals; *vals = *vals_alt; *vals_alt = tv;
     }
     return hipGetLastError();
 }

@@ -164,6 +164,13 @@ struct PartArgs {
     const uint64_t *occ_off;
     uint32_t n_reads, npr;
     const uint32_t *rid;         // read id by occurrence index (distributed mode) or null
+    // sk holds 8-byte records (mix32 << 32 | occurrence index); the loc rank is
+    // re-derived: lr[g] when given (distributed mode), else from the read's
+    // length and the position (lrank[lbase[L - k] + pos])
+    const uint32_t *lr;
+    const int32_t *len;
+    const uint32_t *lbase, *lrank;
+    int32_t k;
     uint32_t *md_list, *ed_list;
     uint4 *rec;                  // [n_occ] by g
     uint32_t *big_list, *big_n;
@@ -177,6 +184,9 @@ struct PartArgs {
 hipError_t launch_part_starts(const uint64_t *sk, uint64_t n, int shift, uint32_t *start, uint32_t np,
                               hipStream_t s);
 hipError_t launch_part_build(const PartArgs &a, bool strict, hipStream_t s);
+// 8-byte records of one big partition -> (mix << lb | locrank, g) for the global scan path
+hipError_t launch_convert_records(const uint64_t *rec8, uint32_t n, const PartArgs &a, uint64_t *okeys,
+                                  uint32_t *ovals, hipStream_t s);
 hipError_t launch_records_from_tables(const uint64_t *sk, const uint32_t *sv, uint32_t ps, uint32_t n, int lb,
                                       const uint8_t *tagtab, const Buckets &b, uint4 *rec, int strict, uint4 *srec,
                                       uint32_t *bkt_nst, uint32_t *bkt_nmd, uint32_t *bkt_first, uint8_t *is_head,
@@ -213,6 +223,9 @@ hipError_t launch_dovetail_p2tb(const DevReads &r, const int32_t *lead, const in
 
 // distributed (multi-GPU) glue, dist.hip
 hipError_t launch_iota(uint32_t *v, uint64_t n, hipStream_t s);
+hipError_t launch_prepare_received(uint64_t *recs, uint64_t n, const uint64_t *occ_off, uint32_t n_reads,
+                                   uint32_t npr, const int32_t *len, const uint32_t *lbase, const uint32_t *lrank,
+                                   int32_t k, uint32_t *rid, uint32_t *lr, hipStream_t s);
 hipError_t launch_read_ids(const uint32_t *g, uint64_t n, const uint64_t *occ_off, uint32_t n_reads, uint32_t npr,
                            uint32_t *rid, hipStream_t s);
 hipError_t launch_local_offsets(const uint32_t *rid, uint64_t n, uint32_t n_reads, uint64_t *loff, hipStream_t s);

@@ -92,8 +92,8 @@ def lib():
         L.sa_get_stage_times.argtypes = [vp, P(C.c_double), P(C.c_uint64), C.c_int]
         L.sa_dist_init.argtypes = [vp, C.c_int, C.c_int, P(C.c_uint32), P(C.c_int32)]
         L.sa_dist_local_kmers.argtypes = [vp, P(C.c_uint64)]
-        L.sa_dist_emit.argtypes = [vp, vp, vp, P(C.c_uint64)]
-        L.sa_dist_count.argtypes = [vp, vp, vp, C.c_uint64, P(C.c_uint64)]
+        L.sa_dist_emit.argtypes = [vp, vp, P(C.c_uint64)]
+        L.sa_dist_count.argtypes = [vp, vp, C.c_uint64, P(C.c_uint64)]
         L.sa_dist_partials.argtypes = [vp, vp, vp, vp]
         L.sa_dist_reduce.argtypes = [vp, vp, vp, vp, C.c_uint64]
         L.sa_dist_codes.argtypes = [vp, vp, vp, P(C.c_uint64)]
@@ -268,14 +268,14 @@ class Overlapper:
     def _counts(self):
         return (C.c_uint64 * self.nranks)()
 
-    def dist_emit(self, send_keys, send_vals):
+    def dist_emit(self, send_recs):
         cnt = self._counts()
-        self._chk(lib().sa_dist_emit(self.h, send_keys, send_vals, cnt))
+        self._chk(lib().sa_dist_emit(self.h, send_recs, cnt))
         return np.array(cnt[:], dtype=np.int64)
 
-    def dist_count(self, recv_keys, recv_vals, n):
+    def dist_count(self, recv_recs, n):
         cnt = self._counts()
-        self._chk(lib().sa_dist_count(self.h, recv_keys, recv_vals, n, cnt))
+        self._chk(lib().sa_dist_count(self.h, recv_recs, n, cnt))
         return np.array(cnt[:], dtype=np.int64)
 
     def dist_partials(self, fst, snd, cnt):

@@ -8,7 +8,8 @@ index + 1).  One build step:
 
   emit       local k-mer records, grouped by owner rank = top log2(P) bits of
              the mixed seqHash (whole buckets per owner)
-  exchange 1 all-to-all of the records (u64 key, u32 global occurrence index)
+  exchange 1 all-to-all of the 8-byte records (mixed hash << 32 | global
+             occurrence index; the loc rank is re-derived by the owner)
   count      owner builds its buckets and counts partial (lead, trail) pairs
              for every read over ITS buckets (KmerTable.calcPairData,
              KmerTable.scala:85-149, restricted to a hash range)
@@ -45,11 +46,11 @@ class HipWorker:
     def local_kmers(self):
         return self.ov.dist_local_kmers()
 
-    def emit(self, send_keys, send_vals):
-        return self.ov.dist_emit(send_keys.data_ptr(), send_vals.data_ptr())
+    def emit(self, send_recs):
+        return self.ov.dist_emit(send_recs.data_ptr())
 
-    def count(self, recv_keys, recv_vals, n):
-        return self.ov.dist_count(recv_keys.data_ptr(), recv_vals.data_ptr(), n)
+    def count(self, recv_recs, n):
+        return self.ov.dist_count(recv_recs.data_ptr(), n)
 
     def partials(self, fst, snd, cnt):
         self.ov.dist_partials(fst.data_ptr(), snd.data_ptr(), cnt.data_ptr())
@@ -122,15 +123,12 @@ class ShardedOverlapper:
         w = self.w
         n = w.local_kmers()
         sk = self._buf("sk", n, torch.int64)
-        sv = self._buf("sv", n, torch.int32)
-        counts = w.emit(sk, sv)
+        counts = w.emit(sk)
         rcounts = self._a2a_counts(counts)
         nr = int(rcounts.sum())
         rk = self._buf("rk", nr, torch.int64)
-        rv = self._buf("rv", nr, torch.int32)
         self._a2a(rk, sk, rcounts, counts)
-        self._a2a(rv, sv, rcounts, counts)
-        pcounts = w.count(rk, rv, nr)
+        pcounts = w.count(rk, nr)
         npart = int(np.sum(pcounts))
         pf = self._buf("pf", npart, torch.int32)
         ps = self._buf("ps", npart, torch.int32)

@@ -39,6 +39,7 @@ class NumpyWorker:
         self.rank, self.P = rank, nranks
         self.starts = np.asarray(starts, dtype=np.int64)
         lengths = np.asarray(lengths, dtype=np.int64)
+        self.lengths = lengths
         self.gocc = np.concatenate([[0], np.cumsum(np.maximum(lengths - self.k + 1, 0))]).astype(np.int64)
         self.logp = int(nranks).bit_length() - 1
 
@@ -48,24 +49,22 @@ class NumpyWorker:
     def local_kmers(self):
         return int(sum(max(len(r) - self.k + 1, 0) for r in self.reads))
 
-    def emit(self, send_keys, send_vals):
+    def emit(self, send_recs):
+        # 8-byte records: hash << 32 | global occurrence index (the owner
+        # re-derives read, position and loc from the index)
         recs = []
         g = int(self.gocc[self.starts[self.rank]])
         for r in self.reads:
-            d = len(r) - self.k
-            for i in range(d + 1):
+            for i in range(len(r) - self.k + 1):
                 h = seq_hash(r[i:i + self.m])
-                loc = np.float32(i) / np.float32(d) if d > 0 else np.float32("nan")
-                key = (h << 32) | int(np.array(loc, dtype=np.float32).view(np.uint32))
-                recs.append((self._owner(h), g, key))
+                recs.append((self._owner(h), (h << 32) | g))
                 g += 1
         recs.sort(key=lambda x: x[0])  # stable: occurrence order within an owner
         n = len(recs)
         if n:
-            send_keys[:n].copy_(_t(np.array([x[2] for x in recs], dtype=np.uint64).view(np.int64)))
-            send_vals[:n].copy_(_t(np.array([x[1] for x in recs], dtype=np.uint32).view(np.int32)))
+            send_recs[:n].copy_(_t(np.array([x[1] for x in recs], dtype=np.uint64).view(np.int64)))
         counts = np.zeros(self.P, dtype=np.int64)
-        for o, _, _ in recs:
+        for o, _ in recs:
             counts[o] += 1
         return counts
 
@@ -75,14 +74,16 @@ class NumpyWorker:
         en = self.tail <= loc
         return st, md, en
 
-    def count(self, recv_keys, recv_vals, n):
-        keys = recv_keys[:n].numpy().view(np.uint64)
-        g = recv_vals[:n].numpy().view(np.uint32).astype(np.int64)
+    def count(self, recv_recs, n):
+        recs = recv_recs[:n].numpy().view(np.uint64)
+        g = (recs & np.uint64(0xFFFFFFFF)).astype(np.int64)
         rid = np.searchsorted(self.gocc, g, side="right") - 1
+        pos = g - self.gocc[rid]
+        d = self.lengths[rid] - self.k
         buckets = {}
-        for key, r in zip(keys.tolist(), rid.tolist()):
+        for key, r, p, dd in zip(recs.tolist(), rid.tolist(), pos.tolist(), d.tolist()):
             h = key >> 32
-            loc = np.array(key & 0xFFFFFFFF, dtype=np.uint32).view(np.float32)[()]
+            loc = np.float32(p) / np.float32(dd) if dd > 0 else np.float32("nan")
             buckets.setdefault(h, []).append((r, loc))
         pairs = {}
         rp = 0
