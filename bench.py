@@ -27,6 +27,7 @@ per-rank datasets instead (no exchange), for comparison.
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -73,7 +74,9 @@ def pmc_traffic(kernels):
     dispatch, uncorrected."""
     import csv
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary_*.csv")))
+    def natural(path):  # pmc_summary_v9 < pmc_summary_v10
+        return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", path)]
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary_*.csv")), key=natural)
     for path in reversed(files):
         with open(path) as f:
             rows = list(csv.DictReader(f))
@@ -109,6 +112,8 @@ def main():
     ap.add_argument("--align-steps", type=int, default=None)
     ap.add_argument("--cpu-sample-reads", type=int, default=100_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--align-kernel", type=int, default=0,
+                    help="SA_OPT_ALIGN_KERNEL: 0 auto, 1 lane-group (LDS), 2 lane-per-pair")
     ap.add_argument("--replicas", action="store_true", help="N>1: independent per-rank datasets, no exchange")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) or gloo (host-staged, testing)")
     args = ap.parse_args()
@@ -138,7 +143,7 @@ def main():
     else:
         bases, offsets = synth_workload(args.reads, args.len, G, args.gc, seed=1 + rank)
     ov = sao.Overlapper(device=local if ws > 1 else 0, timing=True, kmer_size=args.k,
-                        id_mode=sao.SA_IDS_WIDE)
+                        id_mode=sao.SA_IDS_WIDE, align_kernel=args.align_kernel)
     ov.add_packed(bases.tobytes(), offsets)
     so = None
     if sharded:

@@ -13,7 +13,7 @@ step() {  # step <name> <seconds> <cmd...>
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = tests ]; then
     step smoke 240 python __graft_entry__.py smoke
-    step gpu_tests 900 python -m pytest tests -m gpu -q
+    step gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
     step bench 600 python bench.py --steps 10 --warmup 2
