@@ -112,6 +112,8 @@ def main():
     ap.add_argument("--align-steps", type=int, default=None)
     ap.add_argument("--cpu-sample-reads", type=int, default=100_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--quadratic-steps", type=int, default=0,
+                    help="also time --quadratic-align (full-matrix local alignment) over the same dispatch")
     ap.add_argument("--align-kernel", type=int, default=0,
                     help="SA_OPT_ALIGN_KERNEL: 0 auto, 1 lane-group (LDS), 2 lane-per-pair")
     ap.add_argument("--replicas", action="store_true", help="N>1: independent per-rank datasets, no exchange")
@@ -220,6 +222,28 @@ def main():
     astages = ov.stage_times()
     aligned_total = sum_over_ranks(float(ast["aligned"])) * asteps
 
+    # ---- --quadratic-align (generateLocalAlignmentSet) over the same dispatch
+    quad = None
+    if args.quadratic_steps > 0:
+        ov.set_aligner(sao.SA_ALIGNER_QUADRATIC)
+        ov.device_align()  # allocation + warm-up
+        ov.reset_stage_times()
+        barrier()
+        ov.sync()
+        t0 = time.perf_counter()
+        for _ in range(args.quadratic_steps):
+            ov.device_align()
+        ov.sync()
+        barrier()
+        t_quad = max_over_ranks(time.perf_counter() - t0)
+        qst = ov.stats()
+        quad = {"aligned_read_pairs_per_s": round(sum_over_ranks(float(qst["aligned"])) * args.quadratic_steps
+                                                  / t_quad, 1),
+                "ms_per_step": round(t_quad / args.quadratic_steps * 1e3, 3),
+                "dp_cells_per_step": int(qst["dp_cells"]),
+                "gcups": round(sum_over_ranks(float(qst["dp_cells"])) * args.quadratic_steps / t_quad / 1e9, 1)}
+        ov.set_aligner(sao.SA_ALIGNER_LINEAR)
+
     # ---- roofline of the dominant hash-stage kernel ----------------------
     # By time the bucket build dominates the step: part_mark + part_build<1024>
     # + part_build<4096> (the "buckets" stage, one HIP-event scope).  Algorithmic
@@ -306,6 +330,7 @@ def main():
             "dp_cells_per_align_step": int(ast["dp_cells"]),
             "stage_ms_per_step": {k: round(v[0] / max(args.steps, 1), 4) for k, v in stages.items() if v[1]},
             "align_kernel_ms": round(astages["align"][0] / max(astages["align"][1], 1), 4),
+            "quadratic_align": quad,
             "roofline": roofline,
             "roofline_pair_count": roofline_pc,
             "exchange_bytes_per_step_rank0": int(xbytes) if sharded else None,

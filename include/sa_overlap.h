@@ -116,7 +116,8 @@ int sa_get_pairs(sa_ctx *ctx, const int32_t **fst, const int32_t **snd,
                  const int32_t **count, size_t *n);
 
 /* genBlockMTAlign -> generateFastDovetailAlignmentSet for every dispatched pair
- * (Project4.scala:725-790, BioLibs.scala:596-822). */
+ * (Project4.scala:725-790, BioLibs.scala:596-822), or generateLocalAlignmentSet
+ * (BioLibs.scala:267-368) under SA_OPT_ALIGNER = SA_ALIGNER_QUADRATIC. */
 int sa_align(sa_ctx *ctx);
 int sa_get_alignments(sa_ctx *ctx, const sa_alignment **out, size_t *n);
 
@@ -130,12 +131,22 @@ int sa_get_ovl(sa_ctx *ctx, const char **text, size_t *len);
 enum sa_option {
     SA_OPT_KEEP_PAIRS = 1,   /* also materialise PairData for sa_get_pairs */
     SA_OPT_TIMING = 2,       /* record HIP events per stage (sa_get_stage_times) */
-    SA_OPT_ALIGN_KERNEL = 3  /* 0 auto (default): lane-per-pair kernels when every band
+    SA_OPT_ALIGN_KERNEL = 3, /* 0 auto (default): lane-per-pair kernels when every band
                                 fits 15 columns, else lane-group kernel; 1 force the
                                 lane-group kernel; 2 force lane-per-pair (SA_E_ARG if
                                 a band or read does not fit it); 3 lane-per-pair with
                                 per-cell path summaries instead of stored codes */
+    SA_OPT_ALIGNER = 4,      /* enum sa_aligner: which reference aligner sa_align runs */
+    SA_OPT_LOCAL_BATCH_MB = 5 /* quadratic aligner: MiB of traceback codes per launch (16384) */
 };
+
+/* Project4's fdAlign switch (Project4.scala:187-192, :585-604).
+ * LINEAR     --linear-align (default): generateFastDovetailAlignmentSet, banded
+ *            two-phase dovetail DP (BioLibs.scala:596-822).
+ * QUADRATIC  --quadratic-align: generateLocalAlignmentSet, full-matrix affine
+ *            local alignment + greedy backtrack (BioLibs.scala:267-368); trails
+ *            up to 2,048 bp (longer ones fail with SA_E_OVERFLOW), gap costs <= 0. */
+enum sa_aligner { SA_ALIGNER_LINEAR = 0, SA_ALIGNER_QUADRATIC = 1 };
 int sa_set_option(sa_ctx *ctx, int option, int64_t value);
 
 /* Statistics of the last sa_build_candidates / sa_align. */

@@ -338,6 +338,51 @@ def fast_dovetail(idA, A, idB, B, s):  # BioLibs.generateFastDovetailAlignmentSe
     return Alignment(len(A), len(B), idA, idB, (i, j), newEnd, c, e)
 
 
+def local_alignment_set(maxL, idA, A, Bs, s):  # BioLibs.generateLocalAlignmentSet :267-368
+    gO, gE = s.gapOpen, s.gapExtend
+    M = [[0] * (maxL + 1) for _ in range(len(A) + 1)]  # :276-278, reused across the block
+    X = [[0] * (maxL + 1) for _ in range(len(A) + 1)]
+    Y = [[0] * (maxL + 1) for _ in range(len(A) + 1)]
+    for i in range(len(A)):  # :281-285
+        M[i][0] = 0; X[i][0] = 0; Y[i][0] = gO + i * gE
+    for i in range(maxL):  # :287-291
+        M[0][i] = 0; X[0][i] = gO + i * gE; Y[0][i] = 0
+    out = []
+    for idB, B in Bs:  # :293
+        mx, maxLoc = 0, (0, 0)
+        for i in range(1, len(A) + 1):  # :301-324
+            for j in range(1, len(B) + 1):
+                M[i][j] = cost(s, A[i - 1], B[j - 1]) + max(max(M[i - 1][j - 1], Y[i - 1][j - 1]),
+                                                            max(X[i - 1][j - 1], 0))
+                X[i][j] = gE + max(max(M[i][j - 1] + gO, Y[i][j - 1] + gO), max(X[i][j - 1], 0))
+                Y[i][j] = gE + max(max(M[i - 1][j] + gO, Y[i - 1][j]), max(X[i - 1][j] + gO, 0))
+                t = max(M[i][j], max(X[i][j], Y[i][j]))
+                if t > mx:
+                    mx, maxLoc = t, (i, j)
+        opt = maxLoc  # :326-362
+        i, j = maxLoc
+        c = e = 0
+        mx = max(M[i][j], X[i][j], Y[i][j])
+        while True:
+            if M[i][j] == mx:
+                if i - 1 < 0 or j - 1 < 0:
+                    raise IndexError("StringIndexOutOfBounds: degenerate local backtrack")
+                pa, pb = A[i - 1], B[j - 1]; i -= 1; j -= 1
+            elif X[i][j] == mx:
+                pa, pb = A[i - 1], "-"; j -= 1
+            elif Y[i][j] == mx:
+                pa, pb = "-", B[j - 1]; i -= 1
+            if pa != pb:
+                e += 1
+            else:
+                c += 1
+            mx = max(M[i][j], X[i][j], Y[i][j])
+            if not mx > 0:
+                break
+        out.append(Alignment(len(A), len(B), idA, idB, (i, j), opt, c, e))  # :364
+    return out
+
+
 # --------------------------------------------------------------------------
 # KmerTable.scala
 # --------------------------------------------------------------------------
@@ -402,8 +447,10 @@ class KmerTable:
                 yield lead, trails
 
 
-def run(text, s):
-    """Project4 calc-overlaps path (:56-60): returns (.ovl text, table, alignments)."""
+def run(text, s, quadratic=False):
+    """Project4 calc-overlaps path (:56-60): returns (.ovl text, table, alignments).
+    quadratic=True is `--quadratic-align` (fdAlign = false, Project4.scala:187-189):
+    calcLocalAlignmentSet -> generateLocalAlignmentSet (:599-604)."""
     seqs = read_seq(text)
     table = KmerTable()
     for idx, seq in enumerate(seqs):  # genMTKmerTable :531-563 (joined in read order)
@@ -412,9 +459,11 @@ def run(text, s):
     aligns = []
     for lead, trails in table.dispatch_blocks(s):  # genBlockMTAlign :725-790
         A = table.SequenceData[lead]
-        for j in trails:
-            a = fast_dovetail(lead, A, j, table.SequenceData[j], s)
-            if a.valid(s):
-                aligns.append(a)
+        if quadratic:
+            maxL = max(len(table.SequenceData[j]) for j in trails)  # KmerTable.scala:259-264
+            block = local_alignment_set(maxL, lead, A, [(j, table.SequenceData[j]) for j in trails], s)
+        else:
+            block = [fast_dovetail(lead, A, j, table.SequenceData[j], s) for j in trails]
+        aligns.extend(a for a in block if a.valid(s))
     out = "".join(a.ovl_text() + "\n" for a in aligns if a.overlap_valid(s))  # calcOverlaps :795-825
     return out, table, aligns

@@ -68,6 +68,7 @@ def lib():
         L.orc_ovl.restype = C.c_size_t
         L.orc_align_pair.argtypes = [C.c_char_p, C.c_int32, C.c_char_p, C.c_int32, C.c_int32, C.c_int32,
                                      P(Settings), P(Align)]
+        L.orc_align_pair_local.argtypes = L.orc_align_pair.argtypes
         L.orc_trove_order.argtypes = [P(C.c_int32), C.c_size_t, P(C.c_int32), P(C.c_int32)]
         _lib = L
     return _lib
@@ -101,7 +102,7 @@ class Run:
     """Result of one calc-overlaps run of the oracle."""
 
     def __init__(self, reads=None, fasta=None, settings=None, wide=False, keep_kmers=False, skip_align=False,
-                 packed=None):
+                 packed=None, quadratic=False):
         L = lib()
         h = C.c_void_p()
         if packed is not None:
@@ -121,7 +122,8 @@ class Run:
             raise OracleError(rc)
         self.settings = settings or default_settings()
         try:
-            rc = L.orc_run(h, C.byref(self.settings), (1 if wide else 0) | (2 if skip_align else 0))
+            rc = L.orc_run(h, C.byref(self.settings), (1 if wide else 0) | (2 if skip_align else 0) |
+                         (4 if quadratic else 0))
             self.rc = rc
             self.n_reads = L.orc_num_reads(h)
             if keep_kmers:
@@ -162,10 +164,11 @@ class Run:
         return self.aligns[:, ALIGN_FIELDS.index(name)]
 
 
-def align_pair(A, B, id_a=1, id_b=2, settings=None):
+def align_pair(A, B, id_a=1, id_b=2, settings=None, quadratic=False):
     s = settings or default_settings()
     out = Align()
-    rc = lib().orc_align_pair(A.encode(), len(A), B.encode(), len(B), id_a, id_b, C.byref(s), C.byref(out))
+    fn = lib().orc_align_pair_local if quadratic else lib().orc_align_pair
+    rc = fn(A.encode(), len(A), B.encode(), len(B), id_a, id_b, C.byref(s), C.byref(out))
     if rc:
         raise OracleError(rc)
     return {n: getattr(out, n) for n in ALIGN_FIELDS}

@@ -355,6 +355,7 @@ static int hx_code(char ch) { /* defaultHOXD closure, BioLibs.scala:142-160 */
 /* BioLibs.generateFastDovetailAlignmentSet, one trailer (BioLibs.scala:613-820) */
 /* ------------------------------------------------------------------------ */
 typedef struct { int32_t *M, *X, *Y; size_t cap; } dp_buf;
+static void judge(orc_align_t *o, const orc_settings *s);
 
 static int align_one(dp_buf *b, const char *A, int32_t la, const char *B, int32_t lb,
                      int32_t ida, int32_t idb, const orc_settings *s, orc_align_t *o) {
@@ -491,6 +492,98 @@ static int align_one(dp_buf *b, const char *A, int32_t la, const char *B, int32_
 #undef CMAX
 }
 
+/* ------------------------------------------------------------------------ */
+/* BioLibs.generateLocalAlignmentSet, one trailer (BioLibs.scala:267-368):   */
+/* the `--quadratic-align` aligner (full-matrix affine local alignment with  */
+/* the same greedy backtrack).  The block variant reuses its matrices across  */
+/* trailers, but every cell it reads for a trailer was written for that      */
+/* trailer or is a boundary cell, so a per-pair matrix gives the same result. */
+/* ------------------------------------------------------------------------ */
+static int align_local(dp_buf *b, const char *A, int32_t la, const char *B, int32_t lb,
+                       int32_t ida, int32_t idb, const orc_settings *s, orc_align_t *o) {
+    const int32_t gO = s->gap_open, gE = s->gap_extend;
+    const int32_t W = lb + 1;
+    size_t need = (size_t)(la + 1) * (size_t)W;
+    if (need > b->cap) {
+        free(b->M); free(b->X); free(b->Y);
+        b->M = (int32_t *)malloc(need * sizeof(int32_t));
+        b->X = (int32_t *)malloc(need * sizeof(int32_t));
+        b->Y = (int32_t *)malloc(need * sizeof(int32_t));
+        b->cap = need;
+        if (!b->M || !b->X || !b->Y) return ORC_E_NOMEM;
+    }
+    int32_t *M = b->M, *X = b->X, *Y = b->Y;
+    memset(M, 0, need * sizeof(int32_t));
+    memset(X, 0, need * sizeof(int32_t));
+    memset(Y, 0, need * sizeof(int32_t));
+#define AT(P, i, j) P[(size_t)(i) * W + (j)]
+    for (int32_t i = 0; i < la; i++) { AT(Y, i, 0) = gO + i * gE; }  /* :281-285 */
+    for (int32_t i = 0; i < lb; i++) { AT(X, 0, i) = gO + i * gE; }  /* :287-291 (maxL >= lb) */
+    int32_t mx = 0, mi = 0, mj = 0;
+    for (int32_t i = 1; i <= la; i++) { /* :301-324 */
+        int ca = hx_code(A[i - 1]);
+        for (int32_t j = 1; j <= lb; j++) {
+            int cb = hx_code(B[j - 1]);
+            if (ca < 0 || cb < 0) return ORC_E_MATCH;
+            int32_t d = AT(M, i - 1, j - 1);
+            if (AT(Y, i - 1, j - 1) > d) d = AT(Y, i - 1, j - 1);
+            int32_t d2 = AT(X, i - 1, j - 1) > 0 ? AT(X, i - 1, j - 1) : 0;
+            AT(M, i, j) = s->cost[ca * 4 + cb] + (d > d2 ? d : d2);
+            int32_t x1 = AT(M, i, j - 1) + gO, x2 = AT(Y, i, j - 1) + gO;
+            int32_t x3 = AT(X, i, j - 1) > 0 ? AT(X, i, j - 1) : 0;
+            int32_t xm = x1 > x2 ? x1 : x2;
+            AT(X, i, j) = gE + (xm > x3 ? xm : x3);
+            int32_t y1 = AT(M, i - 1, j) + gO, y2 = AT(Y, i - 1, j);
+            int32_t y3 = AT(X, i - 1, j) + gO;
+            if (y3 < 0) y3 = 0;
+            int32_t ym = y1 > y2 ? y1 : y2;
+            AT(Y, i, j) = gE + (ym > y3 ? ym : y3);
+            int32_t t = AT(M, i, j);
+            if (AT(X, i, j) > t) t = AT(X, i, j);
+            if (AT(Y, i, j) > t) t = AT(Y, i, j);
+            if (t > mx) { mx = t; mi = i; mj = j; }
+        }
+    }
+    /* greedy backtrack :326-362; A.charAt(-1) on a matrix with no positive cell */
+#define CMAX(i_, j_) (AT(M, i_, j_) > AT(X, i_, j_) ? (AT(M, i_, j_) > AT(Y, i_, j_) ? AT(M, i_, j_) : AT(Y, i_, j_)) \
+                                                    : (AT(X, i_, j_) > AT(Y, i_, j_) ? AT(X, i_, j_) : AT(Y, i_, j_)))
+    int32_t i = mi, j = mj, c = 0, e = 0;
+    mx = CMAX(i, j);
+    do {
+        char pa = ' ', pb = ' ';
+        if (AT(M, i, j) == mx) {
+            if (i < 1 || j < 1) return ORC_E_INDEX;
+            pa = A[i - 1]; pb = B[j - 1]; i--; j--;
+        } else if (AT(X, i, j) == mx) {
+            if (i < 1 || j < 1) return ORC_E_INDEX;
+            pa = A[i - 1]; pb = '-'; j--;
+        } else if (AT(Y, i, j) == mx) {
+            if (j < 1 || i < 1) return ORC_E_INDEX;
+            pa = '-'; pb = B[j - 1]; i--;
+        }
+        if (pa != pb) e++; else c++;
+        mx = CMAX(i, j);
+    } while (mx > 0);
+    memset(o, 0, sizeof(*o));
+    o->lead = ida; o->trail = idb;
+    o->start_i = i; o->start_j = j; /* Alignment(seqA, seqB, xSeq, ySeq, (i,j), opt, c, e) :364 */
+    o->end_i = mi; o->end_j = mj;
+    o->correct = c; o->error = e;
+    o->len_a = la; o->len_b = lb;
+    return ORC_OK;
+#undef AT
+#undef CMAX
+}
+
+int orc_align_pair_local(const char *A, int32_t la, const char *B, int32_t lb, int32_t ida, int32_t idb,
+                         const orc_settings *s, orc_align_t *out) {
+    dp_buf b = {0};
+    int rc = align_local(&b, A, la, B, lb, ida, idb, s, out);
+    free(b.M); free(b.X); free(b.Y);
+    if (rc == ORC_OK) judge(out, s);
+    return rc;
+}
+
 /* Alignment.valid / Overlap (ObjectStore.scala:99-141) */
 static void judge(orc_align_t *o, const orc_settings *s) {
     float ratio = (float)o->correct / ((float)o->correct + (float)o->error);
@@ -522,7 +615,7 @@ static int cmp_wide_pair(const void *a, const void *b) {
 }
 
 int orc_run(orc_ctx *c, const orc_settings *s, int flags) {
-    const int wide = flags & 1, skip_align = flags & 2;
+    const int wide = flags & 1, skip_align = flags & 2, quadratic = flags & 4;
     free_results(c);
     const int k = s->kmer_size;
     /* AlignSettings derived edges, ObjectStore.scala:30-35 */
@@ -743,7 +836,7 @@ out_kd:
         int32_t la = (int32_t)(c->off[a] - c->off[a - 1]);
         int32_t lb = (int32_t)(c->off[b] - c->off[b - 1]);
         orc_align_t *o = &c->aligns[q];
-        if ((rc = align_one(&db, A, la, B, lb, a, b, s, o))) break;
+        if ((rc = (quadratic ? align_local : align_one)(&db, A, la, B, lb, a, b, s, o))) break;
         judge(o, s);
         if (o->valid && o->ovl_valid) {
             char rec[160];

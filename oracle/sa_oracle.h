@@ -9,6 +9,7 @@
  * (build with -ffp-contract=off, no fast-math):
  *   BioLibs.scala:26-61        readSeq, generateKmerSet
  *   BioLibs.scala:119-161      defaultHOXD
+ *   BioLibs.scala:267-368      generateLocalAlignmentSet (--quadratic-align, per pair)
  *   BioLibs.scala:596-822      generateFastDovetailAlignmentSet (per pair)
  *   KmerTable.scala:41-187     addKmerSet, addKmerPair, calcPairData, calcDispatchData
  *   KmerTable.scala:246-273    dispatchCollisionBlocks
@@ -76,7 +77,9 @@ uint32_t orc_num_reads(const orc_ctx *c);
 /* Run the whole calc-overlaps path.  flags bit 0 (wide) = 0: reference emulation
  * with 32-bit (fst<<16)^snd keys and Trove order (E1/E4); = 1: 64-bit (fst,snd)
  * keys, canonical order (lead descending, trail ascending).  flags bit 1: stop
- * after DispatchData (candidate stage only, for the CPU baseline). */
+ * after DispatchData (candidate stage only, for the CPU baseline).  flags bit 2:
+ * `--quadratic-align` (generateLocalAlignmentSet, BioLibs.scala:267-368) instead
+ * of the banded dovetail aligner. */
 int orc_run(orc_ctx *c, const orc_settings *s, int flags);
 
 /* Results of orc_run (arrays owned by ctx, valid until destroy/next run). */
@@ -100,6 +103,10 @@ size_t orc_ovl(const orc_ctx *c, const char **text);
 /* One banded dovetail alignment (BioLibs.scala:613-820 for one trailer). */
 int orc_align_pair(const char *A, int32_t len_a, const char *B, int32_t len_b,
                    int32_t id_a, int32_t id_b, const orc_settings *s, orc_align_t *out);
+
+/* One full-matrix local alignment (BioLibs.scala:267-368 for one trailer). */
+int orc_align_pair_local(const char *A, int32_t len_a, const char *B, int32_t len_b,
+                         int32_t id_a, int32_t id_b, const orc_settings *s, orc_align_t *out);
 
 /* Trove emulation probe (for fixtures): capacity after inserting n distinct
  * keys in order; and the descending-slot iteration order. */

@@ -96,7 +96,7 @@ struct sa_ctx {
     uint32_t *bkt_rank_dev = nullptr;
     DBuf d_pf, d_ps, d_pc, d_pr, d_ovl, d_cnt;
     DBuf d_okeys, d_ovals, d_okeys2, d_ovals2, d_osort;
-    DBuf d_lead, d_trail, d_count, d_aln, d_p1, d_tb;
+    DBuf d_lead, d_trail, d_count, d_aln, d_p1, d_tb, d_ltb, d_lmax;
     DBuf d_rkey, d_rkey2, d_rord, d_rord2, d_rtmp;
     uint64_t pair_cap = 0;
     uint64_t n_disp = 0;
@@ -115,6 +115,8 @@ struct sa_ctx {
     // options / state
     bool keep_pairs = false, timing = false;
     int align_kernel = 0;  // SA_OPT_ALIGN_KERNEL
+    int aligner = SA_ALIGNER_LINEAR;  // SA_OPT_ALIGNER (--linear-align / --quadratic-align)
+    uint64_t local_batch_bytes = 16ull << 30;  // traceback-code budget of one quadratic launch
     int ablate = 0;  // profiling only: SA_ABLATE env (results are wrong when set)
     bool built = false, aligned = false;
     // results (host)
@@ -868,10 +870,12 @@ int device_align(sa_ctx *c, bool readback) {
             return fail(c, SA_E_ARG, "cost matrix entries must lie in [-128, 127]");
     // lane-per-pair kernel: band <= 15 columns, reads <= 30,000 bp (c << 16 | e packing)
     const bool lane_fits = wmax <= 15 && maxL <= 30000;
-    if (c->align_kernel == 2 && !lane_fits)
+    if (c->aligner == SA_ALIGNER_LINEAR && c->align_kernel == 2 && !lane_fits)
         return fail(c, SA_E_ARG, "SA_OPT_ALIGN_KERNEL=2 but a band or read exceeds the lane kernel");
-    if (c->align_kernel == 3 && !lane_fits)
+    if (c->aligner == SA_ALIGNER_LINEAR && c->align_kernel == 3 && !lane_fits)
         return fail(c, SA_E_ARG, "SA_OPT_ALIGN_KERNEL=3 but a band or read exceeds the lane kernel");
+    if (c->aligner == SA_ALIGNER_QUADRATIC && (c->set.gap_open > 0 || c->set.gap_extend > 0))
+        return fail(c, SA_E_ARG, "--quadratic-align needs gap costs <= 0 (Project4.readArgs negates them)");
     const bool use_lane = c->align_kernel >= 2 || (c->align_kernel == 0 && lane_fits);
     const int32_t wmin = std::max(c->set.kmer_size, (int32_t)floor((double)((float)minL * omm)) + 1);
     const bool exact = wmin == 15 && wmax == 15;  // every band exactly 16 cells wide
@@ -892,7 +896,23 @@ int device_align(sa_ctx *c, bool readback) {
     HIPCHK(hipMemsetAsync(cnt->cells, 0, sizeof(cnt->cells), c->stream));
     {
         StageScope st(c, SA_STAGE_ALIGN);
-        if (use_lane) {
+        if (c->aligner == SA_ALIGNER_QUADRATIC) {
+            // generateLocalAlignmentSet (BioLibs.scala:267-368): one wave per pair,
+            // codes for the greedy walk in HBM, in launches of <= local_batch_bytes
+            const int stripe = local_align_stripe(maxL);
+            const uint32_t wpl = local_align_wpl(stripe, maxL);
+            const uint64_t per_pair = (uint64_t)64 * wpl * 4;
+            uint64_t chunk = std::max<uint64_t>(64, c->local_batch_bytes / per_pair);
+            chunk = std::min<uint64_t>(chunk, std::max<uint64_t>(nd, 1));
+            uint32_t *tb;
+            int4 *lmax;
+            ENSURE(c->d_ltb, chunk * 64 * (uint64_t)wpl, &tb);
+            ENSURE(c->d_lmax, chunk, &lmax);
+            const int32_t *dl = (const int32_t *)c->d_lead.p, *dt = (const int32_t *)c->d_trail.p;
+            for (uint64_t p0 = 0; p0 < nd; p0 += chunk)
+                HIPCHK(launch_local_align(AR, dl, dt, p0, std::min(chunk, nd - p0), P, stripe, wpl, tb, lmax, out,
+                                          &cnt->err, cnt->cells, c->stream));
+        } else if (use_lane) {
             // phase 1, then pairs grouped by phase-2 row count, then phase 2
             int32_t *p1; uint64_t *k0, *k1; uint32_t *v0, *v1; uint8_t *tmp;
             ENSURE(c->d_p1, nd, &p1);
@@ -1139,6 +1159,16 @@ int sa_set_option(sa_ctx *c, int option, int64_t value) {
     case SA_OPT_ALIGN_KERNEL:
         if (value < 0 || value > 3) return fail(c, SA_E_ARG, "SA_OPT_ALIGN_KERNEL must be 0..3");
         c->align_kernel = (int)value;
+        return SA_OK;
+    case SA_OPT_ALIGNER:
+        if (value != SA_ALIGNER_LINEAR && value != SA_ALIGNER_QUADRATIC)
+            return fail(c, SA_E_ARG, "SA_OPT_ALIGNER must be SA_ALIGNER_LINEAR or SA_ALIGNER_QUADRATIC");
+        c->aligner = (int)value;
+        c->aligned = false;
+        return SA_OK;
+    case SA_OPT_LOCAL_BATCH_MB:
+        if (value < 1) return fail(c, SA_E_ARG, "SA_OPT_LOCAL_BATCH_MB must be >= 1");
+        c->local_batch_bytes = (uint64_t)value << 20;
         return SA_OK;
     default: return fail(c, SA_E_ARG, "unknown option");
     }

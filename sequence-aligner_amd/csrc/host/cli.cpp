@@ -41,6 +41,7 @@ int main(int argc, char **argv) {
     std::string input, output, hoxd;
     int device = 0;
     bool stats = false;
+    int aligner = SA_ALIGNER_LINEAR;
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
         auto need = [&](int32_t *iv, float *fv) -> bool {
@@ -84,14 +85,13 @@ int main(int argc, char **argv) {
         else if (a == "-gE" || a == "--gap-extend") { need(&iv, nullptr); s.gap_extend = -iabs(iv); }
         else if (a == "--max-ignore") { need(&iv, nullptr); s.max_ignore = iabs(iv); }
         else if (a == "--st-hash" || a == "--mt-hash" || a == "--st-align" || a == "--mt-align" ||
-                 a == "--block-align" || a == "--single-align" || a == "--linear-align" || a == "--calc-overlaps" ||
+                 a == "--block-align" || a == "--single-align" || a == "--calc-overlaps" ||
                  a == "--sleep-for-debug") {
             // threading / dispatch variants give identical results and order
-        } else if (a == "--debug") stats = true;
-        else if (a == "--quadratic-align") {
-            fprintf(stderr, "--quadratic-align is not implemented on this device path (SURVEY.md 8(f) next)\n");
-            return 1;
-        } else if (a.rfind("--test-", 0) == 0 || a.rfind("--bench-", 0) == 0) {
+        } else if (a == "--linear-align") aligner = SA_ALIGNER_LINEAR;  // fdAlign = true (:190-192)
+        else if (a == "--debug") stats = true;
+        else if (a == "--quadratic-align") aligner = SA_ALIGNER_QUADRATIC;  // fdAlign = false (:187-189)
+        else if (a.rfind("--test-", 0) == 0 || a.rfind("--bench-", 0) == 0) {
             fprintf(stderr, "%s: developer test/bench modes are out of scope; use bench.py\n", a.c_str());
             return 1;
         } else if (a == "--wide-ids") s.id_mode = SA_IDS_WIDE;
@@ -117,7 +117,8 @@ int main(int argc, char **argv) {
         fprintf(stderr, "sa-overlap: no usable gfx950 device (%d)\n", rc);
         return 1;
     }
-    if ((rc = sa_read_fasta(ctx, input.c_str())) == SA_OK && (rc = sa_build_candidates(ctx)) == SA_OK &&
+    rc = sa_set_option(ctx, SA_OPT_ALIGNER, aligner);
+    if (rc == SA_OK && (rc = sa_read_fasta(ctx, input.c_str())) == SA_OK && (rc = sa_build_candidates(ctx)) == SA_OK &&
         (rc = sa_align(ctx)) == SA_OK) {
         rc = sa_write_ovl(ctx, output.empty() ? nullptr : output.c_str());
     }

@@ -221,6 +221,16 @@ hipError_t launch_dovetail_p2tb(const DevReads &r, const int32_t *lead, const in
                                 const uint32_t *order, DevAlignment *out, int32_t *err, uint32_t *tb,
                                 hipStream_t s);
 
+// full-matrix local alignment (`--quadratic-align`, local_align.hip): pairs
+// p0 .. p0+np of the dispatch list; stripe S = columns per lane (4/8/16/32,
+// trails <= 64*S bp), wpl = code words per lane for the longest lead
+// (local_align_wpl), tb = np * 64 * wpl u32 words, lmax = np int4 scratch
+int local_align_stripe(int32_t max_len);
+uint32_t local_align_wpl(int stripe, int32_t max_len);
+hipError_t launch_local_align(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t p0,
+                              uint64_t np, const AlignParams &p, int stripe, uint32_t wpl, uint32_t *tb, int4 *lmax,
+                              DevAlignment *out, int32_t *err, unsigned long long *cells, hipStream_t s);
+
 // distributed (multi-GPU) glue, dist.hip
 hipError_t launch_iota(uint32_t *v, uint64_t n, hipStream_t s);
 hipError_t launch_prepare_received(uint64_t *recs, uint64_t n, const uint64_t *occ_off, uint32_t n_reads,

@@ -22,7 +22,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SA_OVERLAP_LIB") or os.path.join(HERE, "build", "libsa_overlap.so")  # env: experiments
 
 SA_IDS_AUTO, SA_IDS_STRICT, SA_IDS_WIDE = 0, 1, 2
-SA_OPT_KEEP_PAIRS, SA_OPT_TIMING, SA_OPT_ALIGN_KERNEL = 1, 2, 3
+SA_OPT_KEEP_PAIRS, SA_OPT_TIMING, SA_OPT_ALIGN_KERNEL, SA_OPT_ALIGNER, SA_OPT_LOCAL_BATCH_MB = 1, 2, 3, 4, 5
+SA_ALIGNER_LINEAR, SA_ALIGNER_QUADRATIC = 0, 1   # --linear-align / --quadratic-align
 ALIGN_AUTO, ALIGN_GROUP, ALIGN_LANE, ALIGN_LANE_SUMMARY = 0, 1, 2, 3
 STAGES = ("pack", "emit", "sort", "buckets", "pairs", "order", "align")
 ERRORS = {-1: "SA_E_ARG", -2: "SA_E_INPUT", -3: "SA_E_NON_ACGT", -4: "SA_E_ID_RANGE", -5: "SA_E_SHORT_READ",
@@ -135,7 +136,8 @@ def _arr(ptr, n):
 class Overlapper:
     """One context = one AlignSettings + one KmerTable on one GPU."""
 
-    def __init__(self, device=0, timing=False, keep_pairs=False, align_kernel=ALIGN_AUTO, **kw):
+    def __init__(self, device=0, timing=False, keep_pairs=False, align_kernel=ALIGN_AUTO,
+                 aligner=SA_ALIGNER_LINEAR, local_batch_mb=None, **kw):
         self.s = settings(**kw)
         h = C.c_void_p()
         rc = lib().sa_ctx_create(C.byref(self.s), device, C.byref(h))
@@ -148,6 +150,14 @@ class Overlapper:
             self._chk(lib().sa_set_option(h, SA_OPT_KEEP_PAIRS, 1))
         if align_kernel != ALIGN_AUTO:
             self._chk(lib().sa_set_option(h, SA_OPT_ALIGN_KERNEL, align_kernel))
+        if aligner != SA_ALIGNER_LINEAR:
+            self._chk(lib().sa_set_option(h, SA_OPT_ALIGNER, aligner))
+        if local_batch_mb is not None:
+            self._chk(lib().sa_set_option(h, SA_OPT_LOCAL_BATCH_MB, local_batch_mb))
+
+    def set_aligner(self, aligner):
+        """SA_OPT_ALIGNER: SA_ALIGNER_LINEAR (--linear-align) or SA_ALIGNER_QUADRATIC."""
+        self._chk(lib().sa_set_option(self.h, SA_OPT_ALIGNER, aligner))
 
     def close(self):
         if getattr(self, "h", None):

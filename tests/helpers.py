@@ -51,3 +51,36 @@ def synth_reads(n_reads, read_len, genome_len, gc=0.5, seed=1, mixed=None):
 
 def sha256(b):
     return hashlib.sha256(b).hexdigest()
+
+
+def mutate(reads, rng, max_ops):
+    """Up to max_ops substitutions / deletions / insertions per read."""
+    out = []
+    for rd in reads:
+        s = list(rd)
+        for _ in range(int(rng.integers(0, max_ops + 1))):
+            p = int(rng.integers(0, len(s)))
+            op = int(rng.integers(0, 3))
+            if op == 0:
+                s[p] = "ACGT"[int(rng.integers(0, 4))]
+            elif op == 1:
+                del s[p]
+            else:
+                s.insert(p, "ACGT"[int(rng.integers(0, 4))])
+        out.append("".join(s))
+    return out
+
+
+def read_fasta_seqs(path):
+    """Sequences of a FASTA file (headers dropped), like BioLibs.readSeq."""
+    seqs, cur = [], None
+    for line in open(path).read().splitlines():
+        if line.startswith(">"):
+            if cur is not None:
+                seqs.append("".join(cur))
+            cur = []
+        elif cur is not None:
+            cur.append(line.upper())
+    if cur is not None:
+        seqs.append("".join(cur))
+    return seqs

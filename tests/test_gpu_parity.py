@@ -144,21 +144,7 @@ def test_mutated_reads_with_indels(oracle_mod, gaps):
         compare_with_oracle(oracle_mod, ov, r, wide)
 
 
-def mutate(reads, rng, max_ops):
-    out = []
-    for rd in reads:
-        s = list(rd)
-        for _ in range(int(rng.integers(0, max_ops + 1))):
-            p = int(rng.integers(0, len(s)))
-            op = int(rng.integers(0, 3))
-            if op == 0:
-                s[p] = "ACGT"[int(rng.integers(0, 4))]
-            elif op == 1:
-                del s[p]
-            else:
-                s.insert(p, "ACGT"[int(rng.integers(0, 4))])
-        out.append("".join(s))
-    return out
+mutate = H.mutate
 
 
 @pytest.mark.parametrize("gaps", [(-400, -30, 0.98), (-60, -10, 0.98), (-35, -1, 0.98)])

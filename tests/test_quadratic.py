@@ -1,0 +1,165 @@
+"""`--quadratic-align`: BioLibs.generateLocalAlignmentSet (BioLibs.scala:267-368)
+selected by Project4's fdAlign = false (Project4.scala:187-189, :599-604).
+
+CPU: the C oracle's align_local against the Scala-literal golden vectors
+(tests/golden/make_quadratic_golden.py) -- every dispatched pair's (start, end,
+c, e) and the .ovl bytes.  GPU: the HIP kernels (local_align.hip) through the C
+ABI against the golden vectors and the oracle, bit-exact, at every column
+stripe (4 / 8 / 16 / 32 columns per lane), plus the error behaviour.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import helpers as H
+
+FIELDS = ("start_i", "start_j", "end_i", "end_j", "correct", "error")
+CASES = {
+    "crp177_k12": ("crp177.seq", dict(kmer_size=12)),
+    "mut_k10_g200": ("mutated_reads.seq", dict(kmer_size=10, min_collisions=3, min_identity=0.9)),
+    "mut_k10_g40": ("mutated_reads.seq", dict(kmer_size=10, min_collisions=3, min_identity=0.9, gap_open=-40,
+                                              gap_extend=-8)),
+    "mut_k10_g10": ("mutated_reads.seq", dict(kmer_size=10, min_collisions=3, min_identity=0.85, gap_open=-10,
+                                              gap_extend=-1, min_overlap=30)),
+}
+
+
+def golden(name):
+    return (np.load(os.path.join(H.GOLDEN, "quad_%s.npz" % name)),
+            open(os.path.join(H.GOLDEN, "quad_%s.ovl" % name), "rb").read())
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_oracle_matches_literal_golden(oracle_mod, name):
+    fn, st = CASES[name]
+    g, ovl = golden(name)
+    r = oracle_mod.Run(fasta=os.path.join(H.GOLDEN, fn), settings=oracle_mod.default_settings(**st),
+                       quadratic=True)
+    np.testing.assert_array_equal(r.lead, g["lead"])
+    np.testing.assert_array_equal(r.trail, g["trail"])
+    for f in FIELDS:
+        np.testing.assert_array_equal(r.align_field(f), g[f], err_msg=f)
+    assert r.ovl == ovl
+
+
+def test_quadratic_differs_from_banded(oracle_mod):
+    """The fixtures have teeth: with gap moves the two aligners disagree."""
+    fn, st = CASES["mut_k10_g10"]
+    s = oracle_mod.default_settings(**st)
+    q = oracle_mod.Run(fasta=os.path.join(H.GOLDEN, fn), settings=s, quadratic=True)
+    b = oracle_mod.Run(fasta=os.path.join(H.GOLDEN, fn), settings=s)
+    assert not np.array_equal(q.align_field("error"), b.align_field("error"))
+
+
+def test_oracle_local_pair_known_answer(oracle_mod):
+    """Hand-checkable case: B is A's 3' half plus new bases -> a dovetail whose
+    greedy walk starts at (i, 0) and ends at the last row (BioLibs.scala:326-364)."""
+    A = "ACGTTGCAAGGCTTACCGATAGCTTAGGCATCGA"
+    B = A[14:] + "TTGACCAGT"
+    r = oracle_mod.align_pair(A, B, quadratic=True, settings=oracle_mod.default_settings(min_overlap=10))
+    assert (r["start_i"], r["start_j"], r["end_i"], r["end_j"]) == (14, 0, len(A), len(A) - 14)
+    assert (r["correct"], r["error"]) == (len(A) - 14, 0)
+    assert r["valid"] == 1
+
+
+# --------------------------------------------------------------------------- GPU
+sao = pytest.importorskip("saoverlap")
+
+
+def gpu_quadratic(reads=None, fasta=None, wide=False, **kw):
+    ov = sao.Overlapper(id_mode=sao.SA_IDS_WIDE if wide else sao.SA_IDS_STRICT, aligner=sao.SA_ALIGNER_QUADRATIC,
+                        **kw)
+    if fasta:
+        ov.read_fasta(fasta)
+    else:
+        ov.add_reads(reads)
+    ov.build()
+    ov.align()
+    return ov
+
+
+def assert_same(ov, r):
+    lead, trail, _ = ov.dispatch()
+    np.testing.assert_array_equal(lead, r.lead)
+    np.testing.assert_array_equal(trail, r.trail)
+    al = ov.alignments()
+    for f in FIELDS + ("ahg", "bhg"):
+        np.testing.assert_array_equal(al[:, sao.ALIGN_FIELDS.index(f)], r.align_field(f), err_msg=f)
+    flags = al[:, sao.ALIGN_FIELDS.index("flags")]
+    assert not (flags & sao.FLAG_DUD).any()
+    np.testing.assert_array_equal((flags & sao.FLAG_VALID) != 0, r.align_field("valid") != 0)
+    np.testing.assert_array_equal((flags & sao.FLAG_OVL_VALID) != 0,
+                                  (r.align_field("ovl_valid") != 0) & (r.align_field("valid") != 0))
+    assert ov.ovl() == r.ovl
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_gpu_matches_literal_golden(name):
+    fn, st = CASES[name]
+    g, ovl = golden(name)
+    ov = gpu_quadratic(fasta=os.path.join(H.GOLDEN, fn), **st)
+    al = ov.alignments()
+    for f in FIELDS:
+        np.testing.assert_array_equal(al[:, sao.ALIGN_FIELDS.index(f)], g[f], err_msg=f)
+    assert ov.ovl() == ovl
+    la = np.array([len(x) for x in H.read_fasta_seqs(os.path.join(H.GOLDEN, fn))], dtype=np.int64)
+    lead, trail, _ = ov.dispatch()
+    assert ov.stats()["dp_cells"] == int((la[lead - 1] * la[trail - 1]).sum())
+
+
+# (n, read lengths, genome, seed, settings): one case per column stripe
+# (longest read <= 256 -> 4 columns per lane, <= 512 -> 8, <= 1024 -> 16, else 32)
+STRIPES = [
+    (300, (60, 250), 2500, 31, dict(kmer_size=12, min_collisions=3, gap_open=-40, gap_extend=-8,
+                                    min_identity=0.9)),
+    (200, (300, 500), 4000, 32, dict(kmer_size=15, gap_open=-200, gap_extend=-20)),
+    (120, (500, 1000), 6000, 33, dict(kmer_size=15, min_collisions=4, gap_open=-30, gap_extend=-3,
+                                      min_identity=0.95)),
+    (60, (900, 1700), 7000, 34, dict(kmer_size=14, min_collisions=5, gap_open=-100, gap_extend=-10)),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", range(len(STRIPES)))
+@pytest.mark.parametrize("wide", [False, True])
+def test_gpu_stripes_match_oracle(oracle_mod, case, wide):
+    n, mixed, G, seed, st = STRIPES[case]
+    rng = np.random.default_rng(seed)
+    reads = H.mutate(H.synth_reads(n, mixed[0], G, seed=seed, mixed=mixed), rng, 6)
+    r = oracle_mod.Run(reads=reads, settings=oracle_mod.default_settings(**st), wide=wide, quadratic=True)
+    ov = gpu_quadratic(reads=reads, wide=wide, **st)
+    assert ov.stats()["dispatched"] > 50
+    assert_same(ov, r)
+
+
+@pytest.mark.gpu
+def test_gpu_small_batches_match():
+    """Launch splitting (SA_OPT_LOCAL_BATCH_MB) does not change any result."""
+    fn, st = CASES["mut_k10_g40"]
+    a = gpu_quadratic(fasta=os.path.join(H.GOLDEN, fn), **st)
+    b = gpu_quadratic(fasta=os.path.join(H.GOLDEN, fn), local_batch_mb=1, **st)
+    np.testing.assert_array_equal(a.alignments(), b.alignments())
+
+
+@pytest.mark.gpu
+def test_gpu_non_acgt_anywhere_is_matcherror(oracle_mod):
+    """Every cell calls the cost closure (BioLibs.scala:303): a non-ACGT base in
+    any aligned read is a MatchError."""
+    reads = H.synth_reads(80, 120, 900, seed=41)
+    reads = [r[:100] + "N" + r[101:] for r in reads]
+    st = dict(kmer_size=12, min_collisions=3)
+    with pytest.raises(oracle_mod.OracleError):
+        oracle_mod.Run(reads=reads, settings=oracle_mod.default_settings(**st), quadratic=True)
+    with pytest.raises(sao.SAError) as e:
+        gpu_quadratic(reads=reads, **st)
+    assert e.value.name == "SA_E_NON_ACGT"
+
+
+@pytest.mark.gpu
+def test_gpu_trail_limit_overflow():
+    reads = H.synth_reads(30, 2100, 6000, seed=42)
+    with pytest.raises(sao.SAError) as e:
+        gpu_quadratic(reads=reads, kmer_size=15, min_collisions=3, wide=True)
+    assert e.value.name == "SA_E_OVERFLOW"
