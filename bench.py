@@ -47,11 +47,22 @@ def splitmix64(seed, n):
     return z ^ (z >> np.uint64(31))
 
 
-def synth_workload(n_reads, read_len, genome_len, gc, seed, shard=0):
+def synth_lengths(n_reads, read_len, min_len, seed, shard=0):
+    """Read lengths: all read_len, or U[min_len, read_len] from splitmix64 (BASELINE
+    configs[4]'s mixed 100-1000 bp reads)."""
+    if min_len is None or min_len >= read_len:
+        return np.full(n_reads, read_len, dtype=np.int64)
+    with np.errstate(over="ignore"):
+        z = splitmix64((seed ^ 0x5EED) + 104729 * shard, n_reads)
+    return (min_len + (z % np.uint64(read_len - min_len + 1))).astype(np.int64)
+
+
+def synth_workload(n_reads, read_len, genome_len, gc, seed, shard=0, min_len=None):
     """Genome: base i from splitmix64(seed) (GC with probability gc); reads start
     uniformly in [0, G-L] (splitmix64((seed ^ 0xABCDEF) + 7919 * shard): shard
     r of a multi-GPU run samples its own reads of the same genome), forward
-    strand, error-free."""
+    strand, error-free; lengths from synth_lengths."""
+    lens = synth_lengths(n_reads, read_len, min_len, seed, shard)
     with np.errstate(over="ignore"):
         z = splitmix64(seed, genome_len)
         u = (z >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
@@ -59,11 +70,15 @@ def synth_workload(n_reads, read_len, genome_len, gc, seed, shard=0):
         genome = np.where(u < gc, np.where(bit == 1, ord("G"), ord("C")),
                           np.where(bit == 1, ord("T"), ord("A"))).astype(np.uint8)
         rs = (seed ^ 0xABCDEF) + 7919 * shard
-        starts = (splitmix64(rs, n_reads) % np.uint64(genome_len - read_len + 1)).astype(np.int64)
-    idx = starts[:, None] + np.arange(read_len, dtype=np.int64)[None, :]
-    bases = genome[idx].reshape(-1)
-    offsets = np.arange(n_reads + 1, dtype=np.uint64) * np.uint64(read_len)
-    return bases, offsets
+        starts = (splitmix64(rs, n_reads) % (np.uint64(genome_len + 1) - lens.astype(np.uint64))).astype(np.int64)
+    offsets = np.zeros(n_reads + 1, dtype=np.uint64)
+    offsets[1:] = np.cumsum(lens)
+    if lens.min() == lens.max():
+        idx = starts[:, None] + np.arange(read_len, dtype=np.int64)[None, :]
+        return genome[idx].reshape(-1), offsets
+    read_of = np.repeat(np.arange(n_reads, dtype=np.int64), lens)
+    pos = np.arange(int(offsets[-1]), dtype=np.int64) - offsets[:-1].astype(np.int64)[read_of]
+    return genome[starts[read_of] + pos], offsets
 
 
 def pmc_traffic(kernels):
@@ -106,6 +121,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--reads", type=int, default=100_000)
     ap.add_argument("--len", type=int, default=500)
+    ap.add_argument("--min-len", type=int, default=None,
+                    help="mixed lengths U[min-len, len] (configs[4]: 100..1000); default: all --len")
     ap.add_argument("--k", type=int, default=15)
     ap.add_argument("--gc", type=float, default=0.50)
     ap.add_argument("--coverage", type=float, default=20.0)
@@ -137,13 +154,15 @@ def main():
 
     import saoverlap as sao
 
-    G = int(args.reads * args.len / args.coverage)
+    mean_len = args.len if args.min_len is None else (args.len + args.min_len) / 2.0
+    G = int(args.reads * mean_len / args.coverage)
     if sharded:
         # one genome for all ranks (G per GPU, weak scaling), rank r's reads are
         # global ids r*reads+1 .. (r+1)*reads
-        bases, offsets = synth_workload(args.reads, args.len, G * ws, args.gc, seed=1, shard=rank)
+        bases, offsets = synth_workload(args.reads, args.len, G * ws, args.gc, seed=1, shard=rank,
+                                        min_len=args.min_len)
     else:
-        bases, offsets = synth_workload(args.reads, args.len, G, args.gc, seed=1 + rank)
+        bases, offsets = synth_workload(args.reads, args.len, G, args.gc, seed=1 + rank, min_len=args.min_len)
     ov = sao.Overlapper(device=local if ws > 1 else 0, timing=True, kmer_size=args.k,
                         id_mode=sao.SA_IDS_WIDE, align_kernel=args.align_kernel)
     ov.add_packed(bases.tobytes(), offsets)
@@ -151,7 +170,8 @@ def main():
     if sharded:
         from sharded import HipWorker, ShardedOverlapper
         starts = np.arange(ws + 1, dtype=np.int64) * args.reads
-        lengths = np.full(args.reads * ws, args.len, dtype=np.int32)
+        lengths = np.concatenate([synth_lengths(args.reads, args.len, args.min_len, 1, r)
+                                  for r in range(ws)]).astype(np.int32)
         so = ShardedOverlapper(HipWorker(ov), rank, ws, starts, lengths, "cuda:%d" % local)
     build_step = so.build if so is not None else ov.device_build
     red_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
@@ -248,19 +268,25 @@ def main():
     # By time the bucket build dominates the step: part_mark + part_build<1024>
     # + part_build<4096> (the "buckets" stage, one HIP-event scope).  Algorithmic
     # HBM bytes per step: per k-mer 8 B (partition-start scan) +
-    # 12 B (record load) + 16 B (partner record store), + 4 B per partner-list
-    # entry (st/md/en tags of every position: E2 cut table for the workload).
-    d = args.len - args.k
-    npos = d + 1
-    loc = np.arange(npos, dtype=np.float32) / np.float32(d)
+    # 8 B (record load) + 16 B (partner record store), + 4 B per partner-list
+    # entry (st/md/en tags of every position: E2 cut table for each read length).
     f32 = np.float32
     edge, center = f32(0.4), f32(0.4)
-    tags = ((loc <= edge).astype(np.int64) + ((f32(0.5) - center * f32(0.5) <= loc) &
-            (loc <= f32(0.5) + center * f32(0.5))).astype(np.int64) + (f32(1.0) - edge <= loc).astype(np.int64))
-    list_entries = st["kmers"] * float(tags.sum()) / npos
+    lens_here = np.diff(offsets.astype(np.int64))
+    list_entries = 0.0
+    for L, nL in zip(*np.unique(lens_here, return_counts=True)):
+        d = int(L) - args.k
+        if d <= 0:
+            continue
+        loc = np.arange(d + 1, dtype=np.float32) / np.float32(d)
+        tags = ((loc <= edge).astype(np.int64) + ((f32(0.5) - center * f32(0.5) <= loc) &
+                (loc <= f32(0.5) + center * f32(0.5))).astype(np.int64) + (f32(1.0) - edge <= loc).astype(np.int64))
+        list_entries += float(nL) * float(tags.sum())
+    if sharded:  # this rank builds the buckets it owns: ~1/ws of all k-mers
+        list_entries *= st["kmers"] / max(1.0, float(np.sum(np.maximum(lens_here - args.k + 1, 0))))
     bk_ms, bk_n = stages["buckets"]
     bk_avg_ms = bk_ms / max(bk_n, 1)
-    bk_bytes = 36.0 * st["kmers"] + 4.0 * list_entries
+    bk_bytes = 32.0 * st["kmers"] + 4.0 * list_entries
     bk_ach = bk_bytes / (bk_avg_ms * 1e-3) / 1e9 if bk_avg_ms > 0 else 0.0
     bk_traffic, bk_src = pmc_traffic(("part_mark_kernel", "part_build_kernel<1024", "part_build_kernel<4096"))
     roofline = {"bound": "hbm", "achieved": round(bk_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -318,9 +344,11 @@ def main():
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic (splitmix64 genome, error-free 500 bp reads)",
-            "config": {"workload": "configs[1]: %dk synthetic %d bp reads/GPU, k=%d, bucket build + "
-                                   "edge/middle pair filter" % (args.reads // 1000, args.len, args.k),
-                       "reads_per_gpu": args.reads, "read_len": args.len, "k": args.k,
+            "config": {"workload": "configs[1]: %dk synthetic %s bp reads/GPU, k=%d, bucket build + "
+                                   "edge/middle pair filter" % (args.reads // 1000, (
+                                       "%d" % args.len if args.min_len is None else
+                                       "%d-%d" % (args.min_len, args.len)), args.k),
+                       "reads_per_gpu": args.reads, "read_len": args.len, "min_len": args.min_len, "k": args.k,
                        "genome_bp_per_gpu": G, "ids": "wide",
                        "parallelism": ("sharded-a2a-%s" % args.dist_backend if sharded else
                                        "replicas" if ws > 1 else "single")},

@@ -80,6 +80,7 @@ struct sa_ctx {
     // derived (host)
     std::vector<int32_t> len;
     std::vector<uint64_t> woff, occ_off;
+    std::vector<uint32_t> g2r;  // coarse occurrence -> read table (sa_internal.h, G2R_SHIFT)
     std::vector<uint32_t> lbase, lrank;
     std::vector<uint8_t> tagtab;
     int lb = 1, m = 0, maxd = 0, maxL = 0, minL = 0;
@@ -88,7 +89,7 @@ struct sa_ctx {
     uint32_t max_occ = 0;
     int32_t mode = SA_IDS_WIDE;
     // device buffers
-    DBuf d_ascii, d_boff, d_woff, d_len, d_codes, d_bad, d_occ_off, d_lbase, d_lrank, d_tagtab;
+    DBuf d_ascii, d_boff, d_woff, d_len, d_codes, d_bad, d_occ_off, d_lbase, d_lrank, d_tagtab, d_g2r;
     DBuf d_keys, d_vals, d_keys2, d_vals2, d_sorttmp;
     DBuf d_md, d_ed, d_bmdo, d_bedo, d_bstart, d_gbid, d_gmds, d_gede, d_ogid, d_bkttmp;
     DBuf d_mdidx, d_edidx, d_occidx, d_bnst, d_brank, d_bhash, d_bfirst;
@@ -111,7 +112,7 @@ struct sa_ctx {
     uint64_t part_np = 0;            // partial pairs after sa_dist_count
     uint32_t *part_perm = nullptr;   // their ascending-lead order (region-space indices)
     DBuf d_gocc, d_rid, d_loff, d_starts, d_bounds, d_gcodes, d_gwoff, d_glen, d_gbad, d_psum, d_pkeep, d_ppos;
-    DBuf d_scan, d_lr;
+    DBuf d_scan, d_lr, d_bigtot;
     // options / state
     bool keep_pairs = false, timing = false;
     int align_kernel = 0;  // SA_OPT_ALIGN_KERNEL
@@ -259,6 +260,16 @@ int prepare_reads(sa_ctx *c) {
     }
     c->n_occ = c->occ_off[n];
     if (c->n_occ >= 0xFFFFFFF0ull) return fail(c, SA_E_OVERFLOW, "more than 2^32 k-mers on one device");
+    {
+        const uint64_t nb = (c->n_occ >> G2R_SHIFT) + 2;
+        c->g2r.assign(nb, 0);
+        for (uint64_t b = 0; b < nb; ++b) {
+            const uint64_t target = b << G2R_SHIFT;
+            const uint64_t r = (uint64_t)(std::upper_bound(c->occ_off.begin(), c->occ_off.begin() + n, target) -
+                                          c->occ_off.begin());
+            c->g2r[b] = (uint32_t)(r ? r - 1 : 0);
+        }
+    }
     if (c->dist) {
         // loc ranks / tags / sort-key width must agree on every rank: derive
         // them from the lengths of ALL reads, not just this rank's
@@ -340,6 +351,9 @@ int upload_reads(sa_ctx *c) {
     HIPCHK(hipMemcpyAsync(woff, c->woff.data(), (n + 1) * 8, hipMemcpyHostToDevice, c->stream));
     if (n) HIPCHK(hipMemcpyAsync(len, c->len.data(), n * 4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(occ, c->occ_off.data(), (n + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    uint32_t *g2r;
+    ENSURE(c->d_g2r, c->g2r.size(), &g2r);
+    HIPCHK(hipMemcpyAsync(g2r, c->g2r.data(), c->g2r.size() * 4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(lbase, c->lbase.data(), c->lbase.size() * 4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(lrank, c->lrank.data(), c->lrank.size() * 4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(tag, c->tagtab.data(), c->tagtab.size(), hipMemcpyHostToDevice, c->stream));
@@ -411,8 +425,12 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
     // record here shares (the owner rank's bits in distributed mode);
     // partitions use the PB bits below them
     // ---- partition by the top P bits of mix(seqHash): whole buckets per partition
+    // ~700 records per partition (LDS capacity 1,024); up to 2^24 partitions
+    // (1.25M reads of 500 bp = 607M k-mers per GPU -> 2^20), but stay at 16 bits
+    // (two radix passes) while the average still fits the 1,024-record kernel
     int PB = 1;
-    while (PB < 16 && ((uint64_t)700 << PB) < n) ++PB;
+    while (PB < 24 && ((uint64_t)700 << PB) < n) ++PB;
+    if (PB > 16 && (n >> 16) <= 900) PB = 16;
     const uint32_t nparts = 1u << PB;
     const int kbits = 32 + c->lb;  // LDS sort key: mix << lb | loc rank
     {
@@ -429,6 +447,7 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
     PA.tagtab = (const uint8_t *)c->d_tagtab.p;
     PA.occ_off = occ_off;
     PA.n_reads = n_reads; PA.npr = npr; PA.rid = rid;
+    PA.g2r = (rid || npr) ? nullptr : (const uint32_t *)c->d_g2r.p;
     PA.lr = lr;
     PA.len = len;
     PA.lbase = (const uint32_t *)c->d_lbase.p;
@@ -484,6 +503,9 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
             ENSURE(c->d_occidx, 3 * n + 3, &B.occ_idx);
             ENSURE(c->d_bnst2, maxn + 1, &B.bkt_nst);
         }
+        uint32_t *bigtot;
+        ENSURE(c->d_bigtot, 4 * (size_t)big_n, &bigtot);
+        uint32_t bi = 0;
         StageScope st(c, SA_STAGE_BUCKETS);
         for (uint32_t p : bl) {
             const uint32_t ps = starts[p], pn = starts[p + 1] - starts[p];
@@ -501,16 +523,20 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
             B.md_list = PA.md_list + ps;
             B.ed_list = PA.ed_list + 2ull * ps;
             if (strict) { B.md_idx = PA.md_idx + ps; B.ed_idx = PA.ed_idx + 2ull * ps; }
-            HIPCHK(build_buckets(keys2 + ps, vals + ps, pn, c->lb, tagtab, PA.occ_off, n_reads, npr, rid, B,
-                                 cnt->totals, btmp, c->stream));
+            HIPCHK(build_buckets(keys2 + ps, vals + ps, pn, c->lb, tagtab, PA.occ_off, n_reads, npr, rid, PA.g2r, B,
+                                 bigtot + 4 * (size_t)bi, btmp, c->stream));
             if (strict) HIPCHK(build_strict_index(keys2 + ps, vals + ps, pn, c->lb, tagtab, B, c->stream));
             HIPCHK(launch_records_from_tables(keys2, vals, ps, pn, c->lb, tagtab, B, PA.rec, strict ? 1 : 0, PA.srec,
                                               PA.bkt_nst, PA.bkt_nmd, PA.bkt_first, PA.is_head, c->stream));
-            uint32_t tot[4];
-            HIPCHK(hipMemcpyAsync(tot, cnt->totals, 16, hipMemcpyDeviceToHost, c->stream));
-            HIPCHK(hipStreamSynchronize(c->stream));
-            big_buckets += tot[0];
-            big_groups += tot[1];
+            ++bi;
+        }
+        // per-partition totals read back once (no host sync inside the loop)
+        std::vector<uint32_t> tots(4 * (size_t)big_n);
+        HIPCHK(hipMemcpyAsync(tots.data(), bigtot, tots.size() * 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        for (uint32_t i = 0; i < big_n; ++i) {
+            big_buckets += tots[4 * (size_t)i];
+            big_groups += tots[4 * (size_t)i + 1];
         }
     }
     (void)big_groups;

@@ -24,10 +24,14 @@
 namespace sa {
 
 __device__ __forceinline__ uint32_t read_of_g(uint32_t g, const uint64_t *occ_off, uint32_t n_reads, uint32_t npr,
-                                              const uint32_t *rid) {
+                                              const uint32_t *rid, const uint32_t *g2r) {
     if (rid) return rid[g];  // distributed mode: occurrence index -> global read id
     if (npr) return g / npr;
     uint32_t lo = 0, hi = n_reads;  // largest r with occ_off[r] <= g
+    if (g2r) {  // mixed lengths: the owner lies between the owners of the enclosing 1,024-blocks
+        lo = g2r[g >> G2R_SHIFT];
+        hi = g2r[(g >> G2R_SHIFT) + 1] + 1;
+    }
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
         if (occ_off[mid] <= g) lo = mid; else hi = mid;
@@ -42,7 +46,7 @@ __device__ __forceinline__ unsigned long long record_key(uint64_t rec, const Par
     if (A.lr) {
         lr = A.lr[g];
     } else {
-        const uint32_t r = read_of_g(g, A.occ_off, A.n_reads, A.npr, nullptr);
+        const uint32_t r = read_of_g(g, A.occ_off, A.n_reads, A.npr, nullptr, A.g2r);
         const uint32_t pos = A.npr ? g - r * A.npr : g - (uint32_t)A.occ_off[r];
         const int32_t d = A.npr ? (int32_t)A.npr - 1 : A.len[r] - A.k;
         lr = A.lrank[A.lbase[d] + pos];
@@ -304,7 +308,7 @@ __global__ __launch_bounds__(PB_THREADS) void part_build_kernel(PartArgs A, uint
         if (isg) { gh = s; ++ng; }
         const uint32_t t = tagv[j];
         const uint32_t g = S.g[s];
-        const uint32_t r = read_of_g(g, A.occ_off, A.n_reads, A.npr, A.rid);
+        const uint32_t r = read_of_g(g, A.occ_off, A.n_reads, A.npr, A.rid, A.g2r);
         const uint32_t st = (t & TAG_ST) ? 1u : 0u, en = (t & TAG_EN) ? 1u : 0u, md = (t & TAG_MD) ? 1u : 0u;
         const uint32_t mpos = ps + S.mdx[s], epos = 2 * ps + S.edx[s];
         if (!(A.ablate & 4)) {

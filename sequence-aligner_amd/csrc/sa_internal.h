@@ -45,6 +45,11 @@ __device__ __forceinline__ uint32_t mix32(uint32_t h) {
     return h;
 }
 
+// Mixed read lengths: g2r[b] = the read holding occurrence b << G2R_SHIFT (the
+// largest r with occ_off[r] <= b << G2R_SHIFT), so the owner of g lies in
+// [g2r[g >> S], g2r[(g >> S) + 1]] and the binary search spans a few reads.
+constexpr int G2R_SHIFT = 10;
+
 // bit 0 = st, bit 1 = md, bit 2 = en   (KmerTable.scala:106-115)
 enum : uint8_t { TAG_ST = 1, TAG_MD = 2, TAG_EN = 4 };
 
@@ -143,8 +148,8 @@ hipError_t exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, uin
 size_t buckets_temp_bytes(uint64_t n);
 hipError_t build_buckets(const uint64_t *skeys, const uint32_t *svals, uint64_t n, int lb,
                          const uint8_t *tagtab, const uint64_t *occ_off, uint32_t n_reads,
-                         uint32_t uniform_npr, const uint32_t *rid, Buckets &b, uint32_t *totals_dev,
-                         void *tmp, hipStream_t s);
+                         uint32_t uniform_npr, const uint32_t *rid, const uint32_t *g2r, Buckets &b,
+                         uint32_t *totals_dev, void *tmp, hipStream_t s);
 hipError_t build_strict_index(const uint64_t *skeys, const uint32_t *svals, uint64_t n, int lb,
                               const uint8_t *tagtab, Buckets &b, hipStream_t s);
 
@@ -164,6 +169,7 @@ struct PartArgs {
     const uint64_t *occ_off;
     uint32_t n_reads, npr;
     const uint32_t *rid;         // read id by occurrence index (distributed mode) or null
+    const uint32_t *g2r;         // coarse occurrence -> read table (mixed lengths) or null
     // sk holds 8-byte records (mix32 << 32 | occurrence index); the loc rank is
     // re-derived: lr[g] when given (distributed mode), else from the read's
     // length and the position (lrank[lbase[L - k] + pos])
