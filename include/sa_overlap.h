@@ -188,7 +188,10 @@ int sa_sync(sa_ctx *ctx);
  *   sa_dist_count     -> sa_dist_partials -> exchange 2 (partial pair counts)
  *   sa_dist_reduce    (this rank's leads: sum, [min,max] filter, dispatch)
  * and, for alignment, sa_dist_codes -> all-gather -> sa_dist_set_reads, then
- * sa_align / sa_device_align / sa_get_ovl over this rank's leads.  No
+ * sa_align / sa_device_align / sa_get_ovl over this rank's leads.  The
+ * library works on its own non-blocking HIP stream: device buffers handed in
+ * must be complete (synchronise the stream that produced them, e.g. the one a
+ * collective ran on), and buffers it fills are complete when the call returns.  No
  * reference counterpart: the reference is single-process
  * (KmerTable.scala:41-187 is the semantics each rank restates).
  */

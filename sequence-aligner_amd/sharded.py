@@ -106,6 +106,13 @@ class ShardedOverlapper:
         dist.all_to_all_single(r, t, group=self.group)
         return r.cpu().numpy().astype(np.int64)
 
+    def _ready(self):
+        """Device collectives (RCCL) complete on torch's current stream, but the
+        library runs its kernels on its own non-blocking HIP stream: wait for the
+        current stream before handing received buffers to the worker."""
+        if self.dev.type == "cuda":
+            torch.cuda.current_stream(self.dev).synchronize()
+
     def _a2a(self, recv, send, recv_counts, send_counts):
         rs = [int(x) for x in recv_counts]
         ss = [int(x) for x in send_counts]
@@ -128,6 +135,7 @@ class ShardedOverlapper:
         nr = int(rcounts.sum())
         rk = self._buf("rk", nr, torch.int64)
         self._a2a(rk, sk, rcounts, counts)
+        self._ready()
         pcounts = w.count(rk, nr)
         npart = int(np.sum(pcounts))
         pf = self._buf("pf", npart, torch.int32)
@@ -142,6 +150,7 @@ class ShardedOverlapper:
         self._a2a(qf, pf, rp, pcounts)
         self._a2a(qs, ps, rp, pcounts)
         self._a2a(qc, pc, rp, pcounts)
+        self._ready()
         w.reduce(qf, qs, qc, nq)
 
     # -- reads for alignment: all-gather of the packed words ---------------------
@@ -167,6 +176,7 @@ class ShardedOverlapper:
         self.exchanged_bytes += 4 * (mw + mr) * (self.P - 1)
         allc = torch.cat([gc[r * mw:r * mw + per_rank_words[r]] for r in range(self.P)]).to(self.dev)
         allb = torch.cat([gb[r * mr:r * mr + per_rank_reads[r]] for r in range(self.P)]).to(self.dev)
+        self._ready()
         w.set_reads(allc, allb, int(sum(per_rank_words)))
 
     def align(self):

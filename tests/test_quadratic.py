@@ -163,3 +163,23 @@ def test_gpu_trail_limit_overflow():
     with pytest.raises(sao.SAError) as e:
         gpu_quadratic(reads=reads, kmer_size=15, min_collisions=3, wide=True)
     assert e.value.name == "SA_E_OVERFLOW"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("quad", [False, True])
+def test_gpu_cli_matches_golden(tmp_path, quad):
+    """The process boundary AMOS sees: `sa-overlap -i X.seq -o X.ovl -k 12
+    [--quadratic-align]` writes the golden bytes (Rakefile.rb:181-182)."""
+    import subprocess
+    cli = os.path.join(os.path.dirname(H.GOLDEN), "..", "sequence-aligner_amd", "build", "sa-overlap")
+    out = tmp_path / "x.ovl"
+    args = [cli, "-i", os.path.join(H.GOLDEN, "crp177.seq"), "-o", str(out), "-k", "12"]
+    if quad:
+        args.append("--quadratic-align")
+    r = subprocess.run(args, capture_output=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    want = golden("crp177_k12")[1] if quad else open(os.path.join(H.GOLDEN, "crp177_k12.ovl"), "rb").read()
+    assert out.read_bytes() == want
+    # stdout is a clean .ovl stream when -o is absent
+    r = subprocess.run(args[:3] + args[5:], capture_output=True, timeout=120)
+    assert r.returncode == 0 and r.stdout == want
