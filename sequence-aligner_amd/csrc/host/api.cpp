@@ -894,8 +894,10 @@ int device_align(sa_ctx *c, bool readback) {
     for (int x = 0; x < 16; ++x)
         if (c->set.cost[x] < -128 || c->set.cost[x] > 127)
             return fail(c, SA_E_ARG, "cost matrix entries must lie in [-128, 127]");
-    // lane-per-pair kernel: band <= 15 columns, reads <= 30,000 bp (c << 16 | e packing)
-    const bool lane_fits = wmax <= 15 && maxL <= 30000;
+    // lane-per-pair kernels: band <= 31 columns (16 / 24 / 32 registers per row),
+    // reads <= 30,000 bp (c << 16 | e packing)
+    const int lw = dovetail_lane_width(wmax);
+    const bool lane_fits = lw > 0 && maxL <= 30000;
     if (c->aligner == SA_ALIGNER_LINEAR && c->align_kernel == 2 && !lane_fits)
         return fail(c, SA_E_ARG, "SA_OPT_ALIGN_KERNEL=2 but a band or read exceeds the lane kernel");
     if (c->aligner == SA_ALIGNER_LINEAR && c->align_kernel == 3 && !lane_fits)
@@ -904,7 +906,7 @@ int device_align(sa_ctx *c, bool readback) {
         return fail(c, SA_E_ARG, "--quadratic-align needs gap costs <= 0 (Project4.readArgs negates them)");
     const bool use_lane = c->align_kernel >= 2 || (c->align_kernel == 0 && lane_fits);
     const int32_t wmin = std::max(c->set.kmer_size, (int32_t)floor((double)((float)minL * omm)) + 1);
-    const bool exact = wmin == 15 && wmax == 15;  // every band exactly 16 cells wide
+    const bool exact = wmin == 15 && wmax == 15 && lw == 16;  // every band exactly 16 cells wide
     AlignParams P;
     P.k = c->set.kmer_size;
     P.gap_open = c->set.gap_open;
@@ -948,19 +950,19 @@ int device_align(sa_ctx *c, bool readback) {
             ENSURE(c->d_ovals2, nd, &v1);
             ENSURE(c->d_osort, radix_sort_temp_bytes(nd), &tmp);
             const int32_t *dl = (const int32_t *)c->d_lead.p, *dt = (const int32_t *)c->d_trail.p;
-            HIPCHK(launch_dovetail_p1(AR, dl, dt, nd, P, exact, p1, k0, v0, &cnt->err, cnt->cells,
+            HIPCHK(launch_dovetail_p1(AR, dl, dt, nd, P, lw, exact, p1, k0, v0, &cnt->err, cnt->cells,
                                       c->stream));
             HIPCHK(radix_sort(&k0, &v0, &k1, &v1, nd, 0, 20, tmp, c->stream));
             if (c->align_kernel == 3) {  // path summaries forwarded per cell
-                HIPCHK(launch_dovetail_p2(AR, dl, dt, nd, P, exact, p1, v0, out, &cnt->err, c->stream));
+                HIPCHK(launch_dovetail_p2(AR, dl, dt, nd, P, lw, exact, p1, v0, out, &cnt->err, c->stream));
             } else {  // 2-bit traceback codes in HBM + per-lane walk, in launches of <= 4 GiB of codes
-                const uint64_t per_lane = dovetail_tb_words(1, maxL);
+                const uint64_t per_lane = dovetail_tb_words(1, maxL, lw);
                 uint64_t chunk = std::max<uint64_t>(256, ((1ull << 30) / per_lane) & ~255ull);
                 chunk = std::min<uint64_t>(chunk, (nd + 255) & ~255ull);
                 uint32_t *tb;
-                ENSURE(c->d_tb, dovetail_tb_words(chunk, maxL), &tb);
+                ENSURE(c->d_tb, dovetail_tb_words(chunk, maxL, lw), &tb);
                 for (uint64_t t0 = 0; t0 < nd; t0 += chunk)
-                    HIPCHK(launch_dovetail_p2tb(AR, dl, dt, nd, t0, chunk, P, exact, p1, v0, out, &cnt->err, tb,
+                    HIPCHK(launch_dovetail_p2tb(AR, dl, dt, nd, t0, chunk, P, lw, exact, p1, v0, out, &cnt->err, tb,
                                                 c->stream));
             }
         } else

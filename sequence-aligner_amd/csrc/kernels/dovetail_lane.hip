@@ -23,7 +23,8 @@ namespace sa {
 
 namespace {
 
-constexpr int LW = 16;  // band cells per row held in registers (w <= LW - 1)
+// LW = band cells per row held in registers (w <= LW - 1): 16 for every read up
+// to ~750 bp at min identity 0.98 (the bench), 24 / 32 for longer reads
 
 __device__ __forceinline__ int32_t bfe_s8(uint32_t packed, uint32_t shift) {
     return __builtin_amdgcn_sbfe((int32_t)packed, shift, 8);
@@ -47,6 +48,7 @@ __device__ __forceinline__ uint32_t gld(const uint32_t *p, int32_t i) {
 }
 
 // Phase-2 lane state: the band row in registers plus the A / B read windows.
+template <int LW>
 struct Band {
     uint32_t b8[LW];                            // 8 * B[k - zr + u - 1] for the current row u (0 outside B)
     int32_t Tk[LW], Qk[LW], Pk[LW], Ck[LW];     // max(T,0), max(Q,0), stop cell (u << 6 | k), (c << 16 | e)
@@ -61,8 +63,8 @@ struct Band {
 // (matches << 16 | errors).  MASKED rows test 1 <= j <= |B| per cell; EXACT
 // launches have w == LW - 1 for every pair (no per-lane column tests).
 // Q = max(max(M, X) + gO, Y) is kept clamped at 0: the next row's Y is gE + Q.
-template <bool MASKED, bool EXACT>
-__device__ __forceinline__ void band_cell(Band &S, const int k, const int32_t u6, const int32_t jb, const int32_t LB,
+template <int LW, bool MASKED, bool EXACT>
+__device__ __forceinline__ void band_cell(Band<LW> &S, const int k, const int32_t u6, const int32_t jb, const int32_t LB,
                                           const int32_t w, const uint32_t cp, const uint32_t eqsh, const int32_t gO,
                                           const int32_t gE, const bool act, int32_t &Zl, int32_t &Xl, int32_t &Pl,
                                           int32_t &Cl) {
@@ -106,8 +108,8 @@ __device__ __forceinline__ void band_cell(Band &S, const int k, const int32_t u6
 // One phase-2 row u, then advance the A / B windows one base.  Branch-free:
 // lanes past their last row (u > rows2) keep computing but no longer update the
 // argmax, and the window loads are unconditional (clamped to the read).
-template <bool MASKED, bool EXACT>
-__device__ __forceinline__ void band_row(Band &S, const int32_t u, const int32_t rows2, const int32_t zr,
+template <int LW, bool MASKED, bool EXACT>
+__device__ __forceinline__ void band_row(Band<LW> &S, const int32_t u, const int32_t rows2, const int32_t zr,
                                          const int32_t LB, const int32_t w, const uint32_t c0, const uint32_t c1,
                                          const uint32_t c2, const uint32_t c3,
                                          const int32_t gO, const int32_t gE, const uint32_t *Aw, const int32_t awl,
@@ -121,7 +123,7 @@ __device__ __forceinline__ void band_row(Band &S, const int32_t u, const int32_t
     const bool act = u <= rows2;
     int32_t Zl = 0, Xl = 0, Pl = 0, Cl = 0;
 #pragma unroll
-    for (int k = 0; k < LW; ++k) band_cell<MASKED, EXACT>(S, k, u6, jb, LB, w, cp, eqsh, gO, gE, act, Zl, Xl, Pl, Cl);
+    for (int k = 0; k < LW; ++k) band_cell<LW, MASKED, EXACT>(S, k, u6, jb, LB, w, cp, eqsh, gO, gE, act, Zl, Xl, Pl, Cl);
     // two-word windows: the word after the current one was loaded at least one
     // row earlier, so the loads issued here are not waited on until next row
     // Window words are fetched the row before a window crosses into them, so a
@@ -145,7 +147,7 @@ struct LanePair {
     const uint32_t *Aw, *Bw;
 };
 
-template <bool EXACT>
+template <int LW, bool EXACT>
 __device__ __forceinline__ LanePair lane_pair(const DevReads &rd, const int32_t *lead, const int32_t *trail,
                                               uint64_t pair, const AlignParams &P) {
     LanePair q;
@@ -223,6 +225,7 @@ __device__ __forceinline__ void finish_alignment(const AlignParams &P, const Lan
 // to HBM lane-interleaved (one coalesced 256-B store per column).  The walk
 // then runs per lane from the argmax over those words, 16 diagonal steps per
 // word load, counting matches with a 2-bit XOR / popcount.
+template <int LW>
 struct BandTb {
     uint32_t b8[LW];
     int32_t Tk[LW], Qk[LW];
@@ -232,8 +235,8 @@ struct BandTb {
     uint32_t awd, bw, pa, pb;
 };
 
-template <bool MASKED, bool EXACT>
-__device__ __forceinline__ void band_cell_tb(BandTb &S, const int k, const int32_t u6, const int32_t jb,
+template <int LW, bool MASKED, bool EXACT>
+__device__ __forceinline__ void band_cell_tb(BandTb<LW> &S, const int k, const int32_t u6, const int32_t jb,
                                              const int32_t LB, const int32_t w, const uint32_t cp, const int32_t gO,
                                              const int32_t gE, const bool act, const uint32_t c1, const uint32_t c2,
                                              const uint32_t c3, int32_t &Zl, int32_t &Xl) {
@@ -260,8 +263,8 @@ __device__ __forceinline__ void band_cell_tb(BandTb &S, const int k, const int32
     Xl = X;
 }
 
-template <bool MASKED, bool EXACT>
-__device__ __forceinline__ void band_row_tb(BandTb &S, const int32_t u, const int32_t rows2, const int32_t zr,
+template <int LW, bool MASKED, bool EXACT>
+__device__ __forceinline__ void band_row_tb(BandTb<LW> &S, const int32_t u, const int32_t rows2, const int32_t zr,
                                             const int32_t LB, const int32_t w, const uint32_t c0, const uint32_t cq1,
                                             const uint32_t cq2, const uint32_t cq3, const int32_t gO, const int32_t gE,
                                             const uint32_t *Aw, const int32_t awl, const uint32_t *Bw,
@@ -277,7 +280,7 @@ __device__ __forceinline__ void band_row_tb(BandTb &S, const int32_t u, const in
                    k3 = in_vgpr((int32_t)(3u << sh));
     int32_t Zl = 0, Xl = 0;
 #pragma unroll
-    for (int k = 0; k < LW; ++k) band_cell_tb<MASKED, EXACT>(S, k, u6, jb, LB, w, cp, gO, gE, act, k1, k2, k3, Zl, Xl);
+    for (int k = 0; k < LW; ++k) band_cell_tb<LW, MASKED, EXACT>(S, k, u6, jb, LB, w, cp, gO, gE, act, k1, k2, k3, Zl, Xl);
     if ((u & 15) == 15) {  // a full 16-row word per column: out, lane-interleaved
         uint32_t *base = tb + (uint64_t)(u >> 4) * LW * nt;
 #pragma unroll
@@ -310,7 +313,7 @@ __device__ __forceinline__ uint32_t win16_g(const uint32_t *w, int32_t p) {
 // backtrack and the dud test.  p1[pair] = (ds << 1 | dud) or a negative error;
 // rows2[pair] = phase-2 row count (0 when phase 2 does not run) -- the key the
 // host sorts by so each wave of the phase-2 kernel gets pairs of similar length.
-template <bool EXACT>
+template <int LW, bool EXACT>
 __global__ __launch_bounds__(256) void dovetail_p1_kernel(DevReads rd, const int32_t *lead, const int32_t *trail,
                                                           uint64_t npairs, AlignParams P, int32_t *p1,
                                                           uint64_t *rows2_key, uint32_t *order, int32_t *err,
@@ -320,7 +323,7 @@ __global__ __launch_bounds__(256) void dovetail_p1_kernel(DevReads rd, const int
     const int32_t gO = in_vgpr(P.gap_open), gE = in_vgpr(P.gap_extend);
     LanePair q{0, 0, 0, 0, 0, -100, rd.codes, rd.codes};
     if (have) {
-        q = lane_pair<EXACT>(rd, lead, trail, pair, P);
+        q = lane_pair<LW, EXACT>(rd, lead, trail, pair, P);
         if (q.status < 0) set_err(err, q.status);
     }
     const int32_t w = q.w;
@@ -334,11 +337,14 @@ __global__ __launch_bounds__(256) void dovetail_p1_kernel(DevReads rd, const int
         return v;
     };
     const uint32_t cq0 = colpack(0), cq1 = colpack(1), cq2 = colpack(2), cq3 = colpack(3);
-    const uint32_t bw0 = q.status == 0 ? gld(q.Bw, 0) : 0u;  // B[0 .. 16) covers every j <= w <= 15
+    // B[0 .. LW - 1) covers every column j <= w <= LW - 1 (LB >= w, else status -5)
+    const uint32_t bw0 = q.status == 0 ? gld(q.Bw, 0) : 0u;
+    const uint32_t bw1 = (LW > 17 && q.status == 0 && q.LB > 16) ? gld(q.Bw, 1) : 0u;
     uint32_t cb[LW - 1];
 #pragma unroll
     for (int j = 1; j < LW; ++j) {
-        const uint32_t bj = (bw0 >> (30 - 2 * (j - 1))) & 3u;
+        const uint32_t bwj = (j - 1) < 16 ? bw0 : bw1;
+        const uint32_t bj = (bwj >> (30 - 2 * ((j - 1) & 15))) & 3u;
         const uint32_t c01 = (bj & 1) ? cq1 : cq0, c23 = (bj & 1) ? cq3 : cq2;
         cb[j - 1] = (bj & 2) ? c23 : c01;
     }
@@ -419,7 +425,7 @@ __global__ __launch_bounds__(256) void dovetail_p1_kernel(DevReads rd, const int
 
 // Phase 2 (BioLibs.scala:691-819) + Alignment/Overlap validity, one pair per
 // lane, pairs taken in the order `order` (grouped by phase-2 row count).
-template <bool EXACT>
+template <int LW, bool EXACT>
 __global__ __launch_bounds__(256) void dovetail_p2_kernel(DevReads rd, const int32_t *lead, const int32_t *trail,
                                                           uint64_t npairs, AlignParams P, const int32_t *p1,
                                                           const uint32_t *order, DevAlignment *out, int32_t *err) {
@@ -430,7 +436,7 @@ __global__ __launch_bounds__(256) void dovetail_p2_kernel(DevReads rd, const int
     LanePair q{0, 0, 0, 0, 0, -100, rd.codes, rd.codes};
     int32_t r1 = -100;
     if (have) {
-        q = lane_pair<EXACT>(rd, lead, trail, pair, P);
+        q = lane_pair<LW, EXACT>(rd, lead, trail, pair, P);
         r1 = p1[pair];
     }
     const int32_t w = q.w;
@@ -458,12 +464,14 @@ __global__ __launch_bounds__(256) void dovetail_p2_kernel(DevReads rd, const int
         cpa[x] = (uint32_t)(uint8_t)(int8_t)P.cost[x * 4] | ((uint32_t)(uint8_t)(int8_t)P.cost[x * 4 + 1] << 8) |
                  ((uint32_t)(uint8_t)(int8_t)P.cost[x * 4 + 2] << 16) |
                  ((uint32_t)(uint8_t)(int8_t)P.cost[x * 4 + 3] << 24);
-    Band S;
-    const uint32_t bw0 = p2 ? gld(q.Bw, 0) : 0u;  // k - zr <= 15: B[0 .. 16)
+    Band<LW> S;
+    const uint32_t bw0 = p2 ? gld(q.Bw, 0) : 0u;  // k - zr < LW: B[0 .. 32)
+    const uint32_t bw1 = (LW > 16 && p2 && LB > 16) ? gld(q.Bw, 1) : 0u;
 #pragma unroll
     for (int k = 0; k < LW; ++k) {
         const int32_t p = k - zr;
-        S.b8[k] = (p >= 0 && p < LB) ? ((bw0 >> (30 - 2 * p)) & 3u) << 3 : 0u;
+        const uint32_t bwp = p < 16 ? bw0 : bw1;
+        S.b8[k] = (p >= 0 && p < LB) ? ((bwp >> (30 - 2 * (p & 15))) & 3u) << 3 : 0u;
     }
     const int32_t Q0 = max(gO, 0);
 #pragma unroll
@@ -483,11 +491,11 @@ __global__ __launch_bounds__(256) void dovetail_p2_kernel(DevReads rd, const int
     __builtin_amdgcn_s_waitcnt(0);
     int32_t u = 1;
     const int32_t e1 = min(lo - 1, rmax), e2 = min(hi, rmax);
-    for (; u <= e1; ++u) band_row<true, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl,
+    for (; u <= e1; ++u) band_row<LW, true, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl,
                                                     q.Bw, bwl, rd.codes);
-    for (; u <= e2; ++u) band_row<false, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw,
+    for (; u <= e2; ++u) band_row<LW, false, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw,
                                                      awl, q.Bw, bwl, rd.codes);
-    for (; u <= rmax; ++u) band_row<true, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl,
+    for (; u <= rmax; ++u) band_row<LW, true, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl,
                                                     q.Bw, bwl, rd.codes);
 
     if (!have) return;
@@ -497,7 +505,7 @@ __global__ __launch_bounds__(256) void dovetail_p2_kernel(DevReads rd, const int
 // Phase 2 with stored traceback codes: same contract as dovetail_p2_kernel;
 // tb holds 16 columns x rw words for each of the nt lanes of this launch,
 // which covers pairs order[t0 .. t0 + nt).
-template <bool EXACT>
+template <int LW, bool EXACT>
 __global__ __launch_bounds__(256) void dovetail_p2tb_kernel(DevReads rd, const int32_t *lead, const int32_t *trail,
                                                             uint64_t npairs, uint64_t t0, uint64_t nt, AlignParams P,
                                                             const int32_t *p1, const uint32_t *order,
@@ -510,7 +518,7 @@ __global__ __launch_bounds__(256) void dovetail_p2tb_kernel(DevReads rd, const i
     LanePair q{0, 0, 0, 0, 0, -100, rd.codes, rd.codes};
     int32_t r1 = -100;
     if (have) {
-        q = lane_pair<EXACT>(rd, lead, trail, pair, P);
+        q = lane_pair<LW, EXACT>(rd, lead, trail, pair, P);
         r1 = p1[pair];
     }
     const int32_t w = q.w;
@@ -537,12 +545,14 @@ __global__ __launch_bounds__(256) void dovetail_p2tb_kernel(DevReads rd, const i
         cpa[x] = (uint32_t)(uint8_t)(int8_t)P.cost[x * 4] | ((uint32_t)(uint8_t)(int8_t)P.cost[x * 4 + 1] << 8) |
                  ((uint32_t)(uint8_t)(int8_t)P.cost[x * 4 + 2] << 16) |
                  ((uint32_t)(uint8_t)(int8_t)P.cost[x * 4 + 3] << 24);
-    BandTb S;
-    const uint32_t bw0 = p2 ? gld(q.Bw, 0) : 0u;
+    BandTb<LW> S;
+    const uint32_t bw0 = p2 ? gld(q.Bw, 0) : 0u;  // k - zr < LW: B[0 .. 32)
+    const uint32_t bw1 = (LW > 16 && p2 && LB > 16) ? gld(q.Bw, 1) : 0u;
 #pragma unroll
     for (int k = 0; k < LW; ++k) {
         const int32_t p = k - zr;
-        S.b8[k] = (p >= 0 && p < LB) ? ((bw0 >> (30 - 2 * p)) & 3u) << 3 : 0u;
+        const uint32_t bwp = p < 16 ? bw0 : bw1;
+        S.b8[k] = (p >= 0 && p < LB) ? ((bwp >> (30 - 2 * (p & 15))) & 3u) << 3 : 0u;
     }
     const int32_t Q0 = max(gO, 0);
 #pragma unroll
@@ -560,13 +570,13 @@ __global__ __launch_bounds__(256) void dovetail_p2tb_kernel(DevReads rd, const i
     int32_t u = 1;
     const int32_t e1 = min(lo - 1, rmax), e2 = min(hi, rmax);
     for (; u <= e1; ++u)
-        band_row_tb<true, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl, q.Bw,
+        band_row_tb<LW, true, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl, q.Bw,
                                  bwl, rd.codes, tb, nt);
     for (; u <= e2; ++u)
-        band_row_tb<false, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl, q.Bw,
+        band_row_tb<LW, false, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl, q.Bw,
                                   bwl, rd.codes, tb, nt);
     for (; u <= rmax; ++u)
-        band_row_tb<true, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl, q.Bw,
+        band_row_tb<LW, true, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl, q.Bw,
                                  bwl, rd.codes, tb, nt);
     if ((rmax & 15) != 15) {  // the last, partial row block
         uint32_t *base = tb + (uint64_t)(rmax >> 4) * LW * nt;
@@ -612,50 +622,52 @@ __global__ __launch_bounds__(256) void dovetail_p2tb_kernel(DevReads rd, const i
     finish_alignment(P, q, r1, ds, zr, S.best, S.bpos, bstop, bce, out + pair, err);
 }
 
+// LW = 16 (with the EXACT variant: every band exactly 16 cells), 24 or 32
+#define SA_LANE_DISPATCH(KERNEL, GRID, ...)                                                              \
+    do {                                                                                                 \
+        if (lw == 16 && exact) hipLaunchKernelGGL((KERNEL<16, true>), GRID, dim3(256), 0, s, __VA_ARGS__); \
+        else if (lw == 16) hipLaunchKernelGGL((KERNEL<16, false>), GRID, dim3(256), 0, s, __VA_ARGS__);     \
+        else if (lw == 24) hipLaunchKernelGGL((KERNEL<24, false>), GRID, dim3(256), 0, s, __VA_ARGS__);     \
+        else if (lw == 32) hipLaunchKernelGGL((KERNEL<32, false>), GRID, dim3(256), 0, s, __VA_ARGS__);     \
+        else return hipErrorInvalidValue;                                                                \
+    } while (0)
+
+int dovetail_lane_width(int32_t wmax) {
+    return wmax <= 15 ? 16 : (wmax <= 23 ? 24 : (wmax <= 31 ? 32 : 0));
+}
+
 hipError_t launch_dovetail_p1(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
-                              const AlignParams &p, bool exact, int32_t *p1, uint64_t *rows2_key, uint32_t *order,
-                              int32_t *err, unsigned long long *cells, hipStream_t s) {
+                              const AlignParams &p, int lw, bool exact, int32_t *p1, uint64_t *rows2_key,
+                              uint32_t *order, int32_t *err, unsigned long long *cells, hipStream_t s) {
     if (!n) return hipSuccess;
     const dim3 grid((uint32_t)((n + 255) / 256));
-    if (exact)
-        hipLaunchKernelGGL(dovetail_p1_kernel<true>, grid, dim3(256), 0, s, r, lead, trail, n, p, p1, rows2_key, order,
-                           err, cells);
-    else
-        hipLaunchKernelGGL(dovetail_p1_kernel<false>, grid, dim3(256), 0, s, r, lead, trail, n, p, p1, rows2_key, order,
-                           err, cells);
+    SA_LANE_DISPATCH(dovetail_p1_kernel, grid, r, lead, trail, n, p, p1, rows2_key, order, err, cells);
     return hipGetLastError();
 }
 
 hipError_t launch_dovetail_p2(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
-                              const AlignParams &p, bool exact, const int32_t *p1, const uint32_t *order,
+                              const AlignParams &p, int lw, bool exact, const int32_t *p1, const uint32_t *order,
                               DevAlignment *out, int32_t *err, hipStream_t s) {
     if (!n) return hipSuccess;
     const dim3 grid((uint32_t)((n + 255) / 256));
-    if (exact)
-        hipLaunchKernelGGL(dovetail_p2_kernel<true>, grid, dim3(256), 0, s, r, lead, trail, n, p, p1, order, out, err);
-    else
-        hipLaunchKernelGGL(dovetail_p2_kernel<false>, grid, dim3(256), 0, s, r, lead, trail, n, p, p1, order, out, err);
+    SA_LANE_DISPATCH(dovetail_p2_kernel, grid, r, lead, trail, n, p, p1, order, out, err);
     return hipGetLastError();
 }
 
-size_t dovetail_tb_words(uint64_t nt, int32_t max_len) {
+size_t dovetail_tb_words(uint64_t nt, int32_t max_len, int lw) {
     const uint64_t rw = (uint64_t)(max_len + 1 + 15) / 16 + 1;
-    return rw * LW * nt;
+    return rw * (uint64_t)lw * nt;
 }
 
 hipError_t launch_dovetail_p2tb(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
-                                uint64_t t0, uint64_t nt, const AlignParams &p, bool exact, const int32_t *p1,
+                                uint64_t t0, uint64_t nt, const AlignParams &p, int lw, bool exact, const int32_t *p1,
                                 const uint32_t *order, DevAlignment *out, int32_t *err, uint32_t *tb,
                                 hipStream_t s) {
     if (!n || !nt) return hipSuccess;
     const dim3 grid((uint32_t)((nt + 255) / 256));
-    if (exact)
-        hipLaunchKernelGGL(dovetail_p2tb_kernel<true>, grid, dim3(256), 0, s, r, lead, trail, n, t0, nt, p, p1, order,
-                           out, err, tb);
-    else
-        hipLaunchKernelGGL(dovetail_p2tb_kernel<false>, grid, dim3(256), 0, s, r, lead, trail, n, t0, nt, p, p1,
-                           order, out, err, tb);
+    SA_LANE_DISPATCH(dovetail_p2tb_kernel, grid, r, lead, trail, n, t0, nt, p, p1, order, out, err, tb);
     return hipGetLastError();
 }
+#undef SA_LANE_DISPATCH
 
 }  // namespace sa

@@ -210,20 +210,23 @@ hipError_t launch_gather_pairs(const uint32_t *perm, uint64_t n, const uint32_t 
 hipError_t launch_dovetail(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
                            const AlignParams &p, int group_lanes, DevAlignment *out, int32_t *err,
                            unsigned long long *cells, hipStream_t s);
-// one pair per lane, w <= 15, |A| <= 30000 (dovetail_lane.hip); exact: w == 15
-// for every pair.  Phase 1 writes p1 / rows2_key / order (identity); the host
-// sorts (rows2_key, order) and phase 2 takes pairs in that order.
+// one pair per lane, band held in LW = 16 / 24 / 32 registers (w <= LW - 1),
+// |A| <= 30000 (dovetail_lane.hip); exact (LW 16 only): w == 15 for every
+// pair.  dovetail_lane_width(wmax) = the LW for the widest band (0: none fits).
+// Phase 1 writes p1 / rows2_key / order (identity); the host sorts
+// (rows2_key, order) and phase 2 takes pairs in that order.
+int dovetail_lane_width(int32_t wmax);
 hipError_t launch_dovetail_p1(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
-                              const AlignParams &p, bool exact, int32_t *p1, uint64_t *rows2_key, uint32_t *order,
-                              int32_t *err, unsigned long long *cells, hipStream_t s);
+                              const AlignParams &p, int lw, bool exact, int32_t *p1, uint64_t *rows2_key,
+                              uint32_t *order, int32_t *err, unsigned long long *cells, hipStream_t s);
 hipError_t launch_dovetail_p2(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
-                              const AlignParams &p, bool exact, const int32_t *p1, const uint32_t *order,
+                              const AlignParams &p, int lw, bool exact, const int32_t *p1, const uint32_t *order,
                               DevAlignment *out, int32_t *err, hipStream_t s);
 // phase 2 with traceback codes in HBM: lanes t0 .. t0+nt of the order, nt
-// rounded up to 64; tb = dovetail_tb_words(nt, longest lead) u32 words
-size_t dovetail_tb_words(uint64_t nt, int32_t max_len);
+// rounded up to 64; tb = dovetail_tb_words(nt, longest lead, lw) u32 words
+size_t dovetail_tb_words(uint64_t nt, int32_t max_len, int lw);
 hipError_t launch_dovetail_p2tb(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
-                                uint64_t t0, uint64_t nt, const AlignParams &p, bool exact, const int32_t *p1,
+                                uint64_t t0, uint64_t nt, const AlignParams &p, int lw, bool exact, const int32_t *p1,
                                 const uint32_t *order, DevAlignment *out, int32_t *err, uint32_t *tb,
                                 hipStream_t s);
 

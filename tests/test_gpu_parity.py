@@ -161,11 +161,13 @@ def test_full_width_band_500bp(oracle_mod, gaps):
     compare_with_oracle(oracle_mod, ov, r, True)
 
 
-@pytest.mark.parametrize("k,L,minid", [(15, 500, 0.98), (12, 150, 0.92), (12, 300, 0.96), (9, 120, 0.9)])
+@pytest.mark.parametrize("k,L,minid", [(15, 500, 0.98), (12, 150, 0.92), (12, 300, 0.96), (9, 120, 0.9),
+                                        (15, 1000, 0.98), (15, 1450, 0.98), (12, 500, 0.95)])
 def test_align_kernels_agree(k, L, minid):
     """The lane-per-pair kernels (stored codes + walk, and forwarded path
     summaries) and the lane-group kernel give identical alignment tuples on the
-    same dispatch (the default is also checked against the oracle elsewhere)."""
+    same dispatch (the default is also checked against the oracle elsewhere).
+    Band widths 15 (16 registers), 21 (24), 26 and 29 (32)."""
     rng = np.random.default_rng(k * 1000 + L)
     reads = mutate(H.synth_reads(400, L, 20 * L, gc=0.5, seed=k + L), rng, 5)
     st = dict(kmer_size=k, min_identity=minid, min_collisions=3, gap_open=-60, gap_extend=-10)
@@ -364,3 +366,16 @@ def test_sharded_hip_matches_single_gpu(P, tmp_path):
     np.testing.assert_array_equal(np.concatenate([res[r]["al"] for r in order]), ref.alignments())
     assert b"".join(res[r]["ovl"].tobytes() for r in order) == ref.ovl()
     assert sum(int(x["rp"]) for x in res) == ref.stats()["role_pairs"]
+
+
+@pytest.mark.parametrize("mixed,k", [((100, 1000), 15), ((600, 1500), 14)])
+def test_wide_band_lane_kernels_match_oracle(oracle_mod, mixed, k):
+    """Reads up to 1,000-1,500 bp (configs[4]'s shape): bands of 16-31 cells run
+    on the 24- and 32-register lane kernels; bit-exact against the oracle."""
+    rng = np.random.default_rng(mixed[1] + k)
+    reads = mutate(H.synth_reads(160, mixed[1], 12000, gc=0.5, seed=mixed[0] + k, mixed=mixed), rng, 4)
+    st = dict(kmer_size=k, min_collisions=5, gap_open=-60, gap_extend=-10)
+    r = oracle_mod.Run(reads=reads, settings=oracle_settings(oracle_mod, **st), wide=True)
+    ov = gpu_run(reads=reads, wide=True, **st)
+    assert ov.stats()["dispatched"] > 100
+    compare_with_oracle(oracle_mod, ov, r, True)
