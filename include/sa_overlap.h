@@ -101,6 +101,9 @@ int sa_add_reads(sa_ctx *ctx, const char *bases, const uint64_t *offsets, uint32
 /* BioLibs.readSeq (BioLibs.scala:26-50) + sa_add_reads. */
 int sa_read_fasta(sa_ctx *ctx, const char *path);
 uint32_t sa_num_reads(const sa_ctx *ctx);
+/* SequenceData.get (KmerTable.scala:37): read `id` (1-based) as added
+ * (upper-cased); library-owned, valid until reads change or destroy. */
+int sa_get_read(const sa_ctx *ctx, uint32_t id, const char **seq, size_t *len);
 
 /* KmerTable.calcPairData + calcDispatchData (KmerTable.scala:85-187): device
  * k-mer emission, bucket build, edge<->middle pair counting, collision filter. */
@@ -114,6 +117,13 @@ int sa_get_dispatch(sa_ctx *ctx, const int32_t **lead, const int32_t **trail,
  * Requires sa_set_option(ctx, SA_OPT_KEEP_PAIRS, 1) before sa_build_candidates. */
 int sa_get_pairs(sa_ctx *ctx, const int32_t **fst, const int32_t **snd,
                  const int32_t **count, size_t *n);
+
+/* KmerTable.uniqueKmers + kmerCollisionHistogram (KmerTable.scala:189-221), what
+ * `--test-kmer-cover` prints (Project4.scala:299-320): the number of distinct
+ * k-mer hashes and, ascending by size, how many hashes have `size` occurrences.
+ * Works on the added reads at this context's k; independent of
+ * sa_build_candidates.  Arrays are library-owned. */
+int sa_kmer_histogram(sa_ctx *ctx, uint64_t *uniques, const uint64_t **size, const uint64_t **count, size_t *n);
 
 /* genBlockMTAlign -> generateFastDovetailAlignmentSet for every dispatched pair
  * (Project4.scala:725-790, BioLibs.scala:596-822), or generateLocalAlignmentSet

@@ -112,7 +112,10 @@ struct sa_ctx {
     uint64_t part_np = 0;            // partial pairs after sa_dist_count
     uint32_t *part_perm = nullptr;   // their ascending-lead order (region-space indices)
     DBuf d_gocc, d_rid, d_loff, d_starts, d_bounds, d_gcodes, d_gwoff, d_glen, d_gbad, d_psum, d_pkeep, d_ppos;
-    DBuf d_scan, d_lr, d_bigtot;
+    DBuf d_scan, d_lr, d_bigtot, d_items;
+    // k-mer table statistics (sa_kmer_histogram)
+    DBuf d_hk0, d_hk1, d_hflag, d_hidx, d_hpos, d_htmp, d_hist, d_hovf, d_hsmall;
+    std::vector<uint64_t> hsize, hcount;
     // options / state
     bool keep_pairs = false, timing = false;
     int align_kernel = 0;  // SA_OPT_ALIGN_KERNEL
@@ -547,7 +550,8 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
 // partner-residue split pass for reads whose LDS table overflows.  Leaves np
 // entries in the NSHARD output regions of cap_s_out entries each.
 int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bool emit_all,
-               const uint32_t *read_order, uint32_t n_items, Counters *cnt, uint64_t &np, uint64_t &cap_s_out) {
+               const uint32_t *read_order, uint32_t n_items, Counters *cnt, uint64_t &np, uint64_t &cap_s_out,
+               const uint32_t *item_start = nullptr, uint32_t n_multi = 0) {
     // ---- pair counting -------------------------------------------------
     PairParams P;
     P.min_coll = c->set.min_collisions;
@@ -584,7 +588,15 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
         HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(uint32_t), c->stream));
         {
             StageScope st(c, SA_STAGE_PAIRS);
-            HIPCHK(launch_pair_count(E, PI, P, O, read_order, read_order ? ((n_items + 7) & ~7u) : n_items, c->stream));
+            if (item_start) {  // multi-read blocks (sharded path)
+                PairParams PM = P;
+                PM.n_items = n_multi;
+                PM.table = 1024;
+                HIPCHK(launch_pair_count_multi(E, PI, PM, O, item_start, n_multi, c->stream));
+            } else {
+                HIPCHK(launch_pair_count(E, PI, P, O, read_order, read_order ? ((n_items + 7) & ~7u) : n_items,
+                                         c->stream));
+            }
         }
         HIPCHK(hipMemcpyAsync(cur, cnt->cursor, sizeof(cur), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipMemcpyAsync(&ovn, &cnt->overflow_n, 4, hipMemcpyDeviceToHost, c->stream));
@@ -1096,6 +1108,15 @@ int sa_read_fasta(sa_ctx *c, const char *path) {
 
 uint32_t sa_num_reads(const sa_ctx *c) { return c ? (uint32_t)(c->boff.size() - 1) : 0; }
 
+int sa_get_read(const sa_ctx *c, uint32_t id, const char **seq, size_t *len) {
+    if (!c || !seq || !len) return SA_E_ARG;
+    const uint32_t n = (uint32_t)(c->boff.size() - 1);
+    if (id < 1 || id > n) return SA_E_ARG;
+    *seq = c->bases.data() + c->boff[id - 1];
+    *len = (size_t)(c->boff[id] - c->boff[id - 1]);
+    return SA_OK;
+}
+
 int sa_build_candidates(sa_ctx *c) {
     if (!c) return SA_E_ARG;
     (void)hipSetDevice(c->device);
@@ -1123,6 +1144,57 @@ int sa_get_dispatch(sa_ctx *c, const int32_t **lead, const int32_t **trail, cons
     if (trail) *trail = c->trail.data();
     if (count) *count = c->count.data();
     *n = c->n_disp;
+    return SA_OK;
+}
+
+int sa_kmer_histogram(sa_ctx *c, uint64_t *uniques, const uint64_t **size, const uint64_t **count, size_t *n) {
+    if (!c || !uniques || !n) return SA_E_ARG;
+    (void)hipSetDevice(c->device);
+    int rc = ensure_prepared(c);
+    if (rc) return rc;
+    const uint64_t nk = c->n_occ;
+    DevReads R = dev_reads(c);
+    EmitParams E = emit_params(c);
+    uint64_t *k0, *k1;
+    uint32_t *flag, *idx, *pos, *small;
+    uint8_t *tmp;
+    unsigned long long *hist, *ovf;
+    ENSURE(c->d_hk0, nk + 1, &k0);
+    ENSURE(c->d_hk1, nk + 1, &k1);
+    ENSURE(c->d_hflag, nk + 1, &flag);
+    ENSURE(c->d_hidx, nk + 1, &idx);
+    ENSURE(c->d_hpos, nk + 1, &pos);
+    ENSURE(c->d_htmp, std::max(radix_sort_temp_bytes(nk), scan_temp_bytes(nk)), &tmp);
+    ENSURE(c->d_hist, KMER_HIST_CAP, &hist);
+    ENSURE(c->d_hovf, nk / KMER_HIST_CAP + 2, &ovf);  // at most n / CAP buckets that large
+    ENSURE(c->d_hsmall, 2, &small);
+    // generateKmerSet + addKmerSet (BioLibs.scala:54-61, KmerTable.scala:41-53) as
+    // records, fully sorted on the mixed hash, then run lengths
+    HIPCHK(launch_pack_reads(R, c->stream));
+    HIPCHK(launch_kmer_emit(R, E, k0, nullptr, c->stream));
+    uint32_t *nv = nullptr, *nv2 = nullptr;
+    HIPCHK(radix_sort(&k0, &nv, &k1, &nv2, nk, 32, 64, tmp, c->stream));
+    HIPCHK(launch_kmer_hist(k0, nk, flag, idx, pos, small, tmp, hist, ovf, small + 1, c->stream));
+    uint32_t hs[2] = {0, 0};
+    std::vector<unsigned long long> h(KMER_HIST_CAP);
+    HIPCHK(hipMemcpyAsync(hs, small, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(h.data(), hist, KMER_HIST_CAP * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    std::vector<unsigned long long> big(hs[1]);
+    if (hs[1]) HIPCHK(hipMemcpy(big.data(), ovf, (size_t)hs[1] * 8, hipMemcpyDeviceToHost));
+    std::sort(big.begin(), big.end());
+    c->hsize.clear();
+    c->hcount.clear();
+    for (uint32_t q = 1; q < KMER_HIST_CAP; ++q)
+        if (h[q]) { c->hsize.push_back(q); c->hcount.push_back(h[q]); }
+    for (size_t q = 0; q < big.size(); ++q) {
+        if (!c->hsize.empty() && c->hsize.back() == big[q]) ++c->hcount.back();
+        else { c->hsize.push_back(big[q]); c->hcount.push_back(1); }
+    }
+    *uniques = hs[0];
+    if (size) *size = c->hsize.data();
+    if (count) *count = c->hcount.data();
+    *n = c->hsize.size();
     return SA_OK;
 }
 
@@ -1385,8 +1457,14 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, uint64_t n, uint64_t *counts) {
     PI.rec = PA.rec; PI.md_list = PA.md_list; PI.ed_list = PA.ed_list;
     EmitParams E = emit_params(c);
     E.occ_off = loff;  // occurrences of read a on this rank: [loff[a], loff[a+1])
+    // every global read has ~1/P of its occurrences here: blocks take ranges of
+    // reads with ~PCM_TARGET local occurrences (pair_count.hip, multi-read blocks)
+    const uint32_t n_multi = (uint32_t)((n + PCM_TARGET - 1) / PCM_TARGET) + 1;
+    uint32_t *items;
+    ENSURE(c->d_items, (size_t)n_multi + 1, &items);
+    HIPCHK(launch_pc_items(loff, N, PCM_TARGET, n_multi, items, c->stream));
     uint64_t np = 0, cap_s = 0;
-    rc = pair_stage(c, E, PI, false, true, nullptr, N, cnt, np, cap_s);
+    rc = pair_stage(c, E, PI, false, true, nullptr, N, cnt, np, cap_s, items, n_multi);
     if (rc) return rc;
     // partials grouped by the rank owning their lead: ascending (lead, trail)
     uint64_t *ok, *ok2; uint32_t *ov, *ov2; uint8_t *otmp; uint64_t *bounds;

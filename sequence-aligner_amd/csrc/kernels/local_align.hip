@@ -120,6 +120,7 @@ __global__ __launch_bounds__(256) void local_dp_kernel(DevReads rd, const int32_
                     uint32_t bits[NW];
 #pragma unroll
                     for (int w = 0; w < NW; ++w) bits[w] = 0;
+                    int32_t rk = INT32_MIN;  // row argmax key (T << 5 | 31 - s)
 #pragma unroll
                     for (int s = 0; s < S; ++s) {
                         const int32_t c = __builtin_amdgcn_sbfe((int32_t)cb[s], a8, 8);
@@ -135,8 +136,10 @@ __global__ __launch_bounds__(256) void local_dp_kernel(DevReads rd, const int32_
                         Qv[s] = max(max(MX + gO, Y), 0);
                         const uint32_t code = T <= 0 ? 0u : (M == T ? 1u : (X == T ? 2u : 3u));
                         bits[s >> 4] |= code << (2 * (s & 15));
-                        if (T > best) { best = T; bi = i; bs = s; }
+                        rk = max(rk, (T << 5) | (31 - s));  // row max, first column among ties
                     }
+                    // first strict '>' in row-major order: a later row must beat the best
+                    if ((rk >> 5) > best) { best = rk >> 5; bi = i; bs = 31 - (rk & 31); }
                     Rout = R;
                     Pout = Pv[S - 1];
                     // append this row's codes to my stream (row u = i - 1)

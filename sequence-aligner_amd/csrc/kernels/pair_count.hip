@@ -305,6 +305,221 @@ hipError_t launch_pair_count(const EmitParams &e, const PairIn &in, const PairPa
 }
 
 // ---------------------------------------------------------------------------
+// Multi-read blocks (sharded hash stage).  With P ranks every rank counts
+// partial pairs for ALL global reads over its 1/P of the buckets, so a read has
+// ~L/P local occurrences and one-read blocks would be mostly barrier latency
+// (P x 100k blocks of ~60 occurrences at P = 8).  Here a block takes the range
+// of consecutive reads [item_start[b], item_start[b+1]) holding ~PCM_TARGET
+// local occurrences and keys its LDS table by (a, partner) in 64 bits;
+// enumeration and emission are as above.  A block whose table fills appends
+// its reads to the overflow list: they are recounted one read per block.
+// ---------------------------------------------------------------------------
+constexpr int PCM_TAB = 1024;
+constexpr unsigned long long PCM_EMPTY = ~0ull;
+
+struct PcmShared {
+    unsigned long long key[PCM_TAB];
+    uint32_t cnt[PCM_TAB];
+    uint32_t pref[PC_CHUNK + 1];
+    uint4 rec[PC_CHUNK];
+    uint32_t aid[PC_CHUNK];    // read of each occurrence of the chunk
+    uint32_t lds4[PC_THREADS / 64];
+    uint32_t fill, overflow, out_base;
+};
+
+__device__ __forceinline__ uint32_t pcm_hash(unsigned long long k) {
+    const uint32_t x = ((uint32_t)k * 0x9E3779B1u) ^ ((uint32_t)(k >> 32) * 0x85EBCA77u);
+    return x >> (32 - 10);  // log2(PCM_TAB)
+}
+
+__device__ __forceinline__ void pcm_insert(PcmShared &S, unsigned long long key, uint32_t w) {
+    constexpr uint32_t FILL_MAX = PCM_TAB * 3 / 4;
+    uint32_t slot = pcm_hash(key);
+    for (int probe = 0; probe < PCM_TAB; ++probe) {
+        const unsigned long long old = atomicCAS(&S.key[slot], PCM_EMPTY, key);
+        if (old == PCM_EMPTY || old == key) {
+            if (old == PCM_EMPTY && atomicAdd(&S.fill, 1u) >= FILL_MAX) S.overflow = 1;
+            atomicAdd(&S.cnt[slot], w);
+            return;
+        }
+        slot = (slot + 1) & (PCM_TAB - 1);
+    }
+    S.overflow = 1;
+}
+
+__global__ __launch_bounds__(PC_THREADS) void pair_count_multi_kernel(EmitParams e, PairIn in, PairParams p,
+                                                                      PairOut o, const uint32_t *item_start) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    PcmShared &S = *reinterpret_cast<PcmShared *>(smem);
+    const int tid = threadIdx.x;
+    const uint32_t bid = blockIdx.x;
+    if (bid >= p.n_items) return;
+    const uint32_t ra = item_start[bid], rb = item_start[bid + 1];
+    if (ra >= rb) return;  // whole block: before any barrier
+    for (int i = tid; i < PCM_TAB; i += PC_THREADS) {
+        S.key[i] = PCM_EMPTY;
+        S.cnt[i] = 0;
+    }
+    if (tid == 0) { S.fill = 0; S.overflow = 0; }
+    const uint64_t g0 = e.occ_off[ra];
+    const uint32_t nocc = (uint32_t)(e.occ_off[rb] - g0);
+    unsigned long long role_pairs = 0;
+    __syncthreads();
+
+    for (uint32_t c0 = 0; c0 < nocc; c0 += PC_CHUNK) {
+        const uint32_t cn = min((uint32_t)PC_CHUNK, nocc - c0);
+        constexpr int PER = PC_CHUNK / PC_THREADS;
+        uint32_t mytot[PER];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const uint32_t oi = tid * PER + j;  // thread-contiguous
+            uint32_t tot = 0;
+            if (oi < cn) {
+                const uint64_t g = g0 + c0 + oi;
+                const uint4 rc = in.rec[g];
+                S.rec[oi] = rc;
+                tot = (rc.y & 0x3FFFFFFFu) + rc.w;
+                uint32_t lo = ra, hi = rb;  // owning read: largest r with occ_off[r] <= g
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (e.occ_off[mid] <= g) lo = mid; else hi = mid;
+                }
+                S.aid[oi] = lo;
+            }
+            mytot[j] = tot;
+        }
+        uint32_t sum = 0;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) sum += mytot[j];
+        uint32_t total;
+        uint32_t ex = pc_block_excl_scan(sum, S.lds4, &total);
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const uint32_t oi = tid * PER + j;
+            if (oi <= cn) S.pref[oi] = ex;
+            ex += mytot[j];
+        }
+        if (tid == PC_THREADS - 1 && cn == PC_CHUNK) S.pref[PC_CHUNK] = total;
+        role_pairs += total;
+        __syncthreads();
+
+        const uint32_t per = (total + PC_THREADS - 1) / PC_THREADS;
+        const uint32_t t0 = min(total, tid * per), t1 = min(total, t0 + per);
+        if (t0 < t1) {
+            uint32_t lo = 0, hi = cn;  // last oi with pref[oi] <= t0
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (S.pref[mid] <= t0) lo = mid; else hi = mid;
+            }
+            uint32_t oi = lo;
+            uint32_t base = S.pref[oi], nxt = S.pref[oi + 1];
+            for (uint32_t t = t0; t < t1; t += PC_BATCH) {
+                uint32_t part[PC_BATCH], wv[PC_BATCH], own[PC_BATCH];
+#pragma unroll
+                for (int bb = 0; bb < PC_BATCH; ++bb) {
+                    part[bb] = 0;
+                    wv[bb] = 0;  // 0: no role pair in this slot
+                    own[bb] = 0;
+                    const uint32_t tt = t + bb;
+                    if (tt < t1) {
+                        while (tt >= nxt) { ++oi; base = nxt; nxt = S.pref[oi + 1]; }
+                        const uint32_t off = tt - base;
+                        const uint4 rc = S.rec[oi];
+                        const uint32_t nE = rc.y & 0x3FFFFFFFu;
+                        own[bb] = S.aid[oi];
+                        if (off < nE) {
+                            part[bb] = in.md_list[rc.x + off];
+                            wv[bb] = rc.y >> 30;
+                        } else {
+                            part[bb] = in.ed_list[rc.z + (off - nE)];
+                            wv[bb] = 1;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int bb = 0; bb < PC_BATCH; ++bb) {
+                    if (wv[bb] == 0 || part[bb] == own[bb]) continue;  // same read (KmerTable.scala:61-63)
+                    pcm_insert(S, ((unsigned long long)own[bb] << 32) | part[bb], wv[bb]);
+                }
+                if (S.overflow) break;
+            }
+        }
+        __syncthreads();
+    }
+
+    const uint32_t shard = bid % NSHARD;
+    if (tid == 0 && role_pairs) atomicAdd(&o.role_pairs[shard], role_pairs);
+    if (S.overflow) {  // recount these reads one per block (2,048 slots, then the split)
+        if (tid == 0) S.out_base = atomicAdd(o.overflow_n, rb - ra);
+        __syncthreads();
+        for (uint32_t r = tid; r < rb - ra; r += PC_THREADS) o.overflow_list[S.out_base + r] = ra + r;
+        return;
+    }
+    if (tid == 0) atomicAdd(&o.distinct[shard], (unsigned long long)S.fill);
+    constexpr int PERT = PCM_TAB / PC_THREADS;
+    uint32_t keep = 0;
+#pragma unroll
+    for (int j = 0; j < PERT; ++j) {
+        const uint32_t sl = tid * PERT + j;
+        const uint32_t c = S.cnt[sl];
+        if (S.key[sl] != PCM_EMPTY && (p.emit_all || ((int32_t)c >= p.min_coll && (int32_t)c <= p.max_coll)))
+            keep |= 1u << j;
+    }
+    uint32_t total;
+    uint32_t ex = pc_block_excl_scan(__popc(keep), S.lds4, &total);
+    if (total == 0) return;
+    if (tid == 0) S.out_base = (uint32_t)atomicAdd(&o.cursor[shard], (unsigned long long)total);
+    __syncthreads();
+    const unsigned long long base = (unsigned long long)S.out_base + ex;
+    const unsigned long long region = (unsigned long long)shard * o.cap_s;
+    uint32_t k = 0;
+#pragma unroll
+    for (int j = 0; j < PERT; ++j) {
+        if (!(keep & (1u << j))) continue;
+        const uint32_t sl = tid * PERT + j;
+        const unsigned long long lat = base + k++;
+        if (lat < o.cap_s) {
+            const unsigned long long at = region + lat;
+            o.fst[at] = (uint32_t)(S.key[sl] >> 32);
+            o.snd[at] = (uint32_t)S.key[sl];
+            o.cnt[at] = S.cnt[sl];
+        }
+    }
+}
+
+hipError_t launch_pair_count_multi(const EmitParams &e, const PairIn &in, const PairParams &p, PairOut &o,
+                                   const uint32_t *item_start, uint32_t n_items, hipStream_t s) {
+    if (n_items == 0) return hipSuccess;
+    const size_t lds = sizeof(PcmShared);
+    (void)hipFuncSetAttribute((const void *)pair_count_multi_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    hipLaunchKernelGGL(pair_count_multi_kernel, dim3(n_items), dim3(PC_THREADS), lds, s, e, in, p, o, item_start);
+    return hipGetLastError();
+}
+
+// item j = reads [first read with occ_off >= j * target, same for j + 1)
+__global__ void pc_items_kernel(const uint64_t *occ_off, uint32_t n_reads, uint32_t target, uint32_t n_items,
+                                uint32_t *item_start) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j > n_items) return;
+    if (j == n_items) { item_start[j] = n_reads; return; }
+    const uint64_t t = (uint64_t)j * target;
+    uint32_t lo = 0, hi = n_reads;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (occ_off[mid] < t) lo = mid + 1; else hi = mid;
+    }
+    item_start[j] = lo;
+}
+
+hipError_t launch_pc_items(const uint64_t *occ_off, uint32_t n_reads, uint32_t target, uint32_t n_items,
+                           uint32_t *item_start, hipStream_t s) {
+    hipLaunchKernelGGL(pc_items_kernel, dim3((n_items + 1 + 255) / 256), dim3(256), 0, s, occ_off, n_reads, target,
+                       n_items, item_start);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // output ordering helpers
 // ---------------------------------------------------------------------------
 // exclusive prefix of the NSHARD region counts (one tiny block)

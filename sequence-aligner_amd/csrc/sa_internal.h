@@ -155,6 +155,13 @@ hipError_t build_strict_index(const uint64_t *skeys, const uint32_t *svals, uint
 
 hipError_t launch_pair_count(const EmitParams &e, const PairIn &in, const PairParams &p, PairOut &o,
                              const uint32_t *read_list, uint32_t n_blocks, hipStream_t s);
+// sharded path: one block per range of reads with ~PCM_TARGET local occurrences
+// (launch_pc_items builds item_start[n_items + 1] from the occurrence offsets)
+constexpr uint32_t PCM_TARGET = 512;
+hipError_t launch_pair_count_multi(const EmitParams &e, const PairIn &in, const PairParams &p, PairOut &o,
+                                   const uint32_t *item_start, uint32_t n_items, hipStream_t s);
+hipError_t launch_pc_items(const uint64_t *occ_off, uint32_t n_reads, uint32_t target, uint32_t n_items,
+                           uint32_t *item_start, hipStream_t s);
 
 // ---- partition bucket build (partition.hip) ------------------------------
 struct PartArgs {
@@ -239,6 +246,15 @@ uint32_t local_align_wpl(int stripe, int32_t max_len);
 hipError_t launch_local_align(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t p0,
                               uint64_t np, const AlignParams &p, int stripe, uint32_t wpl, uint32_t *tb, int4 *lmax,
                               DevAlignment *out, int32_t *err, unsigned long long *cells, hipStream_t s);
+
+// k-mer table statistics (kmer_hist.hip): records sorted on their top 32 bits
+// -> distinct hashes (*nheads) and hist[s] = hashes with s occurrences for
+// s < KMER_HIST_CAP, larger sizes appended to ovf[0 .. *novf).  flag / idx /
+// pos: n u32 each; scan_tmp: scan_temp_bytes(n).
+constexpr uint32_t KMER_HIST_CAP = 1u << 16;
+hipError_t launch_kmer_hist(const uint64_t *sorted, uint64_t n, uint32_t *flag, uint32_t *idx, uint32_t *pos,
+                            uint32_t *nheads, void *scan_tmp, unsigned long long *hist, unsigned long long *ovf,
+                            uint32_t *novf, hipStream_t s);
 
 // distributed (multi-GPU) glue, dist.hip
 hipError_t launch_iota(uint32_t *v, uint64_t n, hipStream_t s);

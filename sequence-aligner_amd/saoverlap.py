@@ -33,8 +33,8 @@ FLAG_DUD, FLAG_VALID, FLAG_OVL_VALID = 1, 2, 4
 
 # exported symbols declared in include/sa_overlap.h
 EXPORTS = ("sa_default_settings", "sa_ctx_create", "sa_ctx_destroy", "sa_last_error", "sa_load_hoxd",
-           "sa_add_reads", "sa_read_fasta", "sa_num_reads", "sa_build_candidates", "sa_get_dispatch",
-           "sa_get_pairs", "sa_align", "sa_get_alignments", "sa_write_ovl", "sa_get_ovl", "sa_set_option",
+           "sa_add_reads", "sa_read_fasta", "sa_num_reads", "sa_get_read", "sa_build_candidates", "sa_get_dispatch",
+           "sa_get_pairs", "sa_kmer_histogram", "sa_align", "sa_get_alignments", "sa_write_ovl", "sa_get_ovl", "sa_set_option",
            "sa_get_stats", "sa_get_stage_times", "sa_reset_stage_times", "sa_device_build", "sa_device_align",
            "sa_sync", "sa_dist_init", "sa_dist_local_kmers", "sa_dist_emit", "sa_dist_count", "sa_dist_partials",
            "sa_dist_reduce", "sa_dist_codes", "sa_dist_set_reads")
@@ -86,6 +86,8 @@ def lib():
         L.sa_get_dispatch.argtypes = [vp, P(P(C.c_int32)), P(P(C.c_int32)), P(P(C.c_int32)), P(C.c_size_t)]
         L.sa_get_pairs.argtypes = [vp, P(P(C.c_int32)), P(P(C.c_int32)), P(P(C.c_int32)), P(C.c_size_t)]
         L.sa_get_alignments.argtypes = [vp, P(vp), P(C.c_size_t)]
+        L.sa_get_read.argtypes = [vp, C.c_uint32, P(C.c_char_p), P(C.c_size_t)]
+        L.sa_kmer_histogram.argtypes = [vp, P(C.c_uint64), P(P(C.c_uint64)), P(P(C.c_uint64)), P(C.c_size_t)]
         L.sa_write_ovl.argtypes = [vp, C.c_char_p]
         L.sa_get_ovl.argtypes = [vp, P(C.c_char_p), P(C.c_size_t)]
         L.sa_set_option.argtypes = [vp, C.c_int, C.c_int64]
@@ -154,6 +156,15 @@ class Overlapper:
             self._chk(lib().sa_set_option(h, SA_OPT_ALIGNER, aligner))
         if local_batch_mb is not None:
             self._chk(lib().sa_set_option(h, SA_OPT_LOCAL_BATCH_MB, local_batch_mb))
+
+    def kmer_histogram(self):
+        """(uniques, {bucket size: number of hashes}) -- KmerTable.uniqueKmers /
+        kmerCollisionHistogram (KmerTable.scala:189-221)."""
+        u = C.c_uint64()
+        sp, cp = C.POINTER(C.c_uint64)(), C.POINTER(C.c_uint64)()
+        n = C.c_size_t()
+        self._chk(lib().sa_kmer_histogram(self.h, C.byref(u), C.byref(sp), C.byref(cp), C.byref(n)))
+        return u.value, {int(sp[i]): int(cp[i]) for i in range(n.value)}
 
     def set_aligner(self, aligner):
         """SA_OPT_ALIGNER: SA_ALIGNER_LINEAR (--linear-align) or SA_ALIGNER_QUADRATIC."""

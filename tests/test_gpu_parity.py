@@ -339,17 +339,26 @@ def _hip_rank_main(rank, P, port, reads, starts, st, outdir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("P", [2, 4])
-def test_sharded_hip_matches_single_gpu(P, tmp_path):
+@pytest.mark.parametrize("P,repeat", [(2, False), (4, False), (2, True)])
+def test_sharded_hip_matches_single_gpu(P, repeat, tmp_path):
     """P processes share the GPU (gloo, host-staged exchanges) and run the
     sharded stage on the HIP path: the ranks' dispatch, alignments and .ovl in
-    descending rank order equal the single-context wide-id run exactly."""
+    descending rank order equal the single-context wide-id run exactly.  The
+    repeat case (a 15-mer in 2,400 reads) overflows the multi-read blocks'
+    tables, so those reads are recounted one per block."""
     import socket
 
     import torch.multiprocessing as mp
     rng = np.random.default_rng(70 + P)
     reads = mutate(H.synth_reads(1200, 300, 18000, gc=0.5, seed=71 + P, mixed=(250, 340)), rng, 3)
     st = dict(kmer_size=15, min_collisions=5)
+    if repeat:
+        motif = "ACGTTGCAACGTAGC"
+        for i in range(2400):
+            s_ = "".join("ACGT"[x] for x in rng.integers(0, 4, 120))
+            p_ = 5 if i % 2 == 0 else 55
+            reads.append(s_[:p_] + motif + s_[p_ + 15:])
+        st = dict(kmer_size=15, min_collisions=2)
     cut = [0] + [int(len(reads) * f) for f in np.linspace(0.2, 0.75, P - 1)] + [len(reads)]
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
