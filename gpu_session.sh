@@ -21,6 +21,6 @@ fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
     cd /tmp && export TMPDIR=/tmp
     step_dir=$GRAFT_REPO_ROOT/gpurun_out
-    timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $step_dir/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 1 --no-cpu-baseline > $step_dir/prof.log 2>&1
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $step_dir/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 1 --no-cpu-baseline --quadratic-steps 1 > $step_dir/prof.log 2>&1
     echo "prof rc=$?" >> $step_dir/steps.txt
 fi

@@ -17,8 +17,8 @@
 // win against the inner 0 for gap costs <= 0, so they enter as zeros).  Each
 // cell leaves a 2-bit code for the greedy backtrack (:334-360): 0 when
 // max(M, X, Y) <= 0 (the walk stops there), else 1 / 2 / 3 for the first of
-// M / X / Y equal to the cell max.  A lane appends its codes row after row to
-// its own stream in HBM (2S bits per row).  The argmax is the first strict '>'
+// M / X / Y equal to the cell max.  A lane appends its codes step after step
+// to its own stream in HBM (2S bits per step), in whole 64-byte segments.  The argmax is the first strict '>'
 // in row-major order (:318-321): per-lane first best, then a (value desc,
 // i asc, j asc) reduce across the wave.
 //
@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256) void local_dp_kernel(DevReads rd, const int32_
         const int32_t a = lead[pair] - 1, b = trail[pair] - 1;
         const int32_t LA = rd.len[a], LB = rd.len[b];
         int32_t status = 0;
-        if (LB > 64 * S || LA >= (1 << 20) || (uint64_t)LA * BPS > (uint64_t)wpl * 32) status = -11;
+        if (LB > 64 * S || LA >= (1 << 20) || (uint64_t)(LA + 63) * BPS > (uint64_t)wpl * 32) status = -11;
         else if (rd.bad[a] < LA || rd.bad[b] < LB) status = -3;  // every cell calls the cost closure
         if (status != 0) {
             if (lane == 0) {
@@ -103,8 +103,15 @@ __global__ __launch_bounds__(256) void local_dp_kernel(DevReads rd, const int32_
             for (int s = 0; s < S; ++s) { Pv[s] = 0; Qv[s] = 0; }
             int32_t Rout = 0, Pout = 0, Pl = 0;  // right edge of my last row; P(i-1, j0-1) from the left lane
             int32_t best = 0, bi = 0, bs = 0;
-            uint32_t acc = 0;
-            uint32_t *tl = tb + (q * 64 + (uint64_t)lane) * wpl;
+            // My code stream is indexed by step t (row t - lane + 1; idle steps
+            // hold zeros) and leaves in whole, aligned 64-byte segments: 16 words
+            // gathered in registers (uniform slot index -> scalar branches), then
+            // four 16-byte stores, so no partially written line reaches HBM.
+            uint32_t acc = 0, sb[16];
+#pragma unroll
+            for (int w = 0; w < 16; ++w) sb[w] = 0;
+            int32_t widx = 0;
+            uint4 *tl = reinterpret_cast<uint4 *>(tb + (q * 64 + (uint64_t)lane) * wpl);
             const bool mine = lane < nl;
             const int32_t steps = LA + nl - 1;
             // A words: aw holds A[i-1] of the current row, an the next word
@@ -113,13 +120,13 @@ __global__ __launch_bounds__(256) void local_dp_kernel(DevReads rd, const int32_
                 const int32_t Rin = from_left(Rout);
                 const int32_t Pin = from_left(Pout);
                 const int32_t i = t - lane + 1;
+                uint32_t bits[NW];
+#pragma unroll
+                for (int w = 0; w < NW; ++w) bits[w] = 0;
                 if (mine && i >= 1 && i <= LA) {
                     const uint32_t a8 = ((aw >> (30 - 2 * ((i - 1) & 15))) & 3u) * 8u;
                     int32_t Pd = Pl;
                     int32_t R = Rin;
-                    uint32_t bits[NW];
-#pragma unroll
-                    for (int w = 0; w < NW; ++w) bits[w] = 0;
                     int32_t rk = INT32_MIN;  // row argmax key (T << 5 | 31 - s)
 #pragma unroll
                     for (int s = 0; s < S; ++s) {
@@ -135,31 +142,47 @@ __global__ __launch_bounds__(256) void local_dp_kernel(DevReads rd, const int32_
                         Pv[s] = max(T, 0);
                         Qv[s] = max(max(MX + gO, Y), 0);
                         const uint32_t code = T <= 0 ? 0u : (M == T ? 1u : (X == T ? 2u : 3u));
-                        bits[s >> 4] |= code << (2 * (s & 15));
+                        // shift-in (inline-constant codes, no shifted literals):
+                        // column s of a word ends at bits 2 * (15 - (s & 15)) (S >= 16)
+                        // or 2 * (S - 1 - s) (S < 16)
+                        bits[s >> 4] = (bits[s >> 4] << 2) | code;
                         rk = max(rk, (T << 5) | (31 - s));  // row max, first column among ties
                     }
                     // first strict '>' in row-major order: a later row must beat the best
                     if ((rk >> 5) > best) { best = rk >> 5; bi = i; bs = 31 - (rk & 31); }
                     Rout = R;
                     Pout = Pv[S - 1];
-                    // append this row's codes to my stream (row u = i - 1)
-                    const int32_t u = i - 1;
-                    if constexpr (S >= 16) {
-#pragma unroll
-                        for (int w = 0; w < NW; ++w) tl[(uint64_t)u * NW + w] = bits[w];
-                    } else {
-                        acc |= bits[0] << ((u % K) * BPS);
-                        if (u % K == K - 1 || i == LA) {
-                            tl[u / K] = acc;
-                            acc = 0;
-                        }
-                    }
                     if ((i & 15) == 0 && i < LA) {  // next row starts a new A word
                         aw = an;
                         if (((i >> 4) + 1) * 16 < LA) an = gld(Aw, (i >> 4) + 1);
                     }
                 }
                 Pl = Pin;
+                // this step's codes into the segment buffer (t is wave-uniform)
+                auto put = [&](uint32_t v) {
+                    switch (__builtin_amdgcn_readfirstlane(widx)) {  // uniform: scalar branches
+#define SA_PUT(W) case W: sb[W] = v; break;
+                    SA_PUT(0) SA_PUT(1) SA_PUT(2) SA_PUT(3) SA_PUT(4) SA_PUT(5) SA_PUT(6) SA_PUT(7)
+                    SA_PUT(8) SA_PUT(9) SA_PUT(10) SA_PUT(11) SA_PUT(12) SA_PUT(13) SA_PUT(14) SA_PUT(15)
+#undef SA_PUT
+                    }
+                    ++widx;
+                };
+                if constexpr (S >= 16) {
+#pragma unroll
+                    for (int w = 0; w < NW; ++w) put(bits[w]);
+                } else {
+                    acc |= bits[0] << ((t % K) * BPS);
+                    if (t % K == K - 1 || t == steps - 1) { put(acc); acc = 0; }
+                }
+                if (widx == 16 || t == steps - 1) {
+                    const int32_t seg = (t * NW / K) >> 4;  // 16-word segment of this step's last word
+                    tl[4 * seg + 0] = make_uint4(sb[0], sb[1], sb[2], sb[3]);
+                    tl[4 * seg + 1] = make_uint4(sb[4], sb[5], sb[6], sb[7]);
+                    tl[4 * seg + 2] = make_uint4(sb[8], sb[9], sb[10], sb[11]);
+                    tl[4 * seg + 3] = make_uint4(sb[12], sb[13], sb[14], sb[15]);
+                    widx = 0;
+                }
             }
             my_cells = lane == 0 ? (unsigned long long)LA * LB : 0ull;
             // first row-major argmax: value desc, i asc, j asc
@@ -222,7 +245,9 @@ __global__ __launch_bounds__(256) void local_walk_kernel(DevReads rd, const int3
     const uint32_t *tq = tb + q * 64 * (uint64_t)wpl;
     auto code_at = [&](int32_t i, int32_t j) -> uint32_t {
         const int32_t l = (j - 1) / S, s = (j - 1) - l * S;
-        const uint64_t bit = (uint64_t)(i - 1) * BPS + 2 * s;
+        // step t = row - 1 + lane; column s sits at 2 * (last - s) within its word
+        const int32_t sp = S >= 16 ? (s & ~15) + (15 - (s & 15)) : (S - 1 - s);
+        const uint64_t bit = (uint64_t)(i - 1 + l) * BPS + 2 * sp;
         return (gld(tq, (int64_t)l * wpl + (int64_t)(bit >> 5)) >> (bit & 31)) & 3u;
     };
     int32_t i = mx.y, j = mx.z, c = 0, e = 0;
@@ -262,8 +287,10 @@ int local_align_stripe(int32_t max_len) {
 }
 
 uint32_t local_align_wpl(int stripe, int32_t max_len) {
-    const uint64_t bits = (uint64_t)max_len * 2 * stripe;
-    return (uint32_t)((bits + 31) / 32);
+    // a lane's stream: one entry of 2*stripe bits per step, |A| + 63 steps at
+    // most, whole 16-word (64-byte) segments
+    const uint64_t bits = (uint64_t)(max_len + 63) * 2 * stripe;
+    return (uint32_t)(((bits + 31) / 32 + 15) & ~15ull);
 }
 
 hipError_t launch_local_align(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t p0,

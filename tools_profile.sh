@@ -6,7 +6,7 @@ set -u
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
 cd /tmp && export TMPDIR=/tmp
-BENCH="$R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --align-steps 2"
+BENCH="$R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --align-steps 2 --quadratic-steps 1"
 pass() {  # pass <name> <counters...>
     local name=$1; shift
     timeout -k 10 300 rocprofv3 --kernel-trace --pmc "$@" --output-format csv -d $R/gpurun_out/pmc_$name -o pmc -- python3 $BENCH > $R/gpurun_out/pmc_$name.log 2>&1
