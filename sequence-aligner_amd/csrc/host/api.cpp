@@ -56,6 +56,8 @@ struct Counters {
     int32_t err;
     uint32_t totals[4];
     uint32_t big_n;
+    uint32_t mid_n;
+    uint32_t mid2_n;
     uint32_t pad_;
     uint32_t shard_off[NSHARD + 2];
 };
@@ -443,7 +445,7 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
     }
     uint32_t *pstart, *biglist;
     ENSURE(c->d_pstart, nparts + 1, &pstart);
-    ENSURE(c->d_biglist, nparts + 1, &biglist);
+    ENSURE(c->d_biglist, 3 * ((size_t)nparts + 1), &biglist);  // big list, mid list, mid2 list
     PA = PartArgs{};
     PA.sk = keys; PA.sv = nullptr; PA.start = pstart; PA.np = nparts; PA.lb = c->lb; PA.sort_bits = kbits - skip_bits - PB;
     PA.ablate = c->ablate;
@@ -460,6 +462,8 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
     ENSURE(c->d_ed, 2 * n + 2, &PA.ed_list);
     ENSURE(c->d_rec, n + 1, &PA.rec);
     PA.big_list = biglist; PA.big_n = &cnt->big_n;
+    PA.mid_list = biglist + nparts + 1; PA.mid_n = &cnt->mid_n;
+    PA.mid2_list = biglist + 2 * ((size_t)nparts + 1); PA.mid2_n = &cnt->mid2_n;
     PA.counts = cnt->bkt_counts;
     if (strict) {
         ENSURE(c->d_mdidx, n + 1, &PA.md_idx);
@@ -474,6 +478,7 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
     }
     const uint8_t *tagtab = PA.tagtab;
     uint32_t big_n = 0;
+    HIPCHK(hipMemsetAsync(&cnt->mid_n, 0, 2 * sizeof(uint32_t), c->stream));  // mid_n, mid2_n
     {
         StageScope st(c, SA_STAGE_BUCKETS);
         HIPCHK(launch_part_starts(keys, n, 64 - skip_bits - PB, pstart, nparts, c->stream));

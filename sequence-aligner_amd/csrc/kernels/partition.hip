@@ -55,38 +55,6 @@ __device__ __forceinline__ unsigned long long record_key(uint64_t rec, const Par
 }
 
 // ---------------------------------------------------------------------------
-// partition starts: start[p] = first sorted index of partition p (empty -> next)
-// ---------------------------------------------------------------------------
-// (bits above the partition id -- the owner rank's in distributed mode -- are
-// the same for every key and masked off)
-__global__ void part_mark_kernel(const uint64_t *sk, uint64_t n, int shift, uint32_t mask, uint32_t *start) {
-    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= n) return;
-    const uint32_t p = (uint32_t)(sk[s] >> shift) & mask;
-    if (s == 0 || ((uint32_t)(sk[s - 1] >> shift) & mask) != p) start[p] = (uint32_t)s;
-}
-
-// suffix min over start[0..np] (np+1 entries, start[np] = n) in one block
-__global__ __launch_bounds__(1024) void part_fill_kernel(uint32_t *start, uint32_t np, uint32_t n) {
-    __shared__ uint32_t tmin[1024];
-    if (threadIdx.x == 0) start[np] = n;
-    __syncthreads();
-    const uint32_t per = (np + 1 + 1023) / 1024;
-    const uint32_t b = threadIdx.x * per, e = min(np + 1, b + per);
-    uint32_t m = 0xFFFFFFFFu;
-    for (uint32_t i = e; i-- > b;) m = min(m, start[i]);
-    tmin[threadIdx.x] = m;
-    __syncthreads();
-    // exclusive suffix min over threads (threads after me)
-    uint32_t carry = 0xFFFFFFFFu;
-    for (uint32_t t = threadIdx.x + 1; t < 1024; ++t) carry = min(carry, tmin[t]);
-    for (uint32_t i = e; i-- > b;) {
-        carry = min(carry, start[i]);
-        start[i] = carry;
-    }
-}
-
-// ---------------------------------------------------------------------------
 // the LDS partition builder
 // ---------------------------------------------------------------------------
 constexpr int PB_THREADS = 256;
@@ -218,18 +186,23 @@ __device__ __forceinline__ void lds_radix_sort(SH &S, uint32_t n, int bits) {
     }
 }
 
+// One partition p in one block.  Partitions above CAP records are handed on:
+// the 1,024-record kernel lists them for the 2,048-record pass (mid_list), that
+// pass lists its overflow for the 4,096-record pass (mid2_list), and that one
+// lists the partitions above 4,096 for the global path (big_list).
 template <int CAP, bool STRICT>
-__global__ __launch_bounds__(PB_THREADS) void part_build_kernel(PartArgs A, uint32_t lo_cap) {
-    extern __shared__ __align__(16) uint8_t smem_raw[];
-    PartShared<CAP> &S = *reinterpret_cast<PartShared<CAP> *>(smem_raw);
+__device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t p, PartShared<CAP> &S) {
     constexpr int IT = CAP / PB_THREADS;
     const int tid = threadIdx.x;
-    const uint32_t p = blockIdx.x;
     const uint32_t ps = A.start[p], pe = A.start[p + 1];
     const uint32_t n = pe - ps;
-    if (n == 0 || n <= lo_cap) return;
+    if (n == 0) return;
     if (n > (uint32_t)CAP) {
-        if (CAP >= 4096 && tid == 0) A.big_list[atomicAdd(A.big_n, 1u)] = p;
+        if (tid == 0) {
+            if (CAP >= 4096) A.big_list[atomicAdd(A.big_n, 1u)] = p;
+            else if (CAP >= 2048) A.mid2_list[atomicAdd(A.mid2_n, 1u)] = p;
+            else A.mid_list[atomicAdd(A.mid_n, 1u)] = p;
+        }
         return;
     }
     // ---- load, then stable LDS radix sort on the key bits below the partition id
@@ -358,6 +331,27 @@ __global__ __launch_bounds__(PB_THREADS) void part_build_kernel(PartArgs A, uint
     }
 }
 
+// CAP 1,024: one block per partition.  CAP 2,048 / 4,096: a fixed grid walks
+// the list the previous pass handed on (~1% of partitions at 20x coverage) -- no
+// block is spent reading the bounds of a partition already built while holding
+// 44 / 84 KB of LDS, and a partition of ~1,100 records is sorted over 2,048
+// slots, not 4,096 (the tail of the stage is one such block's latency).
+template <int CAP, bool STRICT>
+__global__ __launch_bounds__(PB_THREADS) void part_build_kernel(PartArgs A) {
+    extern __shared__ __align__(16) uint8_t smem_raw[];
+    PartShared<CAP> &S = *reinterpret_cast<PartShared<CAP> *>(smem_raw);
+    if constexpr (CAP < 2048) {
+        part_build_one<CAP, STRICT>(A, blockIdx.x, S);
+    } else {
+        const uint32_t *list = CAP >= 4096 ? A.mid2_list : A.mid_list;
+        const uint32_t m = *(CAP >= 4096 ? A.mid2_n : A.mid_n);
+        for (uint32_t i = blockIdx.x; i < m; i += gridDim.x) {
+            __syncthreads();  // LDS of the previous partition fully consumed
+            part_build_one<CAP, STRICT>(A, list[i], S);
+        }
+    }
+}
+
 template <int CAP>
 static size_t part_lds() { return sizeof(PartShared<CAP>); }
 
@@ -398,29 +392,43 @@ __global__ void records_from_tables_kernel(const uint64_t *sk, const uint32_t *s
 }
 
 // ---------------------------------------------------------------------------
+// partition starts: start[p] = first sorted index whose partition id is >= p
+// (p = 0 .. np; an empty partition gets the next one's start).  One binary
+// search per partition over the sorted records -- log2(n) cached loads each
+// instead of a pass over all n records plus a serial suffix-min fill.  (Bits
+// above the partition id -- the owner rank's in distributed mode -- are the
+// same for every key and masked off.)
+__global__ void part_bounds_kernel(const uint64_t *sk, uint64_t n, int shift, uint32_t mask, uint32_t np,
+                                   uint32_t *start) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p > np) return;
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (((uint32_t)(sk[mid] >> shift) & mask) < p) lo = mid + 1; else hi = mid;
+    }
+    start[p] = (uint32_t)lo;
+}
+
 hipError_t launch_part_starts(const uint64_t *sk, uint64_t n, int shift, uint32_t *start, uint32_t np,
                               hipStream_t s) {
-    hipError_t e = hipMemsetAsync(start, 0xFF, (size_t)(np + 1) * sizeof(uint32_t), s);
-    if (e != hipSuccess) return e;
-    if (n)
-        hipLaunchKernelGGL(part_mark_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, sk, n, shift, np - 1,
-                           start);
-    hipLaunchKernelGGL(part_fill_kernel, dim3(1), dim3(1024), 0, s, start, np, (uint32_t)n);
+    hipLaunchKernelGGL(part_bounds_kernel, dim3((np + 1 + 255) / 256), dim3(256), 0, s, sk, n, shift, np - 1, np,
+                       start);
     return hipGetLastError();
 }
 
 hipError_t launch_part_build(const PartArgs &a, bool strict, hipStream_t s) {
     if (!a.np) return hipSuccess;
-#define PB_LAUNCH(CAPV, LO, ST)                                                                          \
+#define PB_LAUNCH(CAPV, GRID, ST)                                                                          \
     do {                                                                                                 \
         const size_t lds = part_lds<CAPV>();                                                             \
         (void)hipFuncSetAttribute((const void *)part_build_kernel<CAPV, ST>,                             \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                 \
-        hipLaunchKernelGGL((part_build_kernel<CAPV, ST>), dim3(a.np), dim3(PB_THREADS), lds, s, a,       \
-                           (uint32_t)(LO));                                                              \
+        hipLaunchKernelGGL((part_build_kernel<CAPV, ST>), dim3(GRID), dim3(PB_THREADS), lds, s, a);     \
     } while (0)
-    if (strict) { PB_LAUNCH(1024, 0, true); PB_LAUNCH(4096, 1024, true); }
-    else { PB_LAUNCH(1024, 0, false); PB_LAUNCH(4096, 1024, false); }
+    const uint32_t mid_grid = a.np < 1024u ? a.np : 1024u;
+    if (strict) { PB_LAUNCH(1024, a.np, true); PB_LAUNCH(2048, mid_grid, true); PB_LAUNCH(4096, mid_grid, true); }
+    else { PB_LAUNCH(1024, a.np, false); PB_LAUNCH(2048, mid_grid, false); PB_LAUNCH(4096, mid_grid, false); }
 #undef PB_LAUNCH
     return hipGetLastError();
 }

@@ -186,7 +186,9 @@ struct PartArgs {
     int32_t k;
     uint32_t *md_list, *ed_list;
     uint4 *rec;                  // [n_occ] by g
-    uint32_t *big_list, *big_n;
+    uint32_t *big_list, *big_n;  // partitions above 4,096 records (global path)
+    uint32_t *mid_list, *mid_n;    // partitions above 1,024 records (2,048-record LDS pass)
+    uint32_t *mid2_list, *mid2_n;  // partitions above 2,048 records (4,096-record LDS pass)
     unsigned long long *counts;  // [2][NSHARD]: buckets, groups
     // strict
     uint32_t *md_idx, *ed_idx;   // parallel to lists

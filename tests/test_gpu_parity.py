@@ -205,12 +205,15 @@ def test_short_and_degenerate_reads(oracle_mod):
     compare_with_oracle(oracle_mod, ov, r, False)
 
 
-@pytest.mark.parametrize("copies", [4000, 600])
+@pytest.mark.parametrize("copies", [4000, 600, 1500, 3000])
 def test_repeat_overflow_path(oracle_mod, copies):
     """A 12-mer repeated in `copies` reads (half in the leading edge, half in the
     middle) gives every middle-copy read copies/2 partners: 4,000 copies exceed
     both LDS pair tables (256 and 2,048 slots -> 64-way split pass), 600 only
-    the first-pass table (-> the 2,048-slot re-run); counts must not change."""
+    the first-pass table (-> the 2,048-slot re-run); counts must not change.
+    The bucket build sees the motif's partition at 1,500 copies in its
+    2,048-record pass, at 3,000 in the 4,096-record pass and at 4,000 on the
+    global (big partition) path."""
     rng = np.random.default_rng(41)
     motif = "ACGTTGCAACGT"
     reads = []
