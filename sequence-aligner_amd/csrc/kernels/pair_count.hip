@@ -81,7 +81,12 @@ __device__ __forceinline__ void pc_insert(PcShared<TAB> &S, PcSharedStrict<TAB> 
     constexpr uint32_t FILL_MAX = TAB * 3 / 4;
     uint32_t slot = pc_hash<TAB>(partner);
     for (int probe = 0; probe < TAB; ++probe) {
-        const uint32_t old = atomicCAS(&S.key[slot], PC_EMPTY, partner);
+        // a slot's key goes EMPTY -> partner once and never changes again, so a
+        // plain LDS read that sees a key is final: hits (>99% of inserts -- a read
+        // meets each partner in ~100 shared k-mers) take one atomic, not two, and
+        // the CAS only runs on a slot that still reads EMPTY
+        uint32_t old = ((volatile uint32_t *)S.key)[slot];
+        if (old == PC_EMPTY) old = atomicCAS(&S.key[slot], PC_EMPTY, partner);
         if (old == PC_EMPTY || old == partner) {
             if (old == PC_EMPTY && atomicAdd(&S.fill, 1u) >= FILL_MAX) S.overflow = 1;
             atomicAdd(&S.cnt[slot], w);
@@ -336,7 +341,8 @@ __device__ __forceinline__ void pcm_insert(PcmShared &S, unsigned long long key,
     constexpr uint32_t FILL_MAX = PCM_TAB * 3 / 4;
     uint32_t slot = pcm_hash(key);
     for (int probe = 0; probe < PCM_TAB; ++probe) {
-        const unsigned long long old = atomicCAS(&S.key[slot], PCM_EMPTY, key);
+        unsigned long long old = ((volatile unsigned long long *)S.key)[slot];  // final once set (pc_insert)
+        if (old == PCM_EMPTY) old = atomicCAS(&S.key[slot], PCM_EMPTY, key);
         if (old == PCM_EMPTY || old == key) {
             if (old == PCM_EMPTY && atomicAdd(&S.fill, 1u) >= FILL_MAX) S.overflow = 1;
             atomicAdd(&S.cnt[slot], w);

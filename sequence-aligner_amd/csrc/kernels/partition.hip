@@ -19,6 +19,7 @@
 // traversal order is built from, per-bucket |st|, |md| and first occurrence.
 // Partitions larger than the LDS capacity take the global scan path
 // (buckets.hip) and records_from_tables_kernel below.  Bound: HBM / LDS.
+#include <cstdlib>
 #include "../sa_internal.h"
 
 namespace sa {
@@ -113,12 +114,20 @@ template <int CAP>
 struct PartShared {
     unsigned long long key[CAP];
     uint32_t g[CAP];
-    uint32_t mdx[CAP + 1];   // exclusive md count (partition-local)
-    uint32_t edx[CAP + 1];   // exclusive edge-role count
+    // the sort's digit counts are dead once the partition is sorted and the
+    // per-item counts are only written after it: one region, and 16-bit counts
+    // (<= 2 * CAP), so the 1,024-record block fits 16.5 KB -> 8 blocks per CU
+    union {
+        uint32_t cnt[4][256];    // LDS radix sort: per-wave digit counts / bases
+        struct {
+            uint16_t mdx[CAP + 2];   // exclusive md count (partition-local)
+            uint16_t edx[CAP + 2];   // exclusive edge-role count
+        };
+    };
     uint32_t red[3][4];
     uint32_t lbh[4], lgh[4];
-    uint32_t cnt[4][256];    // LDS radix sort: per-wave digit counts / bases
 };
+static_assert(sizeof(PartShared<1024>) <= 20480, "1,024-record block must fit 8 per CU");
 
 // Stable LSD radix sort of the partition's (key, g) in LDS over key bits
 // [0, bits): wave w owns elements [w*CAP/4, (w+1)*CAP/4) (slices of 64), ranks
@@ -419,9 +428,12 @@ hipError_t launch_part_starts(const uint64_t *sk, uint64_t n, int shift, uint32_
 
 hipError_t launch_part_build(const PartArgs &a, bool strict, hipStream_t s) {
     if (!a.np) return hipSuccess;
+    // profiling only (env SA_PB_LDS): pad the 1,024-record block's LDS to cap
+    // its blocks per CU, for occupancy A/B runs on one box
+    static const size_t pb_lds_pad = getenv("SA_PB_LDS") ? (size_t)atol(getenv("SA_PB_LDS")) : 0;
 #define PB_LAUNCH(CAPV, GRID, ST)                                                                          \
     do {                                                                                                 \
-        const size_t lds = part_lds<CAPV>();                                                             \
+        const size_t lds = CAPV == 1024 && pb_lds_pad > part_lds<CAPV>() ? pb_lds_pad : part_lds<CAPV>();  \
         (void)hipFuncSetAttribute((const void *)part_build_kernel<CAPV, ST>,                             \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                 \
         hipLaunchKernelGGL((part_build_kernel<CAPV, ST>), dim3(GRID), dim3(PB_THREADS), lds, s, a);     \

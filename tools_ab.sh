@@ -1,0 +1,17 @@
+#!/bin/bash
+# Same-box A/B of bench variants selected by env (profiling only): each line of
+# gpurun_out/ab.txt is "<label> <bench JSON>".  Stops at the first failure.
+set -u
+mkdir -p gpurun_out
+run() {  # run <label> [VAR=value ...]
+    local label=$1; shift
+    env "$@" timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --align-steps 2 > gpurun_out/ab_$label.log 2>&1
+    local rc=$?
+    echo "$label rc=$rc $(grep '^{' gpurun_out/ab_$label.log | tail -1)" >> gpurun_out/ab.txt
+    [ $rc -eq 0 ] || exit $rc
+}
+run occ8_a
+run occ6_a SA_PB_LDS=24704
+run occ8_b
+run occ6_b SA_PB_LDS=24704
+run occ7 SA_PB_LDS=21000
