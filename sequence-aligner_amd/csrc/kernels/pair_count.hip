@@ -30,7 +30,10 @@ constexpr int PC_THREADS = SA_PC_THREADS;
 constexpr int PC_TAB_SMALL = 256;
 constexpr int PC_TAB_BIG = 2048;
 constexpr int PC_CHUNK = 512;            // occurrences per pass over a read
-constexpr int PC_BATCH = 8;              // partner loads in flight per thread
+#ifndef SA_PC_BATCH
+#define SA_PC_BATCH 8
+#endif
+constexpr int PC_BATCH = SA_PC_BATCH;    // partner loads in flight per thread
 constexpr uint32_t PC_EMPTY = 0xFFFFFFFFu;
 
 template <int TAB>

@@ -1,6 +1,8 @@
 #!/bin/bash
 # Same-box A/B of bench variants selected by env (profiling only): each line of
-# gpurun_out/ab.txt is "<label> <bench JSON>".  Stops at the first failure.
+# gpurun_out/ab.txt is "<label> rc=<rc> <bench JSON>".  Stops at the first failure.
+#   bash tools_ab.sh occ   bucket-build LDS occupancy (SA_PB_LDS pads)
+#   bash tools_ab.sh pc    pair-count compile variants (build_* trees via SA_OVERLAP_LIB)
 set -u
 mkdir -p gpurun_out
 run() {  # run <label> [VAR=value ...]
@@ -10,8 +12,20 @@ run() {  # run <label> [VAR=value ...]
     echo "$label rc=$rc $(grep '^{' gpurun_out/ab_$label.log | tail -1)" >> gpurun_out/ab.txt
     [ $rc -eq 0 ] || exit $rc
 }
-run occ8_a
-run occ6_a SA_PB_LDS=24704
-run occ8_b
-run occ6_b SA_PB_LDS=24704
-run occ7 SA_PB_LDS=21000
+LIBDIR=$PWD/sequence-aligner_amd
+case "${1:-occ}" in
+occ)
+    run occ8_a
+    run occ6_a SA_PB_LDS=24704
+    run occ8_b
+    run occ6_b SA_PB_LDS=24704
+    run occ7 SA_PB_LDS=21000
+    ;;
+pc)
+    run base_a
+    run batch16 SA_OVERLAP_LIB=$LIBDIR/build_b16/libsa_overlap.so
+    run batch4 SA_OVERLAP_LIB=$LIBDIR/build_b4/libsa_overlap.so
+    run threads512 SA_OVERLAP_LIB=$LIBDIR/build_t512/libsa_overlap.so
+    run base_b
+    ;;
+esac
