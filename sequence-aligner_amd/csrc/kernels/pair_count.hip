@@ -34,6 +34,20 @@ constexpr int PC_CHUNK = 512;            // occurrences per pass over a read
 #define SA_PC_BATCH 8
 #endif
 constexpr int PC_BATCH = SA_PC_BATCH;    // partner loads in flight per thread
+// SA_PC_RECNT (compile knob, default 1): stream the per-occurrence records (read once)
+// with non-temporal loads so they do not displace the partner lists from L2.
+#ifndef SA_PC_RECNT
+#define SA_PC_RECNT 1
+#endif
+__device__ __forceinline__ uint4 load_rec(const uint4 *p) {
+#if SA_PC_RECNT
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 w = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+    return make_uint4(w.x, w.y, w.z, w.w);
+#else
+    return *p;
+#endif
+}
 constexpr uint32_t PC_EMPTY = 0xFFFFFFFFu;
 
 template <int TAB>
@@ -143,7 +157,7 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
             const uint32_t oi = tid * PER + j;  // thread-contiguous
             uint32_t tot = 0;
             if (oi < cn) {
-                const uint4 rc = in.rec[g0 + c0 + oi];
+                const uint4 rc = load_rec(in.rec + g0 + c0 + oi);
                 S.rec[oi] = rc;
                 tot = (rc.y & 0x3FFFFFFFu) + rc.w;
                 if constexpr (STRICT) X.srec[oi] = in.srec[g0 + c0 + oi];
@@ -385,7 +399,7 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_multi_kernel(EmitParams
             uint32_t tot = 0;
             if (oi < cn) {
                 const uint64_t g = g0 + c0 + oi;
-                const uint4 rc = in.rec[g];
+                const uint4 rc = load_rec(in.rec + g);
                 S.rec[oi] = rc;
                 tot = (rc.y & 0x3FFFFFFFu) + rc.w;
                 uint32_t lo = ra, hi = rb;  // owning read: largest r with occ_off[r] <= g

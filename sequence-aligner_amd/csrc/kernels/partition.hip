@@ -24,6 +24,21 @@
 
 namespace sa {
 
+// SA_REC_NT (compile knob, default 0): write the scattered per-occurrence records with
+// non-temporal stores (streamed past L2) instead of ordinary ones, for A/B runs.
+#ifndef SA_REC_NT
+#define SA_REC_NT 0
+#endif
+__device__ __forceinline__ void store_rec(uint4 *p, uint4 v) {
+#if SA_REC_NT
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4 *>(p));
+#else
+    *p = v;
+#endif
+}
+
 __device__ __forceinline__ uint32_t read_of_g(uint32_t g, const uint64_t *occ_off, uint32_t n_reads, uint32_t npr,
                                               const uint32_t *rid, const uint32_t *g2r) {
     if (rid) return rid[g];  // distributed mode: occurrence index -> global read id
@@ -38,6 +53,32 @@ __device__ __forceinline__ uint32_t read_of_g(uint32_t g, const uint64_t *occ_of
         if (occ_off[mid] <= g) lo = mid; else hi = mid;
     }
     return lo;
+}
+
+// SA_PB_SKNT (compile knob, default 1): read the sorted 8-byte records (read once per
+// pass) with non-temporal loads, leaving L2 to merge the scattered record stores.
+#ifndef SA_PB_SKNT
+#define SA_PB_SKNT 1
+#endif
+__device__ __forceinline__ uint64_t load_sk(const uint64_t *p) {
+#if SA_PB_SKNT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+
+// SA_PB_LISTNT (compile knob, default 0): write the partner lists with non-temporal
+// stores; A/B only.
+#ifndef SA_PB_LISTNT
+#define SA_PB_LISTNT 0
+#endif
+__device__ __forceinline__ void store_list(uint32_t *p, uint32_t v) {
+#if SA_PB_LISTNT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
 }
 
 // sort key (mix << lb | loc rank) and occurrence index of an 8-byte record
@@ -217,7 +258,7 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
     // ---- load, then stable LDS radix sort on the key bits below the partition id
     for (uint32_t i = tid; i < n; i += PB_THREADS) {
         uint32_t g;
-        S.key[i] = record_key(A.sk[ps + i], A, g);
+        S.key[i] = record_key(load_sk(A.sk + ps + i), A, g);
         S.g[i] = g;
     }
     __syncthreads();
@@ -294,14 +335,14 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
         const uint32_t st = (t & TAG_ST) ? 1u : 0u, en = (t & TAG_EN) ? 1u : 0u, md = (t & TAG_MD) ? 1u : 0u;
         const uint32_t mpos = ps + S.mdx[s], epos = 2 * ps + S.edx[s];
         if (!(A.ablate & 4)) {
-            if (md) A.md_list[mpos] = r;
-            if (st) A.ed_list[epos] = r;
-            if (en) A.ed_list[epos + st] = r;
+            if (md) store_list(A.md_list + mpos, r);
+            if (st) store_list(A.ed_list + epos, r);
+            if (en) store_list(A.ed_list + epos + st, r);
         }
         const uint32_t me = st + en;
         const uint32_t nE = me ? (S.mdx[gh] - S.mdx[bh]) : 0u;
         const uint32_t nD = md ? (S.edx[nextg[j]] - S.edx[bh]) : 0u;
-        if (!(A.ablate & 2)) A.rec[g] = make_uint4(ps + S.mdx[bh], nE | (me << 30), 2 * ps + S.edx[bh], nD);
+        if (!(A.ablate & 2)) store_rec(A.rec + g, make_uint4(ps + S.mdx[bh], nE | (me << 30), 2 * ps + S.edx[bh], nD));
         if constexpr (STRICT) {
             // bucket extent [bh, be)
             uint32_t be = s + 1;

@@ -3,6 +3,10 @@
 # gpurun_out/ab.txt is "<label> rc=<rc> <bench JSON>".  Stops at the first failure.
 #   bash tools_ab.sh occ   bucket-build LDS occupancy (SA_PB_LDS pads)
 #   bash tools_ab.sh pc    pair-count compile variants (build_* trees via SA_OVERLAP_LIB)
+#   bash tools_ab.sh nt    non-temporal record stores in the bucket build (build_nt: -DSA_REC_NT=1)
+#   bash tools_ab.sh pcnt  non-temporal record loads in the pair count (build_pcnt: -DSA_PC_RECNT=1)
+#   bash tools_ab.sh sknt  non-temporal sorted-record loads in the bucket build (build_sknt: -DSA_PB_SKNT=1)
+#   bash tools_ab.sh listnt non-temporal partner-list stores in the bucket build (build_listnt: -DSA_PB_LISTNT=1)
 set -u
 mkdir -p gpurun_out
 run() {  # run <label> [VAR=value ...]
@@ -27,5 +31,37 @@ pc)
     run batch4 SA_OVERLAP_LIB=$LIBDIR/build_b4/libsa_overlap.so
     run threads512 SA_OVERLAP_LIB=$LIBDIR/build_t512/libsa_overlap.so
     run base_b
+    ;;
+nt)
+    run base_a
+    run nt_a SA_OVERLAP_LIB=$LIBDIR/build_nt/libsa_overlap.so
+    run base_b
+    run nt_b SA_OVERLAP_LIB=$LIBDIR/build_nt/libsa_overlap.so
+    ;;
+pcnt)
+    run base_a
+    run pcnt_a SA_OVERLAP_LIB=$LIBDIR/build_pcnt/libsa_overlap.so
+    run base_b
+    run pcnt_b SA_OVERLAP_LIB=$LIBDIR/build_pcnt/libsa_overlap.so
+    ;;
+sknt)
+    run base_a
+    run sknt_a SA_OVERLAP_LIB=$LIBDIR/build_sknt/libsa_overlap.so
+    run base_b
+    run sknt_b SA_OVERLAP_LIB=$LIBDIR/build_sknt/libsa_overlap.so
+    ;;
+listnt)
+    run base_a
+    run listnt_a SA_OVERLAP_LIB=$LIBDIR/build_listnt/libsa_overlap.so
+    run base_b
+    run listnt_b SA_OVERLAP_LIB=$LIBDIR/build_listnt/libsa_overlap.so
+    ;;
+sk3)
+    run base_a
+    run sknt_a SA_OVERLAP_LIB=$LIBDIR/build_sknt/libsa_overlap.so
+    run nosknt_a SA_OVERLAP_LIB=$LIBDIR/build_nosknt/libsa_overlap.so
+    run base_b
+    run sknt_b SA_OVERLAP_LIB=$LIBDIR/build_sknt/libsa_overlap.so
+    run nosknt_b SA_OVERLAP_LIB=$LIBDIR/build_nosknt/libsa_overlap.so
     ;;
 esac
