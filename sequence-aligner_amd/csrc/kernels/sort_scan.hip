@@ -145,6 +145,19 @@ __global__ __launch_bounds__(RS_THREADS) void rs_upsweep_kernel(const uint64_t *
     hist[(uint64_t)threadIdx.x * nblocks + blockIdx.x] = cnt[threadIdx.x];
 }
 
+// SA_RS_KNT (compile knob, default 1): read the scatter's input keys with non-temporal
+// loads so L2 is left to merge the scattered key stores.
+#ifndef SA_RS_KNT
+#define SA_RS_KNT 1
+#endif
+__device__ __forceinline__ unsigned long long rs_load_key(const uint64_t *p) {
+#if SA_RS_KNT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+
 // Stable scatter.  Wave w owns the contiguous sub-tile [base + w*1024, +1024),
 // read as 16 coalesced slices of 64; each element's rank among equal digits of
 // its wave comes from a 64-lane ballot multisplit (8 ballots -> peer mask) plus
@@ -194,7 +207,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep_kernel(const uint64_t
 #pragma unroll
     for (int j = 0; j < RS_SLICES; ++j) {
         const uint64_t i = sub + (uint64_t)j * 64 + lane;
-        k[j] = i < n ? kin[i] : ~0ull;
+        k[j] = i < n ? rs_load_key(kin + i) : ~0ull;
         v[j] = (VALS && i < n) ? vin[i] : 0u;
     }
 #pragma unroll

@@ -7,6 +7,8 @@
 #   bash tools_ab.sh pcnt  non-temporal record loads in the pair count (build_pcnt: -DSA_PC_RECNT=1)
 #   bash tools_ab.sh sknt  non-temporal sorted-record loads in the bucket build (build_sknt: -DSA_PB_SKNT=1)
 #   bash tools_ab.sh listnt non-temporal partner-list stores in the bucket build (build_listnt: -DSA_PB_LISTNT=1)
+#   bash tools_ab.sh sk3   current build vs build_sknt vs build_nosknt (-DSA_PB_SKNT=0)
+#   bash tools_ab.sh rsknt non-temporal key loads in the radix scatter (build_rsknt: -DSA_RS_KNT=1)
 set -u
 mkdir -p gpurun_out
 run() {  # run <label> [VAR=value ...]
@@ -63,5 +65,11 @@ sk3)
     run base_b
     run sknt_b SA_OVERLAP_LIB=$LIBDIR/build_sknt/libsa_overlap.so
     run nosknt_b SA_OVERLAP_LIB=$LIBDIR/build_nosknt/libsa_overlap.so
+    ;;
+rsknt)
+    run base_a
+    run rsknt_a SA_OVERLAP_LIB=$LIBDIR/build_rsknt/libsa_overlap.so
+    run base_b
+    run rsknt_b SA_OVERLAP_LIB=$LIBDIR/build_rsknt/libsa_overlap.so
     ;;
 esac
