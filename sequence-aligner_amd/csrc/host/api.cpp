@@ -161,7 +161,12 @@ int ensure(sa_ctx *c, DBuf &b, size_t count, T **out) {
         b.p = nullptr;
         b.bytes = 0;
         const size_t alloc = need + need / 8;
-        hipError_t e = hipMalloc(&b.p, alloc);
+        // profiling only (env SA_ALLOC_CONTIG=1): ask for physically contiguous VRAM for the
+        // large buffers, for A/B runs on the bucket build's per-process timing modes
+        static const bool contig = getenv("SA_ALLOC_CONTIG") && atoi(getenv("SA_ALLOC_CONTIG")) != 0;
+        hipError_t e = hipErrorOutOfMemory;
+        if (contig && alloc >= (64u << 20)) e = hipExtMallocWithFlags(&b.p, alloc, hipDeviceMallocContiguous);
+        if (e != hipSuccess) e = hipMalloc(&b.p, alloc);
         if (e != hipSuccess) return fail(c, SA_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
         b.bytes = alloc;
     }
