@@ -9,6 +9,7 @@
 #   bash tools_ab.sh listnt non-temporal partner-list stores in the bucket build (build_listnt: -DSA_PB_LISTNT=1)
 #   bash tools_ab.sh sk3   current build vs build_sknt vs build_nosknt (-DSA_PB_SKNT=0)
 #   bash tools_ab.sh rsknt non-temporal key loads in the radix scatter (build_rsknt: -DSA_RS_KNT=1)
+#   bash tools_ab.sh rsvnt non-temporal value loads in the radix scatter (build_rsvnt: -DSA_RS_VNT=1)
 #   bash tools_ab.sh contig physically contiguous large buffers (env SA_ALLOC_CONTIG=1), 4 alternations
 set -u
 mkdir -p gpurun_out
@@ -72,6 +73,12 @@ rsknt)
     run rsknt_a SA_OVERLAP_LIB=$LIBDIR/build_rsknt/libsa_overlap.so
     run base_b
     run rsknt_b SA_OVERLAP_LIB=$LIBDIR/build_rsknt/libsa_overlap.so
+    ;;
+rsvnt)
+    run base_a
+    run rsvnt_a SA_OVERLAP_LIB=$LIBDIR/build_rsvnt/libsa_overlap.so
+    run base_b
+    run rsvnt_b SA_OVERLAP_LIB=$LIBDIR/build_rsvnt/libsa_overlap.so
     ;;
 contig)
     for i in 1 2 3 4; do run base_$i; run contig_$i SA_ALLOC_CONTIG=1; done
