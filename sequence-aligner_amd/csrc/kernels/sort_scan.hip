@@ -130,6 +130,10 @@ constexpr int RS_THREADS = 256;
 constexpr int RS_ITEMS = 16;
 constexpr int RS_TILE = RS_THREADS * RS_ITEMS;
 
+// SA_RS_UNT (compile knob, default 1): non-temporal key loads in the digit histogram.
+#ifndef SA_RS_UNT
+#define SA_RS_UNT 1
+#endif
 __global__ __launch_bounds__(RS_THREADS) void rs_upsweep_kernel(const uint64_t *keys, uint64_t n, int shift,
                                                                 uint32_t *hist, uint32_t nblocks) {
     __shared__ uint32_t cnt[256];
@@ -139,7 +143,14 @@ __global__ __launch_bounds__(RS_THREADS) void rs_upsweep_kernel(const uint64_t *
 #pragma unroll 4
     for (int j = 0; j < RS_ITEMS; ++j) {
         const uint64_t i = base + (uint64_t)j * RS_THREADS + threadIdx.x;
-        if (i < n) atomicAdd(&cnt[(uint32_t)(keys[i] >> shift) & 255u], 1u);
+        if (i < n) {
+#if SA_RS_UNT
+            const uint64_t key = __builtin_nontemporal_load(keys + i);
+#else
+            const uint64_t key = keys[i];
+#endif
+            atomicAdd(&cnt[(uint32_t)(key >> shift) & 255u], 1u);
+        }
     }
     __syncthreads();
     hist[(uint64_t)threadIdx.x * nblocks + blockIdx.x] = cnt[threadIdx.x];

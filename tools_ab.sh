@@ -10,6 +10,7 @@
 #   bash tools_ab.sh sk3   current build vs build_sknt vs build_nosknt (-DSA_PB_SKNT=0)
 #   bash tools_ab.sh rsknt non-temporal key loads in the radix scatter (build_rsknt: -DSA_RS_KNT=1)
 #   bash tools_ab.sh rsvnt non-temporal value loads in the radix scatter (build_rsvnt: -DSA_RS_VNT=1)
+#   bash tools_ab.sh rsunt non-temporal key loads in the radix histogram (build_rsunt: -DSA_RS_UNT=1)
 #   bash tools_ab.sh contig physically contiguous large buffers (env SA_ALLOC_CONTIG=1), 4 alternations
 set -u
 mkdir -p gpurun_out
@@ -79,6 +80,12 @@ rsvnt)
     run rsvnt_a SA_OVERLAP_LIB=$LIBDIR/build_rsvnt/libsa_overlap.so
     run base_b
     run rsvnt_b SA_OVERLAP_LIB=$LIBDIR/build_rsvnt/libsa_overlap.so
+    ;;
+rsunt)
+    run base_a
+    run rsunt_a SA_OVERLAP_LIB=$LIBDIR/build_rsunt/libsa_overlap.so
+    run base_b
+    run rsunt_b SA_OVERLAP_LIB=$LIBDIR/build_rsunt/libsa_overlap.so
     ;;
 contig)
     for i in 1 2 3 4; do run base_$i; run contig_$i SA_ALLOC_CONTIG=1; done
