@@ -251,6 +251,86 @@ def default_hoxd_table():  # BioLibs.defaultHOXD :119-140 (A0 C1 G2 T3)
 _HX = {"A": 0, "C": 1, "G": 2, "T": 3}
 
 
+class JvmError(Exception):
+    """An exception that would end the reference run (NPE, MatchError, ...)."""
+
+
+def _java_split(s):  # String.split(","): trailing empty strings removed
+    if s == "":
+        return [""]
+    parts = s.split(",")
+    while parts and parts[-1] == "":
+        parts.pop()
+    return parts
+
+
+def _java_trim(s):  # String.trim: code points <= U+0020 off both ends
+    b, e = 0, len(s)
+    while b < e and ord(s[b]) <= 0x20:
+        b += 1
+    while e > b and ord(s[e - 1]) <= 0x20:
+        e -= 1
+    return s[b:e]
+
+
+def _java_parse_int(s):  # Integer.parseInt(s): [+-]?[0-9]+ within Int range
+    t = s[1:] if s[:1] in ("+", "-") else s
+    if not t or any(c not in "0123456789" for c in t):
+        raise JvmError("NumberFormatException: " + repr(s))
+    v = int(s)
+    if not -2 ** 31 <= v < 2 ** 31:
+        raise JvmError("NumberFormatException: " + repr(s))
+    return v
+
+
+def _java_read_lines(data):  # BufferedReader.readLine over the whole file
+    out, cur, i = [], [], 0
+    pending = False
+    while i < len(data):
+        c = data[i]
+        if c in "\r\n":
+            out.append("".join(cur))
+            cur, pending = [], False
+            if c == "\r" and i + 1 < len(data) and data[i + 1] == "\n":
+                i += 1
+        else:
+            cur.append(c)
+            pending = True
+        i += 1
+    if pending:
+        out.append("".join(cur))
+    return out
+
+
+def read_hoxd(path):  # BioLibs.readHOXD :66-114 -> 4x4 table (A0 C1 G2 T3) or JvmError
+    costs = [[0] * 4 for _ in range(4)]  # Array.ofDim(4,4) :68
+    lines = _java_read_lines(open(path, "rb").read().decode("latin-1"))
+    if len(lines) < 2:
+        raise JvmError("NullPointerException: readLine() == null")
+    col = _java_split(lines[1])  # :71
+    li = 2
+    while li < len(lines) and lines[li] != "":  # :75
+        row = _java_split(lines[li])
+        for i in range(1, len(row)):  # :77
+            r0 = _java_trim(row[0])
+            if not r0:
+                raise JvmError("StringIndexOutOfBoundsException")
+            if r0[0].upper() not in _HX:
+                raise JvmError("MatchError")
+            A = _HX[r0[0].upper()]
+            if i >= len(col):
+                raise JvmError("ArrayIndexOutOfBoundsException")
+            ci = _java_trim(col[i])
+            if not ci:
+                raise JvmError("StringIndexOutOfBoundsException")
+            if ci[0].upper() not in _HX:
+                raise JvmError("MatchError")
+            B = _HX[ci[0].upper()]
+            costs[A][B] = _java_parse_int(row[i])  # :90
+        li += 1
+    return costs
+
+
 def cost(s, a, b):  # the closure at :142-160 (MatchError on non-ACGT)
     return s.cost[_HX[a.upper()]][_HX[b.upper()]]
 

@@ -123,7 +123,6 @@ struct sa_ctx {
     int align_kernel = 0;  // SA_OPT_ALIGN_KERNEL
     int aligner = SA_ALIGNER_LINEAR;  // SA_OPT_ALIGNER (--linear-align / --quadratic-align)
     uint64_t local_batch_bytes = 16ull << 30;  // traceback-code budget of one quadratic launch
-    int ablate = 0;  // profiling only: SA_ABLATE env (results are wrong when set)
     bool built = false, aligned = false;
     // results (host)
     std::vector<int32_t> lead, trail, count;
@@ -161,12 +160,7 @@ int ensure(sa_ctx *c, DBuf &b, size_t count, T **out) {
         b.p = nullptr;
         b.bytes = 0;
         const size_t alloc = need + need / 8;
-        // profiling only (env SA_ALLOC_CONTIG=1): ask for physically contiguous VRAM for the
-        // large buffers, for A/B runs on the bucket build's per-process timing modes
-        static const bool contig = getenv("SA_ALLOC_CONTIG") && atoi(getenv("SA_ALLOC_CONTIG")) != 0;
-        hipError_t e = hipErrorOutOfMemory;
-        if (contig && alloc >= (64u << 20)) e = hipExtMallocWithFlags(&b.p, alloc, hipDeviceMallocContiguous);
-        if (e != hipSuccess) e = hipMalloc(&b.p, alloc);
+        hipError_t e = hipMalloc(&b.p, alloc);
         if (e != hipSuccess) return fail(c, SA_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
         b.bytes = alloc;
     }
@@ -346,7 +340,7 @@ int upload_reads(sa_ctx *c) {
     const uint32_t n = (uint32_t)(c->boff.size() - 1);
     uint8_t *ascii; uint64_t *boff, *woff, *occ; int32_t *len; uint32_t *codes; int32_t *bad;
     uint32_t *lbase, *lrank; uint8_t *tag;
-    ENSURE(c->d_ascii, c->bases.size() + 16, &ascii);
+    ENSURE(c->d_ascii, c->bases.size() + 32, &ascii);  // pack_reads reads 20 bytes past a word start
     ENSURE(c->d_boff, n + 1, &boff);
     ENSURE(c->d_woff, n + 1, &woff);
     ENSURE(c->d_len, n + 1, &len);
@@ -453,7 +447,6 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
     ENSURE(c->d_biglist, 3 * ((size_t)nparts + 1), &biglist);  // big list, mid list, mid2 list
     PA = PartArgs{};
     PA.sk = keys; PA.sv = nullptr; PA.start = pstart; PA.np = nparts; PA.lb = c->lb; PA.sort_bits = kbits - skip_bits - PB;
-    PA.ablate = c->ablate;
     PA.tagtab = (const uint8_t *)c->d_tagtab.p;
     PA.occ_off = occ_off;
     PA.n_reads = n_reads; PA.npr = npr; PA.rid = rid;
@@ -570,7 +563,6 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
     P.strict = strict ? 1 : 0;
     P.split = 1;
     P.max_occ = c->max_occ;
-    P.ablate = c->ablate;
     P.n_items = n_items;
     P.xcd_swizzle = read_order ? 1 : 0;
     P.table = 256;
@@ -912,10 +904,27 @@ int device_align(sa_ctx *c, bool readback) {
     const int G = wmax <= 15 ? 16 : (wmax <= 31 ? 32 : 64);
     const uint32_t rw_fit = (160u * 1024u / (256u * 4u) - 1u) | 1u;
     const uint32_t rw = std::min<uint32_t>((uint32_t)((maxL + 1 + 15) / 16) | 1u, rw_fit);
-    // both kernels hold the cost matrix as int8 bytes (HOXD70 spans -125..100)
-    for (int x = 0; x < 16; ++x)
-        if (c->set.cost[x] < -128 || c->set.cost[x] > 127)
-            return fail(c, SA_E_ARG, "cost matrix entries must lie in [-128, 127]");
+    // The DP kernels hold the cost matrix as int8 bytes (HOXD70 spans -125..100).
+    // Every recurrence (BioLibs.scala:645-668, :725-764; :171-263 for the
+    // quadratic aligner) is max-plus and linear in (costs, gO, gE) with 0, so
+    // dividing all of them by their common divisor g scales every cell by 1/g
+    // exactly: argmax, walk codes and the alignment are unchanged (a x10 HOXD
+    // matrix with gap costs -200 / -20 runs as HOXD70).
+    int32_t cost[16], gap_open = c->set.gap_open, gap_extend = c->set.gap_extend;
+    {
+        auto gcd = [](int64_t a, int64_t b) { a = a < 0 ? -a : a; b = b < 0 ? -b : b; while (b) { int64_t t = a % b; a = b; b = t; } return a; };
+        int64_t g = gcd(gap_open, gap_extend);
+        for (int x = 0; x < 16; ++x) g = gcd(g, c->set.cost[x]);
+        if (g <= 1) g = 1;
+        for (int x = 0; x < 16; ++x) {
+            cost[x] = (int32_t)(c->set.cost[x] / g);
+            if (cost[x] < -128 || cost[x] > 127)
+                return fail(c, SA_E_OVERFLOW, "cost matrix entries (divided by their common divisor with the gap "
+                                              "costs) must lie in [-128, 127]");
+        }
+        gap_open = (int32_t)(gap_open / g);
+        gap_extend = (int32_t)(gap_extend / g);
+    }
     // lane-per-pair kernels: band <= 31 columns (16 / 24 / 32 registers per row),
     // reads <= 30,000 bp (c << 16 | e packing)
     const int lw = dovetail_lane_width(wmax);
@@ -931,13 +940,13 @@ int device_align(sa_ctx *c, bool readback) {
     const bool exact = wmin == 15 && wmax == 15 && lw == 16;  // every band exactly 16 cells wide
     AlignParams P;
     P.k = c->set.kmer_size;
-    P.gap_open = c->set.gap_open;
-    P.gap_extend = c->set.gap_extend;
+    P.gap_open = gap_open;
+    P.gap_extend = gap_extend;
     P.min_overlap = c->set.min_overlap;
     P.one_minus_minid = omm;
     P.min_identity = c->set.min_identity;
     P.max_ignore = (float)c->set.max_ignore;
-    memcpy(P.cost, c->set.cost, sizeof(P.cost));
+    memcpy(P.cost, cost, sizeof(P.cost));
     P.rw = rw;
     Counters *cnt = (Counters *)c->d_cnt.p;
     DevAlignment *out;
@@ -1064,7 +1073,6 @@ int sa_ctx_create(const sa_settings *s, int device, sa_ctx **out) {
     sa_ctx *c = new sa_ctx();
     c->set = *s;
     c->device = device;
-    if (const char *ab = getenv("SA_ABLATE")) c->ablate = atoi(ab);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return SA_E_HIP;

@@ -8,20 +8,25 @@
 
 namespace sa {
 
-// ASCII -> 2-bit HOXD code (A0 C1 G2 T3), after readSeq's toUpperCase.
-__device__ __forceinline__ int base_code(uint32_t ch, bool &ok) {
-    ch |= 0x20u;  // fold to lower case (non-letters stay non-ACGT)
-    ok = true;
-    switch (ch) {
-    case 'a': return 0;
-    case 'c': return 1;
-    case 'g': return 2;
-    case 't': return 3;
-    default: ok = false; return 0;
+// 2-bit code of each byte of x (A0 C1 G2 T3 after folding to lower case) and a
+// mask of the bytes that are not ACGT.  'a' 0x61, 'c' 0x63, 'g' 0x67, 't' 0x74.
+__device__ __forceinline__ uint32_t codes4(uint32_t x, uint32_t &badm) {
+    uint32_t code = 0;
+    badm = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const uint32_t ch = ((x >> (8 * b)) & 0xFFu) | 0x20u;
+        const uint32_t c = ch == 'c' ? 1u : ch == 'g' ? 2u : ch == 't' ? 3u : 0u;
+        const bool ok = c != 0u || ch == 'a';
+        code |= c << (2 * b);
+        badm |= ok ? 0u : (1u << b);
     }
+    return code;  // byte b -> bits [2b, 2b+2)
 }
 
-// One wave per read, lane = one 16-base word.
+// One wave per read, lane = one 16-base word.  A lane reads its 16 bytes as
+// five aligned dwords (the ASCII buffer is padded) and funnel-shifts them into
+// place: one coalesced kilobyte per wave-instruction instead of 16 byte loads.
 __global__ __launch_bounds__(256) void pack_reads_kernel(DevReads r) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -33,18 +38,29 @@ __global__ __launch_bounds__(256) void pack_reads_kernel(DevReads r) {
         const int32_t nw = (L + 15) >> 4;
         int32_t first_bad = INT32_MAX;
         for (int32_t q = lane; q < nw; q += 64) {
-            uint32_t word = 0;
             const int32_t p0 = q << 4;
+            const uint64_t a = b0 + (uint64_t)p0;
+            const uint32_t *wp = reinterpret_cast<const uint32_t *>(r.ascii + (a & ~3ull));
+            const uint32_t sh = (uint32_t)(a & 3u);
+            uint32_t d[5];
 #pragma unroll
-            for (int t = 0; t < 16; ++t) {
-                const int32_t p = p0 + t;
-                if (p < L) {
-                    bool ok;
-                    const int c = base_code(r.ascii[b0 + p], ok);
-                    word |= (uint32_t)c << (30 - 2 * t);
-                    if (!ok && p < first_bad) first_bad = p;
-                }
+            for (int j = 0; j < 5; ++j) d[j] = wp[j];
+            const int32_t valid = min(16, L - p0);  // bytes of this word inside the read
+            uint32_t word = 0, badm = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t x = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);  // bytes 4j .. 4j+3
+                uint32_t bm;
+                const uint32_t c = codes4(x, bm);
+                // MSB-first: base t of the word at bits 30 - 2t
+#pragma unroll
+                for (int b = 0; b < 4; ++b) word |= ((c >> (2 * b)) & 3u) << (30 - 2 * (4 * j + b));
+                badm |= bm << (4 * j);
             }
+            const uint32_t vmask = valid >= 16 ? 0xFFFFu : ((1u << valid) - 1u);
+            word &= valid >= 16 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> (2 * valid));
+            badm &= vmask;
+            if (badm) first_bad = min(first_bad, p0 + (int32_t)__builtin_ctz(badm));
             r.codes[w0 + q] = word;
         }
         // wave-wide min of first_bad

@@ -55,12 +55,18 @@ __device__ __forceinline__ uint32_t pc_hash(uint32_t p) {
     return (p * 0x9E3779B1u) >> (32 - __builtin_ctz((unsigned)TAB));
 }
 
+// Elements (role pairs) of a chunk are enumerated in windows of PC_WIN; eo[e]
+// = 1 + the occurrence holding element w0 + e, built from one marker per
+// occurrence start and an inclusive max-scan (pref is non-decreasing).
+constexpr int PC_WIN = 2048;
+
 template <int TAB>
 struct PcShared {
     uint32_t key[TAB];
     uint32_t cnt[TAB];
     uint32_t pref[PC_CHUNK + 1];
     uint4 rec[PC_CHUNK];       // per-occurrence partner ranges (partition.hip)
+    uint16_t eo[PC_WIN];       // element -> occurrence (+1) of the current window
     uint32_t lds4[PC_THREADS / 64];
     uint32_t fill, overflow, out_base;
 };
@@ -90,6 +96,25 @@ __device__ __forceinline__ uint32_t pc_block_excl_scan(uint32_t v, uint32_t *lds
     __syncthreads();
     *total = tot;
     return off + inc - v;
+}
+
+__device__ __forceinline__ uint32_t pc_block_excl_max(uint32_t v, uint32_t *lds4) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = __shfl_up(inc, off, 64);
+        if (lane >= off) inc = max(inc, t);
+    }
+    uint32_t ex = __shfl_up(inc, 1, 64);
+    if (lane == 0) ex = 0;
+    if (lane == 63) lds4[w] = inc;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < PC_THREADS / 64; ++i)
+        if (i < w) ex = max(ex, lds4[i]);
+    __syncthreads();
+    return ex;
 }
 
 template <bool STRICT, int TAB>
@@ -177,21 +202,38 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
         }
         if (tid == PC_THREADS - 1 && cn == PC_CHUNK) S.pref[PC_CHUNK] = total;
         role_pairs += total;
-        __syncthreads();
 
-        // --- load-balanced enumeration: each thread a contiguous slice, partner
-        //     ids fetched PC_BATCH at a time so the gathers overlap
-        const uint32_t per = (total + PC_THREADS - 1) / PC_THREADS;
-        const uint32_t t0 = min(total, tid * per), t1 = min(total, t0 + per);
-        if (t0 < t1) {
-            uint32_t lo = 0, hi = cn;  // last oi with pref[oi] <= t0
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (S.pref[mid] <= t0) lo = mid; else hi = mid;
+        // --- lane-interleaved enumeration: consecutive lanes take consecutive
+        //     elements, so a wave's partner loads walk one occurrence's list range
+        //     (a few cache lines per instruction, not 64)
+        for (uint32_t w0 = 0; w0 < total; w0 += PC_WIN) {
+            __syncthreads();  // pref / rec written; the previous window's eo consumed
+            static_assert(PC_WIN == 8 * PC_THREADS, "one 16-byte eo slice per thread");
+            reinterpret_cast<uint4 *>(S.eo)[tid] = make_uint4(0, 0, 0, 0);
+            __syncthreads();
+            for (uint32_t oi = tid; oi < cn; oi += PC_THREADS) {
+                const uint32_t s0 = S.pref[oi], s1 = S.pref[oi + 1];
+                if (s1 > s0) {
+                    if (s0 >= w0 && s0 < w0 + PC_WIN) S.eo[s0 - w0] = (uint16_t)(oi + 1);
+                    else if (s0 < w0 && s1 > w0) S.eo[0] = (uint16_t)(oi + 1);  // runs into the window
+                }
             }
-            uint32_t oi = lo;
-            uint32_t base = S.pref[oi], nxt = S.pref[oi + 1];
-            for (uint32_t t = t0; t < t1; t += PC_BATCH) {
+            __syncthreads();
+            {   // inclusive max-scan of eo: 8 entries per thread, then across threads
+                const uint4 v = reinterpret_cast<const uint4 *>(S.eo)[tid];
+                uint32_t x[8] = {v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16,
+                                 v.z & 0xFFFFu, v.z >> 16, v.w & 0xFFFFu, v.w >> 16};
+#pragma unroll
+                for (int j = 1; j < 8; ++j) x[j] = max(x[j], x[j - 1]);
+                const uint32_t before = pc_block_excl_max(x[7], S.lds4);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) x[j] = max(x[j], before);
+                reinterpret_cast<uint4 *>(S.eo)[tid] =
+                    make_uint4(x[0] | (x[1] << 16), x[2] | (x[3] << 16), x[4] | (x[5] << 16), x[6] | (x[7] << 16));
+            }
+            __syncthreads();
+            const uint32_t wn = min((uint32_t)PC_WIN, total - w0);
+            for (uint32_t e0 = 0; e0 < wn; e0 += PC_THREADS * PC_BATCH) {
                 uint32_t part[PC_BATCH], wv[PC_BATCH];
                 unsigned long long rk[PC_BATCH];
 #pragma unroll
@@ -199,10 +241,10 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
                     part[bb] = a;  // "same read" = skip
                     wv[bb] = 0;
                     rk[bb] = 0;
-                    const uint32_t tt = t + bb;
-                    if (tt < t1) {
-                        while (tt >= nxt) { ++oi; base = nxt; nxt = S.pref[oi + 1]; }
-                        const uint32_t off = tt - base;
+                    const uint32_t el = e0 + bb * PC_THREADS + tid;
+                    if (el < wn) {
+                        const uint32_t oi = (uint32_t)S.eo[el] - 1u;
+                        const uint32_t off = w0 + el - S.pref[oi];
                         const uint4 rc = S.rec[oi];
                         const uint32_t nE = rc.y & 0x3FFFFFFFu;
                         if (off < nE) {
@@ -211,12 +253,12 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
                             wv[bb] = rc.y >> 30;
                             if constexpr (STRICT) {
                                 const uint4 sr = X.srec[oi];
-                                const uint32_t bid = sr.x;
-                                const uint32_t nmd = in.bkt_nmd[bid], nst = in.bkt_nst[bid];
+                                const uint32_t hb = sr.x;
+                                const uint32_t nmd = in.bkt_nmd[hb], nst = in.bkt_nst[hb];
                                 const unsigned long long within =
                                     (unsigned long long)(sr.y >> 31) * nst * nmd +
                                     (unsigned long long)(sr.y & 0x7FFFFFFFu) * nmd + in.md_idx[q];
-                                rk[bb] = ((unsigned long long)in.bkt_rank[bid] << 37) | within;
+                                rk[bb] = ((unsigned long long)in.bkt_rank[hb] << 37) | within;
                             }
                         } else {
                             const uint32_t q = rc.z + (off - nE);
@@ -224,13 +266,13 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
                             wv[bb] = 1;
                             if constexpr (STRICT) {
                                 const uint4 sr = X.srec[oi];
-                                const uint32_t bid = sr.x;
-                                const uint32_t nmd = in.bkt_nmd[bid], nst = in.bkt_nst[bid];
+                                const uint32_t hb = sr.x;
+                                const uint32_t nmd = in.bkt_nmd[hb], nst = in.bkt_nst[hb];
                                 const uint32_t pe = in.ed_idx[q];
                                 const unsigned long long within =
                                     (unsigned long long)(pe >> 31) * nst * nmd +
                                     (unsigned long long)(pe & 0x7FFFFFFFu) * nmd + sr.z;
-                                rk[bb] = ((unsigned long long)in.bkt_rank[bid] << 37) | within;
+                                rk[bb] = ((unsigned long long)in.bkt_rank[hb] << 37) | within;
                             }
                         }
                     }
@@ -240,7 +282,6 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
                     const uint32_t partner = part[bb];
                     if (partner == a) continue;                 // same read (KmerTable.scala:61-63)
                     if (split > 1 && (partner % split) != residue) continue;
-                    if (p.ablate & 16) { if (partner == 0xFFFFFFF0u) S.fill = 0; continue; }
                     pc_insert<STRICT, TAB>(S, X, partner, wv[bb], rk[bb]);
                 }
                 if (S.overflow) break;
@@ -260,7 +301,6 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
         return;
     }
     // --- emit (a, partner, count[, rank]) --------------------------------
-    if (p.ablate & 32) return;
     constexpr int PER = TAB / PC_THREADS;
     uint32_t keep = 0;
 #pragma unroll

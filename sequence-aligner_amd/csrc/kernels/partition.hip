@@ -19,25 +19,9 @@
 // traversal order is built from, per-bucket |st|, |md| and first occurrence.
 // Partitions larger than the LDS capacity take the global scan path
 // (buckets.hip) and records_from_tables_kernel below.  Bound: HBM / LDS.
-#include <cstdlib>
 #include "../sa_internal.h"
 
 namespace sa {
-
-// SA_REC_NT (compile knob, default 0): write the scattered per-occurrence records with
-// non-temporal stores (streamed past L2) instead of ordinary ones, for A/B runs.
-#ifndef SA_REC_NT
-#define SA_REC_NT 0
-#endif
-__device__ __forceinline__ void store_rec(uint4 *p, uint4 v) {
-#if SA_REC_NT
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    u32x4 w = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(w, reinterpret_cast<u32x4 *>(p));
-#else
-    *p = v;
-#endif
-}
 
 __device__ __forceinline__ uint32_t read_of_g(uint32_t g, const uint64_t *occ_off, uint32_t n_reads, uint32_t npr,
                                               const uint32_t *rid, const uint32_t *g2r) {
@@ -65,19 +49,6 @@ __device__ __forceinline__ uint64_t load_sk(const uint64_t *p) {
     return __builtin_nontemporal_load(p);
 #else
     return *p;
-#endif
-}
-
-// SA_PB_LISTNT (compile knob, default 0): write the partner lists with non-temporal
-// stores; A/B only.
-#ifndef SA_PB_LISTNT
-#define SA_PB_LISTNT 0
-#endif
-__device__ __forceinline__ void store_list(uint32_t *p, uint32_t v) {
-#if SA_PB_LISTNT
-    __builtin_nontemporal_store(v, p);
-#else
-    *p = v;
 #endif
 }
 
@@ -262,7 +233,7 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
         S.g[i] = g;
     }
     __syncthreads();
-    if (!(A.ablate & 1)) lds_radix_sort<CAP>(S, n, A.sort_bits);
+    lds_radix_sort<CAP>(S, n, A.sort_bits);
     // ---- per-thread contiguous items: flags and local aggregates -----------
     const int lb = A.lb;
     const unsigned long long lbm = (1ull << lb) - 1;
@@ -334,15 +305,13 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
         const uint32_t r = read_of_g(g, A.occ_off, A.n_reads, A.npr, A.rid, A.g2r);
         const uint32_t st = (t & TAG_ST) ? 1u : 0u, en = (t & TAG_EN) ? 1u : 0u, md = (t & TAG_MD) ? 1u : 0u;
         const uint32_t mpos = ps + S.mdx[s], epos = 2 * ps + S.edx[s];
-        if (!(A.ablate & 4)) {
-            if (md) store_list(A.md_list + mpos, r);
-            if (st) store_list(A.ed_list + epos, r);
-            if (en) store_list(A.ed_list + epos + st, r);
-        }
+        if (md) A.md_list[mpos] = r;
+        if (st) A.ed_list[epos] = r;
+        if (en) A.ed_list[epos + st] = r;
         const uint32_t me = st + en;
         const uint32_t nE = me ? (S.mdx[gh] - S.mdx[bh]) : 0u;
         const uint32_t nD = md ? (S.edx[nextg[j]] - S.edx[bh]) : 0u;
-        if (!(A.ablate & 2)) store_rec(A.rec + g, make_uint4(ps + S.mdx[bh], nE | (me << 30), 2 * ps + S.edx[bh], nD));
+        A.rec[g] = make_uint4(ps + S.mdx[bh], nE | (me << 30), 2 * ps + S.edx[bh], nD);
         if constexpr (STRICT) {
             // bucket extent [bh, be)
             uint32_t be = s + 1;
@@ -469,12 +438,9 @@ hipError_t launch_part_starts(const uint64_t *sk, uint64_t n, int shift, uint32_
 
 hipError_t launch_part_build(const PartArgs &a, bool strict, hipStream_t s) {
     if (!a.np) return hipSuccess;
-    // profiling only (env SA_PB_LDS): pad the 1,024-record block's LDS to cap
-    // its blocks per CU, for occupancy A/B runs on one box
-    static const size_t pb_lds_pad = getenv("SA_PB_LDS") ? (size_t)atol(getenv("SA_PB_LDS")) : 0;
 #define PB_LAUNCH(CAPV, GRID, ST)                                                                          \
     do {                                                                                                 \
-        const size_t lds = CAPV == 1024 && pb_lds_pad > part_lds<CAPV>() ? pb_lds_pad : part_lds<CAPV>();  \
+        const size_t lds = part_lds<CAPV>();                                                             \
         (void)hipFuncSetAttribute((const void *)part_build_kernel<CAPV, ST>,                             \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                 \
         hipLaunchKernelGGL((part_build_kernel<CAPV, ST>), dim3(GRID), dim3(PB_THREADS), lds, s, a);     \

@@ -169,18 +169,6 @@ __device__ __forceinline__ unsigned long long rs_load_key(const uint64_t *p) {
 #endif
 }
 
-// SA_RS_VNT (compile knob, default 0): the same for the scatter's input values; A/B only.
-#ifndef SA_RS_VNT
-#define SA_RS_VNT 0
-#endif
-__device__ __forceinline__ uint32_t rs_load_val(const uint32_t *p) {
-#if SA_RS_VNT
-    return __builtin_nontemporal_load(p);
-#else
-    return *p;
-#endif
-}
-
 // Stable scatter.  Wave w owns the contiguous sub-tile [base + w*1024, +1024),
 // read as 16 coalesced slices of 64; each element's rank among equal digits of
 // its wave comes from a 64-lane ballot multisplit (8 ballots -> peer mask) plus
@@ -231,7 +219,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep_kernel(const uint64_t
     for (int j = 0; j < RS_SLICES; ++j) {
         const uint64_t i = sub + (uint64_t)j * 64 + lane;
         k[j] = i < n ? rs_load_key(kin + i) : ~0ull;
-        v[j] = (VALS && i < n) ? rs_load_val(vin + i) : 0u;
+        v[j] = (VALS && i < n) ? vin[i] : 0u;
     }
 #pragma unroll
     for (int j = 0; j < RS_SLICES; ++j) {

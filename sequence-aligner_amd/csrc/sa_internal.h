@@ -91,7 +91,6 @@ struct PairParams {
     int32_t strict;        // compute first-occurrence ranks
     int32_t split;         // partner residue classes (overflow fallback)
     uint32_t max_occ;      // max occurrences of one read (LDS sizing)
-    int32_t ablate;        // profiling only (env SA_ABLATE): 16 skip inserts, 32 skip emission
     uint32_t n_items;      // reads (x split) to process; blocks beyond it exit
     int32_t xcd_swizzle;   // 1: XCD-contiguous block -> item map (grid % 8 == 0)
     int32_t table;         // LDS hash slots per read: 256 (first pass) or 2048
@@ -171,7 +170,6 @@ struct PartArgs {
     uint32_t np;
     int lb;
     int sort_bits;               // key bits below the partition id (sorted in LDS)
-    int ablate;                  // profiling only (env SA_ABLATE): 1 skip sort, 2 skip record scatter, 4 skip lists
     const uint8_t *tagtab;
     const uint64_t *occ_off;
     uint32_t n_reads, npr;
