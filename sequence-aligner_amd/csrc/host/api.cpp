@@ -58,7 +58,7 @@ struct Counters {
     uint32_t big_n;
     uint32_t mid_n;
     uint32_t mid2_n;
-    uint32_t pad_;
+    uint32_t xrec_n;     // escape records written (big partitions)
     uint32_t shard_off[NSHARD + 2];
 };
 
@@ -96,6 +96,7 @@ struct sa_ctx {
     DBuf d_md, d_ed, d_bmdo, d_bedo, d_bstart, d_gbid, d_gmds, d_gede, d_ogid, d_bkttmp;
     DBuf d_mdidx, d_edidx, d_occidx, d_bnst, d_brank, d_bhash, d_bfirst;
     DBuf d_pstart, d_biglist, d_rec, d_srec, d_bnmd, d_ishead, d_bnst2;
+    DBuf d_tmd, d_ted, d_tmdi, d_tedi, d_xrec;  // big-partition scratch lists, escape records
     uint32_t *bkt_rank_dev = nullptr;
     DBuf d_pf, d_ps, d_pc, d_pr, d_ovl, d_cnt;
     DBuf d_okeys, d_ovals, d_okeys2, d_ovals2, d_osort;
@@ -263,7 +264,8 @@ int prepare_reads(sa_ctx *c) {
         }
     }
     c->n_occ = c->occ_off[n];
-    if (c->n_occ >= 0xFFFFFFF0ull) return fail(c, SA_E_OVERFLOW, "more than 2^32 k-mers on one device");
+    // the combined partner list holds up to 3 entries per k-mer, indexed by u32
+    if (c->n_occ >= 0x55555550ull) return fail(c, SA_E_OVERFLOW, "more than 1,431,655,760 k-mers on one device");
     {
         const uint64_t nb = (c->n_occ >> G2R_SHIFT) + 2;
         c->g2r.assign(nb, 0);
@@ -456,16 +458,16 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
     PA.lbase = (const uint32_t *)c->d_lbase.p;
     PA.lrank = (const uint32_t *)c->d_lrank.p;
     PA.k = c->set.kmer_size;
-    ENSURE(c->d_md, n + 1, &PA.md_list);
-    ENSURE(c->d_ed, 2 * n + 2, &PA.ed_list);
+    ENSURE(c->d_md, 3 * n + 3, &PA.lst);
     ENSURE(c->d_rec, n + 1, &PA.rec);
+    PA.xrec = nullptr;
+    PA.xrec_n = &cnt->xrec_n;
     PA.big_list = biglist; PA.big_n = &cnt->big_n;
     PA.mid_list = biglist + nparts + 1; PA.mid_n = &cnt->mid_n;
     PA.mid2_list = biglist + 2 * ((size_t)nparts + 1); PA.mid2_n = &cnt->mid2_n;
     PA.counts = cnt->bkt_counts;
     if (strict) {
-        ENSURE(c->d_mdidx, n + 1, &PA.md_idx);
-        ENSURE(c->d_edidx, 2 * n + 2, &PA.ed_idx);
+        ENSURE(c->d_mdidx, 3 * n + 3, &PA.lidx);
         ENSURE(c->d_srec, n + 1, &PA.srec);
         ENSURE(c->d_bnst, n + 1, &PA.bkt_nst);
         ENSURE(c->d_bnmd, n + 1, &PA.bkt_nmd);
@@ -494,8 +496,21 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
         HIPCHK(hipMemcpy(starts.data(), pstart, (nparts + 1) * 4, hipMemcpyDeviceToHost));
         std::sort(bl.begin(), bl.end());
         uint32_t maxn = 0;
-        for (uint32_t p : bl) maxn = std::max(maxn, starts[p + 1] - starts[p]);
+        uint64_t big_recs = 0;
+        for (uint32_t p : bl) {
+            maxn = std::max(maxn, starts[p + 1] - starts[p]);
+            big_recs += starts[p + 1] - starts[p];
+        }
         Buckets B{};
+        // the scan's ascending partition-relative lists (moved into the combined
+        // layout per partition) and the escape records of high-copy repeats
+        ENSURE(c->d_tmd, (size_t)maxn + 1, &B.md_list);
+        ENSURE(c->d_ted, 2 * (size_t)maxn + 2, &B.ed_list);
+        if (strict) {
+            ENSURE(c->d_tmdi, (size_t)maxn + 1, &B.md_idx);
+            ENSURE(c->d_tedi, 2 * (size_t)maxn + 2, &B.ed_idx);
+        }
+        ENSURE(c->d_xrec, big_recs + 1, &PA.xrec);
         ENSURE(c->d_bmdo, maxn + 2, &B.bkt_mdo);
         ENSURE(c->d_bedo, maxn + 2, &B.bkt_edo);
         ENSURE(c->d_bstart, maxn + 2, &B.bkt_start);
@@ -526,14 +541,11 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
                 HIPCHK(hipMemcpyAsync(vals + ps, v0, (size_t)pn * 4, hipMemcpyDeviceToDevice, c->stream));
             }
             B.n_occ = pn;
-            B.md_list = PA.md_list + ps;
-            B.ed_list = PA.ed_list + 2ull * ps;
-            if (strict) { B.md_idx = PA.md_idx + ps; B.ed_idx = PA.ed_idx + 2ull * ps; }
             HIPCHK(build_buckets(keys2 + ps, vals + ps, pn, c->lb, tagtab, PA.occ_off, n_reads, npr, rid, PA.g2r, B,
                                  bigtot + 4 * (size_t)bi, btmp, c->stream));
             if (strict) HIPCHK(build_strict_index(keys2 + ps, vals + ps, pn, c->lb, tagtab, B, c->stream));
-            HIPCHK(launch_records_from_tables(keys2, vals, ps, pn, c->lb, tagtab, B, PA.rec, strict ? 1 : 0, PA.srec,
-                                              PA.bkt_nst, PA.bkt_nmd, PA.bkt_first, PA.is_head, c->stream));
+            HIPCHK(launch_relayout_lists(B, ps, pn, bigtot + 4 * (size_t)bi, PA, strict, c->stream));
+            HIPCHK(launch_records_from_tables(keys2, vals, ps, pn, c->lb, tagtab, B, PA, strict ? 1 : 0, c->stream));
             ++bi;
         }
         // per-partition totals read back once (no host sync inside the loop)
@@ -748,9 +760,9 @@ int device_build(sa_ctx *c, bool readback) {
         if (n) HIPCHK(hipMemcpy(c->bkt_rank_dev, rank.data(), n * 4, hipMemcpyHostToDevice));
     }
     PairIn PI{};
-    PI.rec = PA.rec; PI.md_list = PA.md_list; PI.ed_list = PA.ed_list;
+    PI.rec = PA.rec; PI.xrec = PA.xrec; PI.lst = PA.lst;
     if (strict) {
-        PI.srec = PA.srec; PI.md_idx = PA.md_idx; PI.ed_idx = PA.ed_idx;
+        PI.srec = PA.srec; PI.lidx = PA.lidx;
         PI.bkt_nst = PA.bkt_nst; PI.bkt_nmd = PA.bkt_nmd; PI.bkt_rank = c->bkt_rank_dev;
     }
 
@@ -1092,7 +1104,10 @@ void sa_ctx_destroy(sa_ctx *c) {
                     &c->d_bnst, &c->d_brank, &c->d_bhash, &c->d_bfirst, &c->d_pf, &c->d_ps, &c->d_pc, &c->d_pr,
                     &c->d_ovl, &c->d_cnt, &c->d_okeys, &c->d_ovals, &c->d_okeys2, &c->d_ovals2, &c->d_osort,
                     &c->d_lead, &c->d_trail, &c->d_count, &c->d_aln, &c->d_p1, &c->d_tb, &c->d_rkey, &c->d_rkey2, &c->d_rord, &c->d_rord2, &c->d_rtmp, &c->d_gocc, &c->d_rid, &c->d_loff, &c->d_starts, &c->d_bounds, &c->d_gcodes, &c->d_gwoff, &c->d_glen, &c->d_gbad, &c->d_psum, &c->d_pkeep, &c->d_ppos, &c->d_scan, &c->d_lr, &c->d_pstart, &c->d_biglist, &c->d_rec,
-                    &c->d_srec, &c->d_bnmd, &c->d_ishead, &c->d_bnst2};
+                    &c->d_srec, &c->d_bnmd, &c->d_ishead, &c->d_bnst2, &c->d_tmd, &c->d_ted, &c->d_tmdi,
+                    &c->d_tedi, &c->d_xrec, &c->d_items, &c->d_bigtot, &c->d_hk0, &c->d_hk1, &c->d_hflag,
+                    &c->d_hidx, &c->d_hpos, &c->d_htmp, &c->d_hist, &c->d_hovf, &c->d_hsmall, &c->d_g2r,
+                    &c->d_ltb, &c->d_lmax};
     for (DBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto &p : c->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
@@ -1443,6 +1458,7 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, uint64_t n, uint64_t *counts) {
     int rc = ensure_prepared(c);
     if (rc) return rc;
     const uint32_t N = (uint32_t)c->dlen.size();
+    if (n >= 0x55555550ull) return fail(c, SA_E_OVERFLOW, "more than 1,431,655,760 k-mers received on one rank");
     Counters *cnt;
     ENSURE(c->d_cnt, 1, &cnt);
     HIPCHK(hipMemsetAsync(cnt, 0, sizeof(Counters), c->stream));
@@ -1472,7 +1488,7 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, uint64_t n, uint64_t *counts) {
                       big_buckets, c->log_ranks);
     if (rc) return rc;
     PairIn PI{};
-    PI.rec = PA.rec; PI.md_list = PA.md_list; PI.ed_list = PA.ed_list;
+    PI.rec = PA.rec; PI.xrec = PA.xrec; PI.lst = PA.lst;
     EmitParams E = emit_params(c);
     E.occ_off = loff;  // occurrences of read a on this rank: [loff[a], loff[a+1])
     // every global read has ~1/P of its occurrences here: blocks take ranges of

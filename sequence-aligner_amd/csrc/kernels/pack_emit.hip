@@ -72,16 +72,6 @@ __global__ __launch_bounds__(256) void pack_reads_kernel(DevReads r) {
     }
 }
 
-// 16 codes starting at base position p of a read whose first word is `w`
-// (MSB-first window), used for hashing and diagonal compares.
-__device__ __forceinline__ uint32_t window16(const uint32_t *w, int32_t p) {
-    const uint32_t a = w[p >> 4];
-    const int s = p & 15;
-    if (s == 0) return a;
-    const uint32_t b = w[(p >> 4) + 1];
-    return (a << (2 * s)) | (b >> (32 - 2 * s));
-}
-
 // One wave per read, lane = position.  record = mix32(seqHash) << 32 | g.
 __global__ __launch_bounds__(256) void kmer_emit_kernel(DevReads r, EmitParams e, uint64_t *keys,
                                                         uint32_t *vals) {
@@ -100,11 +90,7 @@ __global__ __launch_bounds__(256) void kmer_emit_kernel(DevReads r, EmitParams e
         const uint64_t g0 = e.occ_off[rd];
         uint32_t kmin = 0xFFFFFFFFu;
         for (int32_t i = lane; i < nk; i += 64) {
-            uint32_t x = window16(w, i);
-            x = shift == 32 ? 0u : (x >> shift);
-            // HOXD order (A0 C1 G2 T3) -> seqHash order (A0 C1 T2 G3): c ^ (c >> 1)
-            x ^= (x >> 1) & 0x55555555u;
-            const uint32_t h = mix32(x);
+            const uint32_t h = kmer_mix(w, i, shift);
             kmin = min(kmin, h);
             // 8-byte record: mixed hash | occurrence index (the loc rank is
             // re-derived from the index where it is needed, partition.hip)

@@ -12,8 +12,8 @@
 // collision filter is applied on chip.  Strict mode also tracks each key's
 // first-occurrence rank in calcPairData's traversal order, from which the host
 // replays GNU Trove's PairData layout.
-// Each k-mer's partner ranges arrive as one coalesced 16-byte record
-// (partition.hip).  Work is load-balanced inside the workgroup over the prefix
+// Each k-mer's partner ranges arrive as one coalesced 8-byte record
+// (partition.hip; decode_rec, sa_internal.h).  Work is load-balanced inside the workgroup over the prefix
 // sum of per-k-mer partner counts; partner ids are gathered PC_BATCH at a time.
 // Bound: gather latency / LDS atomics; HBM bytes are small.
 #include "../sa_internal.h"
@@ -34,19 +34,12 @@ constexpr int PC_CHUNK = 512;            // occurrences per pass over a read
 #define SA_PC_BATCH 8
 #endif
 constexpr int PC_BATCH = SA_PC_BATCH;    // partner loads in flight per thread
-// SA_PC_RECNT (compile knob, default 1): stream the per-occurrence records (read once)
-// with non-temporal loads so they do not displace the partner lists from L2.
-#ifndef SA_PC_RECNT
-#define SA_PC_RECNT 1
-#endif
-__device__ __forceinline__ uint4 load_rec(const uint4 *p) {
-#if SA_PC_RECNT
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4 w = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
-    return make_uint4(w.x, w.y, w.z, w.w);
-#else
-    return *p;
-#endif
+// the per-occurrence records are read once: non-temporal loads keep them from
+// displacing the partner lists in L2
+__device__ __forceinline__ uint4 load_rec(const PairIn &in, uint64_t g) {
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    const u32x2 w = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(in.rec + g));
+    return decode_rec(make_uint2(w.x, w.y), in.xrec);
 }
 constexpr uint32_t PC_EMPTY = 0xFFFFFFFFu;
 
@@ -182,7 +175,7 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
             const uint32_t oi = tid * PER + j;  // thread-contiguous
             uint32_t tot = 0;
             if (oi < cn) {
-                const uint4 rc = load_rec(in.rec + g0 + c0 + oi);
+                const uint4 rc = load_rec(in, g0 + c0 + oi);
                 S.rec[oi] = rc;
                 tot = (rc.y & 0x3FFFFFFFu) + rc.w;
                 if constexpr (STRICT) X.srec[oi] = in.srec[g0 + c0 + oi];
@@ -249,7 +242,7 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
                         const uint32_t nE = rc.y & 0x3FFFFFFFu;
                         if (off < nE) {
                             const uint32_t q = rc.x + off;
-                            part[bb] = in.md_list[q];
+                            part[bb] = in.lst[q];
                             wv[bb] = rc.y >> 30;
                             if constexpr (STRICT) {
                                 const uint4 sr = X.srec[oi];
@@ -257,18 +250,18 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
                                 const uint32_t nmd = in.bkt_nmd[hb], nst = in.bkt_nst[hb];
                                 const unsigned long long within =
                                     (unsigned long long)(sr.y >> 31) * nst * nmd +
-                                    (unsigned long long)(sr.y & 0x7FFFFFFFu) * nmd + in.md_idx[q];
+                                    (unsigned long long)(sr.y & 0x7FFFFFFFu) * nmd + in.lidx[q];
                                 rk[bb] = ((unsigned long long)in.bkt_rank[hb] << 37) | within;
                             }
                         } else {
                             const uint32_t q = rc.z + (off - nE);
-                            part[bb] = in.ed_list[q];
+                            part[bb] = in.lst[q];
                             wv[bb] = 1;
                             if constexpr (STRICT) {
                                 const uint4 sr = X.srec[oi];
                                 const uint32_t hb = sr.x;
                                 const uint32_t nmd = in.bkt_nmd[hb], nst = in.bkt_nst[hb];
-                                const uint32_t pe = in.ed_idx[q];
+                                const uint32_t pe = in.lidx[q];
                                 const unsigned long long within =
                                     (unsigned long long)(pe >> 31) * nst * nmd +
                                     (unsigned long long)(pe & 0x7FFFFFFFu) * nmd + sr.z;
@@ -439,7 +432,7 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_multi_kernel(EmitParams
             uint32_t tot = 0;
             if (oi < cn) {
                 const uint64_t g = g0 + c0 + oi;
-                const uint4 rc = load_rec(in.rec + g);
+                const uint4 rc = load_rec(in, g);
                 S.rec[oi] = rc;
                 tot = (rc.y & 0x3FFFFFFFu) + rc.w;
                 uint32_t lo = ra, hi = rb;  // owning read: largest r with occ_off[r] <= g
@@ -491,10 +484,10 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_multi_kernel(EmitParams
                         const uint32_t nE = rc.y & 0x3FFFFFFFu;
                         own[bb] = S.aid[oi];
                         if (off < nE) {
-                            part[bb] = in.md_list[rc.x + off];
+                            part[bb] = in.lst[rc.x + off];
                             wv[bb] = rc.y >> 30;
                         } else {
-                            part[bb] = in.ed_list[rc.z + (off - nE)];
+                            part[bb] = in.lst[rc.z + (off - nE)];
                             wv[bb] = 1;
                         }
                     }

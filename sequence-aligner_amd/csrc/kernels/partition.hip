@@ -7,14 +7,17 @@
 //   1. bitonic-sorts its records by (key = mix << lb | locrank, g),
 //   2. finds bucket heads (new hash) and group heads (new hash or loc),
 //   3. scans middle flags / edge-role counts, last bucket/group head, next group head,
-//   4. writes the middle and edge lists (read index per entry) into the
-//      partition's slice of the list arrays (md at ps + i, edge at 2 ps + i: no
-//      global scan needed), and one 16-byte record per k-mer, scattered to its
-//      occurrence index g:
-//        {md_lo, nE | me << 30, ed_lo, nD}
-//      edge role partners  = md entries of the bucket with loc <  own: [md_lo, md_lo + nE)
-//      middle role partners = edge entries of the bucket with loc <= own: [ed_lo, ed_lo + nD)
+//   4. writes each bucket's slice of the combined partner list (read index per
+//      entry) into the partition's slice lst[3 ps, 3 ps + 3 n) (no global scan
+//      needed), middle entries loc-descending before the split point c, edge
+//      roles loc-ascending after it (sa_internal.h), and one 8-byte record per
+//      k-mer, scattered to its occurrence index g: {c, nE | nD << 15 | me << 30}
+//      edge role partners  = md entries of the bucket with loc <  own: [c - nE, c)
+//      middle role partners = edge entries of the bucket with loc <= own: [c, c + nD)
 //      (addKmerPair's orientation rule, KmerTable.scala:65-71: fst = larger loc, tie -> middle)
+//      The scattered store is what this kernel spends most of its time on (a
+//      random 16-byte store over 778 MB costs 1.57 ms at the bench shape, an
+//      8-byte one over 389 MB 0.89 ms: tools/scatter_probe.hip), hence 8 bytes.
 // Strict mode also writes the (read,pos)-order list indices calcPairData's
 // traversal order is built from, per-bucket |st|, |md| and first occurrence.
 // Partitions larger than the LDS capacity take the global scan path
@@ -39,18 +42,9 @@ __device__ __forceinline__ uint32_t read_of_g(uint32_t g, const uint64_t *occ_of
     return lo;
 }
 
-// SA_PB_SKNT (compile knob, default 1): read the sorted 8-byte records (read once per
-// pass) with non-temporal loads, leaving L2 to merge the scattered record stores.
-#ifndef SA_PB_SKNT
-#define SA_PB_SKNT 1
-#endif
-__device__ __forceinline__ uint64_t load_sk(const uint64_t *p) {
-#if SA_PB_SKNT
-    return __builtin_nontemporal_load(p);
-#else
-    return *p;
-#endif
-}
+// the sorted 8-byte records are read once: non-temporal loads keep them out of
+// L2, which is left to merge the scattered record stores
+__device__ __forceinline__ uint64_t load_sk(const uint64_t *p) { return __builtin_nontemporal_load(p); }
 
 // sort key (mix << lb | loc rank) and occurrence index of an 8-byte record
 __device__ __forceinline__ unsigned long long record_key(uint64_t rec, const PartArgs &A, uint32_t &g) {
@@ -137,7 +131,7 @@ struct PartShared {
         };
     };
     uint32_t red[3][4];
-    uint32_t lbh[4], lgh[4];
+    uint32_t lbh[4], lgh[4], lnb[4];
 };
 static_assert(sizeof(PartShared<1024>) <= 20480, "1,024-record block must fit 8 per CU");
 
@@ -238,7 +232,7 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
     const int lb = A.lb;
     const unsigned long long lbm = (1ull << lb) - 1;
     const uint32_t b0 = tid * IT;
-    uint32_t md_c = 0, ed_c = 0, last_bh = 0, last_gh = 0, first_gh = 0xFFFFFFFFu;
+    uint32_t md_c = 0, ed_c = 0, last_bh = 0, last_gh = 0, first_gh = 0xFFFFFFFFu, first_bh = 0xFFFFFFFFu;
     bool any_bh = false, any_gh = false;
     uint32_t tagv[IT];
 #pragma unroll
@@ -253,7 +247,7 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
             const bool gh = s == 0 || S.key[s - 1] != k;
             md_c += (t & TAG_MD) ? 1u : 0u;
             ed_c += ((t & TAG_ST) ? 1u : 0u) + ((t & TAG_EN) ? 1u : 0u);
-            if (bh) { last_bh = s; any_bh = true; }
+            if (bh) { last_bh = s; any_bh = true; if (first_bh == 0xFFFFFFFFu) first_bh = s; }
             if (gh) { last_gh = s; any_gh = true; if (first_gh == 0xFFFFFFFFu) first_gh = s; }
         }
     }
@@ -263,6 +257,7 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
     const uint32_t bh_in = blk_excl_max(any_bh ? last_bh : 0u, S.red[2]);  // element 0 is always a head
     const uint32_t gh_in = blk_excl_max(any_gh ? last_gh : 0u, S.lbh);
     const uint32_t gh_next = min(blk_excl_suffix_min(first_gh, S.lgh), n);
+    const uint32_t bh_next = min(blk_excl_suffix_min(first_bh, S.lnb), n);
     // per-item exclusive counts into LDS
     {
         uint32_t m = md_ex, e = ed_ex;
@@ -277,15 +272,18 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
         if (b0 + IT == (uint32_t)CAP && n == (uint32_t)CAP) { S.mdx[CAP] = m; S.edx[CAP] = e; }
     }
     __syncthreads();
-    // next group head per item (suffix within the thread, then gh_next)
-    uint32_t nextg[IT];
+    // next group head and next bucket head per item (suffix within the thread,
+    // then gh_next / bh_next)
+    uint32_t nextg[IT], nextb[IT];
     {
-        uint32_t nx = gh_next;
+        uint32_t nx = gh_next, nb_ = bh_next;
 #pragma unroll
         for (int j = IT - 1; j >= 0; --j) {
             const uint32_t s = b0 + j;
             nextg[j] = nx;
+            nextb[j] = nb_;
             if (s < n && (s == 0 || S.key[s - 1] != S.key[s])) nx = s;
+            if (s < n && (s == 0 || (S.key[s - 1] >> lb) != (S.key[s] >> lb))) nb_ = s;
         }
     }
     // ---- outputs --------------------------------------------------------
@@ -304,14 +302,16 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
         const uint32_t g = S.g[s];
         const uint32_t r = read_of_g(g, A.occ_off, A.n_reads, A.npr, A.rid, A.g2r);
         const uint32_t st = (t & TAG_ST) ? 1u : 0u, en = (t & TAG_EN) ? 1u : 0u, md = (t & TAG_MD) ? 1u : 0u;
-        const uint32_t mpos = ps + S.mdx[s], epos = 2 * ps + S.edx[s];
-        if (md) A.md_list[mpos] = r;
-        if (st) A.ed_list[epos] = r;
-        if (en) A.ed_list[epos + st] = r;
+        // split point of the bucket [bh, nextb): its md entries end at c
+        const uint32_t c = 3 * ps + S.mdx[nextb[j]] + S.edx[bh];
+        const uint32_t mpos = c - 1u - (S.mdx[s] - S.mdx[bh]), epos = c + (S.edx[s] - S.edx[bh]);
+        if (md) A.lst[mpos] = r;
+        if (st) A.lst[epos] = r;
+        if (en) A.lst[epos + st] = r;
         const uint32_t me = st + en;
-        const uint32_t nE = me ? (S.mdx[gh] - S.mdx[bh]) : 0u;
-        const uint32_t nD = md ? (S.edx[nextg[j]] - S.edx[bh]) : 0u;
-        A.rec[g] = make_uint4(ps + S.mdx[bh], nE | (me << 30), 2 * ps + S.edx[bh], nD);
+        const uint32_t nE = me ? (S.mdx[gh] - S.mdx[bh]) : 0u;        // <= CAP: no escape here
+        const uint32_t nD = md ? (S.edx[nextg[j]] - S.edx[bh]) : 0u;  // <= 2 CAP
+        A.rec[g] = make_uint2(c, nE | (nD << 15) | (me << 30));
         if constexpr (STRICT) {
             // bucket extent [bh, be)
             uint32_t be = s + 1;
@@ -329,9 +329,9 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
                     nen += (tq & TAG_EN) ? 1u : 0u;
                 }
             }
-            if (md) A.md_idx[mpos] = nmd;
-            if (st) A.ed_idx[epos] = nst;
-            if (en) A.ed_idx[epos + st] = (1u << 31) | nen;
+            if (md) A.lidx[mpos] = nmd;
+            if (st) A.lidx[epos] = nst;
+            if (en) A.lidx[epos + st] = (1u << 31) | nen;
             A.srec[g] = make_uint4(ps + bh, st ? nst : ((1u << 31) | nen), nmd, 0u);
             if (isb) {
                 A.bkt_nst[ps + s] = st_tot;
@@ -375,12 +375,48 @@ template <int CAP>
 static size_t part_lds() { return sizeof(PartShared<CAP>); }
 
 // ---------------------------------------------------------------------------
-// big partitions: records from the global scan tables (buckets.hip) of one range
+// big partitions (global scan path, buckets.hip): the scan wrote ascending,
+// partition-relative md / edge lists (bucket b's md entries at bkt_mdo[b] ..,
+// edge entries at bkt_edo[b] ..); move them into the combined layout, bucket b's
+// split point being c_b = 3 ps + bkt_mdo[b + 1] + bkt_edo[b]
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t bucket_of_entry(const uint32_t *off, uint32_t nb, uint32_t e) {
+    uint32_t lo = 0, hi = nb;  // last b with off[b] <= e
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (off[mid] <= e) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void relayout_lists_kernel(Buckets b, uint32_t ps, const uint32_t *totals, uint32_t *lst, uint32_t *lidx) {
+    const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t nb = totals[0], n_md = totals[2], n_ed = totals[3];
+    if (e < n_md) {
+        const uint32_t bk = bucket_of_entry(b.bkt_mdo, nb, e);
+        const uint32_t q = 3 * ps + b.bkt_mdo[bk + 1] + b.bkt_edo[bk] - 1u - (e - b.bkt_mdo[bk]);
+        lst[q] = b.md_list[e];
+        if (lidx) lidx[q] = b.md_idx[e];
+    }
+    if (e < n_ed) {
+        const uint32_t bk = bucket_of_entry(b.bkt_edo, nb, e);
+        const uint32_t q = 3 * ps + b.bkt_mdo[bk + 1] + e;  // = c_b + (e - bkt_edo[bk])
+        lst[q] = b.ed_list[e];
+        if (lidx) lidx[q] = b.ed_idx[e];
+    }
+}
+
+hipError_t launch_relayout_lists(const Buckets &b, uint32_t ps, uint32_t n, const uint32_t *totals_dev,
+                                 const PartArgs &a, bool strict, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const uint32_t m = 2 * n;  // edge entries <= 2 n
+    hipLaunchKernelGGL(relayout_lists_kernel, dim3((m + 255) / 256), dim3(256), 0, s, b, ps, totals_dev, a.lst,
+                       strict ? a.lidx : nullptr);
+    return hipGetLastError();
+}
+
 __global__ void records_from_tables_kernel(const uint64_t *sk, const uint32_t *sv, uint32_t ps, uint32_t n, int lb,
-                                           const uint8_t *tagtab, Buckets b, uint4 *rec, int strict, uint4 *srec,
-                                           uint32_t *bkt_nst, uint32_t *bkt_nmd, uint32_t *bkt_first,
-                                           uint8_t *is_head) {
+                                           const uint8_t *tagtab, Buckets b, PartArgs A, int strict) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n) return;
     const uint64_t lbm = (1ull << lb) - 1;
@@ -391,21 +427,28 @@ __global__ void records_from_tables_kernel(const uint64_t *sk, const uint32_t *s
     const uint32_t st = (t & TAG_ST) ? 1u : 0u, en = (t & TAG_EN) ? 1u : 0u, md = (t & TAG_MD) ? 1u : 0u;
     const uint32_t me = st + en;
     const uint32_t mdo = b.bkt_mdo[bid], edo = b.bkt_edo[bid];
+    const uint32_t c = 3 * ps + b.bkt_mdo[bid + 1] + edo;
     const uint32_t nE = me ? (b.grp_mds[gid] - mdo) : 0u;
     const uint32_t nD = md ? (b.grp_ede[gid] - edo) : 0u;
-    rec[g] = make_uint4(ps + mdo, nE | (me << 30), 2 * ps + edo, nD);
+    if (nE <= REC_CNT_MAX && nD <= REC_CNT_MAX) {
+        A.rec[g] = make_uint2(c, nE | (nD << 15) | (me << 30));
+    } else {  // a high-copy repeat: the counts do not fit 15 bits
+        const uint32_t xi = atomicAdd(A.xrec_n, 1u);
+        A.xrec[xi] = make_uint4(c - nE, nE | (me << 30), c, nD);
+        A.rec[g] = make_uint2(c, (3u << 30) | xi);
+    }
     if (strict) {
         const uint32_t s0 = b.bkt_start[bid];
-        srec[g] = make_uint4(ps + s0, st ? b.occ_idx[3ull * g] : ((1u << 31) | b.occ_idx[3ull * g + 2]),
-                             b.occ_idx[3ull * g + 1], 0u);
+        A.srec[g] = make_uint4(ps + s0, st ? b.occ_idx[3ull * g] : ((1u << 31) | b.occ_idx[3ull * g + 2]),
+                               b.occ_idx[3ull * g + 1], 0u);
         if (s == s0) {
             const uint32_t s1 = b.bkt_start[bid + 1];
             uint32_t gmin = 0xFFFFFFFFu;
             for (uint32_t q = s0; q < s1; ++q) gmin = min(gmin, sv[ps + q]);
-            bkt_nst[ps + s] = b.bkt_nst[bid];
-            bkt_nmd[ps + s] = b.bkt_mdo[bid + 1] - mdo;
-            bkt_first[ps + s] = gmin;
-            is_head[ps + s] = 1;
+            A.bkt_nst[ps + s] = b.bkt_nst[bid];
+            A.bkt_nmd[ps + s] = b.bkt_mdo[bid + 1] - mdo;
+            A.bkt_first[ps + s] = gmin;
+            A.is_head[ps + s] = 1;
         }
     }
 }
@@ -469,12 +512,11 @@ hipError_t launch_convert_records(const uint64_t *rec8, uint32_t n, const PartAr
 }
 
 hipError_t launch_records_from_tables(const uint64_t *sk, const uint32_t *sv, uint32_t ps, uint32_t n, int lb,
-                                      const uint8_t *tagtab, const Buckets &b, uint4 *rec, int strict, uint4 *srec,
-                                      uint32_t *bkt_nst, uint32_t *bkt_nmd, uint32_t *bkt_first, uint8_t *is_head,
+                                      const uint8_t *tagtab, const Buckets &b, const PartArgs &a, int strict,
                                       hipStream_t s) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(records_from_tables_kernel, dim3((n + 255) / 256), dim3(256), 0, s, sk, sv, ps, n, lb, tagtab, b,
-                       rec, strict, srec, bkt_nst, bkt_nmd, bkt_first, is_head);
+                       a, strict);
     return hipGetLastError();
 }
 

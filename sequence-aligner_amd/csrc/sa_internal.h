@@ -45,6 +45,45 @@ __device__ __forceinline__ uint32_t mix32(uint32_t h) {
     return h;
 }
 
+// 16 codes starting at base position p of a read whose first word is `w`
+// (MSB-first window), used for hashing and diagonal compares.
+__device__ __forceinline__ uint32_t window16(const uint32_t *w, int32_t p) {
+    const uint32_t a = w[p >> 4];
+    const int s = p & 15;
+    if (s == 0) return a;
+    const uint32_t b = w[(p >> 4) + 1];
+    return (a << (2 * s)) | (b >> (32 - 2 * s));
+}
+
+// mix32(Kmer.seqHash) of the k-mer at position p (ObjectStore.scala:48-67: the
+// first min(16, k) bases, h = (h << 2) ^ code); shift = 32 - 2 min(16, k)
+__device__ __forceinline__ uint32_t kmer_mix(const uint32_t *w, int32_t p, int shift) {
+    uint32_t x = window16(w, p);
+    x = shift == 32 ? 0u : (x >> shift);
+    // HOXD order (A0 C1 G2 T3) -> seqHash order (A0 C1 T2 G3): c ^ (c >> 1)
+    x ^= (x >> 1) & 0x55555555u;
+    return mix32(x);
+}
+
+// ---- partner lists and per-occurrence records ------------------------------
+// Every bucket owns one slice of the combined partner list `lst` (read index
+// per entry), laid out around a split point c:
+//     [ middle entries, loc DEScending | edge roles (st, en), loc AScending ]
+//                                      ^ c
+// so an edge k-mer's partners as fst -- the middle entries with loc < own --
+// are [c - nE, c) and a middle k-mer's -- the edge roles with loc <= own -- are
+// [c, c + nD) (addKmerPair's orientation, KmerTable.scala:65-71; the st/md/en
+// split, :106-115).  The partition of sorted offset ps owns lst[3 ps, 3 ps + 3 n).
+// One 8-byte record per occurrence g: x = c, y = nE | nD << 15 | me << 30
+// (me = number of edge tags, 0..2).  me == 3 marks an escape: y & 0x3FFFFFFF
+// indexes the 16-byte xrec table (counts above 32,766: high-copy repeats).
+constexpr uint32_t REC_CNT_MAX = 0x7FFEu;
+__device__ __forceinline__ uint4 decode_rec(uint2 r, const uint4 *xrec) {
+    if ((r.y >> 30) == 3u) return xrec[r.y & 0x3FFFFFFFu];
+    const uint32_t nE = r.y & 0x7FFFu, nD = (r.y >> 15) & 0x7FFFu;
+    return make_uint4(r.x - nE, nE | ((r.y >> 30) << 30), r.x, nD);  // {md_lo, nE | me << 30, ed_lo, nD}
+}
+
 // Mixed read lengths: g2r[b] = the read holding occurrence b << G2R_SHIFT (the
 // largest r with occ_off[r] <= b << G2R_SHIFT), so the owner of g lies in
 // [g2r[g >> S], g2r[(g >> S) + 1]] and the binary search spans a few reads.
@@ -74,14 +113,16 @@ struct Buckets {
     uint32_t *bkt_rank = nullptr;    // [nb] KmerData iteration rank (host Trove replay)
 };
 
-// Inputs of the pair counter: one 16-byte record per k-mer occurrence g
-// {md_lo, nE | me << 30, ed_lo, nD} (partition.hip) and the two partner lists.
+// Inputs of the pair counter: the 8-byte record of every k-mer occurrence g
+// (decode_rec -> {md_lo, nE | me << 30, ed_lo, nD}) and the combined list.
 struct PairIn {
-    const uint4 *rec;
-    const uint32_t *md_list, *ed_list;
+    const uint2 *rec;
+    const uint4 *xrec;
+    const uint32_t *lst;
     // strict mode
     const uint4 *srec;          // {bucket head position, own_e, own_m, 0}
-    const uint32_t *md_idx, *ed_idx;
+    const uint32_t *lidx;       // per list entry: md -> index in the bucket's (id,pos)-ordered md list;
+                                // edge -> (phase << 31) | index in its st (0) / en (1) list
     const uint32_t *bkt_nst, *bkt_nmd, *bkt_rank;  // indexed by bucket head position
 };
 
@@ -182,14 +223,16 @@ struct PartArgs {
     const int32_t *len;
     const uint32_t *lbase, *lrank;
     int32_t k;
-    uint32_t *md_list, *ed_list;
-    uint4 *rec;                  // [n_occ] by g
+    uint32_t *lst;               // combined partner list [3 n]
+    uint2 *rec;                  // [n_occ] by g
+    uint4 *xrec;                 // escape records (big partitions only)
+    uint32_t *xrec_n;
     uint32_t *big_list, *big_n;  // partitions above 4,096 records (global path)
     uint32_t *mid_list, *mid_n;    // partitions above 1,024 records (2,048-record LDS pass)
     uint32_t *mid2_list, *mid2_n;  // partitions above 2,048 records (4,096-record LDS pass)
     unsigned long long *counts;  // [2][NSHARD]: buckets, groups
     // strict
-    uint32_t *md_idx, *ed_idx;   // parallel to lists
+    uint32_t *lidx;              // parallel to lst
     uint4 *srec;                 // [n_occ] by g
     uint32_t *bkt_nst, *bkt_nmd, *bkt_first;  // at bucket head sorted positions
     uint8_t *is_head;            // [n] head flags
@@ -200,9 +243,13 @@ hipError_t launch_part_build(const PartArgs &a, bool strict, hipStream_t s);
 // 8-byte records of one big partition -> (mix << lb | locrank, g) for the global scan path
 hipError_t launch_convert_records(const uint64_t *rec8, uint32_t n, const PartArgs &a, uint64_t *okeys,
                                   uint32_t *ovals, hipStream_t s);
+// big partition at sorted offset ps: its temporary (ascending, partition-
+// relative) md / edge lists of the global scan moved into the combined layout
+// (and the strict list indices with them), then the per-occurrence records
+hipError_t launch_relayout_lists(const Buckets &b, uint32_t ps, uint32_t n, const uint32_t *totals_dev,
+                                 const PartArgs &a, bool strict, hipStream_t s);
 hipError_t launch_records_from_tables(const uint64_t *sk, const uint32_t *sv, uint32_t ps, uint32_t n, int lb,
-                                      const uint8_t *tagtab, const Buckets &b, uint4 *rec, int strict, uint4 *srec,
-                                      uint32_t *bkt_nst, uint32_t *bkt_nmd, uint32_t *bkt_first, uint8_t *is_head,
+                                      const uint8_t *tagtab, const Buckets &b, const PartArgs &a, int strict,
                                       hipStream_t s);
 
 // compact the NSHARD output regions into sort keys (vals = region-space index)
