@@ -13,16 +13,21 @@ pairs per second summed over ranks.  The end-to-end config (banded HOXD
 dovetail alignment of every dispatched pair) is timed in a second loop and
 reported as aligned_read_pairs_per_s.
 
-Multi-GPU: one process per GPU (torchrun), backend "nccl"
-(RCCL over xGMI).  Weak scaling: the genome grows with the GPU count (20x
-coverage kept), each rank holds 100,000 reads of it (global ids by rank), and
-a step is the SHARDED hash stage -- local k-mer emit, all-to-all of the
-records to the rank owning their hash range, bucket build + partial pair
-counts there, all-to-all of the partials to the rank owning the lead,
-reduce + collision filter (sharded.py).  Reads are all-gathered once for the
-alignment of each rank's own leads.  Barrier + max-over-ranks timing;
-`value` sums the role pairs over all ranks.  `--replicas` runs independent
-per-rank datasets instead (no exchange), for comparison.
+Multi-GPU: the sharded context of libsa_overlap
+(include/sa_overlap.h, multi.cpp) -- local k-mer emit, RCCL all-to-all of the
+records to the shard owning their hash range, bucket build + partial pair
+counts there, RCCL all-to-all of the partials to the shard owning the lead,
+reduce + collision filter; the packed reads are all-gathered once for the
+alignment of each shard's own leads.  Weak scaling: the genome grows with the
+GPU count (20x coverage kept) and every GPU holds 100,000 reads of it.
+  torchrun --nproc-per-node N bench.py --gpus N   one process per GPU
+      (sa_ctx_create_rank; the RCCL unique id and the barrier / max-over-ranks
+      timing go over a gloo process group on the host);
+  bench.py --gpus N                              one process driving devices
+      0..N-1 (sa_ctx_create_multi), one host thread per device.
+`value` sums the role pairs over all GPUs.  `--shards S` runs S virtual shards
+on one GPU (the exchanges as device copies); `--replicas` (torchrun) runs
+independent per-rank datasets with no exchange, for comparison.
 """
 import argparse
 import json
@@ -81,30 +86,56 @@ def synth_workload(n_reads, read_len, genome_len, gc, seed, shard=0, min_len=Non
     return genome[starts[read_of] + pos], offsets
 
 
-def pmc_traffic(kernels):
-    """HBM bytes per step of the named kernels (substrings) from the newest
-    committed PMC summary (profiles/*/pmc_summary_*.csv, written from separate
-    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench by
-    tools_profile.sh): sum of (FETCH_SIZE + WRITE_SIZE) KiB x 1024 per
-    dispatch, uncorrected."""
+def pmc_summary():
+    """Per-kernel counter averages of the newest committed PMC summary
+    (profiles/<round>/pmc_summary*.csv, written by tools/pmc_summary.py from
+    separate rocprofv3 --pmc passes of this bench, tools_profile.sh)."""
     import csv
     import glob
-    def natural(path):  # pmc_summary_v9 < pmc_summary_v10
+
+    def natural(path):  # r02 after r01, pmc_summary_v9 < pmc_summary_v10
         return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", path)]
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary_*.csv")), key=natural)
-    for path in reversed(files):
-        with open(path) as f:
-            rows = list(csv.DictReader(f))
-        tot, found = 0.0, 0
-        for kname in kernels:
-            for row in rows:
-                if kname in row["kernel"] and row.get("FETCH_SIZE_avg") and row.get("WRITE_SIZE_avg"):
-                    tot += (float(row["FETCH_SIZE_avg"]) + float(row["WRITE_SIZE_avg"])) * 1024.0
-                    found += 1
-                    break
-        if found == len(kernels):
-            return int(tot), os.path.relpath(path, ROOT)
-    return None, None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary*.csv")), key=natural)
+    if not files:
+        return {}, None
+    with open(files[-1]) as f:
+        rows = {r["kernel"]: r for r in csv.DictReader(f)}
+    return rows, os.path.relpath(files[-1], ROOT)
+
+
+def pmc_sum(rows, kernels, col):
+    """Sum over the named kernels (name prefixes) of one counter's per-dispatch
+    average; None if a kernel or the counter is missing."""
+    tot = 0.0
+    for kname in kernels:
+        hit = [r for k, r in rows.items() if k.startswith(kname) and r.get(col)]
+        if not hit:
+            return None
+        tot += float(hit[0][col])
+    return tot
+
+
+def hbm_traffic(rows, kernels):
+    """HBM bytes per launch of the named kernels from the PMC passes, corrected
+    as MI355X_MICROARCH.md's HBM section prescribes: FETCH_SIZE reports half the
+    bytes of coalesced streaming reads on gfx950 (x2), WRITE_SIZE as is (both in
+    KiB).  Raw values kept beside it: these kernels' accesses are 8-byte records
+    and 4-byte gathers, which the guide leaves uncalibrated."""
+    f = pmc_sum(rows, kernels, "FETCH_SIZE_avg")
+    w = pmc_sum(rows, kernels, "WRITE_SIZE_avg")
+    if f is None or w is None:
+        return None, None, None
+    return int((2 * f + w) * 1024), int(f * 1024), int(w * 1024)
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def dist_env():
@@ -133,48 +164,57 @@ def main():
                     help="also time --quadratic-align (full-matrix local alignment) over the same dispatch")
     ap.add_argument("--align-kernel", type=int, default=0,
                     help="SA_OPT_ALIGN_KERNEL: 0 auto, 1 lane-group (LDS), 2 lane-per-pair")
-    ap.add_argument("--replicas", action="store_true", help="N>1: independent per-rank datasets, no exchange")
-    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) or gloo (host-staged, testing)")
+    ap.add_argument("--replicas", action="store_true", help="torchrun: independent per-rank datasets, no exchange")
+    ap.add_argument("--shards", type=int, default=1, help="virtual shards on one GPU (sharded path, device copies)")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
+    if ws > 1 and args.gpus not in (1, ws):
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE %d" % (args.gpus, ws))
+    n_gpus = ws if ws > 1 else args.gpus
+    # rank: one process per GPU (torchrun); process: one process over n_gpus
+    # devices; virtual: --shards on one GPU; replicas / single: no exchange
+    mode = ("replicas" if args.replicas else "rank") if ws > 1 else (
+        "process" if args.gpus > 1 else "virtual" if args.shards > 1 else "single")
     dist = None
-    sharded = ws > 1 and not args.replicas
     if ws > 1:
         import torch
         import torch.distributed as dist_
         dist = dist_
-        ndev = torch.cuda.device_count()
-        local = local % max(ndev, 1)  # (gloo tests may run several ranks on one GPU)
+        local = local % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local)
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(args.dist_backend)
+        # host-side group: RCCL unique id broadcast, barriers, max-over-ranks
+        # timing; the data path's collectives are RCCL inside libsa_overlap
+        dist.init_process_group("gloo")
 
     import saoverlap as sao
 
     mean_len = args.len if args.min_len is None else (args.len + args.min_len) / 2.0
     G = int(args.reads * mean_len / args.coverage)
-    if sharded:
-        # one genome for all ranks (G per GPU, weak scaling), rank r's reads are
+    common = dict(timing=True, kmer_size=args.k, id_mode=sao.SA_IDS_WIDE, align_kernel=args.align_kernel)
+    sharded = mode in ("rank", "process", "virtual")
+    if mode == "rank":
+        # one genome for all ranks (G per GPU, weak scaling); rank r's reads are
         # global ids r*reads+1 .. (r+1)*reads
         bases, offsets = synth_workload(args.reads, args.len, G * ws, args.gc, seed=1, shard=rank,
                                         min_len=args.min_len)
+        uid = [sao.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        ov = sao.Overlapper(device=local, rank=rank, nranks=ws, rccl_id=uid[0], **common)
+        ov.add_packed(bases.tobytes(), offsets)
+    elif mode in ("process", "virtual"):
+        P = n_gpus if mode == "process" else args.shards
+        ov = sao.Overlapper(gpus=n_gpus, shards=P, **common)
+        for r in range(P):  # the same reads the torchrun ranks would hold, in rank order
+            b_r, o_r = synth_workload(args.reads, args.len, G * P, args.gc, seed=1, shard=r, min_len=args.min_len)
+            ov.add_packed(b_r.tobytes(), o_r)
     else:
         bases, offsets = synth_workload(args.reads, args.len, G, args.gc, seed=1 + rank, min_len=args.min_len)
-    ov = sao.Overlapper(device=local if ws > 1 else 0, timing=True, kmer_size=args.k,
-                        id_mode=sao.SA_IDS_WIDE, align_kernel=args.align_kernel)
-    ov.add_packed(bases.tobytes(), offsets)
-    so = None
-    if sharded:
-        from sharded import HipWorker, ShardedOverlapper
-        starts = np.arange(ws + 1, dtype=np.int64) * args.reads
-        lengths = np.concatenate([synth_lengths(args.reads, args.len, args.min_len, 1, r)
-                                  for r in range(ws)]).astype(np.int32)
-        so = ShardedOverlapper(HipWorker(ov), rank, ws, starts, lengths, "cuda:%d" % local)
-    build_step = so.build if so is not None else ov.device_build
-    red_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
+        ov = sao.Overlapper(device=local if ws > 1 else 0, **common)
+        ov.add_packed(bases.tobytes(), offsets)
+    if mode in ("process", "virtual"):  # one shard's reads (the per-GPU byte model)
+        offsets = np.concatenate([[0], np.cumsum(synth_lengths(args.reads, args.len, args.min_len, 1, 0))])
+    build_step = ov.device_build
 
     def barrier():
         if dist is not None:
@@ -186,7 +226,7 @@ def main():
         if dist is None:
             return x
         import torch
-        t = torch.tensor([x], dtype=torch.float64, device=red_dev)
+        t = torch.tensor([x], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -194,7 +234,7 @@ def main():
         if dist is None:
             return x
         import torch
-        t = torch.tensor([x], dtype=torch.float64, device=red_dev)
+        t = torch.tensor([x], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return float(t.item())
 
@@ -203,7 +243,7 @@ def main():
     for _ in range(args.warmup):
         build_step()
     ov.reset_stage_times()
-    xb0 = so.exchanged_bytes if so is not None else 0
+    xb0 = ov.exchanged_bytes()
     barrier()
     ov.sync()
     t0 = time.perf_counter()
@@ -219,16 +259,14 @@ def main():
 
     # ---- end-to-end incl. banded HOXD alignment (configs[2]) --------------
     asteps = args.align_steps if args.align_steps is not None else max(1, args.steps // 2)
-    xbytes = (so.exchanged_bytes - xb0) / max(args.steps, 1) if so is not None else 0
-    t_gather = None
-    if so is not None:  # the reads every rank needs to align its own leads
-        barrier()
-        t0 = time.perf_counter()
-        so.gather_reads()
-        ov.sync()
-        barrier()
-        t_gather = max_over_ranks(time.perf_counter() - t0)
+    xbytes = (ov.exchanged_bytes() - xb0) / max(args.steps, 1)
+    # first align of a sharded context all-gathers the packed reads: timed apart
+    barrier()
+    t0 = time.perf_counter()
     ov.device_align()
+    ov.sync()
+    barrier()
+    t_gather = max_over_ranks(time.perf_counter() - t0) if sharded else None
     ov.reset_stage_times()
     barrier()
     ov.sync()
@@ -264,54 +302,77 @@ def main():
                 "gcups": round(sum_over_ranks(float(qst["dp_cells"])) * args.quadratic_steps / t_quad / 1e9, 1)}
         ov.set_aligner(sao.SA_ALIGNER_LINEAR)
 
-    # ---- roofline of the dominant hash-stage kernel ----------------------
-    # By time the bucket build dominates the step: part_bounds + part_build<1024>
-    # + part_build<2048> + part_build<4096> (the "buckets" stage, one HIP-event scope).  Algorithmic
-    # HBM bytes per step: per k-mer 8 B (record load) + 16 B
-    # (partner record store), + 4 B per partner-list entry (st/md/en tags of
-    # every position: E2 cut table for each read length).  The partition starts
-    # are binary searches (np log2 n cached loads), not a pass over the records.
-    f32 = np.float32
-    edge, center = f32(0.4), f32(0.4)
-    lens_here = np.diff(offsets.astype(np.int64))
-    list_entries = 0.0
-    for L, nL in zip(*np.unique(lens_here, return_counts=True)):
-        d = int(L) - args.k
-        if d <= 0:
-            continue
-        loc = np.arange(d + 1, dtype=np.float32) / np.float32(d)
-        tags = ((loc <= edge).astype(np.int64) + ((f32(0.5) - center * f32(0.5) <= loc) &
-                (loc <= f32(0.5) + center * f32(0.5))).astype(np.int64) + (f32(1.0) - edge <= loc).astype(np.int64))
-        list_entries += float(nL) * float(tags.sum())
-    if sharded:  # this rank builds the buckets it owns: ~1/ws of all k-mers
-        list_entries *= st["kmers"] / max(1.0, float(np.sum(np.maximum(lens_here - args.k + 1, 0))))
-    bk_ms, bk_n = stages["buckets"]
-    bk_avg_ms = bk_ms / max(bk_n, 1)
-    bk_bytes = 24.0 * st["kmers"] + 4.0 * list_entries
-    bk_ach = bk_bytes / (bk_avg_ms * 1e-3) / 1e9 if bk_avg_ms > 0 else 0.0
-    bk_traffic, bk_src = pmc_traffic(("part_bounds_kernel", "part_build_kernel<1024", "part_build_kernel<2048", "part_build_kernel<4096"))
-    roofline = {"bound": "hbm", "achieved": round(bk_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(bk_ach / HBM_PEAK_GBS, 4), "traffic": bk_traffic,
-                "kernel": "bucket build: part_bounds + part_build<1024|2048|4096>",
-                "launch_ms": round(bk_avg_ms, 4), "algorithmic_bytes_per_launch": int(bk_bytes),
-                "traffic_source": bk_src}
-    # the candidate counter itself (the metric's unit is its work):
-    # per k-mer 8 B (record) + 4 B per role pair (partner id) + 12 B per dispatched pair
-    pc_ms, pc_n = stages["pairs"]
-    pc_avg_ms = pc_ms / max(pc_n, 1)
-    alg_bytes = 8.0 * st["kmers"] + 4.0 * st["role_pairs"] + 12.0 * st["dispatched"]
-    achieved = alg_bytes / (pc_avg_ms * 1e-3) / 1e9 if pc_avg_ms > 0 else 0.0
-    traffic, tsrc = pmc_traffic(("pair_count_kernel<false",))
-    roofline_pc = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                   "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                   "kernel": "pair_count_kernel<false, 256>", "launch_ms": round(pc_avg_ms, 4),
-                   "algorithmic_bytes_per_launch": int(alg_bytes), "traffic_source": tsrc}
+    # ---- rooflines --------------------------------------
+    # Units of ONE GPU's share of the step (rank mode: this rank's; one process
+    # over P shards: the total / P).  Config-2 byte model: N*L/4 (2-bit packed
+    # reads) + 32 B per k-mer occurrence (8 emit write + 16 bucket-build read +
+    # write + 8 pairing read) + 16 B per distinct ordered read pair (count write
+    # + read); role pairs are aggregated on chip and cost no HBM bytes.
+    P_here = 1 if mode in ("rank", "single", "replicas") else (n_gpus if mode == "process" else args.shards)
+    kmers_g = st["kmers"] / P_here
+    pairs_g = st["pairs"] / P_here
+    bases_g = float(offsets[-1])
+    step_bytes = bases_g / 4.0 + 32.0 * kmers_g + 16.0 * pairs_g
+    rows, pmc_src = pmc_summary()
+    ms_step = t_build / args.steps * 1e3
 
-    # ---- CPU baseline: the C oracle (port of the reference), 1 thread -----
+    def roof(bytes_, ms, kernels, name):
+        ach = bytes_ / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+        tr, fr, wr = hbm_traffic(rows, kernels) if kernels else (None, None, None)
+        return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr, "kernel": name, "launch_ms": round(ms, 4),
+                "algorithmic_bytes_per_launch": int(bytes_), "traffic_fetch_raw": fr, "traffic_write_raw": wr,
+                "traffic_source": pmc_src if tr is not None else None}
+
+    def per_launch(stage):
+        ms_, n_ = stages[stage]
+        return ms_ / max(n_, 1)
+
+    # dominant kernel by time: the bucket build (part_bounds + part_build at the
+    # 1,024 / 2,048 / 4,096-record tiers, one HIP-event scope on the library's
+    # stream); 16 B per k-mer in the model
+    bk_kernels = ("sa::part_bounds_kernel", "void sa::part_build_kernel<1024", "void sa::part_build_kernel<2048",
+                  "void sa::part_build_kernel<4096")
+    roofline = roof(16.0 * kmers_g, per_launch("buckets"), bk_kernels,
+                    "bucket build: part_bounds + part_build<1024|2048|4096>")
+    roofline_pc = roof(8.0 * kmers_g + 16.0 * pairs_g, per_launch("pairs"), ("void sa::pair_count_kernel<false, 256",),
+                       "pair_count_kernel<false, 256>")
+    pc_conf = pmc_sum(rows, ("void sa::pair_count_kernel<false, 256",), "SQ_LDS_BANK_CONFLICT_avg")
+    pc_act = pmc_sum(rows, ("void sa::pair_count_kernel<false, 256",), "SQ_LDS_IDX_ACTIVE_avg")
+    roofline_pc["lds_bank_conflict_rate"] = round(pc_conf / pc_act, 4) if pc_conf is not None and pc_act else None
+    roofline_step = roof(step_bytes, ms_step, None, "whole hash step (every kernel, wall clock)")
+    # the aligner (configs[2]): integer VALU, MFMA unused.  Peak = 256 CUs x 4
+    # SIMD-32 x 32 lanes x 2.4 GHz = 78.6 T lane-ops/s (a wave64 VALU op issues
+    # over 2 cycles, MI355X_MICROARCH.md).  achieved = measured SQ_INSTS_VALU of
+    # the dovetail kernels x 64 lanes / their event time; nominal = SURVEY.md
+    # 8(d)'s 18 int32 ops per DP cell.
+    VALU_PEAK = 256 * 4 * 32 * 2.4e9 / 1e12
+    al_ms = astages["align"][0] / max(astages["align"][1], 1)
+    cells_g = ast["dp_cells"] / P_here
+    valu = pmc_sum(rows, ("void sa::dovetail_p1_kernel<16, true>", "void sa::dovetail_p2tb_kernel<16, true>"),
+                   "SQ_INSTS_VALU_avg")
+    valu_ach = valu * 64 / (al_ms * 1e-3) / 1e12 if valu is not None and al_ms > 0 else None
+    roofline_align = {"bound": "valu", "unit": "T lane-ops/s", "peak": round(VALU_PEAK, 1),
+                      "achieved": round(valu_ach, 2) if valu_ach is not None else None,
+                      "frac": round(valu_ach / VALU_PEAK, 4) if valu_ach is not None else None,
+                      "kernel": "dovetail_p1<16> + dovetail_p2tb<16> (+ phase-2 pair regrouping sort)",
+                      "launch_ms": round(al_ms, 4), "dp_cells_per_launch": int(cells_g),
+                      "nominal_18_ops_per_cell": round(18.0 * cells_g / (al_ms * 1e-3) / 1e12, 2) if al_ms else None,
+                      "valu_wave_insts_per_launch": int(valu) if valu is not None else None,
+                      "lds_bank_conflict_rate": "n/a: the lane kernels keep the band in registers (no LDS)",
+                      "source": pmc_src if valu is not None else None}
+    grp_conf = pmc_sum(rows, ("void sa::dovetail_kernel",), "SQ_LDS_BANK_CONFLICT_avg")
+    grp_act = pmc_sum(rows, ("void sa::dovetail_kernel",), "SQ_LDS_IDX_ACTIVE_avg")
+    if grp_conf is not None and grp_act:
+        roofline_align["lds_bank_conflict_rate_group_kernel"] = round(grp_conf / grp_act, 4)
+
+    # ---- CPU baselines (rank 0, N = 1): the C oracle on this box's cores ---
     cpu = None
-    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+    config0 = None
+    if rank == 0 and n_gpus == 1 and mode == "single" and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
+        cores_all = oracle.max_threads()
         n_s = args.cpu_sample_reads
         G_s = int(n_s * args.len / args.coverage)
         b_s, o_s = synth_workload(n_s, args.len, G_s, args.gc, seed=1)
@@ -324,47 +385,97 @@ def main():
         ovs.add_packed(b_s.tobytes(), o_s)
         ovs.build()
         rp_s = ovs.stats()["role_pairs"]
-        assert len(r.lead) == ovs.stats()["dispatched"], "CPU/GPU candidate mismatch on the baseline sample"
+        lead_s, trail_s, _ = ovs.dispatch()
+        assert np.array_equal(r.lead, lead_s) and np.array_equal(r.trail, trail_s), \
+            "CPU/GPU dispatch mismatch on the baseline sample"
+        # aligner: the same dispatch (first pairs of it), 1 thread and all threads,
+        # each tuple checked against the GPU's
+        ovs.align()
+        gal = ovs.alignments()
+        na1, naa = min(len(lead_s), 20000), min(len(lead_s), 200000)
+        b_bytes = b_s.tobytes()
+        t0 = time.perf_counter()
+        c1 = oracle.align_batch(b_bytes, o_s, lead_s[:na1], trail_s[:na1], settings=s, threads=1)
+        t_a1 = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        ca = oracle.align_batch(b_bytes, o_s, lead_s[:naa], trail_s[:naa], settings=s, threads=0)
+        t_aa = time.perf_counter() - t0
+        for name in ("start_i", "start_j", "end_i", "end_j", "correct", "error", "ahg", "bhg"):
+            assert np.array_equal(ca[:, oracle.ALIGN_FIELDS.index(name)],
+                                  gal[:naa, sao.ALIGN_FIELDS.index(name)]), "CPU/GPU alignment mismatch: " + name
         ovs.close()
         cpu = {"value": round(rp_s / t_cpu, 1), "unit": "candidate k-mer pairs/s", "cores": 1, "kind": "port",
                "sample": "%d reads x %d bp, %d bp genome (same 20x coverage), k=%d, hash stage "
-                         "(KmerTable.calcPairData+calcDispatchData restated in C, wide ids), %.1f s"
-                         % (n_s, args.len, G_s, args.k, t_cpu)}
+                         "(KmerTable.calcPairData + calcDispatchData restated in C, one thread: the reference's "
+                         "KmerTable is single-writer), %.1f s; dispatch equal to the GPU's"
+                         % (n_s, args.len, G_s, args.k, t_cpu),
+               "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+               "align": {"unit": "aligned read-pairs/s", "kind": "port",
+                         "value_1_thread": round(na1 / t_a1, 1), "value_all_threads": round(naa / t_aa, 1),
+                         "threads_all": cores_all,
+                         "sample": "first %d / %d dispatched pairs of the sample, generateFastDovetailAlignment"
+                                   "Set restated in C (OpenMP over pairs, as genBlockMTAlign's actor pool); "
+                                   "%.1f s / %.1f s; tuples equal to the GPU's" % (na1, naa, t_a1, t_aa)}}
+        # configs[0]: reconstructed c_ruddii reads (32,000 x 100 bp, ids in .seq
+        # order), k = 15, strict ids, whole calc-overlaps path -> .ovl bytes
+        z = np.load(os.path.join(ROOT, "tests", "golden", "c_ruddii_layout.npz"))
+        contig = z["contig"].tobytes()
+        cr = [contig[o:o + 100] for o in z["offset"][1:]]
+        t0 = time.perf_counter()
+        rc0 = oracle.Run(reads=cr, settings=oracle.default_settings(kmer_size=15))
+        t_c0 = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        o0 = sao.Overlapper(kmer_size=15)
+        o0.add_reads(cr)
+        o0.build()
+        o0.align()
+        g_ovl = o0.ovl()
+        t_g0 = time.perf_counter() - t0
+        o0.close()
+        config0 = {"workload": "configs[0]: c_ruddii reconstructed 32,000 x 100 bp reads, k=15, strict ids, "
+                               "FASTA reads in host memory -> .ovl bytes",
+                   "cpu_port_1_thread_s": round(t_c0, 3), "gpu_end_to_end_s": round(t_g0, 4),
+                   "ovl_records": g_ovl.count(b"{OVL"), "ovl_identical": g_ovl == rc0.ovl}
 
     if rank == 0:
         line = {
             "metric": "candidate k-mer pairs/sec (hash stage) + aligned read-pairs/sec, k=15, 500 bp reads",
             "value": round(value, 1),
             "unit": "candidate k-mer pairs/s",
-            "n_gpus": ws,
+            "n_gpus": n_gpus,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(t_build / args.steps * 1e3, 3),
+            "ms_per_step": round(ms_step, 3),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int32",
-            "data": "synthetic (splitmix64 genome, error-free 500 bp reads)",
+            "data": "synthetic (splitmix64 genome, error-free reads)",
             "config": {"workload": "configs[1]: %dk synthetic %s bp reads/GPU, k=%d, bucket build + "
                                    "edge/middle pair filter" % (args.reads // 1000, (
                                        "%d" % args.len if args.min_len is None else
                                        "%d-%d" % (args.min_len, args.len)), args.k),
                        "reads_per_gpu": args.reads, "read_len": args.len, "min_len": args.min_len, "k": args.k,
                        "genome_bp_per_gpu": G, "ids": "wide",
-                       "parallelism": ("sharded-a2a-%s" % args.dist_backend if sharded else
-                                       "replicas" if ws > 1 else "single")},
+                       "parallelism": {"rank": "rccl-a2a, one process per GPU", "process":
+                                       "rccl-a2a, one process over %d devices" % n_gpus,
+                                       "virtual": "%d virtual shards on one GPU" % args.shards,
+                                       "replicas": "replicas (no exchange)", "single": "single"}[mode]},
             "aligned_read_pairs_per_s": round(aligned_total / t_align, 1),
             "ms_per_align_step": round(t_align / asteps * 1e3, 3),
             "per_gpu": {k: int(v) for k, v in st.items() if k not in ("aligned", "ovl_records", "dp_cells")},
             "dp_cells_per_align_step": int(ast["dp_cells"]),
             "stage_ms_per_step": {k: round(v[0] / max(args.steps, 1), 4) for k, v in stages.items() if v[1]},
-            "align_kernel_ms": round(astages["align"][0] / max(astages["align"][1], 1), 4),
+            "align_kernel_ms": round(al_ms, 4),
             "quadratic_align": quad,
             "roofline": roofline,
+            "roofline_step": roofline_step,
             "roofline_pair_count": roofline_pc,
-            "exchange_bytes_per_step_rank0": int(xbytes) if sharded else None,
+            "roofline_align": roofline_align,
+            "exchange_bytes_per_step": int(xbytes) if sharded else None,
             "read_allgather_ms": round(t_gather * 1e3, 3) if t_gather is not None else None,
             "cpu_baseline": cpu,
+            "config0": config0,
         }
         print(json.dumps(line), flush=True)
     ov.close()

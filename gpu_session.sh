@@ -13,14 +13,11 @@ step() {  # step <name> <seconds> <cmd...>
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = tests ]; then
     step smoke 240 python __graft_entry__.py smoke
-    step gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+    step gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
     step bench 600 python bench.py --steps 10 --warmup 2
 fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
-    cd /tmp && export TMPDIR=/tmp
-    step_dir=$GRAFT_REPO_ROOT/gpurun_out
-    timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $step_dir/prof -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 1 --no-cpu-baseline --quadratic-steps 1 > $step_dir/prof.log 2>&1
-    echo "prof rc=$?" >> $step_dir/steps.txt
+    bash tools_profile.sh
 fi

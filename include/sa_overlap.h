@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define SA_ABI_VERSION 1
+#define SA_ABI_VERSION 2
 
 enum sa_status {
     SA_OK = 0,
@@ -177,7 +177,9 @@ int sa_get_stats(const sa_ctx *ctx, sa_stats *out);
 /* Per-stage device time accumulated since the last reset (SA_OPT_TIMING). */
 enum sa_stage {
     SA_STAGE_PACK = 0, SA_STAGE_EMIT, SA_STAGE_SORT, SA_STAGE_BUCKETS, SA_STAGE_PAIRS,
-    SA_STAGE_ORDER, SA_STAGE_ALIGN, SA_NUM_STAGES
+    SA_STAGE_ORDER, SA_STAGE_ALIGN,
+    SA_STAGE_EXCHANGE,  /* sharded contexts: inter-shard exchanges (host wall clock) */
+    SA_NUM_STAGES
 };
 int sa_get_stage_times(const sa_ctx *ctx, double *ms, uint64_t *launches, int n);
 int sa_reset_stage_times(sa_ctx *ctx);
@@ -188,7 +190,48 @@ int sa_device_build(sa_ctx *ctx);   /* == sa_build_candidates without host readb
 int sa_device_align(sa_ctx *ctx);   /* == sa_align without host readback */
 int sa_sync(sa_ctx *ctx);
 
-/* ---- Sharded hash stage, one process (context) per GPU ----
+/* ---- Sharded contexts: `--gpus P` ---------------------
+ * One context over P shards of the read set: read ids are split into P
+ * contiguous ranges; every shard emits its k-mers, an all-to-all sends each
+ * record to the shard owning its hash range, that shard builds its buckets and
+ * counts partial (lead, trail) pairs, a second all-to-all sends the partials to
+ * the shard owning the lead, which sums them and applies [min, max]; for
+ * alignment the 2-bit packed reads are all-gathered once and every shard aligns
+ * its own leads.  Every call above works on a sharded context, and dispatch,
+ * alignments and .ovl bytes are identical to a single-device context's for any
+ * P (the shards' outputs, concatenated in descending shard order).  The
+ * reference is one JVM process (Project4.scala:517-563, :725-790): sharding
+ * has no reference counterpart beyond reproducing its output.
+ * Inputs in the reference's own id domain (strict ids, < 32,768 reads) need one
+ * PairData table for the Trove order: a sharded context runs them unsharded on
+ * its first device.  SA_OPT_KEEP_PAIRS is refused on a sharded build. */
+
+/* One process, devices 0 .. n_gpus-1 with one shard each (n_shards == n_gpus),
+ * exchanges over RCCL (send/recv groups over xGMI), or n_gpus == 1 with
+ * n_shards virtual shards on device 0 exchanged in HBM (the sharded path on one
+ * GPU).  n_shards is a power of two <= 256.  Replaces the reference's
+ * single-process genMTKmerTable / genBlockMTAlign drivers (Project4.scala:531-563,
+ * :725-790) under `sa-overlap --gpus P`. */
+int sa_ctx_create_multi(const sa_settings *s, int n_gpus, int n_shards, sa_ctx **out);
+
+/* One process per GPU (e.g. launched by torchrun): rank `rank` of `nranks`
+ * (power of two), joined by an RCCL unique id that one rank creates with
+ * sa_rccl_unique_id and the caller broadcasts.  Each rank adds only its own
+ * reads; ranks hold consecutive id ranges in rank order.  sa_build_candidates,
+ * sa_device_build, sa_align, sa_device_align and sa_write_ovl are collective
+ * (every rank calls them); sa_get_dispatch / sa_get_alignments / sa_get_ovl /
+ * sa_get_stats cover this rank's leads; sa_write_ovl writes all ranks' records
+ * from rank 0.  Wide ids only (SA_IDS_STRICT is refused). */
+#define SA_RCCL_ID_BYTES 128
+int sa_rccl_unique_id(void *id, size_t cap);
+int sa_ctx_create_rank(const sa_settings *s, int device, int rank, int nranks, const void *id, sa_ctx **out);
+/* Bytes this process's shards sent to other shards (exchanges 1 and 2, read
+ * all-gather) since the context was created. */
+uint64_t sa_exchanged_bytes(const sa_ctx *ctx);
+
+/* ---- Per-shard entry points, one process (context) per GPU ----
+ * What a sharded context runs on each shard; exposed for callers that move the
+ * data between ranks themselves (e.g. with torch.distributed).
  * Rank r holds reads [starts[r], starts[r+1]) of the global read set (0-based,
  * global id = index + 1), added to its context with sa_add_reads as usual.
  * The caller moves data between ranks (all-to-all / all-gather, e.g. with

@@ -70,6 +70,9 @@ def lib():
                                      P(Settings), P(Align)]
         L.orc_align_pair_local.argtypes = L.orc_align_pair.argtypes
         L.orc_trove_order.argtypes = [P(C.c_int32), C.c_size_t, P(C.c_int32), P(C.c_int32)]
+        L.orc_align_batch.argtypes = [C.c_char_p, P(C.c_uint64), C.c_uint32, P(C.c_int32), P(C.c_int32), C.c_size_t,
+                                      P(Settings), C.c_int, P(Align)]
+        L.orc_max_threads.restype = C.c_int
         _lib = L
     return _lib
 
@@ -172,6 +175,27 @@ def align_pair(A, B, id_a=1, id_b=2, settings=None, quadratic=False):
     if rc:
         raise OracleError(rc)
     return {n: getattr(out, n) for n in ALIGN_FIELDS}
+
+
+def align_batch(bases, offsets, lead, trail, settings=None, threads=1):
+    """Dovetail alignments of the given pairs (ids 1-based) on `threads` OpenMP
+    threads (0 = all): the aligner leg of bench.py's CPU baseline."""
+    s = settings or default_settings()
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ld = np.ascontiguousarray(lead, dtype=np.int32)
+    tr = np.ascontiguousarray(trail, dtype=np.int32)
+    out = (Align * max(len(ld), 1))()
+    P = C.POINTER
+    rc = lib().orc_align_batch(bases, off.ctypes.data_as(P(C.c_uint64)), len(off) - 1, ld.ctypes.data_as(P(C.c_int32)),
+                               tr.ctypes.data_as(P(C.c_int32)), len(ld), C.byref(s), threads, out)
+    if rc:
+        raise OracleError(rc)
+    raw = np.ctypeslib.as_array(C.cast(out, P(C.c_int32)), shape=(max(len(ld), 1) * len(ALIGN_FIELDS),))
+    return raw.reshape(-1, len(ALIGN_FIELDS))[:len(ld)].copy()
+
+
+def max_threads():
+    return int(lib().orc_max_threads())
 
 
 def trove_order(keys):

@@ -4,6 +4,9 @@
  * Every function cites the Scala line range (under /root/reference/src) it follows.
  */
 #include "sa_oracle.h"
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 #include "trove_primes.h"
 
 #include <math.h>
@@ -605,6 +608,53 @@ int orc_align_pair(const char *A, int32_t la, const char *B, int32_t lb, int32_t
     if (rc == ORC_OK) judge(out, s);
     return rc;
 }
+
+/* all cores: OMP_NUM_THREADS when set (the GPU box sets it to this job's CPU
+ * share), else every processor */
+int orc_max_threads(void) {
+    const char *e = getenv("OMP_NUM_THREADS");
+    if (e && atoi(e) > 0) return atoi(e);
+#ifdef _OPENMP
+    return omp_get_num_procs();
+#else
+    return 1;
+#endif
+}
+
+/* genBlockMTAlign's alignment work over a given dispatch list (Project4.scala:
+ * 725-790 runs one future per block on the actor pool; pairs are independent):
+ * the CPU baseline of the aligner, on `threads` OpenMP threads (0 = all).  The
+ * reads are the caller's buffers (ids 1-based).  Returns the first error. */
+int orc_align_batch(const char *bases, const uint64_t *offsets, uint32_t n_reads, const int32_t *lead,
+                    const int32_t *trail, size_t n_pairs, const orc_settings *s, int threads, orc_align_t *out) {
+    int err = ORC_OK;
+    /* an explicit team size: omp_set_num_threads would leave the caller's
+     * default changed for every later call (a 1-thread run then an all-core
+     * run would both use one thread) */
+    const int nt = threads > 0 ? threads : orc_max_threads();
+    (void)nt;
+#pragma omp parallel num_threads(nt)
+    {
+        dp_buf b = {0};
+#pragma omp for schedule(dynamic, 256)
+        for (size_t i = 0; i < n_pairs; ++i) {
+            const uint32_t a = (uint32_t)lead[i] - 1u, t = (uint32_t)trail[i] - 1u;
+            int rc = ORC_E_INPUT;
+            if (a < n_reads && t < n_reads) {
+                rc = align_one(&b, bases + offsets[a], (int32_t)(offsets[a + 1] - offsets[a]), bases + offsets[t],
+                               (int32_t)(offsets[t + 1] - offsets[t]), lead[i], trail[i], s, &out[i]);
+                if (rc == ORC_OK) judge(&out[i], s);
+            }
+            if (rc != ORC_OK) {
+#pragma omp critical
+                if (err == ORC_OK) err = rc;
+            }
+        }
+        free(b.M); free(b.X); free(b.Y);
+    }
+    return err;
+}
+
 
 /* ------------------------------------------------------------------------ */
 /* the calc-overlaps path                                                    */

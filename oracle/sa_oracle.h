@@ -104,6 +104,13 @@ size_t orc_ovl(const orc_ctx *c, const char **text);
 int orc_align_pair(const char *A, int32_t len_a, const char *B, int32_t len_b,
                    int32_t id_a, int32_t id_b, const orc_settings *s, orc_align_t *out);
 
+/* The dovetail aligner over a dispatch list on `threads` OpenMP threads (0 =
+ * all): the aligner leg of the CPU baseline (genBlockMTAlign's actor pool,
+ * Project4.scala:725-790; pairs are independent). */
+int orc_align_batch(const char *bases, const uint64_t *offsets, uint32_t n_reads, const int32_t *lead,
+                    const int32_t *trail, size_t n_pairs, const orc_settings *s, int threads, orc_align_t *out);
+int orc_max_threads(void);
+
 /* One full-matrix local alignment (BioLibs.scala:267-368 for one trailer). */
 int orc_align_pair_local(const char *A, int32_t len_a, const char *B, int32_t len_b,
                          int32_t id_a, int32_t id_b, const orc_settings *s, orc_align_t *out);

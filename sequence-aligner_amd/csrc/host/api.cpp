@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "../sa_internal.h"
+#include "ctx.h"
 #include "trove.h"
 
 namespace sa {
@@ -35,109 +36,6 @@ hipError_t launch_bucket_first(const uint64_t *skeys, const uint32_t *svals, con
 }  // namespace sa
 
 using namespace sa;
-
-namespace {
-
-struct DBuf {
-    void *p = nullptr;
-    size_t bytes = 0;
-};
-
-// device-resident counters, one memset per build; the hot ones are NSHARD-way
-// sharded (see sa_internal.h) and summed here
-struct Counters {
-    unsigned long long cursor[NSHARD];
-    unsigned long long role_pairs[NSHARD];
-    unsigned long long role_pairs_dummy[NSHARD];
-    unsigned long long distinct[NSHARD];
-    unsigned long long cells[NSHARD];
-    unsigned long long bkt_counts[2 * NSHARD];
-    uint32_t overflow_n;
-    int32_t err;
-    uint32_t totals[4];
-    uint32_t big_n;
-    uint32_t mid_n;
-    uint32_t mid2_n;
-    uint32_t xrec_n;     // escape records written (big partitions)
-    uint32_t shard_off[NSHARD + 2];
-};
-
-unsigned long long shard_sum(const unsigned long long *v) {
-    unsigned long long t = 0;
-    for (int i = 0; i < NSHARD; ++i) t += v[i];
-    return t;
-}
-
-}  // namespace
-
-struct sa_ctx {
-    sa_settings set{};
-    int device = 0;
-    hipStream_t stream = nullptr;
-    std::string err;
-    // reads (host)
-    std::vector<char> bases;
-    std::vector<uint64_t> boff{0};
-    bool reads_dirty = true, uploaded = false;
-    // derived (host)
-    std::vector<int32_t> len;
-    std::vector<uint64_t> woff, occ_off;
-    std::vector<uint32_t> g2r;  // coarse occurrence -> read table (sa_internal.h, G2R_SHIFT)
-    std::vector<uint32_t> lbase, lrank;
-    std::vector<uint8_t> tagtab;
-    int lb = 1, m = 0, maxd = 0, maxL = 0, minL = 0;
-    uint32_t uniform_npr = 0;
-    uint64_t n_occ = 0, n_words = 0;
-    uint32_t max_occ = 0;
-    int32_t mode = SA_IDS_WIDE;
-    // device buffers
-    DBuf d_ascii, d_boff, d_woff, d_len, d_codes, d_bad, d_occ_off, d_lbase, d_lrank, d_tagtab, d_g2r;
-    DBuf d_keys, d_vals, d_keys2, d_vals2, d_sorttmp;
-    DBuf d_md, d_ed, d_bmdo, d_bedo, d_bstart, d_gbid, d_gmds, d_gede, d_ogid, d_bkttmp;
-    DBuf d_mdidx, d_edidx, d_occidx, d_bnst, d_brank, d_bhash, d_bfirst;
-    DBuf d_pstart, d_biglist, d_rec, d_srec, d_bnmd, d_ishead, d_bnst2;
-    DBuf d_tmd, d_ted, d_tmdi, d_tedi, d_xrec;  // big-partition scratch lists, escape records
-    uint32_t *bkt_rank_dev = nullptr;
-    DBuf d_pf, d_ps, d_pc, d_pr, d_ovl, d_cnt;
-    DBuf d_okeys, d_ovals, d_okeys2, d_ovals2, d_osort;
-    DBuf d_lead, d_trail, d_count, d_aln, d_p1, d_tb, d_ltb, d_lmax;
-    DBuf d_rkey, d_rkey2, d_rord, d_rord2, d_rtmp;
-    uint64_t pair_cap = 0;
-    uint64_t n_disp = 0;
-    // distributed mode (sa_dist_*): this rank's slice of a global read set
-    bool dist = false, dist_reads = false;
-    int rank = 0, nranks = 1, log_ranks = 0;
-    std::vector<uint32_t> dstarts;   // [nranks+1] first global read of each rank
-    std::vector<int32_t> dlen;       // length of every global read
-    std::vector<uint64_t> gocc;      // global occurrence offsets [N+1]
-    uint32_t gnpr = 0;               // uniform k-mers per read over all reads (0: mixed)
-    int32_t gmaxL = 0, gminL = 0;
-    uint64_t part_np = 0;            // partial pairs after sa_dist_count
-    uint32_t *part_perm = nullptr;   // their ascending-lead order (region-space indices)
-    DBuf d_gocc, d_rid, d_loff, d_starts, d_bounds, d_gcodes, d_gwoff, d_glen, d_gbad, d_psum, d_pkeep, d_ppos;
-    DBuf d_scan, d_lr, d_bigtot, d_items;
-    // k-mer table statistics (sa_kmer_histogram)
-    DBuf d_hk0, d_hk1, d_hflag, d_hidx, d_hpos, d_htmp, d_hist, d_hovf, d_hsmall;
-    std::vector<uint64_t> hsize, hcount;
-    // options / state
-    bool keep_pairs = false, timing = false;
-    int align_kernel = 0;  // SA_OPT_ALIGN_KERNEL
-    int aligner = SA_ALIGNER_LINEAR;  // SA_OPT_ALIGNER (--linear-align / --quadratic-align)
-    uint64_t local_batch_bytes = 16ull << 30;  // traceback-code budget of one quadratic launch
-    bool built = false, aligned = false;
-    // results (host)
-    std::vector<int32_t> lead, trail, count;
-    std::vector<int32_t> pfst, psnd, pcnt;
-    std::vector<sa_alignment> alns;
-    std::string ovl;
-    sa_stats stats{};
-    // timing
-    struct Pending { int stage; hipEvent_t a, b; };
-    std::vector<Pending> pending;
-    std::vector<hipEvent_t> ev_pool;
-    double stage_ms[SA_NUM_STAGES] = {0};
-    uint64_t stage_n[SA_NUM_STAGES] = {0};
-};
 
 namespace {
 
@@ -1050,6 +948,16 @@ int device_align(sa_ctx *c, bool readback) {
 
 }  // namespace
 
+int single_build(sa_ctx *c, bool readback) {
+    (void)hipSetDevice(c->device);
+    return device_build(c, readback);
+}
+
+int single_align(sa_ctx *c, bool readback) {
+    (void)hipSetDevice(c->device);
+    return device_align(c, readback);
+}
+
 // ===========================================================================
 // C ABI
 // ===========================================================================
@@ -1095,6 +1003,7 @@ int sa_ctx_create(const sa_settings *s, int device, sa_ctx **out) {
 
 void sa_ctx_destroy(sa_ctx *c) {
     if (!c) return;
+    if (c->multi) multi_destroy(c);
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     DBuf *bufs[] = {&c->d_ascii, &c->d_boff, &c->d_woff, &c->d_len, &c->d_codes, &c->d_bad, &c->d_occ_off,
@@ -1128,6 +1037,7 @@ int sa_add_reads(sa_ctx *c, const char *bases, const uint64_t *offsets, uint32_t
     for (uint32_t r = 0; r < n; ++r) c->boff.push_back(base0 + (offsets[r + 1] - offsets[0]));
     c->reads_dirty = true;
     c->built = c->aligned = false;
+    ++c->reads_gen;
     return SA_OK;
 }
 
@@ -1152,20 +1062,23 @@ int sa_get_read(const sa_ctx *c, uint32_t id, const char **seq, size_t *len) {
 
 int sa_build_candidates(sa_ctx *c) {
     if (!c) return SA_E_ARG;
-    (void)hipSetDevice(c->device);
-    return device_build(c, true);
+    if (c->multi) return multi_build(c, true, single_build);
+    return single_build(c, true);
 }
 
 int sa_device_build(sa_ctx *c) {
     if (!c) return SA_E_ARG;
-    (void)hipSetDevice(c->device);
-    return device_build(c, false);
+    if (c->multi) return multi_build(c, false, single_build);
+    return single_build(c, false);
 }
 
 int sa_get_dispatch(sa_ctx *c, const int32_t **lead, const int32_t **trail, const int32_t **count, size_t *n) {
     if (!c || !n) return SA_E_ARG;
     if (!c->built) return fail(c, SA_E_STATE, "no candidates built");
-    if (c->lead.size() != c->n_disp) {  // device-only build: fetch now
+    if (multi_sharded(c)) {
+        int rc = multi_dispatch(c);
+        if (rc) return rc;
+    } else if (c->lead.size() != c->n_disp) {  // device-only build: fetch now
         c->lead.resize(c->n_disp); c->trail.resize(c->n_disp); c->count.resize(c->n_disp);
         if (c->n_disp) {
             HIPCHK(hipMemcpy(c->lead.data(), c->d_lead.p, c->n_disp * 4, hipMemcpyDeviceToHost));
@@ -1243,20 +1156,23 @@ int sa_get_pairs(sa_ctx *c, const int32_t **fst, const int32_t **snd, const int3
 
 int sa_align(sa_ctx *c) {
     if (!c) return SA_E_ARG;
-    (void)hipSetDevice(c->device);
-    return device_align(c, true);
+    if (c->multi) return multi_align(c, true, single_align);
+    return single_align(c, true);
 }
 
 int sa_device_align(sa_ctx *c) {
     if (!c) return SA_E_ARG;
-    (void)hipSetDevice(c->device);
-    return device_align(c, false);
+    if (c->multi) return multi_align(c, false, single_align);
+    return single_align(c, false);
 }
 
 int sa_get_alignments(sa_ctx *c, const sa_alignment **out, size_t *n) {
     if (!c || !out || !n) return SA_E_ARG;
     if (!c->aligned) return fail(c, SA_E_STATE, "no alignments");
-    if (c->alns.size() != c->n_disp) {
+    if (multi_sharded(c)) {
+        int rc = multi_alignments(c);
+        if (rc) return rc;
+    } else if (c->alns.size() != c->n_disp) {
         c->alns.resize(c->n_disp);
         if (c->n_disp)
             HIPCHK(hipMemcpy(c->alns.data(), c->d_aln.p, c->n_disp * sizeof(sa_alignment), hipMemcpyDeviceToHost));
@@ -1277,34 +1193,43 @@ int sa_get_ovl(sa_ctx *c, const char **text, size_t *len) {
 int sa_write_ovl(sa_ctx *c, const char *path) {
     if (!c) return SA_E_ARG;
     if (!c->aligned) return fail(c, SA_E_STATE, "no alignments");
+    const std::string *text = &c->ovl;
+    std::string all;
+    if (multi_rank_mode(c)) {  // collective: rank 0 writes every rank's records
+        int rc = multi_gather_ovl(c, all);
+        if (rc) return rc;
+        if (multi_rank(c) != 0) return SA_OK;
+        text = &all;
+    }
     FILE *f = path ? fopen(path, "wb") : stdout;  // the file is deleted and recreated (Project4.scala:797-805)
     if (!f) return fail(c, SA_E_INPUT, std::string("cannot write ") + path);
-    const size_t w = fwrite(c->ovl.data(), 1, c->ovl.size(), f);
+    const size_t w = fwrite(text->data(), 1, text->size(), f);
     if (path) fclose(f); else fflush(f);
-    return w == c->ovl.size() ? SA_OK : fail(c, SA_E_INPUT, "short write");
+    return w == text->size() ? SA_OK : fail(c, SA_E_INPUT, "short write");
 }
 
 int sa_set_option(sa_ctx *c, int option, int64_t value) {
     if (!c) return SA_E_ARG;
     switch (option) {
-    case SA_OPT_KEEP_PAIRS: c->keep_pairs = value != 0; return SA_OK;
-    case SA_OPT_TIMING: c->timing = value != 0; return SA_OK;
+    case SA_OPT_KEEP_PAIRS: c->keep_pairs = value != 0; break;
+    case SA_OPT_TIMING: c->timing = value != 0; break;
     case SA_OPT_ALIGN_KERNEL:
         if (value < 0 || value > 3) return fail(c, SA_E_ARG, "SA_OPT_ALIGN_KERNEL must be 0..3");
         c->align_kernel = (int)value;
-        return SA_OK;
+        break;
     case SA_OPT_ALIGNER:
         if (value != SA_ALIGNER_LINEAR && value != SA_ALIGNER_QUADRATIC)
             return fail(c, SA_E_ARG, "SA_OPT_ALIGNER must be SA_ALIGNER_LINEAR or SA_ALIGNER_QUADRATIC");
         c->aligner = (int)value;
         c->aligned = false;
-        return SA_OK;
+        break;
     case SA_OPT_LOCAL_BATCH_MB:
         if (value < 1) return fail(c, SA_E_ARG, "SA_OPT_LOCAL_BATCH_MB must be >= 1");
         c->local_batch_bytes = (uint64_t)value << 20;
-        return SA_OK;
+        break;
     default: return fail(c, SA_E_ARG, "unknown option");
     }
+    return c->multi ? multi_set_option(c, option, value) : SA_OK;
 }
 
 int sa_get_stats(const sa_ctx *c, sa_stats *out) {
@@ -1315,9 +1240,13 @@ int sa_get_stats(const sa_ctx *c, sa_stats *out) {
 
 int sa_get_stage_times(const sa_ctx *c, double *ms, uint64_t *launches, int n) {
     if (!c) return SA_E_ARG;
+    double m[SA_NUM_STAGES];
+    uint64_t k[SA_NUM_STAGES];
+    for (int i = 0; i < SA_NUM_STAGES; ++i) { m[i] = c->stage_ms[i]; k[i] = c->stage_n[i]; }
+    if (c->multi) multi_stage_times(c, m, k);
     for (int i = 0; i < n && i < SA_NUM_STAGES; ++i) {
-        if (ms) ms[i] = c->stage_ms[i];
-        if (launches) launches[i] = c->stage_n[i];
+        if (ms) ms[i] = m[i];
+        if (launches) launches[i] = k[i];
     }
     return SA_OK;
 }
@@ -1325,20 +1254,25 @@ int sa_get_stage_times(const sa_ctx *c, double *ms, uint64_t *launches, int n) {
 int sa_reset_stage_times(sa_ctx *c) {
     if (!c) return SA_E_ARG;
     for (int i = 0; i < SA_NUM_STAGES; ++i) { c->stage_ms[i] = 0; c->stage_n[i] = 0; }
+    if (c->multi) multi_reset_stage_times(c);
     return SA_OK;
 }
 
 int sa_sync(sa_ctx *c) {
     if (!c) return SA_E_ARG;
+    (void)hipSetDevice(c->device);
     HIPCHK(hipStreamSynchronize(c->stream));
-    return SA_OK;
+    return c->multi ? multi_sync(c) : SA_OK;
 }
+
+uint64_t sa_exchanged_bytes(const sa_ctx *c) { return c ? multi_exchanged_bytes(c) : 0; }
 
 // ---------------------------------------------------------------------------
 // sharded hash stage; the exchanges are the caller's
 // ---------------------------------------------------------------------------
 int sa_dist_init(sa_ctx *c, int rank, int nranks, const uint32_t *starts, const int32_t *lengths) {
     if (!c || !starts || !lengths) return SA_E_ARG;
+    if (c->multi) return fail(c, SA_E_STATE, "a sharded context exchanges internally (sa_dist_* are per-shard calls)");
     if (nranks < 1 || nranks > 256 || (nranks & (nranks - 1)) || rank < 0 || rank >= nranks)
         return fail(c, SA_E_ARG, "nranks must be a power of two <= 256 and 0 <= rank < nranks");
     if (c->set.id_mode == SA_IDS_STRICT) return fail(c, SA_E_ARG, "the sharded path runs in wide-id mode only");

@@ -7,7 +7,10 @@
 // The developer modes (--test-* / --bench-*, :61-98) print what Project4
 // prints, except --test-alignment / --test-overlaps (alignment strings).
 // Diagnostics go to stderr so stdout stays a clean .ovl stream.
-// Extra flags: --wide-ids / --strict-ids, --device N, --stats.
+// Extra flags: --wide-ids / --strict-ids, --device N, --stats,
+// --gpus P (one process over devices 0..P-1, one shard each, RCCL exchanges;
+// SURVEY.md 8(b)) and --shards S (S virtual shards on one device: the sharded
+// path on one GPU).  The output is identical for any P and S.
 #include <ctype.h>
 #include <math.h>
 #include <stdio.h>
@@ -89,6 +92,14 @@ static std::string java_float(float f) {
     return sign + out;
 }
 
+// --gpus / --shards: a sharded context (sa_ctx_create_multi) or one device
+static int g_gpus = 1, g_shards = 1;
+static int new_ctx(const sa_settings *s, int device, sa_ctx **ctx) {
+    if (g_gpus > 1) return sa_ctx_create_multi(s, g_gpus, g_gpus, ctx);
+    if (g_shards > 1) return sa_ctx_create_multi(s, 1, g_shards, ctx);
+    return sa_ctx_create(s, device, ctx);
+}
+
 static void die_ctx(sa_ctx *ctx, int rc) {
     fprintf(stderr, "sa-overlap: %s (%d)\n", ctx ? sa_last_error(ctx) : "error", rc);
     if (ctx) sa_ctx_destroy(ctx);
@@ -97,7 +108,7 @@ static void die_ctx(sa_ctx *ctx, int rc) {
 
 static sa_ctx *open_ctx(const sa_settings &s, int device, const std::string &input, int aligner) {
     sa_ctx *ctx = nullptr;
-    const int rc0 = sa_ctx_create(&s, device, &ctx);
+    const int rc0 = new_ctx(&s, device, &ctx);
     if (rc0 != SA_OK) {
         fprintf(stderr, "sa-overlap: no usable gfx950 device (%d)\n", rc0);
         exit(1);
@@ -126,7 +137,7 @@ static int mode_test_fasta_read(const sa_settings &s, int device, const std::str
 // Project4.benchFastaRead (:288-296)
 static int mode_bench_fasta_read(const sa_settings &s, int device, const std::string &input) {
     sa_ctx *ctx = nullptr;
-    if (sa_ctx_create(&s, device, &ctx) != SA_OK) {
+    if (new_ctx(&s, device, &ctx) != SA_OK) {
         fprintf(stderr, "sa-overlap: no usable gfx950 device\n");
         return 1;
     }
@@ -220,7 +231,7 @@ static int mode_bench_kmer(const sa_settings &s, int device, const std::string &
     if (!analysis) {
         for (int pass = 0; pass < 2; ++pass) {  // "sequentially", "in parellel": one device path
             sa_ctx *ctx = nullptr;
-            if (sa_ctx_create(&s, device, &ctx) != SA_OK) {
+            if (new_ctx(&s, device, &ctx) != SA_OK) {
                 fprintf(stderr, "sa-overlap: no usable gfx950 device\n");
                 return 1;
             }
@@ -356,6 +367,14 @@ int main(int argc, char **argv) {
         } else if (a == "--wide-ids") s.id_mode = SA_IDS_WIDE;
         else if (a == "--strict-ids") s.id_mode = SA_IDS_STRICT;
         else if (a == "--device") { need(&iv, nullptr); device = iv; }
+        else if (a == "--gpus" || a == "--shards") {
+            need(&iv, nullptr);
+            if (iv < 1 || iv > 256 || (iv & (iv - 1))) {
+                fprintf(stderr, "Invalid value for %s : %d (a power of two <= 256)\n", a.c_str(), iv);
+                return 1;
+            }
+            (a == "--gpus" ? g_gpus : g_shards) = iv;
+        }
         else if (a == "--stats") stats = true;
         else {
             fprintf(stderr, "Invalid Argument : %s\nExiting Program.\n", a.c_str());
@@ -385,7 +404,7 @@ int main(int argc, char **argv) {
         return 1;
     }
     sa_ctx *ctx = nullptr;
-    int rc = sa_ctx_create(&s, device, &ctx);
+    int rc = new_ctx(&s, device, &ctx);
     if (rc != SA_OK) {
         fprintf(stderr, "sa-overlap: no usable gfx950 device (%d)\n", rc);
         return 1;

@@ -1,0 +1,143 @@
+// ctx.h -- the library context (struct sa_ctx behind include/sa_overlap.h) and
+// host helpers shared by api.cpp (one device) and multi.cpp (sharded contexts).
+#pragma once
+#include "../../../include/sa_overlap.h"
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../sa_internal.h"
+
+struct sa_multi;
+
+namespace sa {
+
+struct DBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+};
+
+// device-resident counters, one memset per build; the hot ones are NSHARD-way
+// sharded (see sa_internal.h) and summed here
+struct Counters {
+    unsigned long long cursor[NSHARD];
+    unsigned long long role_pairs[NSHARD];
+    unsigned long long role_pairs_dummy[NSHARD];
+    unsigned long long distinct[NSHARD];
+    unsigned long long cells[NSHARD];
+    unsigned long long bkt_counts[2 * NSHARD];
+    uint32_t overflow_n;
+    int32_t err;
+    uint32_t totals[4];
+    uint32_t big_n;
+    uint32_t mid_n;
+    uint32_t mid2_n;
+    uint32_t xrec_n;     // escape records written (big partitions)
+    uint32_t shard_off[NSHARD + 2];
+};
+
+inline unsigned long long shard_sum(const unsigned long long *v) {
+    unsigned long long t = 0;
+    for (int i = 0; i < NSHARD; ++i) t += v[i];
+    return t;
+}
+
+}  // namespace sa
+
+using sa::DBuf;
+
+struct sa_ctx {
+    // sharded context (sa_ctx_create_multi / sa_ctx_create_rank): its shards and
+    // exchanges (multi.cpp); null for a plain single-device context
+    sa_multi *multi = nullptr;
+    uint64_t reads_gen = 0;  // bumped by every sa_add_reads (shards re-split on change)
+    sa_settings set{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // reads (host)
+    std::vector<char> bases;
+    std::vector<uint64_t> boff{0};
+    bool reads_dirty = true, uploaded = false;
+    // derived (host)
+    std::vector<int32_t> len;
+    std::vector<uint64_t> woff, occ_off;
+    std::vector<uint32_t> g2r;  // coarse occurrence -> read table (sa_internal.h, G2R_SHIFT)
+    std::vector<uint32_t> lbase, lrank;
+    std::vector<uint8_t> tagtab;
+    int lb = 1, m = 0, maxd = 0, maxL = 0, minL = 0;
+    uint32_t uniform_npr = 0;
+    uint64_t n_occ = 0, n_words = 0;
+    uint32_t max_occ = 0;
+    int32_t mode = SA_IDS_WIDE;
+    // device buffers
+    DBuf d_ascii, d_boff, d_woff, d_len, d_codes, d_bad, d_occ_off, d_lbase, d_lrank, d_tagtab, d_g2r;
+    DBuf d_keys, d_vals, d_keys2, d_vals2, d_sorttmp;
+    DBuf d_md, d_ed, d_bmdo, d_bedo, d_bstart, d_gbid, d_gmds, d_gede, d_ogid, d_bkttmp;
+    DBuf d_mdidx, d_edidx, d_occidx, d_bnst, d_brank, d_bhash, d_bfirst;
+    DBuf d_pstart, d_biglist, d_rec, d_srec, d_bnmd, d_ishead, d_bnst2;
+    DBuf d_tmd, d_ted, d_tmdi, d_tedi, d_xrec;  // big-partition scratch lists, escape records
+    uint32_t *bkt_rank_dev = nullptr;
+    DBuf d_pf, d_ps, d_pc, d_pr, d_ovl, d_cnt;
+    DBuf d_okeys, d_ovals, d_okeys2, d_ovals2, d_osort;
+    DBuf d_lead, d_trail, d_count, d_aln, d_p1, d_tb, d_ltb, d_lmax;
+    DBuf d_rkey, d_rkey2, d_rord, d_rord2, d_rtmp;
+    uint64_t pair_cap = 0;
+    uint64_t n_disp = 0;
+    // distributed mode (sa_dist_*): this rank's slice of a global read set
+    bool dist = false, dist_reads = false;
+    int rank = 0, nranks = 1, log_ranks = 0;
+    std::vector<uint32_t> dstarts;   // [nranks+1] first global read of each rank
+    std::vector<int32_t> dlen;       // length of every global read
+    std::vector<uint64_t> gocc;      // global occurrence offsets [N+1]
+    uint32_t gnpr = 0;               // uniform k-mers per read over all reads (0: mixed)
+    int32_t gmaxL = 0, gminL = 0;
+    uint64_t part_np = 0;            // partial pairs after sa_dist_count
+    uint32_t *part_perm = nullptr;   // their ascending-lead order (region-space indices)
+    DBuf d_gocc, d_rid, d_loff, d_starts, d_bounds, d_gcodes, d_gwoff, d_glen, d_gbad, d_psum, d_pkeep, d_ppos;
+    DBuf d_scan, d_lr, d_bigtot, d_items;
+    // k-mer table statistics (sa_kmer_histogram)
+    DBuf d_hk0, d_hk1, d_hflag, d_hidx, d_hpos, d_htmp, d_hist, d_hovf, d_hsmall;
+    std::vector<uint64_t> hsize, hcount;
+    // options / state
+    bool keep_pairs = false, timing = false;
+    int align_kernel = 0;  // SA_OPT_ALIGN_KERNEL
+    int aligner = SA_ALIGNER_LINEAR;  // SA_OPT_ALIGNER (--linear-align / --quadratic-align)
+    uint64_t local_batch_bytes = 16ull << 30;  // traceback-code budget of one quadratic launch
+    bool built = false, aligned = false;
+    // results (host)
+    std::vector<int32_t> lead, trail, count;
+    std::vector<int32_t> pfst, psnd, pcnt;
+    std::vector<sa_alignment> alns;
+    std::string ovl;
+    sa_stats stats{};
+    // timing
+    struct Pending { int stage; hipEvent_t a, b; };
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> ev_pool;
+    double stage_ms[SA_NUM_STAGES] = {0};
+    uint64_t stage_n[SA_NUM_STAGES] = {0};
+};
+
+// sharded contexts (multi.cpp); api.cpp routes the public calls of a context
+// with c->multi here.  single_build / single_align run the one-device path on
+// the context itself (strict-id inputs of a multi context).
+namespace sa {
+bool multi_sharded(const sa_ctx *c);
+bool multi_rank_mode(const sa_ctx *c);
+int multi_rank(const sa_ctx *c);
+void multi_destroy(sa_ctx *c);
+int multi_build(sa_ctx *c, bool readback, int (*single_build)(sa_ctx *, bool));
+int multi_dispatch(sa_ctx *c);
+int multi_align(sa_ctx *c, bool readback, int (*single_align)(sa_ctx *, bool));
+int multi_alignments(sa_ctx *c);
+int multi_gather_ovl(sa_ctx *c, std::string &all);
+int multi_set_option(sa_ctx *c, int option, int64_t value);
+void multi_stage_times(const sa_ctx *c, double *ms, uint64_t *n);
+void multi_reset_stage_times(sa_ctx *c);
+int multi_sync(sa_ctx *c);
+uint64_t multi_exchanged_bytes(const sa_ctx *c);
+}  // namespace sa

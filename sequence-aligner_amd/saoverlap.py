@@ -25,7 +25,7 @@ SA_IDS_AUTO, SA_IDS_STRICT, SA_IDS_WIDE = 0, 1, 2
 SA_OPT_KEEP_PAIRS, SA_OPT_TIMING, SA_OPT_ALIGN_KERNEL, SA_OPT_ALIGNER, SA_OPT_LOCAL_BATCH_MB = 1, 2, 3, 4, 5
 SA_ALIGNER_LINEAR, SA_ALIGNER_QUADRATIC = 0, 1   # --linear-align / --quadratic-align
 ALIGN_AUTO, ALIGN_GROUP, ALIGN_LANE, ALIGN_LANE_SUMMARY = 0, 1, 2, 3
-STAGES = ("pack", "emit", "sort", "buckets", "pairs", "order", "align")
+STAGES = ("pack", "emit", "sort", "buckets", "pairs", "order", "align", "exchange")
 ERRORS = {-1: "SA_E_ARG", -2: "SA_E_INPUT", -3: "SA_E_NON_ACGT", -4: "SA_E_ID_RANGE", -5: "SA_E_SHORT_READ",
           -6: "SA_E_DEGENERATE", -7: "SA_E_HIP", -8: "SA_E_NOMEM", -9: "SA_E_RCCL", -10: "SA_E_STATE",
           -11: "SA_E_OVERFLOW"}
@@ -37,7 +37,9 @@ EXPORTS = ("sa_default_settings", "sa_ctx_create", "sa_ctx_destroy", "sa_last_er
            "sa_get_pairs", "sa_kmer_histogram", "sa_align", "sa_get_alignments", "sa_write_ovl", "sa_get_ovl", "sa_set_option",
            "sa_get_stats", "sa_get_stage_times", "sa_reset_stage_times", "sa_device_build", "sa_device_align",
            "sa_sync", "sa_dist_init", "sa_dist_local_kmers", "sa_dist_emit", "sa_dist_count", "sa_dist_partials",
-           "sa_dist_reduce", "sa_dist_codes", "sa_dist_set_reads")
+           "sa_dist_reduce", "sa_dist_codes", "sa_dist_set_reads", "sa_ctx_create_multi", "sa_rccl_unique_id",
+           "sa_ctx_create_rank", "sa_exchanged_bytes")
+RCCL_ID_BYTES = 128
 
 
 class Settings(C.Structure):
@@ -101,8 +103,23 @@ def lib():
         L.sa_dist_reduce.argtypes = [vp, vp, vp, vp, C.c_uint64]
         L.sa_dist_codes.argtypes = [vp, vp, vp, P(C.c_uint64)]
         L.sa_dist_set_reads.argtypes = [vp, vp, vp, C.c_uint64]
+        L.sa_ctx_create_multi.argtypes = [P(Settings), C.c_int, C.c_int, P(vp)]
+        L.sa_rccl_unique_id.argtypes = [C.c_char_p, C.c_size_t]
+        L.sa_ctx_create_rank.argtypes = [P(Settings), C.c_int, C.c_int, C.c_int, C.c_char_p, P(vp)]
+        L.sa_exchanged_bytes.argtypes = [vp]
+        L.sa_exchanged_bytes.restype = C.c_uint64
         _lib = L
     return _lib
+
+
+def rccl_unique_id():
+    """An RCCL unique id (bytes) for Overlapper(rank=..., nranks=..., rccl_id=...):
+    create it on one rank and broadcast it to the others."""
+    buf = C.create_string_buffer(RCCL_ID_BYTES)
+    rc = lib().sa_rccl_unique_id(buf, RCCL_ID_BYTES)
+    if rc:
+        raise SAError(rc, "ncclGetUniqueId failed")
+    return buf.raw
 
 
 class SAError(RuntimeError):
@@ -136,15 +153,24 @@ def _arr(ptr, n):
 
 
 class Overlapper:
-    """One context = one AlignSettings + one KmerTable on one GPU."""
+    """One context = one AlignSettings + one KmerTable, on one GPU or sharded:
+    gpus=P (devices 0..P-1, RCCL exchanges), shards=S (virtual shards on one
+    device), or rank/nranks/rccl_id (one process per GPU, collective calls)."""
 
     def __init__(self, device=0, timing=False, keep_pairs=False, align_kernel=ALIGN_AUTO,
-                 aligner=SA_ALIGNER_LINEAR, local_batch_mb=None, **kw):
+                 aligner=SA_ALIGNER_LINEAR, local_batch_mb=None, gpus=1, shards=1, rank=None, nranks=None,
+                 rccl_id=None, **kw):
         self.s = settings(**kw)
         h = C.c_void_p()
-        rc = lib().sa_ctx_create(C.byref(self.s), device, C.byref(h))
+        if rank is not None:
+            rc = lib().sa_ctx_create_rank(C.byref(self.s), device, rank, nranks, rccl_id, C.byref(h))
+        elif gpus > 1 or shards > 1:
+            rc = lib().sa_ctx_create_multi(C.byref(self.s), gpus, max(gpus, shards), C.byref(h))
+        else:
+            rc = lib().sa_ctx_create(C.byref(self.s), device, C.byref(h))
         if rc:
-            raise SAError(rc, "no usable gfx950 device %d" % device)
+            raise SAError(rc, "cannot create the context (device %d, gpus %d, shards %d, rank %s)"
+                          % (device, gpus, shards, rank))
         self.h = h
         if timing:
             self._chk(lib().sa_set_option(h, SA_OPT_TIMING, 1))
@@ -271,6 +297,10 @@ class Overlapper:
 
     def reset_stage_times(self):
         self._chk(lib().sa_reset_stage_times(self.h))
+
+    def exchanged_bytes(self):
+        """Bytes sent to other shards so far (sharded contexts)."""
+        return int(lib().sa_exchanged_bytes(self.h))
 
     # ---- sharded hash stage (include/sa_overlap.h, sa_dist_*); buffers are
     # device pointers (ints), e.g. torch_tensor.data_ptr() on this context's GPU

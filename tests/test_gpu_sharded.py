@@ -1,0 +1,155 @@
+"""Sharded contexts through the C ABI (SURVEY.md 8(b) `--gpus P`, 8(e)).  GPU only.
+
+A sharded context splits the read ids into P ranges, exchanges k-mer records
+and partial pair counts between shards and all-gathers the packed reads for
+alignment -- all inside libsa_overlap (multi.cpp).  On one MI355X the shards are
+virtual (exchanges are device copies) or a one-rank RCCL communicator (the RCCL
+send/recv path to self); the bar is the single-device output, bit for bit,
+for any P: dispatch, alignment tuples and .ovl bytes.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import helpers as H
+
+pytestmark = pytest.mark.gpu
+
+sao = pytest.importorskip("saoverlap")
+
+CLI = os.path.join(os.path.dirname(sao.__file__), "build", "sa-overlap")
+
+
+def run(reads, build_twice=False, **kw):
+    ov = sao.Overlapper(**kw)
+    ov.add_reads(reads)
+    ov.build()
+    if build_twice:
+        ov.build()  # buffers reused, shards keep their reads
+    ov.align()
+    return ov
+
+
+def assert_same(a, b):
+    for x, y in zip(a.dispatch(), b.dispatch()):
+        np.testing.assert_array_equal(x, y)
+    np.testing.assert_array_equal(a.alignments(), b.alignments())
+    assert a.ovl() == b.ovl()
+    sa, sb = a.stats(), b.stats()
+    for k in ("kmers", "buckets", "role_pairs", "pairs", "dispatched", "aligned", "ovl_records", "dp_cells"):
+        assert sa[k] == sb[k], k
+
+
+def workload(seed, repeat=False):
+    rng = np.random.default_rng(seed)
+    reads = H.mutate(H.synth_reads(1500, 300, 20000, gc=0.5, seed=seed, mixed=(250, 340)), rng, 3)
+    st = dict(kmer_size=15, min_collisions=5, id_mode=sao.SA_IDS_WIDE)
+    if repeat:  # a 15-mer in 2,400 reads: multi-read pair-count blocks overflow and recount
+        motif = "ACGTTGCAACGTAGC"
+        for i in range(2400):
+            s_ = "".join("ACGT"[x] for x in rng.integers(0, 4, 120))
+            p_ = 5 if i % 2 == 0 else 55
+            reads.append(s_[:p_] + motif + s_[p_ + 15:])
+        st["min_collisions"] = 2
+    return reads, st
+
+
+@pytest.mark.parametrize("P,repeat", [(2, False), (4, False), (8, False), (4, True)])
+def test_virtual_shards_match_single_gpu(P, repeat):
+    reads, st = workload(90 + P, repeat)
+    ref = run(reads, **st)
+    assert ref.stats()["dispatched"] > 1000
+    got = run(reads, shards=P, build_twice=True, **st)
+    assert_same(got, ref)
+    # the exchanges moved data between shards
+    assert got.exchanged_bytes() > 0
+
+
+def test_virtual_shards_device_only_path():
+    """sa_device_build / sa_device_align on a sharded context, results fetched after."""
+    reads, st = workload(97)
+    ref = run(reads, **st)
+    ov = sao.Overlapper(shards=4, timing=True, **st)
+    ov.add_reads(reads)
+    for _ in range(2):
+        ov.device_build()
+        ov.device_align()
+    for x, y in zip(ov.dispatch(), ref.dispatch()):
+        np.testing.assert_array_equal(x, y)
+    np.testing.assert_array_equal(ov.alignments(), ref.alignments())
+    t = ov.stage_times()
+    assert t["exchange"][1] > 0 and t["pairs"][1] >= 2
+
+
+def test_virtual_shards_reads_added_later():
+    """Reads added after a build are re-split over the shards."""
+    reads, st = workload(98)
+    ov = sao.Overlapper(shards=2, **st)
+    ov.add_reads(reads[:700])
+    ov.build()
+    ov.add_reads(reads[700:])
+    ov.build()
+    ov.align()
+    assert_same(ov, run(reads, **st))
+
+
+def test_sharded_strict_inputs_run_unsharded():
+    """crp177 (the reference's own id domain): a 4-shard context reproduces the
+    golden .ovl, Trove order included."""
+    ov = sao.Overlapper(shards=4, kmer_size=12)
+    ov.read_fasta(H.crp177_path())
+    ov.build()
+    ov.align()
+    assert ov.stats()["id_mode"] == sao.SA_IDS_STRICT
+    assert ov.ovl() == open(os.path.join(H.GOLDEN, "crp177_k12.ovl"), "rb").read()
+
+
+def test_rank_mode_one_rank_rccl(tmp_path):
+    """sa_ctx_create_rank with one rank: every exchange is an RCCL send/recv to
+    self, so the RCCL code path (group calls, stream hand-off, count exchange,
+    length all-gather, .ovl gather to rank 0) runs on the one GPU."""
+    reads, st = workload(99)
+    ref = run(reads, **st)
+    uid = sao.rccl_unique_id()
+    ov = sao.Overlapper(rank=0, nranks=1, rccl_id=uid, **st)
+    ov.add_reads(reads)
+    ov.build()
+    ov.build()
+    ov.align()
+    assert_same(ov, ref)
+    path = str(tmp_path / "r.ovl")
+    ov.write_ovl(path)
+    assert open(path, "rb").read() == ref.ovl()
+
+
+def test_multi_gpu_context_if_available():
+    """gpus=2 (RCCL between devices 0 and 1) where the box has them."""
+    reads, st = workload(100)
+    try:
+        ov = sao.Overlapper(gpus=2, **st)
+    except sao.SAError as e:
+        if e.name in ("SA_E_HIP", "SA_E_RCCL"):
+            pytest.skip("one GPU on this box")
+        raise
+    ov.add_reads(reads)
+    ov.build()
+    ov.align()
+    assert_same(ov, run(reads, **st))
+
+
+def test_cli_shards_match_single(tmp_path):
+    """`sa-overlap --shards 4` (and `--gpus 1`) writes the single-device bytes."""
+    reads, _ = workload(101)
+    fa = tmp_path / "reads.seq"
+    fa.write_bytes(H.reads_fasta_bytes(reads))
+    outs = []
+    for extra in ([], ["--shards", "4"], ["--gpus", "1", "--shards", "2"]):
+        o = tmp_path / ("o%d.ovl" % len(outs))
+        r = subprocess.run([CLI, "-i", str(fa), "-o", str(o), "-k", "15", "--min-collisions", "5", "--wide-ids"]
+                           + extra, capture_output=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        outs.append(o.read_bytes())
+    assert outs[0].count(b"{OVL") > 100
+    assert outs[1] == outs[0] and outs[2] == outs[0]
