@@ -1,0 +1,108 @@
+"""Parity at the BASELINE configs' own sizes.  GPU only.
+
+* configs[1]/[2]: the bench workload itself -- 100,000 synthetic 500 bp reads
+  (bench.synth_workload, seed 1, 2.5 Mbp genome), k = 15, wide ids: dispatch,
+  every alignment tuple and the .ovl bytes against the C oracle's full
+  calc-overlaps run (one core, ~1 min on the box).
+* configs[4]: mixed 100-1,000 bp reads at k = 12 and at k = 15 (its two
+  passes), which exercise the float32 loc comparison across read lengths
+  (KmerTable.scala:65) and the per-length band width (BioLibs.scala:619-620).
+* README:164-175's sample record, pinned exactly.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import helpers as H
+
+pytestmark = pytest.mark.gpu
+
+sao = pytest.importorskip("saoverlap")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402  (the bench's workload generator)
+
+ALIGN_CMP = ("start_i", "start_j", "end_i", "end_j", "correct", "error", "ahg", "bhg")
+
+# README:164-175 (the reference's documented calc-overlaps output sample)
+README_RECORD = b"{OVL\nadj:N\nrds:18,22\nscr:0\nahg:20\nbhg:20\n}\n"
+
+
+def compare(ov, r, pairs=True):
+    lead, trail, count = ov.dispatch()
+    np.testing.assert_array_equal(lead, r.lead)
+    np.testing.assert_array_equal(trail, r.trail)
+    if pairs:
+        pf, ps, pc = ov.pairs()
+        np.testing.assert_array_equal(pf, r.pair_fst)
+        np.testing.assert_array_equal(ps, r.pair_snd)
+        np.testing.assert_array_equal(pc, r.pair_cnt)
+    al = ov.alignments()
+    for name in ALIGN_CMP:
+        np.testing.assert_array_equal(al[:, sao.ALIGN_FIELDS.index(name)], r.align_field(name), err_msg=name)
+    flags = al[:, sao.ALIGN_FIELDS.index("flags")]
+    np.testing.assert_array_equal((flags & sao.FLAG_DUD) != 0, r.align_field("is_dud") != 0)
+    np.testing.assert_array_equal((flags & sao.FLAG_VALID) != 0, r.align_field("valid") != 0)
+    assert ov.ovl() == r.ovl
+
+
+def test_bench_workload_matches_oracle(oracle_mod):
+    """configs[1] + [2] at full size: 100k x 500 bp, k = 15, wide ids."""
+    b, o = bench.synth_workload(100000, 500, 2500000, 0.5, seed=1)
+    ov = sao.Overlapper(kmer_size=15, id_mode=sao.SA_IDS_WIDE)
+    ov.add_packed(b.tobytes(), o)
+    ov.build()
+    ov.align()
+    st = ov.stats()
+    assert st["kmers"] == 48600000 and st["dispatched"] > 600000
+    r = oracle_mod.Run(packed=(b.tobytes(), o), settings=oracle_mod.default_settings(kmer_size=15), wide=True)
+    compare(ov, r, pairs=False)
+    _, _, count = ov.dispatch()
+    assert ((count >= 7) & (count <= 222)).all()
+    assert st["ovl_records"] == ov.ovl().count(b"{OVL") > 100000
+
+
+@pytest.mark.parametrize("k", [15, 12])
+def test_mixed_100_1000_matches_oracle(oracle_mod, k):
+    """configs[4]'s read shape and both of its k values: 2,000 mixed 100-1,000 bp
+    reads with indels/substitutions at ~20x coverage, wide ids, every stage."""
+    rng = np.random.default_rng(400 + k)
+    reads = H.mutate(H.synth_reads(2000, 1000, 55000, gc=0.5, seed=500 + k, mixed=(100, 1000)), rng, 2)
+    st = dict(kmer_size=k, min_collisions=7)
+    r = oracle_mod.Run(reads=reads, settings=oracle_mod.default_settings(**st), wide=True)
+    ov = sao.Overlapper(keep_pairs=True, id_mode=sao.SA_IDS_WIDE, **st)
+    ov.add_reads(reads)
+    ov.build()
+    ov.align()
+    assert ov.stats()["dispatched"] > 5000
+    compare(ov, r)
+
+
+def test_mixed_lengths_dense_buckets_match_oracle(oracle_mod):
+    """configs[4]'s k = 12 pass is a bucket-density stress (~1,600 occurrences
+    per 12-mer at 50M reads).  At test size the same density comes from a
+    smaller k: k = 8 on 1,200 mixed 100-1,000 bp reads of a 2 Mbp genome
+    (~10 random collisions per 8-mer plus the true overlaps), strict ids."""
+    reads = H.synth_reads(1200, 1000, 2000000, gc=0.5, seed=808, mixed=(100, 1000))
+    st = dict(kmer_size=8, min_collisions=7, max_collisions=222)
+    r = oracle_mod.Run(reads=reads, settings=oracle_mod.default_settings(**st))
+    ov = sao.Overlapper(keep_pairs=True, id_mode=sao.SA_IDS_STRICT, **st)
+    ov.add_reads(reads)
+    ov.build()
+    ov.align()
+    assert ov.stats()["dispatched"] > 100
+    compare(ov, r)
+
+
+def test_readme_record_pinned():
+    """The README's sample {OVL} record is produced exactly by crp177 at the
+    reference defaults (k = 12), at the place the Trove order puts it."""
+    ov = sao.Overlapper()
+    ov.read_fasta(H.crp177_path())
+    ov.build()
+    ov.align()
+    out = ov.ovl()
+    assert out.count(README_RECORD) == 1
+    golden = open(os.path.join(H.GOLDEN, "crp177_k12.ovl"), "rb").read()
+    assert out.index(README_RECORD) == golden.index(README_RECORD)

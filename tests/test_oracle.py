@@ -121,6 +121,16 @@ def test_record_format_matches_readme(oracle_mod):
     assert all(pat.match(x) for x in recs)
 
 
+def test_readme_sample_record_is_produced(oracle_mod):
+    """README:164-175's sample record, exactly: crp177 at the reference defaults
+    (k = 12) produces it once, where the Scala-literal golden .ovl has it."""
+    rec = b"{OVL\nadj:N\nrds:18,22\nscr:0\nahg:20\nbhg:20\n}\n"
+    r = oracle_mod.Run(fasta=H.crp177_path())
+    assert r.ovl.count(rec) == 1
+    golden = open(os.path.join(GOLD, "crp177_k12.ovl"), "rb").read()
+    assert r.ovl.index(rec) == golden.index(rec)
+
+
 def test_recall_against_amos_hash_overlap(oracle_mod):
     """Set-level sanity only (not a parity gate): the AMOS overlapper's crp177.ovl
     pairs (a<b, ahg==bhg) vs ours (lead,trail) -- most true dovetails recovered."""
