@@ -472,6 +472,7 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
     P.emit_all = emit_all ? 1 : 0;
     P.strict = strict ? 1 : 0;
     P.split = 1;
+    P.coded = 0;
     P.max_occ = c->max_occ;
     P.n_items = n_items;
     P.xcd_swizzle = read_order ? 1 : 0;
@@ -490,7 +491,9 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
         ENSURE(c->d_pc, tot_cap, &O.cnt);
         O.rank = nullptr;
         if (strict) ENSURE(c->d_pr, tot_cap, &O.rank);
-        ENSURE(c->d_ovl, 3 * (uint64_t)n_items + 3, &O.overflow_list);
+        ENSURE(c->d_ovl, (uint64_t)n_items + 3, &O.overflow_list);  // reads whose table overflowed
+        ENSURE(c->d_ovlrp, (uint64_t)n_items + 3, &O.overflow_rp);  // and their role pairs
+        if (item_start) O.overflow_rp = nullptr;  // multi-read blocks: the host routes by table
         O.cursor = cnt->cursor;
         O.cap_s = cap_s;
         O.role_pairs = cnt->role_pairs;
@@ -513,48 +516,81 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
         HIPCHK(hipMemcpyAsync(cur, cnt->cursor, sizeof(cur), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipMemcpyAsync(&ovn, &cnt->overflow_n, 4, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
-        // reads whose 256-slot table overflowed (> 192 partners) are recounted
-        // with 2,048 slots; those that fill that too (> 1,536 partners: high-copy
-        // repeats) in 64 partner-residue passes of up to 1,536 partners each
-        uint32_t *list = O.overflow_list;
-        if (ovn > 0 && cur_max() <= cap_s) {
-            PairParams P1 = P;
-            P1.table = 2048;
-            P1.n_items = ovn;
-            P1.xcd_swizzle = 0;
-            PairOut O1 = O;
-            O1.role_pairs = cnt->role_pairs_dummy;
-            O1.overflow_list = list + ovn;  // keep the read list intact
+        // Reads whose 256-slot table overflowed (> 192 partners) are recounted
+        // one per block in bigger tables: 2,048 slots unless their partner count
+        // -- extrapolated from how fast the first pass filled -- is far beyond it,
+        // 16,384 slots (128 KB of
+        // LDS, wide ids) for the rest and for 2,048-slot failures, then in 8 and
+        // 64 partner-residue classes -- refining only the classes that
+        // overflowed.  Strict ids: 2,048 slots, then 64 classes.  Items are
+        // codes (read << 6 | residue class).
+        if (ovn > 0 && n_items >= (1u << 26))
+            return fail(c, SA_E_OVERFLOW, "recount tiers address reads with 26 bits");
+        std::vector<uint32_t> q_big, q_huge;
+        if (ovn > 0) {
+            std::vector<uint32_t> codes(ovn), rps(ovn, 0);
+            HIPCHK(hipMemcpy(codes.data(), O.overflow_list, (size_t)ovn * 4, hipMemcpyDeviceToHost));
+            if (O.overflow_rp) HIPCHK(hipMemcpy(rps.data(), O.overflow_rp, (size_t)ovn * 4, hipMemcpyDeviceToHost));
+            for (uint32_t i = 0; i < ovn; ++i)
+                // rps: the partner estimate; it over-reads reads whose partners
+                // recur (found early, met again later), so only a clear excess
+                // skips the 2,048-slot tier (whose overflow stops early anyway)
+                (strict || rps[i] <= 4u * 1536u ? q_big : q_huge).push_back(codes[i]);
+        }
+        // one tier over host-side items; returns its failures (codes)
+        auto run_tier = [&](int table, int split, const std::vector<uint32_t> &items,
+                            std::vector<uint32_t> &failed) -> int {
+            failed.clear();
+            if (items.empty() || cur_max() > cap_s) return SA_OK;
+            uint32_t *tl, *fl;
+            ENSURE(c->d_tier, items.size(), &tl);
+            ENSURE(c->d_ovl, items.size() + 3, &fl);  // at most one failure per item
+            HIPCHK(hipMemcpy(tl, items.data(), items.size() * 4, hipMemcpyHostToDevice));
+            PairParams PT = P;
+            PT.table = table;
+            PT.split = split;
+            PT.coded = 1;
+            PT.n_items = (uint32_t)items.size();
+            PT.xcd_swizzle = 0;
+            PairOut OT = O;
+            OT.role_pairs = cnt->role_pairs_dummy;
+            OT.overflow_list = fl;
+            OT.overflow_rp = nullptr;
             HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(uint32_t), c->stream));
             {
                 StageScope st(c, SA_STAGE_PAIRS);
-                HIPCHK(launch_pair_count(E, PI, P1, O1, list, ovn, c->stream));
+                HIPCHK(launch_pair_count(E, PI, PT, OT, tl, PT.n_items, c->stream));
             }
+            uint32_t nf = 0;
             HIPCHK(hipMemcpyAsync(cur, cnt->cursor, sizeof(cur), hipMemcpyDeviceToHost, c->stream));
-            list += ovn;
-            HIPCHK(hipMemcpyAsync(&ovn, &cnt->overflow_n, 4, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipMemcpyAsync(&nf, &cnt->overflow_n, 4, hipMemcpyDeviceToHost, c->stream));
             HIPCHK(hipStreamSynchronize(c->stream));
+            failed.resize(nf);
+            if (nf) HIPCHK(hipMemcpy(failed.data(), fl, (size_t)nf * 4, hipMemcpyDeviceToHost));
+            return SA_OK;
+        };
+        // the failed classes of a tier at split s, refined into f sub-classes
+        auto refine = [](const std::vector<uint32_t> &codes_, uint32_t s_, uint32_t f) {
+            std::vector<uint32_t> out;
+            out.reserve(codes_.size() * f);
+            for (uint32_t cd : codes_)
+                for (uint32_t j = 0; j < f; ++j) out.push_back(cd + s_ * j);
+            return out;
+        };
+        std::vector<uint32_t> failed;
+        int rc_t;
+        if ((rc_t = run_tier(2048, 1, q_big, failed))) return rc_t;
+        if (strict) {
+            if ((rc_t = run_tier(2048, 64, refine(failed, 1, 64), failed))) return rc_t;
+        } else {
+            q_huge.insert(q_huge.end(), failed.begin(), failed.end());
+            if ((rc_t = run_tier(16384, 1, q_huge, failed))) return rc_t;
+            if ((rc_t = run_tier(16384, 8, refine(failed, 1, 8), failed))) return rc_t;
+            if ((rc_t = run_tier(16384, 64, refine(failed, 8, 8), failed))) return rc_t;
         }
-        if (ovn > 0 && cur_max() <= cap_s) {
-            const uint32_t split = 64;
-            PairParams P2 = P;
-            P2.table = 2048;
-            P2.split = (int32_t)split;
-            P2.n_items = ovn * split;
-            P2.xcd_swizzle = 0;
-            PairOut O2 = O;
-            O2.role_pairs = cnt->role_pairs_dummy;
-            O2.overflow_list = list + ovn;
-            HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(uint32_t), c->stream));
-            {
-                StageScope st(c, SA_STAGE_PAIRS);
-                HIPCHK(launch_pair_count(E, PI, P2, O2, list, ovn * split, c->stream));
-            }
-            HIPCHK(hipMemcpyAsync(cur, cnt->cursor, sizeof(cur), hipMemcpyDeviceToHost, c->stream));
-            HIPCHK(hipMemcpyAsync(&ovn, &cnt->overflow_n, 4, hipMemcpyDeviceToHost, c->stream));
-            HIPCHK(hipStreamSynchronize(c->stream));
-            if (ovn) return fail(c, SA_E_OVERFLOW, "a read has more than 98,304 distinct partners");
-        }
+        if (!failed.empty() && cur_max() <= cap_s)
+            return fail(c, SA_E_OVERFLOW, strict ? "a read has more than 98,304 distinct partners"
+                                                 : "a read has more than 786,432 distinct partners");
         if (cur_max() <= cap_s) break;
         cap_s = cur_max() + cur_max() / 4 + 1024;  // grow and recount
         c->pair_cap = cap_s * NSHARD;
@@ -1014,7 +1050,7 @@ void sa_ctx_destroy(sa_ctx *c) {
                     &c->d_ovl, &c->d_cnt, &c->d_okeys, &c->d_ovals, &c->d_okeys2, &c->d_ovals2, &c->d_osort,
                     &c->d_lead, &c->d_trail, &c->d_count, &c->d_aln, &c->d_p1, &c->d_tb, &c->d_rkey, &c->d_rkey2, &c->d_rord, &c->d_rord2, &c->d_rtmp, &c->d_gocc, &c->d_rid, &c->d_loff, &c->d_starts, &c->d_bounds, &c->d_gcodes, &c->d_gwoff, &c->d_glen, &c->d_gbad, &c->d_psum, &c->d_pkeep, &c->d_ppos, &c->d_scan, &c->d_lr, &c->d_pstart, &c->d_biglist, &c->d_rec,
                     &c->d_srec, &c->d_bnmd, &c->d_ishead, &c->d_bnst2, &c->d_tmd, &c->d_ted, &c->d_tmdi,
-                    &c->d_tedi, &c->d_xrec, &c->d_items, &c->d_bigtot, &c->d_hk0, &c->d_hk1, &c->d_hflag,
+                    &c->d_tedi, &c->d_xrec, &c->d_tier, &c->d_ovlrp, &c->d_items, &c->d_bigtot, &c->d_hk0, &c->d_hk1, &c->d_hflag,
                     &c->d_hidx, &c->d_hpos, &c->d_htmp, &c->d_hist, &c->d_hovf, &c->d_hsmall, &c->d_g2r,
                     &c->d_ltb, &c->d_lmax};
     for (DBuf *b : bufs)

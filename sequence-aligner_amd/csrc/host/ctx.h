@@ -80,6 +80,7 @@ struct sa_ctx {
     DBuf d_mdidx, d_edidx, d_occidx, d_bnst, d_brank, d_bhash, d_bfirst;
     DBuf d_pstart, d_biglist, d_rec, d_srec, d_bnmd, d_ishead, d_bnst2;
     DBuf d_tmd, d_ted, d_tmdi, d_tedi, d_xrec;  // big-partition scratch lists, escape records
+    DBuf d_tier, d_ovlrp;                       // pair-count recount tier items, overflow role pairs
     uint32_t *bkt_rank_dev = nullptr;
     DBuf d_pf, d_ps, d_pc, d_pr, d_ovl, d_cnt;
     DBuf d_okeys, d_ovals, d_okeys2, d_ovals2, d_osort;

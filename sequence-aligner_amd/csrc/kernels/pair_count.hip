@@ -26,9 +26,12 @@ namespace sa {
 constexpr int PC_THREADS = SA_PC_THREADS;
 // LDS hash slots per read: a read has ~20-60 distinct partners at 20x coverage,
 // so the first pass runs a 256-slot table (small LDS -> 8 workgroups per CU);
-// reads that fill it (repeats) are re-run with 2,048 slots, then split
+// reads that fill it (repeats, random short-k collisions) are re-run with 2,048
+// slots, then 16,384 (128 KB of LDS: one workgroup per CU; wide ids only), then
+// split into partner-residue classes
 constexpr int PC_TAB_SMALL = 256;
 constexpr int PC_TAB_BIG = 2048;
+constexpr int PC_TAB_HUGE = 16384;
 constexpr int PC_CHUNK = 512;            // occurrences per pass over a read
 #ifndef SA_PC_BATCH
 #define SA_PC_BATCH 8
@@ -42,6 +45,7 @@ __device__ __forceinline__ uint4 load_rec(const PairIn &in, uint64_t g) {
     return decode_rec(make_uint2(w.x, w.y), in.xrec);
 }
 constexpr uint32_t PC_EMPTY = 0xFFFFFFFFu;
+constexpr int PC_PROBE_MAX = 256;
 
 template <int TAB>
 __device__ __forceinline__ uint32_t pc_hash(uint32_t p) {
@@ -115,7 +119,16 @@ __device__ __forceinline__ void pc_insert(PcShared<TAB> &S, PcSharedStrict<TAB> 
                                           unsigned long long rank) {
     constexpr uint32_t FILL_MAX = TAB * 3 / 4;
     uint32_t slot = pc_hash<TAB>(partner);
-    for (int probe = 0; probe < TAB; ++probe) {
+    // probe runs are bounded: at <= 3/4 load they average < 9 slots, and a run
+    // of TAB / 4 (<= PC_PROBE_MAX) only happens in a table that is (nearly) full -- it is
+    // then recounted by a bigger tier, so every insert stays O(PC_PROBE_MAX).
+    // The recount tiers (big tables, reads with thousands of partners) also
+    // stop as soon as another lane has marked the table full; the first pass
+    // does not poll (it keeps its SGPRs for the hot loop)
+    constexpr int PMAX = TAB / 4 < PC_PROBE_MAX ? TAB / 4 : PC_PROBE_MAX;
+    for (int probe = 0; probe < PMAX; ++probe) {
+        if constexpr (TAB >= PC_TAB_BIG)
+            if ((probe & 15) == 15 && ((volatile uint32_t *)&S.overflow)[0]) return;
         // a slot's key goes EMPTY -> partner once and never changes again, so a
         // plain LDS read that sees a key is final: hits (>99% of inserts -- a read
         // meets each partner in ~100 shared k-mers) take one atomic, not two, and
@@ -149,9 +162,16 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
         bid = (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);
     }
     if (bid >= p.n_items) return;  // whole block: before any barrier
-    const uint32_t item = bid / split;
-    const uint32_t residue = bid % split;
-    const uint32_t a = read_list ? read_list[item] : item;
+    // recount tiers take codes (read << 6 | residue class); the first pass reads
+    uint32_t a, residue;
+    if (p.coded) {
+        const uint32_t code = read_list[bid];
+        a = code >> 6;
+        residue = code & 63u;
+    } else {
+        a = read_list ? read_list[bid] : bid;
+        residue = 0;
+    }
 
     for (int i = tid; i < TAB; i += PC_THREADS) {
         S.key[i] = PC_EMPTY;
@@ -163,11 +183,12 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
     const uint64_t g0 = e.occ_off[a];
     const uint32_t nocc = (uint32_t)(e.occ_off[a + 1] - g0);
     unsigned long long role_pairs = 0;
+    unsigned long long x_over = ~0ull;  // role pairs enumerated when the table filled
     __syncthreads();
 
     for (uint32_t c0 = 0; c0 < nocc; c0 += PC_CHUNK) {
         const uint32_t cn = min((uint32_t)PC_CHUNK, nocc - c0);
-        // --- per-occurrence partner ranges: one coalesced 16-byte record each
+        // --- per-occurrence partner ranges: one 8-byte record each
         constexpr int PER = PC_CHUNK / PC_THREADS;
         uint32_t mytot[PER];
 #pragma unroll
@@ -201,6 +222,12 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
         //     (a few cache lines per instruction, not 64)
         for (uint32_t w0 = 0; w0 < total; w0 += PC_WIN) {
             __syncthreads();  // pref / rec written; the previous window's eo consumed
+            // an overflowed table is recounted by the next tier: skip the rest of
+            // the enumeration (the chunk totals -- role pairs -- are still summed)
+            if (S.overflow) {
+                if (x_over == ~0ull) x_over = role_pairs - total + w0;
+                break;
+            }
             static_assert(PC_WIN == 8 * PC_THREADS, "one 16-byte eo slice per thread");
             reinterpret_cast<uint4 *>(S.eo)[tid] = make_uint4(0, 0, 0, 0);
             __syncthreads();
@@ -284,44 +311,55 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
     }
 
     const uint32_t shard = blockIdx.x % NSHARD;
-    if (tid == 0 && residue == 0 && role_pairs) atomicAdd(&o.role_pairs[shard], role_pairs);
+    if (tid == 0 && role_pairs) atomicAdd(&o.role_pairs[shard], role_pairs);  // recount tiers: a dummy counter
     if (tid == 0 && !S.overflow) atomicAdd(&o.distinct[shard], (unsigned long long)S.fill);
-    if (S.overflow) {
-        if (tid == 0 && residue == 0) {
+    if (S.overflow) {  // recounted by the next tier: this read's class only
+        if (tid == 0) {
             const uint32_t at = atomicAdd(o.overflow_n, 1u);
-            o.overflow_list[at] = a;
+            o.overflow_list[at] = (a << 6) | residue;
+            // its distinct partners, extrapolated from the fill rate (FILL_MAX
+            // partners in the first x_over role pairs): the host picks the tier
+            if (o.overflow_rp) {
+                const unsigned long long x = x_over == ~0ull || x_over == 0 ? role_pairs : x_over;
+                const unsigned long long est = (unsigned long long)(TAB * 3 / 4) * role_pairs / (x ? x : 1);
+                o.overflow_rp[at] = est > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)est;
+            }
         }
         return;
     }
-    // --- emit (a, partner, count[, rank]) --------------------------------
+    // --- emit (a, partner, count[, rank]), 32 slots per thread at a time ---
     constexpr int PER = TAB / PC_THREADS;
-    uint32_t keep = 0;
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        const uint32_t sl = tid * PER + j;
-        const uint32_t c = S.cnt[sl];
-        if (S.key[sl] != PC_EMPTY && (p.emit_all || ((int32_t)c >= p.min_coll && (int32_t)c <= p.max_coll)))
-            keep |= 1u << j;
-    }
-    uint32_t total;
-    uint32_t ex = pc_block_excl_scan(__popc(keep), S.lds4, &total);
-    if (total == 0) return;
-    if (tid == 0) S.out_base = (uint32_t)atomicAdd(&o.cursor[shard], (unsigned long long)total);
-    __syncthreads();
-    const unsigned long long base = (unsigned long long)S.out_base + ex;
+    constexpr int CH = PER < 32 ? PER : 32;
     const unsigned long long region = (unsigned long long)shard * o.cap_s;
-    uint32_t k = 0;
+    for (int c0 = 0; c0 < PER; c0 += CH) {
+        uint32_t keep = 0;
 #pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        if (!(keep & (1u << j))) continue;
-        const uint32_t sl = tid * PER + j;
-        const unsigned long long lat = base + k++;
-        const unsigned long long at = region + lat;
-        if (lat < o.cap_s) {
-            o.fst[at] = a;
-            o.snd[at] = S.key[sl];
-            o.cnt[at] = S.cnt[sl];
-            if constexpr (STRICT) o.rank[at] = X.rank[sl];
+        for (int j = 0; j < CH; ++j) {
+            const uint32_t sl = tid * PER + c0 + j;
+            const uint32_t c = S.cnt[sl];
+            if (S.key[sl] != PC_EMPTY && (p.emit_all || ((int32_t)c >= p.min_coll && (int32_t)c <= p.max_coll)))
+                keep |= 1u << j;
+        }
+        uint32_t total;
+        const uint32_t ex = pc_block_excl_scan(__popc(keep), S.lds4, &total);
+        if (total == 0) continue;  // uniform: every thread sees the same total
+        if (tid == 0) S.out_base = (uint32_t)atomicAdd(&o.cursor[shard], (unsigned long long)total);
+        __syncthreads();
+        const unsigned long long base = (unsigned long long)S.out_base + ex;
+        __syncthreads();  // out_base read before the next chunk's atomic overwrites it
+        uint32_t k = 0;
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            if (!(keep & (1u << j))) continue;
+            const uint32_t sl = tid * PER + c0 + j;
+            const unsigned long long lat = base + k++;
+            const unsigned long long at = region + lat;
+            if (lat < o.cap_s) {
+                o.fst[at] = a;
+                o.snd[at] = S.key[sl];
+                o.cnt[at] = S.cnt[sl];
+                if constexpr (STRICT) o.rank[at] = X.rank[sl];
+            }
         }
     }
 }
@@ -348,13 +386,15 @@ static void pc_launch(const EmitParams &e, const PairIn &in, const PairParams &p
 hipError_t launch_pair_count(const EmitParams &e, const PairIn &in, const PairParams &p, PairOut &o,
                              const uint32_t *read_list, uint32_t n_blocks, hipStream_t s) {
     if (n_blocks == 0) return hipSuccess;
-    const bool big = p.table != PC_TAB_SMALL;
     if (p.strict) {
-        if (big) pc_launch<true, PC_TAB_BIG>(e, in, p, o, read_list, n_blocks, s);
-        else pc_launch<true, PC_TAB_SMALL>(e, in, p, o, read_list, n_blocks, s);
+        if (p.table == PC_TAB_SMALL) pc_launch<true, PC_TAB_SMALL>(e, in, p, o, read_list, n_blocks, s);
+        else if (p.table == PC_TAB_BIG) pc_launch<true, PC_TAB_BIG>(e, in, p, o, read_list, n_blocks, s);
+        else return hipErrorInvalidValue;  // strict ids stop at 2,048 slots (then split)
     } else {
-        if (big) pc_launch<false, PC_TAB_BIG>(e, in, p, o, read_list, n_blocks, s);
-        else pc_launch<false, PC_TAB_SMALL>(e, in, p, o, read_list, n_blocks, s);
+        if (p.table == PC_TAB_SMALL) pc_launch<false, PC_TAB_SMALL>(e, in, p, o, read_list, n_blocks, s);
+        else if (p.table == PC_TAB_BIG) pc_launch<false, PC_TAB_BIG>(e, in, p, o, read_list, n_blocks, s);
+        else if (p.table == PC_TAB_HUGE) pc_launch<false, PC_TAB_HUGE>(e, in, p, o, read_list, n_blocks, s);
+        else return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }
@@ -390,7 +430,7 @@ __device__ __forceinline__ uint32_t pcm_hash(unsigned long long k) {
 __device__ __forceinline__ void pcm_insert(PcmShared &S, unsigned long long key, uint32_t w) {
     constexpr uint32_t FILL_MAX = PCM_TAB * 3 / 4;
     uint32_t slot = pcm_hash(key);
-    for (int probe = 0; probe < PCM_TAB; ++probe) {
+    for (int probe = 0; probe < PC_PROBE_MAX; ++probe) {  // bounded as in pc_insert
         unsigned long long old = ((volatile unsigned long long *)S.key)[slot];  // final once set (pc_insert)
         if (old == PCM_EMPTY) old = atomicCAS(&S.key[slot], PCM_EMPTY, key);
         if (old == PCM_EMPTY || old == key) {
@@ -461,7 +501,7 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_multi_kernel(EmitParams
 
         const uint32_t per = (total + PC_THREADS - 1) / PC_THREADS;
         const uint32_t t0 = min(total, tid * per), t1 = min(total, t0 + per);
-        if (t0 < t1) {
+        if (t0 < t1 && !S.overflow) {  // (an overflowed table: totals only, the reads are recounted)
             uint32_t lo = 0, hi = cn;  // last oi with pref[oi] <= t0
             while (hi - lo > 1) {
                 const uint32_t mid = (lo + hi) >> 1;
@@ -508,7 +548,7 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_multi_kernel(EmitParams
     if (S.overflow) {  // recount these reads one per block (2,048 slots, then the split)
         if (tid == 0) S.out_base = atomicAdd(o.overflow_n, rb - ra);
         __syncthreads();
-        for (uint32_t r = tid; r < rb - ra; r += PC_THREADS) o.overflow_list[S.out_base + r] = ra + r;
+        for (uint32_t r = tid; r < rb - ra; r += PC_THREADS) o.overflow_list[S.out_base + r] = (ra + r) << 6;
         return;
     }
     if (tid == 0) atomicAdd(&o.distinct[shard], (unsigned long long)S.fill);

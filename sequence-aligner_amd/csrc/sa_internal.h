@@ -130,7 +130,8 @@ struct PairParams {
     int32_t min_coll, max_coll;
     int32_t emit_all;      // 1: every distinct pair (PairData); 0: dispatched only
     int32_t strict;        // compute first-occurrence ranks
-    int32_t split;         // partner residue classes (overflow fallback)
+    int32_t split;         // partner residue classes (overflow fallback): partner % split == residue
+    int32_t coded;         // read_list holds (read << 6 | residue) codes (recount tiers)
     uint32_t max_occ;      // max occurrences of one read (LDS sizing)
     uint32_t n_items;      // reads (x split) to process; blocks beyond it exit
     int32_t xcd_swizzle;   // 1: XCD-contiguous block -> item map (grid % 8 == 0)
@@ -151,7 +152,8 @@ struct PairOut {
     unsigned long long cap_s;
     unsigned long long *role_pairs;  // [NSHARD]
     unsigned long long *distinct;    // [NSHARD] distinct (a, partner) keys counted
-    uint32_t *overflow_list;     // reads whose LDS table overflowed
+    uint32_t *overflow_list;     // (read << 6 | residue) of the blocks whose LDS table overflowed
+    uint32_t *overflow_rp;       // their role-pair totals (nullable)
     uint32_t *overflow_n;
 };
 

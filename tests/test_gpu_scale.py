@@ -106,3 +106,33 @@ def test_readme_record_pinned():
     assert out.count(README_RECORD) == 1
     golden = open(os.path.join(H.GOLDEN, "crp177_k12.ovl"), "rb").read()
     assert out.index(README_RECORD) == golden.index(README_RECORD)
+
+
+@pytest.mark.parametrize("n_edge", [5000, 12800, 110000])
+def test_many_partner_reads_recount_tiers(oracle_mod, n_edge):
+    """Reads with thousands to >98k distinct partners (configs[4]'s k = 12
+    stress in miniature): 8 reads carry a 17 bp motif in their middle region,
+    n_edge reads carry it at their start, so each middle read leads a pair with
+    every edge read (the 15-mers inside the motif, plus those straddling its
+    edges that share their few random bases).  5,000 partners take the
+    16,384-slot tier, 12,800 its 8-way residue split, 110,000 the 64-way split
+    (which refines only the classes that overflowed).  Dispatch and counts vs
+    the oracle, wide ids."""
+    rng = np.random.default_rng(n_edge)
+    motif = "".join("ACGT"[x] for x in rng.integers(0, 4, 17))
+    n_mid = 8
+    reads = []
+    for i in range(n_mid + n_edge):
+        s_ = "".join("ACGT"[x] for x in rng.integers(0, 4, 120))
+        p_ = 55 if i < n_mid else 5   # loc 0.52 (md) vs 0.05 (st), L - k = 105
+        reads.append(s_[:p_] + motif + s_[p_ + 17:])
+    st = dict(kmer_size=15, min_collisions=3)
+    ov = sao.Overlapper(id_mode=sao.SA_IDS_WIDE, **st)
+    ov.add_reads(reads)
+    ov.build()
+    lead, trail, count = ov.dispatch()
+    r = oracle_mod.Run(reads=reads, settings=oracle_mod.default_settings(**st), wide=True, skip_align=True)
+    np.testing.assert_array_equal(lead, r.lead)
+    np.testing.assert_array_equal(trail, r.trail)
+    assert (lead <= n_mid).sum() == n_mid * n_edge  # every middle read leads every edge read
+    assert ov.stats()["role_pairs"] > 3 * n_mid * n_edge
