@@ -291,6 +291,7 @@ EmitParams emit_params(sa_ctx *c) {
     e.rkey = nullptr;
     e.rord = nullptr;
     e.g_base = 0;
+    e.pos_bits = 0;
     return e;
 }
 
@@ -356,6 +357,8 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
     PA.lbase = (const uint32_t *)c->d_lbase.p;
     PA.lrank = (const uint32_t *)c->d_lrank.p;
     PA.k = c->set.kmer_size;
+    PA.pos_bits = rid ? 0 : c->pos_bits;  // (distributed mode: local indices + rid / lr arrays)
+    PA.meta = (const uint2 *)c->d_meta.p;
     ENSURE(c->d_md, 3 * n + 3, &PA.lst);
     ENSURE(c->d_rec, n + 1, &PA.rec);
     PA.xrec = nullptr;
@@ -641,6 +644,30 @@ int device_build(sa_ctx *c, bool readback) {
     ENSURE(c->d_rtmp, radix_sort_temp_bytes(nr), &rtmp);
     E.rkey = rk0;
     E.rord = ro0;
+    // mixed read lengths, wide ids: records carry (read, pos) and the bucket
+    // build finds a k-mer's occurrence index and loc rank with one meta load
+    c->pos_bits = 0;
+    if (!strict && c->uniform_npr == 0 && nr > 0) {
+        const int pb = bits_for((uint64_t)std::max(c->maxd, 1));
+        if (pb < 32 && (uint64_t)nr < (1ull << (32 - pb))) {
+            if (c->meta_gen != c->reads_gen || c->meta_k != c->set.kmer_size) {
+                std::vector<uint32_t> meta(2 * (size_t)nr);
+                for (uint32_t r = 0; r < nr; ++r) {
+                    meta[2 * r] = (uint32_t)c->occ_off[r];
+                    const int32_t d = c->len[r] - c->set.kmer_size;
+                    meta[2 * r + 1] = d >= 0 ? c->lbase[d] : 0u;
+                }
+                uint32_t *dm;
+                ENSURE(c->d_meta, 2 * (size_t)nr, &dm);
+                HIPCHK(hipMemcpyAsync(dm, meta.data(), meta.size() * 4, hipMemcpyHostToDevice, c->stream));
+                HIPCHK(hipStreamSynchronize(c->stream));
+                c->meta_gen = c->reads_gen;
+                c->meta_k = c->set.kmer_size;
+            }
+            c->pos_bits = pb;
+        }
+    }
+    E.pos_bits = c->pos_bits;
     {
         StageScope st(c, SA_STAGE_EMIT);
         HIPCHK(launch_kmer_emit(R, E, keys, vals, c->stream));
@@ -1050,7 +1077,7 @@ void sa_ctx_destroy(sa_ctx *c) {
                     &c->d_ovl, &c->d_cnt, &c->d_okeys, &c->d_ovals, &c->d_okeys2, &c->d_ovals2, &c->d_osort,
                     &c->d_lead, &c->d_trail, &c->d_count, &c->d_aln, &c->d_p1, &c->d_tb, &c->d_rkey, &c->d_rkey2, &c->d_rord, &c->d_rord2, &c->d_rtmp, &c->d_gocc, &c->d_rid, &c->d_loff, &c->d_starts, &c->d_bounds, &c->d_gcodes, &c->d_gwoff, &c->d_glen, &c->d_gbad, &c->d_psum, &c->d_pkeep, &c->d_ppos, &c->d_scan, &c->d_lr, &c->d_pstart, &c->d_biglist, &c->d_rec,
                     &c->d_srec, &c->d_bnmd, &c->d_ishead, &c->d_bnst2, &c->d_tmd, &c->d_ted, &c->d_tmdi,
-                    &c->d_tedi, &c->d_xrec, &c->d_tier, &c->d_ovlrp, &c->d_items, &c->d_bigtot, &c->d_hk0, &c->d_hk1, &c->d_hflag,
+                    &c->d_tedi, &c->d_xrec, &c->d_tier, &c->d_ovlrp, &c->d_meta, &c->d_items, &c->d_bigtot, &c->d_hk0, &c->d_hk1, &c->d_hflag,
                     &c->d_hidx, &c->d_hpos, &c->d_htmp, &c->d_hist, &c->d_hovf, &c->d_hsmall, &c->d_g2r,
                     &c->d_ltb, &c->d_lmax};
     for (DBuf *b : bufs)

@@ -81,6 +81,10 @@ struct sa_ctx {
     DBuf d_pstart, d_biglist, d_rec, d_srec, d_bnmd, d_ishead, d_bnst2;
     DBuf d_tmd, d_ted, d_tmdi, d_tedi, d_xrec;  // big-partition scratch lists, escape records
     DBuf d_tier, d_ovlrp;                       // pair-count recount tier items, overflow role pairs
+    DBuf d_meta;                                // mixed lengths: {first occurrence, lrank base} per read
+    int pos_bits = 0;                           // > 0: records carry read << pos_bits | pos
+    uint64_t meta_gen = ~0ull;
+    int meta_k = 0;
     uint32_t *bkt_rank_dev = nullptr;
     DBuf d_pf, d_ps, d_pc, d_pr, d_ovl, d_cnt;
     DBuf d_okeys, d_ovals, d_okeys2, d_ovals2, d_osort;

@@ -92,9 +92,11 @@ __global__ __launch_bounds__(256) void kmer_emit_kernel(DevReads r, EmitParams e
         for (int32_t i = lane; i < nk; i += 64) {
             const uint32_t h = kmer_mix(w, i, shift);
             kmin = min(kmin, h);
-            // 8-byte record: mixed hash | occurrence index (the loc rank is
-            // re-derived from the index where it is needed, partition.hip)
-            keys[g0 + i] = ((uint64_t)h << 32) | (uint64_t)((uint32_t)(g0 + i) + e.g_base);
+            // 8-byte record: mixed hash | occurrence index, or read << pos_bits |
+            // pos for mixed lengths (the loc rank is re-derived where it is
+            // needed, partition.hip)
+            const uint32_t occ = e.pos_bits ? (rd << e.pos_bits) | (uint32_t)i : (uint32_t)(g0 + i) + e.g_base;
+            keys[g0 + i] = ((uint64_t)h << 32) | (uint64_t)occ;
         }
         if (e.rkey) {
             // locality key: reads sharing their minimum k-mer overlap, so sorting

@@ -46,11 +46,18 @@ __device__ __forceinline__ uint32_t read_of_g(uint32_t g, const uint64_t *occ_of
 // L2, which is left to merge the scattered record stores
 __device__ __forceinline__ uint64_t load_sk(const uint64_t *p) { return __builtin_nontemporal_load(p); }
 
-// sort key (mix << lb | loc rank) and occurrence index of an 8-byte record
-__device__ __forceinline__ unsigned long long record_key(uint64_t rec, const PartArgs &A, uint32_t &g) {
-    g = (uint32_t)rec;
+// sort key (mix << lb | loc rank) and occurrence code of an 8-byte record: the
+// occurrence index g, or (pos_bits > 0: mixed read lengths) read << pos_bits |
+// pos, whose read meta {first occurrence, loc-rank base} gives g and the loc
+// rank with one load (instead of a search over the occurrence offsets)
+__device__ __forceinline__ unsigned long long record_key(uint64_t rec, const PartArgs &A, uint32_t &code) {
+    code = (uint32_t)rec;
+    const uint32_t g = code;
     uint32_t lr;
-    if (A.lr) {
+    if (A.pos_bits) {
+        const uint32_t pos = code & ((1u << A.pos_bits) - 1u);
+        lr = A.lrank[A.meta[code >> A.pos_bits].y + pos];
+    } else if (A.lr) {
         lr = A.lr[g];
     } else {
         const uint32_t r = read_of_g(g, A.occ_off, A.n_reads, A.npr, nullptr, A.g2r);
@@ -299,8 +306,15 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
         if (isb) { bh = s; ++nb; }
         if (isg) { gh = s; ++ng; }
         const uint32_t t = tagv[j];
-        const uint32_t g = S.g[s];
-        const uint32_t r = read_of_g(g, A.occ_off, A.n_reads, A.npr, A.rid, A.g2r);
+        const uint32_t code = S.g[s];
+        uint32_t r, g;
+        if (A.pos_bits) {  // read << pos_bits | pos (record_key)
+            r = code >> A.pos_bits;
+            g = A.meta[r].x + (code & ((1u << A.pos_bits) - 1u));
+        } else {
+            g = code;
+            r = read_of_g(g, A.occ_off, A.n_reads, A.npr, A.rid, A.g2r);
+        }
         const uint32_t st = (t & TAG_ST) ? 1u : 0u, en = (t & TAG_EN) ? 1u : 0u, md = (t & TAG_MD) ? 1u : 0u;
         // split point of the bucket [bh, nextb): its md entries end at c
         const uint32_t c = 3 * ps + S.mdx[nextb[j]] + S.edx[bh];
@@ -499,9 +513,10 @@ __global__ void convert_records_kernel(const uint64_t *rec8, uint32_t n, PartArg
                                        uint32_t *ovals) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    uint32_t g;
-    okeys[i] = record_key(rec8[i], A, g);
-    ovals[i] = g;
+    uint32_t code;
+    okeys[i] = record_key(rec8[i], A, code);
+    // the global scan path indexes by occurrence: decode a (read, pos) code
+    ovals[i] = A.pos_bits ? A.meta[code >> A.pos_bits].x + (code & ((1u << A.pos_bits) - 1u)) : code;
 }
 
 hipError_t launch_convert_records(const uint64_t *rec8, uint32_t n, const PartArgs &a, uint64_t *okeys,

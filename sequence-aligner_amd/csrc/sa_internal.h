@@ -34,6 +34,7 @@ struct EmitParams {
     uint64_t *rkey;            // [n] per-read locality key (min k-mer mix; nullable)
     uint32_t *rord;            // [n] read ids (sort payload for rkey)
     uint32_t g_base;           // occurrence index of this device's first k-mer (distributed mode)
+    int32_t pos_bits;          // > 0: the record's low word is read << pos_bits | pos (mixed lengths)
 };
 
 // bijective 32-bit mix of the seqHash: equal mix <=> equal hash, so a bucket
@@ -225,6 +226,10 @@ struct PartArgs {
     const int32_t *len;
     const uint32_t *lbase, *lrank;
     int32_t k;
+    // mixed read lengths, wide ids: records carry read << pos_bits | pos and
+    // meta[read] = {first occurrence index, lrank offset of its length}
+    int32_t pos_bits;
+    const uint2 *meta;
     uint32_t *lst;               // combined partner list [3 n]
     uint2 *rec;                  // [n_occ] by g
     uint4 *xrec;                 // escape records (big partitions only)
