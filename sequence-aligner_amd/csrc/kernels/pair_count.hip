@@ -20,10 +20,7 @@
 
 namespace sa {
 
-#ifndef SA_PC_THREADS
-#define SA_PC_THREADS 256
-#endif
-constexpr int PC_THREADS = SA_PC_THREADS;
+constexpr int PC_THREADS = 256;
 // LDS hash slots per read: a read has ~20-60 distinct partners at 20x coverage,
 // so the first pass runs a 256-slot table (small LDS -> 8 workgroups per CU);
 // reads that fill it (repeats, random short-k collisions) are re-run with 2,048
@@ -33,10 +30,7 @@ constexpr int PC_TAB_SMALL = 256;
 constexpr int PC_TAB_BIG = 2048;
 constexpr int PC_TAB_HUGE = 16384;
 constexpr int PC_CHUNK = 512;            // occurrences per pass over a read
-#ifndef SA_PC_BATCH
-#define SA_PC_BATCH 8
-#endif
-constexpr int PC_BATCH = SA_PC_BATCH;    // partner loads in flight per thread
+constexpr int PC_BATCH = 8;              // partner loads in flight per thread
 // the per-occurrence records are read once: non-temporal loads keep them from
 // displacing the partner lists in L2
 __device__ __forceinline__ uint4 load_rec(const PairIn &in, uint64_t g) {

@@ -130,10 +130,6 @@ constexpr int RS_THREADS = 256;
 constexpr int RS_ITEMS = 16;
 constexpr int RS_TILE = RS_THREADS * RS_ITEMS;
 
-// SA_RS_UNT (compile knob, default 1): non-temporal key loads in the digit histogram.
-#ifndef SA_RS_UNT
-#define SA_RS_UNT 1
-#endif
 __global__ __launch_bounds__(RS_THREADS) void rs_upsweep_kernel(const uint64_t *keys, uint64_t n, int shift,
                                                                 uint32_t *hist, uint32_t nblocks) {
     __shared__ uint32_t cnt[256];
@@ -144,11 +140,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_upsweep_kernel(const uint64_t *
     for (int j = 0; j < RS_ITEMS; ++j) {
         const uint64_t i = base + (uint64_t)j * RS_THREADS + threadIdx.x;
         if (i < n) {
-#if SA_RS_UNT
-            const uint64_t key = __builtin_nontemporal_load(keys + i);
-#else
-            const uint64_t key = keys[i];
-#endif
+            const uint64_t key = __builtin_nontemporal_load(keys + i);  // read once per pass
             atomicAdd(&cnt[(uint32_t)(key >> shift) & 255u], 1u);
         }
     }
@@ -156,18 +148,9 @@ __global__ __launch_bounds__(RS_THREADS) void rs_upsweep_kernel(const uint64_t *
     hist[(uint64_t)threadIdx.x * nblocks + blockIdx.x] = cnt[threadIdx.x];
 }
 
-// SA_RS_KNT (compile knob, default 1): read the scatter's input keys with non-temporal
-// loads so L2 is left to merge the scattered key stores.
-#ifndef SA_RS_KNT
-#define SA_RS_KNT 1
-#endif
-__device__ __forceinline__ unsigned long long rs_load_key(const uint64_t *p) {
-#if SA_RS_KNT
-    return __builtin_nontemporal_load(p);
-#else
-    return *p;
-#endif
-}
+// the scatter's input keys are read once: non-temporal loads leave L2 to merge
+// the digit-run stores
+__device__ __forceinline__ unsigned long long rs_load_key(const uint64_t *p) { return __builtin_nontemporal_load(p); }
 
 // Stable scatter.  Wave w owns the contiguous sub-tile [base + w*1024, +1024),
 // read as 16 coalesced slices of 64; each element's rank among equal digits of
