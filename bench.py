@@ -81,9 +81,16 @@ def synth_workload(n_reads, read_len, genome_len, gc, seed, shard=0, min_len=Non
     if lens.min() == lens.max():
         idx = starts[:, None] + np.arange(read_len, dtype=np.int64)[None, :]
         return genome[idx].reshape(-1), offsets
-    read_of = np.repeat(np.arange(n_reads, dtype=np.int64), lens)
-    pos = np.arange(int(offsets[-1]), dtype=np.int64) - offsets[:-1].astype(np.int64)[read_of]
-    return genome[starts[read_of] + pos], offsets
+    # each read is the first len bases of a read_len window at its start (the
+    # genome padded so every window exists); chunks of reads bound host memory
+    win = np.lib.stride_tricks.sliding_window_view(np.concatenate([genome, np.zeros(read_len, np.uint8)]),
+                                                   read_len)
+    keep = np.arange(read_len, dtype=np.int64)[None, :]
+    out = np.empty(int(offsets[-1]), dtype=np.uint8)
+    for r0 in range(0, n_reads, 1 << 19):
+        r1 = min(n_reads, r0 + (1 << 19))
+        out[int(offsets[r0]):int(offsets[r1])] = win[starts[r0:r1]][keep < lens[r0:r1, None]]
+    return out, offsets
 
 
 def pmc_summary():
@@ -145,6 +152,14 @@ def dist_env():
     return ws, rank, local
 
 
+def note(msg):
+    """Progress on stderr (long runs keep their log growing)."""
+    print("[bench %.1fs] %s" % (time.perf_counter() - T_START, msg), file=sys.stderr, flush=True)
+
+
+T_START = time.perf_counter()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -166,6 +181,9 @@ def main():
                     help="SA_OPT_ALIGN_KERNEL: 0 auto, 1 lane-group (LDS), 2 lane-per-pair")
     ap.add_argument("--replicas", action="store_true", help="torchrun: independent per-rank datasets, no exchange")
     ap.add_argument("--shards", type=int, default=1, help="virtual shards on one GPU (sharded path, device copies)")
+    ap.add_argument("--check-shards", type=int, default=0,
+                    help="single mode: afterwards rebuild the same reads over S virtual shards and require the "
+                         "identical dispatch (a size-independent parity property at full size)")
     args = ap.parse_args()
 
     ws, rank, local = dist_env()
@@ -239,7 +257,9 @@ def main():
         return float(t.item())
 
     # ---- hash stage (configs[1]) ------------------------------------------
+    note("inputs ready (%d reads)" % (len(offsets) - 1))
     build_step()  # allocations happen here, outside the timed region
+    note("first build done")
     for _ in range(args.warmup):
         build_step()
     ov.reset_stage_times()
@@ -257,6 +277,7 @@ def main():
     role_pairs_total = sum_over_ranks(float(st["role_pairs"])) * args.steps
     value = role_pairs_total / t_build
 
+    note("hash stage timed: %.3f ms/step" % (t_build / args.steps * 1e3))
     # ---- end-to-end incl. banded HOXD alignment (configs[2]) --------------
     asteps = args.align_steps if args.align_steps is not None else max(1, args.steps // 2)
     xbytes = (ov.exchanged_bytes() - xb0) / max(args.steps, 1)
@@ -437,6 +458,26 @@ def main():
                    "cpu_port_1_thread_s": round(t_c0, 3), "gpu_end_to_end_s": round(t_g0, 4),
                    "ovl_records": g_ovl.count(b"{OVL"), "ovl_identical": g_ovl == rc0.ovl}
 
+    note("aligner timed")
+    # ---- full-size parity property: S virtual shards == one device ----------
+    check = None
+    if args.check_shards > 1 and mode == "single":
+        lead1, trail1, cnt1 = (np.array(x) for x in ov.dispatch())
+        ov.close()  # its HBM back before the sharded context allocates
+        t0 = time.perf_counter()
+        check = {"shards": args.check_shards, "dispatched": int(len(lead1))}
+        try:
+            ovx = sao.Overlapper(shards=args.check_shards, **common)
+            ovx.add_packed(bases.tobytes(), offsets)
+            ovx.device_build()
+            lead2, trail2, cnt2 = ovx.dispatch()
+            check["dispatch_identical"] = bool(np.array_equal(lead1, lead2) and np.array_equal(trail1, trail2)
+                                               and np.array_equal(cnt1, cnt2))
+            check["sharded_build_s"] = round(time.perf_counter() - t0, 3)
+            ovx.close()
+        except sao.SAError as e:  # e.g. SA_E_NOMEM: the record is kept, the line still printed
+            check["error"] = str(e)
+
     if rank == 0:
         line = {
             "metric": "candidate k-mer pairs/sec (hash stage) + aligned read-pairs/sec, k=15, 500 bp reads",
@@ -476,6 +517,7 @@ def main():
             "read_allgather_ms": round(t_gather * 1e3, 3) if t_gather is not None else None,
             "cpu_baseline": cpu,
             "config0": config0,
+            "check_shards": check,
         }
         print(json.dumps(line), flush=True)
     ov.close()

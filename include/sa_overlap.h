@@ -253,13 +253,15 @@ uint64_t sa_exchanged_bytes(const sa_ctx *ctx);
 int sa_dist_init(sa_ctx *ctx, int rank, int nranks, const uint32_t *starts, const int32_t *lengths);
 /* k-mer occurrences of this rank's reads (the size of the exchange-1 send buffers). */
 int sa_dist_local_kmers(sa_ctx *ctx, uint64_t *n);
-/* Emit this rank's k-mer records (u64[n]: mixed hash << 32 | global occurrence
- * index) into send_recs, grouped by owner rank; counts[nranks] = records per owner. */
+/* Emit this rank's k-mer records (u64[n]: mixed hash << 32 | occurrence index
+ * local to this rank, so only each rank's k-mer count is bounded by 2^32) into
+ * send_recs, grouped by owner rank; counts[nranks] = records per owner. */
 int sa_dist_emit(sa_ctx *ctx, void *send_recs, uint64_t *counts);
-/* Records received in exchange 1 (concatenated in source-rank order; the
- * buffer is consumed and overwritten): build this rank's buckets and count
- * partial pairs for every read; counts[nranks] = partials per lead owner. */
-int sa_dist_count(sa_ctx *ctx, void *recv_recs, uint64_t n, uint64_t *counts);
+/* Records received in exchange 1, concatenated in source-rank order with
+ * recv_counts[s] (host, nranks entries) records from rank s (the buffer is
+ * consumed and overwritten): build this rank's buckets and count partial pairs
+ * for every read; counts[nranks] = partials per lead owner. */
+int sa_dist_count(sa_ctx *ctx, void *recv_recs, const uint64_t *recv_counts, uint64_t *counts);
 /* Copy the partials (u32 lead, trail, count; 0-based ids) grouped by lead owner. */
 int sa_dist_partials(sa_ctx *ctx, void *fst, void *snd, void *cnt);
 /* Partials received in exchange 2: sum, filter, dispatch this rank's leads

@@ -162,18 +162,8 @@ int prepare_reads(sa_ctx *c) {
         }
     }
     c->n_occ = c->occ_off[n];
-    // the combined partner list holds up to 3 entries per k-mer, indexed by u32
-    if (c->n_occ >= 0x55555550ull) return fail(c, SA_E_OVERFLOW, "more than 1,431,655,760 k-mers on one device");
-    {
-        const uint64_t nb = (c->n_occ >> G2R_SHIFT) + 2;
-        c->g2r.assign(nb, 0);
-        for (uint64_t b = 0; b < nb; ++b) {
-            const uint64_t target = b << G2R_SHIFT;
-            const uint64_t r = (uint64_t)(std::upper_bound(c->occ_off.begin(), c->occ_off.begin() + n, target) -
-                                          c->occ_off.begin());
-            c->g2r[b] = (uint32_t)(r ? r - 1 : 0);
-        }
-    }
+    // occurrence indices are u32 (records: mix << 32 | occurrence)
+    if (c->n_occ >= 0xFFFFFFF0ull) return fail(c, SA_E_OVERFLOW, "more than 2^32 - 16 k-mers on one device");
     if (c->dist) {
         // loc ranks / tags / sort-key width must agree on every rank: derive
         // them from the lengths of ALL reads, not just this rank's
@@ -255,9 +245,6 @@ int upload_reads(sa_ctx *c) {
     HIPCHK(hipMemcpyAsync(woff, c->woff.data(), (n + 1) * 8, hipMemcpyHostToDevice, c->stream));
     if (n) HIPCHK(hipMemcpyAsync(len, c->len.data(), n * 4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(occ, c->occ_off.data(), (n + 1) * 8, hipMemcpyHostToDevice, c->stream));
-    uint32_t *g2r;
-    ENSURE(c->d_g2r, c->g2r.size(), &g2r);
-    HIPCHK(hipMemcpyAsync(g2r, c->g2r.data(), c->g2r.size() * 4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(lbase, c->lbase.data(), c->lbase.size() * 4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(lrank, c->lrank.data(), c->lrank.size() * 4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(tag, c->tagtab.data(), c->tagtab.size(), hipMemcpyHostToDevice, c->stream));
@@ -290,8 +277,8 @@ EmitParams emit_params(sa_ctx *c) {
     e.maxd = c->maxd;
     e.rkey = nullptr;
     e.rord = nullptr;
-    e.g_base = 0;
     e.pos_bits = 0;
+    e.occ_rid = e.occ_lr = nullptr;
     return e;
 }
 
@@ -351,13 +338,12 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
     PA.tagtab = (const uint8_t *)c->d_tagtab.p;
     PA.occ_off = occ_off;
     PA.n_reads = n_reads; PA.npr = npr; PA.rid = rid;
-    PA.g2r = (rid || npr) ? nullptr : (const uint32_t *)c->d_g2r.p;
     PA.lr = lr;
     PA.len = len;
     PA.lbase = (const uint32_t *)c->d_lbase.p;
     PA.lrank = (const uint32_t *)c->d_lrank.p;
     PA.k = c->set.kmer_size;
-    PA.pos_bits = rid ? 0 : c->pos_bits;  // (distributed mode: local indices + rid / lr arrays)
+    PA.pos_bits = rid ? 0 : c->pos_bits;  // (occurrence indices + rid / lr tables)
     PA.meta = (const uint2 *)c->d_meta.p;
     ENSURE(c->d_md, 3 * n + 3, &PA.lst);
     ENSURE(c->d_rec, n + 1, &PA.rec);
@@ -442,7 +428,7 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
                 HIPCHK(hipMemcpyAsync(vals + ps, v0, (size_t)pn * 4, hipMemcpyDeviceToDevice, c->stream));
             }
             B.n_occ = pn;
-            HIPCHK(build_buckets(keys2 + ps, vals + ps, pn, c->lb, tagtab, PA.occ_off, n_reads, npr, rid, PA.g2r, B,
+            HIPCHK(build_buckets(keys2 + ps, vals + ps, pn, c->lb, tagtab, PA.occ_off, n_reads, npr, rid, B,
                                  bigtot + 4 * (size_t)bi, btmp, c->stream));
             if (strict) HIPCHK(build_strict_index(keys2 + ps, vals + ps, pn, c->lb, tagtab, B, c->stream));
             HIPCHK(launch_relayout_lists(B, ps, pn, bigtot + 4 * (size_t)bi, PA, strict, c->stream));
@@ -668,6 +654,16 @@ int device_build(sa_ctx *c, bool readback) {
         }
     }
     E.pos_bits = c->pos_bits;
+    // mixed lengths without (read, pos) codes (too many reads, or strict ids):
+    // the emit kernel also writes each occurrence's read and loc rank, so the
+    // bucket build looks both up with one load each instead of a search
+    uint32_t *orid = nullptr, *olr = nullptr;
+    if (c->uniform_npr == 0 && c->pos_bits == 0) {
+        ENSURE(c->d_rid, n + 1, &orid);
+        ENSURE(c->d_lr, n + 1, &olr);
+        E.occ_rid = orid;
+        E.occ_lr = olr;
+    }
     {
         StageScope st(c, SA_STAGE_EMIT);
         HIPCHK(launch_kmer_emit(R, E, keys, vals, c->stream));
@@ -678,7 +674,7 @@ int device_build(sa_ctx *c, bool readback) {
     PartArgs PA{};
     unsigned long long big_buckets = 0;
     rc = bucket_stage(c, keys, keys2, vals, vals2, n, (const uint64_t *)c->d_occ_off.p, nr, c->uniform_npr,
-                      nullptr, nullptr, (const int32_t *)c->d_len.p, strict, stmp, cnt, PA, big_buckets);
+                      orid, olr, (const int32_t *)c->d_len.p, strict, stmp, cnt, PA, big_buckets);
     if (rc) return rc;
     if (strict) {
         // KmerData iteration rank of every bucket: replay its Trove layout over the
@@ -1075,10 +1071,10 @@ void sa_ctx_destroy(sa_ctx *c) {
                     &c->d_gmds, &c->d_gede, &c->d_ogid, &c->d_bkttmp, &c->d_mdidx, &c->d_edidx, &c->d_occidx,
                     &c->d_bnst, &c->d_brank, &c->d_bhash, &c->d_bfirst, &c->d_pf, &c->d_ps, &c->d_pc, &c->d_pr,
                     &c->d_ovl, &c->d_cnt, &c->d_okeys, &c->d_ovals, &c->d_okeys2, &c->d_ovals2, &c->d_osort,
-                    &c->d_lead, &c->d_trail, &c->d_count, &c->d_aln, &c->d_p1, &c->d_tb, &c->d_rkey, &c->d_rkey2, &c->d_rord, &c->d_rord2, &c->d_rtmp, &c->d_gocc, &c->d_rid, &c->d_loff, &c->d_starts, &c->d_bounds, &c->d_gcodes, &c->d_gwoff, &c->d_glen, &c->d_gbad, &c->d_psum, &c->d_pkeep, &c->d_ppos, &c->d_scan, &c->d_lr, &c->d_pstart, &c->d_biglist, &c->d_rec,
+                    &c->d_lead, &c->d_trail, &c->d_count, &c->d_aln, &c->d_p1, &c->d_tb, &c->d_rkey, &c->d_rkey2, &c->d_rord, &c->d_rord2, &c->d_rtmp, &c->d_gocc, &c->d_seg, &c->d_rid, &c->d_loff, &c->d_starts, &c->d_bounds, &c->d_gcodes, &c->d_gwoff, &c->d_glen, &c->d_gbad, &c->d_psum, &c->d_pkeep, &c->d_ppos, &c->d_scan, &c->d_lr, &c->d_pstart, &c->d_biglist, &c->d_rec,
                     &c->d_srec, &c->d_bnmd, &c->d_ishead, &c->d_bnst2, &c->d_tmd, &c->d_ted, &c->d_tmdi,
                     &c->d_tedi, &c->d_xrec, &c->d_tier, &c->d_ovlrp, &c->d_meta, &c->d_items, &c->d_bigtot, &c->d_hk0, &c->d_hk1, &c->d_hflag,
-                    &c->d_hidx, &c->d_hpos, &c->d_htmp, &c->d_hist, &c->d_hovf, &c->d_hsmall, &c->d_g2r,
+                    &c->d_hidx, &c->d_hpos, &c->d_htmp, &c->d_hist, &c->d_hovf, &c->d_hsmall,
                     &c->d_ltb, &c->d_lmax};
     for (DBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
@@ -1371,7 +1367,10 @@ int sa_dist_init(sa_ctx *c, int rank, int nranks, const uint32_t *starts, const 
         if (uni < 0) uni = L;
         if (L != uni || L < k) uniform = false;
     }
-    if (c->gocc[N] >= 0xFFFFFFF0ull) return fail(c, SA_E_OVERFLOW, "more than 2^32 k-mers in the global read set");
+    // records carry occurrence indices local to their source rank
+    for (int r = 0; r < nranks; ++r)
+        if (c->gocc[starts[r + 1]] - c->gocc[starts[r]] >= 0xFFFFFFF0ull)
+            return fail(c, SA_E_OVERFLOW, "more than 2^32 k-mers on one rank");
     c->gnpr = uniform ? (uint32_t)(uni - k + 1) : 0;
     c->reads_dirty = true;  // loc tables come from all lengths now
     c->built = c->aligned = false;
@@ -1409,7 +1408,6 @@ int sa_dist_emit(sa_ctx *c, void *send_recs, uint64_t *counts) {
     if (n && !send_recs) return SA_E_ARG;
     DevReads R = dev_reads(c);
     EmitParams E = emit_params(c);
-    E.g_base = (uint32_t)c->gocc[c->dstarts[c->rank]];
     uint64_t *keys, *keys2; uint8_t *stmp;
     ENSURE(c->d_keys, n, &keys);
     ENSURE(c->d_sorttmp, std::max(radix_sort_temp_bytes(n), buckets_temp_bytes(n)), &stmp);
@@ -1448,20 +1446,32 @@ int sa_dist_emit(sa_ctx *c, void *send_recs, uint64_t *counts) {
     return SA_OK;
 }
 
-int sa_dist_count(sa_ctx *c, void *recv_recs, uint64_t n, uint64_t *counts) {
-    if (!c || !counts || (n && !recv_recs)) return SA_E_ARG;
+int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint64_t *counts) {
+    if (!c || !counts || !recv_counts) return SA_E_ARG;
     if (!c->dist) return fail(c, SA_E_STATE, "sa_dist_init first");
+    const int P = c->nranks;
+    // seg[s] = first received record of source s; seg[P + 1 + s] = the global
+    // occurrence index of source s's first k-mer (its records carry local ones)
+    std::vector<uint64_t> seg(2 * (size_t)P + 1, 0);
+    for (int s = 0; s < P; ++s) {
+        seg[s + 1] = seg[s] + recv_counts[s];
+        seg[P + 1 + s] = c->gocc[c->dstarts[s]];
+    }
+    const uint64_t n = seg[P];
+    if (n && !recv_recs) return SA_E_ARG;
     (void)hipSetDevice(c->device);
     int rc = ensure_prepared(c);
     if (rc) return rc;
     const uint32_t N = (uint32_t)c->dlen.size();
-    if (n >= 0x55555550ull) return fail(c, SA_E_OVERFLOW, "more than 1,431,655,760 k-mers received on one rank");
+    if (n >= 0xFFFFFFF0ull) return fail(c, SA_E_OVERFLOW, "more than 2^32 - 16 k-mers received on one rank");
     Counters *cnt;
     ENSURE(c->d_cnt, 1, &cnt);
     HIPCHK(hipMemsetAsync(cnt, 0, sizeof(Counters), c->stream));
     // received records are in global occurrence order (sources in rank order,
     // each in occurrence order): local index i <-> i-th owned occurrence
-    uint32_t *rid, *lr, *vals, *vals2; uint64_t *loff, *keys2; uint8_t *stmp;
+    uint32_t *rid, *lr, *vals, *vals2; uint64_t *loff, *keys2, *dseg; uint8_t *stmp;
+    ENSURE(c->d_seg, seg.size(), &dseg);
+    HIPCHK(hipMemcpyAsync(dseg, seg.data(), seg.size() * 8, hipMemcpyHostToDevice, c->stream));
     ENSURE(c->d_rid, n, &rid);
     ENSURE(c->d_lr, n, &lr);
     ENSURE(c->d_loff, (size_t)N + 1, &loff);
@@ -1474,7 +1484,8 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, uint64_t n, uint64_t *counts) {
         StageScope st(c, SA_STAGE_EMIT);
         // read id and loc rank of every received occurrence; the record's low
         // word becomes its local index (record i of this rank)
-        HIPCHK(launch_prepare_received(keys, n, (const uint64_t *)c->d_gocc.p, N, c->gnpr,
+        HIPCHK(launch_prepare_received(keys, n, dseg, (uint32_t)P, (const uint32_t *)c->d_starts.p,
+                                       (const uint64_t *)c->d_gocc.p, c->gnpr,
                                        (const int32_t *)c->d_glen.p, (const uint32_t *)c->d_lbase.p,
                                        (const uint32_t *)c->d_lrank.p, c->set.kmer_size, rid, lr, c->stream));
         HIPCHK(launch_local_offsets(rid, n, N, loff, c->stream));

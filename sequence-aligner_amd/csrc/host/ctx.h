@@ -65,7 +65,6 @@ struct sa_ctx {
     // derived (host)
     std::vector<int32_t> len;
     std::vector<uint64_t> woff, occ_off;
-    std::vector<uint32_t> g2r;  // coarse occurrence -> read table (sa_internal.h, G2R_SHIFT)
     std::vector<uint32_t> lbase, lrank;
     std::vector<uint8_t> tagtab;
     int lb = 1, m = 0, maxd = 0, maxL = 0, minL = 0;
@@ -74,7 +73,7 @@ struct sa_ctx {
     uint32_t max_occ = 0;
     int32_t mode = SA_IDS_WIDE;
     // device buffers
-    DBuf d_ascii, d_boff, d_woff, d_len, d_codes, d_bad, d_occ_off, d_lbase, d_lrank, d_tagtab, d_g2r;
+    DBuf d_ascii, d_boff, d_woff, d_len, d_codes, d_bad, d_occ_off, d_lbase, d_lrank, d_tagtab;
     DBuf d_keys, d_vals, d_keys2, d_vals2, d_sorttmp;
     DBuf d_md, d_ed, d_bmdo, d_bedo, d_bstart, d_gbid, d_gmds, d_gede, d_ogid, d_bkttmp;
     DBuf d_mdidx, d_edidx, d_occidx, d_bnst, d_brank, d_bhash, d_bfirst;
@@ -102,7 +101,7 @@ struct sa_ctx {
     int32_t gmaxL = 0, gminL = 0;
     uint64_t part_np = 0;            // partial pairs after sa_dist_count
     uint32_t *part_perm = nullptr;   // their ascending-lead order (region-space indices)
-    DBuf d_gocc, d_rid, d_loff, d_starts, d_bounds, d_gcodes, d_gwoff, d_glen, d_gbad, d_psum, d_pkeep, d_ppos;
+    DBuf d_gocc, d_seg, d_rid, d_loff, d_starts, d_bounds, d_gcodes, d_gwoff, d_glen, d_gbad, d_psum, d_pkeep, d_ppos;
     DBuf d_scan, d_lr, d_bigtot, d_items;
     // k-mer table statistics (sa_kmer_histogram)
     DBuf d_hk0, d_hk1, d_hflag, d_hidx, d_hpos, d_htmp, d_hist, d_hovf, d_hsmall;

@@ -369,7 +369,7 @@ int multi_build(sa_ctx *c, bool readback, int (*single_build)(sa_ctx *, bool)) {
     // ---- count: buckets of this hash range, partial pairs by lead owner
     rc = for_shards(c, [&](Shard &s) {
         s.cnt.assign(P, 0);
-        int r = sa_dist_count(s.child, s.rk.p, s.n_recv, s.cnt.data());
+        int r = sa_dist_count(s.child, s.rk.p, s.rcnt.data(), s.cnt.data());
         if (r) return r;
         s.n_part = 0;
         for (uint64_t v : s.cnt) s.n_part += v;

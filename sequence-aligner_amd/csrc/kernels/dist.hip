@@ -21,43 +21,46 @@ inline dim3 grid_for(uint64_t n) {
     return dim3((uint32_t)(b ? b : 1));
 }
 
-__device__ __forceinline__ uint32_t read_of_occ(uint32_t g, const uint64_t *occ_off, uint32_t n_reads,
-                                                uint32_t npr) {
-    if (npr) return g / npr;
-    uint32_t lo = 0, hi = n_reads;  // largest r with occ_off[r] <= g
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (occ_off[mid] <= g) lo = mid; else hi = mid;
-    }
-    return lo;
-}
-
 __global__ void iota_kernel(uint32_t *v, uint64_t n) {
     const uint64_t i = (uint64_t)blockIdx.x * DT + threadIdx.x;
     if (i < n) v[i] = (uint32_t)i;
 }
 
-// received 8-byte records (mix << 32 | global occurrence g): rid[i] = read of
-// g, lr[i] = its loc rank (lrank[lbase[L - k] + pos]); the low word becomes i
-__global__ void prepare_received_kernel(uint64_t *recs, uint64_t n, const uint64_t *occ_off, uint32_t n_reads,
-                                        uint32_t npr, const int32_t *len, const uint32_t *lbase,
-                                        const uint32_t *lrank, int32_t k, uint32_t *rid, uint32_t *lr) {
+// received 8-byte records (mix << 32 | occurrence index local to the source
+// rank): seg[s] = first record from source s (s < P, seg[P] = n), seg[P+1+s] =
+// the global occurrence index of source s's first k-mer, starts[s] its first
+// read.  rid[i] = read of the occurrence, lr[i] = its loc rank
+// (lrank[lbase[L - k] + pos]); the low word becomes i
+__global__ void prepare_received_kernel(uint64_t *recs, uint64_t n, const uint64_t *seg, uint32_t P,
+                                        const uint32_t *starts, const uint64_t *occ_off, uint32_t npr,
+                                        const int32_t *len, const uint32_t *lbase, const uint32_t *lrank, int32_t k,
+                                        uint32_t *rid, uint32_t *lr) {
     const uint64_t i = (uint64_t)blockIdx.x * DT + threadIdx.x;
     if (i >= n) return;
+    uint32_t s = 0, hi = P;  // the source whose segment holds i
+    while (hi - s > 1) {
+        const uint32_t mid = (s + hi) >> 1;
+        if (seg[mid] <= i) s = mid; else hi = mid;
+    }
     const uint64_t rec = recs[i];
-    const uint32_t g = (uint32_t)rec;
-    const uint32_t r = read_of_occ(g, occ_off, n_reads, npr);
-    const uint32_t pos = g - (uint32_t)occ_off[r];
+    const uint32_t local = (uint32_t)rec;
+    uint32_t r, pos;
+    if (npr) {
+        r = starts[s] + local / npr;
+        pos = local % npr;
+    } else {
+        const uint64_t g = seg[P + 1 + s] + local;
+        uint32_t lo = starts[s], up = starts[s + 1];  // largest r with occ_off[r] <= g
+        while (up - lo > 1) {
+            const uint32_t mid = (lo + up) >> 1;
+            if (occ_off[mid] <= g) lo = mid; else up = mid;
+        }
+        r = lo;
+        pos = (uint32_t)(g - occ_off[r]);
+    }
     rid[i] = r;
     lr[i] = lrank[lbase[len[r] - k] + pos];
     recs[i] = (rec & 0xFFFFFFFF00000000ull) | (uint32_t)i;
-}
-
-// rid[i] = global read of global occurrence g[i]
-__global__ void read_ids_kernel(const uint32_t *g, uint64_t n, const uint64_t *occ_off, uint32_t n_reads,
-                                uint32_t npr, uint32_t *rid) {
-    const uint64_t i = (uint64_t)blockIdx.x * DT + threadIdx.x;
-    if (i < n) rid[i] = read_of_occ(g[i], occ_off, n_reads, npr);
 }
 
 // loff[a] = first i with rid[i] >= a, for a in [0, n_reads] (rid ascending):
@@ -168,19 +171,13 @@ hipError_t launch_iota(uint32_t *v, uint64_t n, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_prepare_received(uint64_t *recs, uint64_t n, const uint64_t *occ_off, uint32_t n_reads,
-                                   uint32_t npr, const int32_t *len, const uint32_t *lbase, const uint32_t *lrank,
-                                   int32_t k, uint32_t *rid, uint32_t *lr, hipStream_t s) {
+hipError_t launch_prepare_received(uint64_t *recs, uint64_t n, const uint64_t *seg, uint32_t P,
+                                   const uint32_t *starts, const uint64_t *occ_off, uint32_t npr, const int32_t *len,
+                                   const uint32_t *lbase, const uint32_t *lrank, int32_t k, uint32_t *rid,
+                                   uint32_t *lr, hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(prepare_received_kernel, grid_for(n), dim3(DT), 0, s, recs, n, occ_off, n_reads, npr, len,
-                       lbase, lrank, k, rid, lr);
-    return hipGetLastError();
-}
-
-hipError_t launch_read_ids(const uint32_t *g, uint64_t n, const uint64_t *occ_off, uint32_t n_reads, uint32_t npr,
-                           uint32_t *rid, hipStream_t s) {
-    if (!n) return hipSuccess;
-    hipLaunchKernelGGL(read_ids_kernel, grid_for(n), dim3(DT), 0, s, g, n, occ_off, n_reads, npr, rid);
+    hipLaunchKernelGGL(prepare_received_kernel, grid_for(n), dim3(DT), 0, s, recs, n, seg, P, starts, occ_off, npr,
+                       len, lbase, lrank, k, rid, lr);
     return hipGetLastError();
 }
 

@@ -261,9 +261,9 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
                         const uint32_t off = w0 + el - S.pref[oi];
                         const uint4 rc = S.rec[oi];
                         const uint32_t nE = rc.y & 0x3FFFFFFFu;
+                        const uint64_t q = rec_entry(rc, off);
+                        part[bb] = in.lst[q];
                         if (off < nE) {
-                            const uint32_t q = rc.x + off;
-                            part[bb] = in.lst[q];
                             wv[bb] = rc.y >> 30;
                             if constexpr (STRICT) {
                                 const uint4 sr = X.srec[oi];
@@ -275,8 +275,6 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
                                 rk[bb] = ((unsigned long long)in.bkt_rank[hb] << 37) | within;
                             }
                         } else {
-                            const uint32_t q = rc.z + (off - nE);
-                            part[bb] = in.lst[q];
                             wv[bb] = 1;
                             if constexpr (STRICT) {
                                 const uint4 sr = X.srec[oi];
@@ -517,13 +515,8 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_multi_kernel(EmitParams
                         const uint4 rc = S.rec[oi];
                         const uint32_t nE = rc.y & 0x3FFFFFFFu;
                         own[bb] = S.aid[oi];
-                        if (off < nE) {
-                            part[bb] = in.lst[rc.x + off];
-                            wv[bb] = rc.y >> 30;
-                        } else {
-                            part[bb] = in.lst[rc.z + (off - nE)];
-                            wv[bb] = 1;
-                        }
+                        part[bb] = in.lst[rec_entry(rc, off)];
+                        wv[bb] = off < nE ? rc.y >> 30 : 1u;
                     }
                 }
 #pragma unroll

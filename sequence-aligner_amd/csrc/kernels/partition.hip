@@ -27,14 +27,10 @@
 namespace sa {
 
 __device__ __forceinline__ uint32_t read_of_g(uint32_t g, const uint64_t *occ_off, uint32_t n_reads, uint32_t npr,
-                                              const uint32_t *rid, const uint32_t *g2r) {
-    if (rid) return rid[g];  // distributed mode: occurrence index -> global read id
+                                              const uint32_t *rid) {
+    if (rid) return rid[g];  // occurrence table (distributed mode, mixed lengths)
     if (npr) return g / npr;
     uint32_t lo = 0, hi = n_reads;  // largest r with occ_off[r] <= g
-    if (g2r) {  // mixed lengths: the owner lies between the owners of the enclosing 1,024-blocks
-        lo = g2r[g >> G2R_SHIFT];
-        hi = g2r[(g >> G2R_SHIFT) + 1] + 1;
-    }
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
         if (occ_off[mid] <= g) lo = mid; else hi = mid;
@@ -60,7 +56,7 @@ __device__ __forceinline__ unsigned long long record_key(uint64_t rec, const Par
     } else if (A.lr) {
         lr = A.lr[g];
     } else {
-        const uint32_t r = read_of_g(g, A.occ_off, A.n_reads, A.npr, nullptr, A.g2r);
+        const uint32_t r = read_of_g(g, A.occ_off, A.n_reads, A.npr, nullptr);
         const uint32_t pos = A.npr ? g - r * A.npr : g - (uint32_t)A.occ_off[r];
         const int32_t d = A.npr ? (int32_t)A.npr - 1 : A.len[r] - A.k;
         lr = A.lrank[A.lbase[d] + pos];
@@ -313,19 +309,19 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
             g = A.meta[r].x + (code & ((1u << A.pos_bits) - 1u));
         } else {
             g = code;
-            r = read_of_g(g, A.occ_off, A.n_reads, A.npr, A.rid, A.g2r);
+            r = read_of_g(g, A.occ_off, A.n_reads, A.npr, A.rid);
         }
         const uint32_t st = (t & TAG_ST) ? 1u : 0u, en = (t & TAG_EN) ? 1u : 0u, md = (t & TAG_MD) ? 1u : 0u;
         // split point of the bucket [bh, nextb): its md entries end at c
-        const uint32_t c = 3 * ps + S.mdx[nextb[j]] + S.edx[bh];
-        const uint32_t mpos = c - 1u - (S.mdx[s] - S.mdx[bh]), epos = c + (S.edx[s] - S.edx[bh]);
+        const uint64_t c = 3ull * ps + S.mdx[nextb[j]] + S.edx[bh];
+        const uint64_t mpos = c - 1u - (S.mdx[s] - S.mdx[bh]), epos = c + (S.edx[s] - S.edx[bh]);
         if (md) A.lst[mpos] = r;
         if (st) A.lst[epos] = r;
         if (en) A.lst[epos + st] = r;
         const uint32_t me = st + en;
         const uint32_t nE = me ? (S.mdx[gh] - S.mdx[bh]) : 0u;        // <= CAP: no escape here
         const uint32_t nD = md ? (S.edx[nextg[j]] - S.edx[bh]) : 0u;  // <= 2 CAP
-        A.rec[g] = make_uint2(c, nE | (nD << 15) | (me << 30));
+        A.rec[g] = encode_rec(c, nE, nD, me);
         if constexpr (STRICT) {
             // bucket extent [bh, be)
             uint32_t be = s + 1;
@@ -408,13 +404,13 @@ __global__ void relayout_lists_kernel(Buckets b, uint32_t ps, const uint32_t *to
     const uint32_t nb = totals[0], n_md = totals[2], n_ed = totals[3];
     if (e < n_md) {
         const uint32_t bk = bucket_of_entry(b.bkt_mdo, nb, e);
-        const uint32_t q = 3 * ps + b.bkt_mdo[bk + 1] + b.bkt_edo[bk] - 1u - (e - b.bkt_mdo[bk]);
+        const uint64_t q = 3ull * ps + b.bkt_mdo[bk + 1] + b.bkt_edo[bk] - 1u - (e - b.bkt_mdo[bk]);
         lst[q] = b.md_list[e];
         if (lidx) lidx[q] = b.md_idx[e];
     }
     if (e < n_ed) {
         const uint32_t bk = bucket_of_entry(b.bkt_edo, nb, e);
-        const uint32_t q = 3 * ps + b.bkt_mdo[bk + 1] + e;  // = c_b + (e - bkt_edo[bk])
+        const uint64_t q = 3ull * ps + b.bkt_mdo[bk + 1] + e;  // = c_b + (e - bkt_edo[bk])
         lst[q] = b.ed_list[e];
         if (lidx) lidx[q] = b.ed_idx[e];
     }
@@ -441,15 +437,15 @@ __global__ void records_from_tables_kernel(const uint64_t *sk, const uint32_t *s
     const uint32_t st = (t & TAG_ST) ? 1u : 0u, en = (t & TAG_EN) ? 1u : 0u, md = (t & TAG_MD) ? 1u : 0u;
     const uint32_t me = st + en;
     const uint32_t mdo = b.bkt_mdo[bid], edo = b.bkt_edo[bid];
-    const uint32_t c = 3 * ps + b.bkt_mdo[bid + 1] + edo;
+    const uint64_t c = 3ull * ps + b.bkt_mdo[bid + 1] + edo;
     const uint32_t nE = me ? (b.grp_mds[gid] - mdo) : 0u;
     const uint32_t nD = md ? (b.grp_ede[gid] - edo) : 0u;
     if (nE <= REC_CNT_MAX && nD <= REC_CNT_MAX) {
-        A.rec[g] = make_uint2(c, nE | (nD << 15) | (me << 30));
-    } else {  // a high-copy repeat: the counts do not fit 15 bits
+        A.rec[g] = encode_rec(c, nE, nD, me);
+    } else {  // a high-copy repeat: the counts do not fit 14 bits
         const uint32_t xi = atomicAdd(A.xrec_n, 1u);
-        A.xrec[xi] = make_uint4(c - nE, nE | (me << 30), c, nD);
-        A.rec[g] = make_uint2(c, (3u << 30) | xi);
+        A.xrec[xi] = decoded_rec(c, nE, nD, me);
+        A.rec[g] = make_uint2((uint32_t)c, (3u << 30) | xi);
     }
     if (strict) {
         const uint32_t s0 = b.bkt_start[bid];

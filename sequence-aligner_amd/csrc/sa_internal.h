@@ -33,8 +33,10 @@ struct EmitParams {
     int32_t maxd;
     uint64_t *rkey;            // [n] per-read locality key (min k-mer mix; nullable)
     uint32_t *rord;            // [n] read ids (sort payload for rkey)
-    uint32_t g_base;           // occurrence index of this device's first k-mer (distributed mode)
     int32_t pos_bits;          // > 0: the record's low word is read << pos_bits | pos (mixed lengths)
+    // mixed lengths without pos_bits codes: per-occurrence read and loc rank
+    // tables (nullable), so the bucket build finds both with one load each
+    uint32_t *occ_rid, *occ_lr;
 };
 
 // bijective 32-bit mix of the seqHash: equal mix <=> equal hash, so a bucket
@@ -74,21 +76,30 @@ __device__ __forceinline__ uint32_t kmer_mix(const uint32_t *w, int32_t p, int s
 // so an edge k-mer's partners as fst -- the middle entries with loc < own --
 // are [c - nE, c) and a middle k-mer's -- the edge roles with loc <= own -- are
 // [c, c + nD) (addKmerPair's orientation, KmerTable.scala:65-71; the st/md/en
-// split, :106-115).  The partition of sorted offset ps owns lst[3 ps, 3 ps + 3 n).
-// One 8-byte record per occurrence g: x = c, y = nE | nD << 15 | me << 30
-// (me = number of edge tags, 0..2).  me == 3 marks an escape: y & 0x3FFFFFFF
-// indexes the 16-byte xrec table (counts above 32,766: high-copy repeats).
-constexpr uint32_t REC_CNT_MAX = 0x7FFEu;
+// split, :106-115).  The partition of sorted offset ps owns lst[3 ps, 3 ps + 3 n),
+// so c < 3 n < 2^34 (n < 2^32 k-mers per device).
+// One 8-byte record per occurrence g: x = c mod 2^32, y = nE | nD << 14 |
+// (c >> 32) << 28 | me << 30 (me = number of edge tags, 0..2).  me == 3 marks an
+// escape: y & 0x3FFFFFFF indexes the 16-byte xrec table, which holds the
+// decoded form (counts above 16,382: high-copy repeats).
+constexpr uint32_t REC_CNT_MAX = 0x3FFEu;
+__device__ __forceinline__ uint2 encode_rec(uint64_t c, uint32_t nE, uint32_t nD, uint32_t me) {
+    return make_uint2((uint32_t)c, nE | (nD << 14) | ((uint32_t)(c >> 32) << 28) | (me << 30));
+}
+// decoded: {c mod 2^32, nE | me << 30, c >> 32, nD}
+__device__ __forceinline__ uint4 decoded_rec(uint64_t c, uint32_t nE, uint32_t nD, uint32_t me) {
+    return make_uint4((uint32_t)c, nE | (me << 30), (uint32_t)(c >> 32), nD);
+}
 __device__ __forceinline__ uint4 decode_rec(uint2 r, const uint4 *xrec) {
     if ((r.y >> 30) == 3u) return xrec[r.y & 0x3FFFFFFFu];
-    const uint32_t nE = r.y & 0x7FFFu, nD = (r.y >> 15) & 0x7FFFu;
-    return make_uint4(r.x - nE, nE | ((r.y >> 30) << 30), r.x, nD);  // {md_lo, nE | me << 30, ed_lo, nD}
+    return decoded_rec(((uint64_t)((r.y >> 28) & 3u) << 32) | r.x, r.y & 0x3FFFu, (r.y >> 14) & 0x3FFFu, r.y >> 30);
+}
+// list index of a decoded record's off-th partner entry (off < nE: the middle
+// entries [c - nE, c); then the edge roles [c, c + nD))
+__device__ __forceinline__ uint64_t rec_entry(const uint4 &rc, uint32_t off) {
+    return (((uint64_t)rc.z << 32) | rc.x) - (rc.y & 0x3FFFFFFFu) + off;
 }
 
-// Mixed read lengths: g2r[b] = the read holding occurrence b << G2R_SHIFT (the
-// largest r with occ_off[r] <= b << G2R_SHIFT), so the owner of g lies in
-// [g2r[g >> S], g2r[(g >> S) + 1]] and the binary search spans a few reads.
-constexpr int G2R_SHIFT = 10;
 
 // bit 0 = st, bit 1 = md, bit 2 = en   (KmerTable.scala:106-115)
 enum : uint8_t { TAG_ST = 1, TAG_MD = 2, TAG_EN = 4 };
@@ -191,7 +202,7 @@ hipError_t exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, uin
 size_t buckets_temp_bytes(uint64_t n);
 hipError_t build_buckets(const uint64_t *skeys, const uint32_t *svals, uint64_t n, int lb,
                          const uint8_t *tagtab, const uint64_t *occ_off, uint32_t n_reads,
-                         uint32_t uniform_npr, const uint32_t *rid, const uint32_t *g2r, Buckets &b,
+                         uint32_t uniform_npr, const uint32_t *rid, Buckets &b,
                          uint32_t *totals_dev, void *tmp, hipStream_t s);
 hipError_t build_strict_index(const uint64_t *skeys, const uint32_t *svals, uint64_t n, int lb,
                               const uint8_t *tagtab, Buckets &b, hipStream_t s);
@@ -217,11 +228,10 @@ struct PartArgs {
     const uint8_t *tagtab;
     const uint64_t *occ_off;
     uint32_t n_reads, npr;
-    const uint32_t *rid;         // read id by occurrence index (distributed mode) or null
-    const uint32_t *g2r;         // coarse occurrence -> read table (mixed lengths) or null
+    const uint32_t *rid;         // read id by occurrence index (distributed mode, mixed lengths) or null
     // sk holds 8-byte records (mix32 << 32 | occurrence index); the loc rank is
-    // re-derived: lr[g] when given (distributed mode), else from the read's
-    // length and the position (lrank[lbase[L - k] + pos])
+    // lr[g] when given (distributed mode, mixed lengths), else re-derived from
+    // the read's length and the position (lrank[lbase[L - k] + pos])
     const uint32_t *lr;
     const int32_t *len;
     const uint32_t *lbase, *lrank;
@@ -312,11 +322,10 @@ hipError_t launch_kmer_hist(const uint64_t *sorted, uint64_t n, uint32_t *flag, 
 
 // distributed (multi-GPU) glue, dist.hip
 hipError_t launch_iota(uint32_t *v, uint64_t n, hipStream_t s);
-hipError_t launch_prepare_received(uint64_t *recs, uint64_t n, const uint64_t *occ_off, uint32_t n_reads,
-                                   uint32_t npr, const int32_t *len, const uint32_t *lbase, const uint32_t *lrank,
-                                   int32_t k, uint32_t *rid, uint32_t *lr, hipStream_t s);
-hipError_t launch_read_ids(const uint32_t *g, uint64_t n, const uint64_t *occ_off, uint32_t n_reads, uint32_t npr,
-                           uint32_t *rid, hipStream_t s);
+hipError_t launch_prepare_received(uint64_t *recs, uint64_t n, const uint64_t *seg, uint32_t P,
+                                   const uint32_t *starts, const uint64_t *occ_off, uint32_t npr, const int32_t *len,
+                                   const uint32_t *lbase, const uint32_t *lrank, int32_t k, uint32_t *rid,
+                                   uint32_t *lr, hipStream_t s);
 hipError_t launch_local_offsets(const uint32_t *rid, uint64_t n, uint32_t n_reads, uint64_t *loff, hipStream_t s);
 hipError_t launch_owner_bounds(const uint64_t *keys, uint64_t n, int shift, uint32_t P, uint64_t *bounds,
                                hipStream_t s);

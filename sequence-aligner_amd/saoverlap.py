@@ -98,7 +98,7 @@ def lib():
         L.sa_dist_init.argtypes = [vp, C.c_int, C.c_int, P(C.c_uint32), P(C.c_int32)]
         L.sa_dist_local_kmers.argtypes = [vp, P(C.c_uint64)]
         L.sa_dist_emit.argtypes = [vp, vp, P(C.c_uint64)]
-        L.sa_dist_count.argtypes = [vp, vp, C.c_uint64, P(C.c_uint64)]
+        L.sa_dist_count.argtypes = [vp, vp, P(C.c_uint64), P(C.c_uint64)]
         L.sa_dist_partials.argtypes = [vp, vp, vp, vp]
         L.sa_dist_reduce.argtypes = [vp, vp, vp, vp, C.c_uint64]
         L.sa_dist_codes.argtypes = [vp, vp, vp, P(C.c_uint64)]
@@ -324,9 +324,11 @@ class Overlapper:
         self._chk(lib().sa_dist_emit(self.h, send_recs, cnt))
         return np.array(cnt[:], dtype=np.int64)
 
-    def dist_count(self, recv_recs, n):
+    def dist_count(self, recv_recs, recv_counts):
+        """recv_counts[s]: records received from rank s (concatenated in rank order)."""
         cnt = self._counts()
-        self._chk(lib().sa_dist_count(self.h, recv_recs, n, cnt))
+        rc = (C.c_uint64 * self.nranks)(*[int(x) for x in recv_counts])
+        self._chk(lib().sa_dist_count(self.h, recv_recs, rc, cnt))
         return np.array(cnt[:], dtype=np.int64)
 
     def dist_partials(self, fst, snd, cnt):

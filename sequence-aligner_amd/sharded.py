@@ -8,8 +8,9 @@ index + 1).  One build step:
 
   emit       local k-mer records, grouped by owner rank = top log2(P) bits of
              the mixed seqHash (whole buckets per owner)
-  exchange 1 all-to-all of the 8-byte records (mixed hash << 32 | global
-             occurrence index; the loc rank is re-derived by the owner)
+  exchange 1 all-to-all of the 8-byte records (mixed hash << 32 | the
+             occurrence index local to the source rank; the owner re-derives
+             read and loc rank from the source's segment of its receive buffer)
   count      owner builds its buckets and counts partial (lead, trail) pairs
              for every read over ITS buckets (KmerTable.calcPairData,
              KmerTable.scala:85-149, restricted to a hash range)
@@ -49,8 +50,8 @@ class HipWorker:
     def emit(self, send_recs):
         return self.ov.dist_emit(send_recs.data_ptr())
 
-    def count(self, recv_recs, n):
-        return self.ov.dist_count(recv_recs.data_ptr(), n)
+    def count(self, recv_recs, recv_counts):
+        return self.ov.dist_count(recv_recs.data_ptr(), recv_counts)
 
     def partials(self, fst, snd, cnt):
         self.ov.dist_partials(fst.data_ptr(), snd.data_ptr(), cnt.data_ptr())
@@ -136,7 +137,7 @@ class ShardedOverlapper:
         rk = self._buf("rk", nr, torch.int64)
         self._a2a(rk, sk, rcounts, counts)
         self._ready()
-        pcounts = w.count(rk, nr)
+        pcounts = w.count(rk, rcounts)
         npart = int(np.sum(pcounts))
         pf = self._buf("pf", npart, torch.int32)
         ps = self._buf("ps", npart, torch.int32)

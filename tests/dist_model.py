@@ -50,10 +50,10 @@ class NumpyWorker:
         return int(sum(max(len(r) - self.k + 1, 0) for r in self.reads))
 
     def emit(self, send_recs):
-        # 8-byte records: hash << 32 | global occurrence index (the owner
-        # re-derives read, position and loc from the index)
+        # 8-byte records: hash << 32 | occurrence index local to this rank (the
+        # owner re-derives read, position and loc from it and the source rank)
         recs = []
-        g = int(self.gocc[self.starts[self.rank]])
+        g = 0
         for r in self.reads:
             for i in range(len(r) - self.k + 1):
                 h = seq_hash(r[i:i + self.m])
@@ -74,9 +74,11 @@ class NumpyWorker:
         en = self.tail <= loc
         return st, md, en
 
-    def count(self, recv_recs, n):
+    def count(self, recv_recs, recv_counts):
+        n = int(np.sum(recv_counts))
         recs = recv_recs[:n].numpy().view(np.uint64)
-        g = (recs & np.uint64(0xFFFFFFFF)).astype(np.int64)
+        src = np.repeat(np.arange(self.P), np.asarray(recv_counts, dtype=np.int64))
+        g = (recs & np.uint64(0xFFFFFFFF)).astype(np.int64) + self.gocc[self.starts[src]]
         rid = np.searchsorted(self.gocc, g, side="right") - 1
         pos = g - self.gocc[rid]
         d = self.lengths[rid] - self.k
