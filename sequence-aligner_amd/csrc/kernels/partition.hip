@@ -70,98 +70,56 @@ __device__ __forceinline__ unsigned long long record_key(uint64_t rec, const Par
 constexpr int PB_THREADS = 256;
 
 
-// ---- block (256-thread) scans: wave shuffles + one LDS slot per wave ------
-__device__ __forceinline__ uint32_t blk_excl_sum(uint32_t v, uint32_t *lds) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t inc = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t t = __shfl_up(inc, off, 64);
-        if (lane >= off) inc += t;
-    }
-    if (lane == 63) lds[w] = inc;
-    __syncthreads();
-    uint32_t pre = 0;
-    for (int i = 0; i < w; ++i) pre += lds[i];
-    __syncthreads();
-    return pre + inc - v;
-}
-__device__ __forceinline__ uint32_t blk_excl_max(uint32_t v, uint32_t *lds) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t inc = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t t = __shfl_up(inc, off, 64);
-        if (lane >= off) inc = max(inc, t);
-    }
-    uint32_t ex = __shfl_up(inc, 1, 64);
-    if (lane == 0) ex = 0;
-    if (lane == 63) lds[w] = inc;
-    __syncthreads();
-    for (int i = 0; i < w; ++i) ex = max(ex, lds[i]);
-    __syncthreads();
-    return ex;
-}
-__device__ __forceinline__ uint32_t blk_excl_suffix_min(uint32_t v, uint32_t *lds) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t inc = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t t = __shfl_down(inc, off, 64);
-        if (lane + off < 64) inc = min(inc, t);
-    }
-    uint32_t ex = __shfl_down(inc, 1, 64);
-    if (lane == 63) ex = 0xFFFFFFFFu;
-    if (lane == 0) lds[w] = inc;
-    __syncthreads();
-    for (int i = w + 1; i < PB_THREADS / 64; ++i) ex = min(ex, lds[i]);
-    __syncthreads();
-    return ex;
-}
-
 template <int CAP>
 struct PartShared {
     unsigned long long key[CAP];
     uint32_t g[CAP];
     // the sort's digit counts are dead once the partition is sorted and the
     // per-item counts are only written after it: one region, and 16-bit counts
-    // (<= 2 * CAP), so the 1,024-record block fits 16.5 KB -> 8 blocks per CU
+    // (<= 2 * CAP), so the 1,024-record block fits 18.5 KB -> 8 blocks per CU
     union {
-        uint32_t cnt[4][256];    // LDS radix sort: per-wave digit counts / bases
+        struct {
+            uint32_t cnt[4][256];    // LDS radix sort: per-wave digit counts
+            uint16_t ofs[4][256];    // each wave's scatter base per digit
+        };
         struct {
             uint16_t mdx[CAP + 2];   // exclusive md count (partition-local)
             uint16_t edx[CAP + 2];   // exclusive edge-role count
         };
     };
-    uint32_t red[3][4];
-    uint32_t lbh[4], lgh[4], lnb[4];
+    uint4 agg[4];                    // per-wave inclusive aggregates of the combined block scan
+    uint2 aggu[4];
 };
 static_assert(sizeof(PartShared<1024>) <= 20480, "1,024-record block must fit 8 per CU");
 
 // Stable LSD radix sort of the partition's (key, g) in LDS over key bits
 // [0, bits): wave w owns elements [w*CAP/4, (w+1)*CAP/4) (slices of 64), ranks
 // come from a 64-lane ballot multisplit + wave-private counts, elements are held
-// in registers across the scatter, so one LDS buffer and 3 barriers per pass.
+// in registers across the scatter.  Every wave derives its own scatter bases
+// from all waves' counts (lane l: digits 4l..4l+3), so a pass has two block
+// barriers (counts complete; scatter complete).
 template <int CAP, class SH>
 __device__ __forceinline__ void lds_radix_sort(SH &S, uint32_t n, int bits) {
     constexpr int SUB = CAP / 4, SL = SUB / 64;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     for (int shift = 0; shift < bits; shift += 8) {
-        for (int q = lane; q < 256; q += 64) S.cnt[w][q] = 0;
+        reinterpret_cast<uint4 *>(S.cnt[w])[lane] = make_uint4(0, 0, 0, 0);
         unsigned long long k[SL];
-        uint32_t gv[SL], rk[SL];
+        uint32_t gv[SL], rk[SL], dg[SL];
 #pragma unroll
         for (int j = 0; j < SL; ++j) {
             const uint32_t i = w * SUB + j * 64 + lane;
             k[j] = i < n ? S.key[i] : 0ull;
             gv[j] = i < n ? S.g[i] : 0u;
         }
+        __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int j = 0; j < SL; ++j) {
             const uint32_t i = w * SUB + j * 64 + lane;
             const bool valid = i < n;
             const uint32_t d = (uint32_t)(k[j] >> shift) & 255u;
+            dg[j] = d;
             uint64_t peer = __ballot(valid);
 #pragma unroll
             for (int b = 0; b < 8; ++b) {
@@ -175,32 +133,40 @@ __device__ __forceinline__ void lds_radix_sort(SH &S, uint32_t n, int bits) {
             if (valid && (peer & lt_mask) == 0) S.cnt[w][d] = before + __popcll(peer);
             __builtin_amdgcn_wave_barrier();
         }
-        __syncthreads();
-        {   // digit tid: exclusive scan over digits, then per-wave bases in place
-            uint32_t tot = 0;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) tot += S.cnt[q][tid];
-            const uint32_t lo = blk_excl_sum(tot, S.red[0]);
-            uint32_t acc = lo;
+        __syncthreads();  // counts complete; every element is in registers
+        {
+            uint32_t tot[4] = {0, 0, 0, 0}, mine[4] = {0, 0, 0, 0};
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const uint32_t c = S.cnt[q][tid];
-                S.cnt[q][tid] = acc;
-                acc += c;
+                const uint4 c = reinterpret_cast<const uint4 *>(S.cnt[q])[lane];
+                tot[0] += c.x; tot[1] += c.y; tot[2] += c.z; tot[3] += c.w;
+                if (q < w) { mine[0] += c.x; mine[1] += c.y; mine[2] += c.z; mine[3] += c.w; }
+            }
+            const uint32_t lsum = tot[0] + tot[1] + tot[2] + tot[3];
+            uint32_t inc = lsum;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t t = __shfl_up(inc, off, 64);
+                if (lane >= off) inc += t;
+            }
+            uint32_t acc = inc - lsum;  // digits below 4 * lane, all waves
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                S.ofs[w][4 * lane + i] = (uint16_t)(acc + mine[i]);
+                acc += tot[i];
             }
         }
-        __syncthreads();
+        __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int j = 0; j < SL; ++j) {
             const uint32_t i = w * SUB + j * 64 + lane;
             if (i < n) {
-                const uint32_t d = (uint32_t)(k[j] >> shift) & 255u;
-                const uint32_t pos = S.cnt[w][d] + rk[j];
+                const uint32_t pos = S.ofs[w][dg[j]] + rk[j];
                 S.key[pos] = k[j];
                 S.g[pos] = gv[j];
             }
         }
-        __syncthreads();
+        __syncthreads();  // scatter complete; the counts may be cleared
     }
 }
 
@@ -236,7 +202,7 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
     const unsigned long long lbm = (1ull << lb) - 1;
     const uint32_t b0 = tid * IT;
     uint32_t md_c = 0, ed_c = 0, last_bh = 0, last_gh = 0, first_gh = 0xFFFFFFFFu, first_bh = 0xFFFFFFFFu;
-    bool any_bh = false, any_gh = false;
+    uint32_t n_bh = 0, n_gh = 0;
     uint32_t tagv[IT];
 #pragma unroll
     for (int j = 0; j < IT; ++j) {
@@ -250,17 +216,46 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
             const bool gh = s == 0 || S.key[s - 1] != k;
             md_c += (t & TAG_MD) ? 1u : 0u;
             ed_c += ((t & TAG_ST) ? 1u : 0u) + ((t & TAG_EN) ? 1u : 0u);
-            if (bh) { last_bh = s; any_bh = true; if (first_bh == 0xFFFFFFFFu) first_bh = s; }
-            if (gh) { last_gh = s; any_gh = true; if (first_gh == 0xFFFFFFFFu) first_gh = s; }
+            if (bh) { last_bh = s; ++n_bh; if (first_bh == 0xFFFFFFFFu) first_bh = s; }
+            if (gh) { last_gh = s; ++n_gh; if (first_gh == 0xFFFFFFFFu) first_gh = s; }
         }
     }
-    // block-wide exclusive prefix sums / prefix max and suffix min (wave shuffles + LDS)
-    const uint32_t md_ex = blk_excl_sum(md_c, S.red[0]);
-    const uint32_t ed_ex = blk_excl_sum(ed_c, S.red[1]);
-    const uint32_t bh_in = blk_excl_max(any_bh ? last_bh : 0u, S.red[2]);  // element 0 is always a head
-    const uint32_t gh_in = blk_excl_max(any_gh ? last_gh : 0u, S.lbh);
-    const uint32_t gh_next = min(blk_excl_suffix_min(first_gh, S.lgh), n);
-    const uint32_t bh_next = min(blk_excl_suffix_min(first_bh, S.lnb), n);
+    // one combined block scan (wave shuffles, one barrier): exclusive sums of
+    // (md | edge << 16) and (bucket heads | group heads << 16), exclusive prefix
+    // max of the last bucket / group head, exclusive suffix min of the first
+    // group / bucket head (element 0 is always a head; counts < 2^16)
+    uint32_t sme = md_c | (ed_c << 16), shd = n_bh | (n_gh << 16);
+    uint32_t mbh = last_bh, mgh = last_gh, ugh = first_gh, ubh = first_bh;
+    const uint32_t sme0 = sme;
+    const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t a1 = __shfl_up(sme, off, 64), a2 = __shfl_up(shd, off, 64);
+        const uint32_t a3 = __shfl_up(mbh, off, 64), a4 = __shfl_up(mgh, off, 64);
+        const uint32_t a5 = __shfl_down(ugh, off, 64), a6 = __shfl_down(ubh, off, 64);
+        if (lane >= off) { sme += a1; shd += a2; mbh = max(mbh, a3); mgh = max(mgh, a4); }
+        if (lane + off < 64) { ugh = min(ugh, a5); ubh = min(ubh, a6); }
+    }
+    if (lane == 63) S.agg[wv] = make_uint4(sme, shd, mbh, mgh);
+    if (lane == 0) S.aggu[wv] = make_uint2(ugh, ubh);
+    uint32_t xbh = __shfl_up(mbh, 1, 64), xgh = __shfl_up(mgh, 1, 64);
+    uint32_t xugh = __shfl_down(ugh, 1, 64), xubh = __shfl_down(ubh, 1, 64);
+    if (lane == 0) { xbh = 0; xgh = 0; }
+    if (lane == 63) { xugh = 0xFFFFFFFFu; xubh = 0xFFFFFFFFu; }
+    sme -= sme0;
+    __syncthreads();
+    uint32_t blk_heads = 0;
+#pragma unroll
+    for (int q = 0; q < PB_THREADS / 64; ++q) {
+        const uint4 a = S.agg[q];
+        const uint2 u = S.aggu[q];
+        blk_heads += a.y;
+        if (q < wv) { sme += a.x; xbh = max(xbh, a.z); xgh = max(xgh, a.w); }
+        if (q > wv) { xugh = min(xugh, u.x); xubh = min(xubh, u.y); }
+    }
+    const uint32_t md_ex = sme & 0xFFFFu, ed_ex = sme >> 16;
+    const uint32_t bh_in = xbh, gh_in = xgh;
+    const uint32_t gh_next = min(xugh, n), bh_next = min(xubh, n);
     // per-item exclusive counts into LDS
     {
         uint32_t m = md_ex, e = ed_ex;
@@ -290,7 +285,6 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
         }
     }
     // ---- outputs --------------------------------------------------------
-    uint32_t nb = 0, ng = 0;
     uint32_t bh = bh_in, gh = gh_in;
 #pragma unroll
     for (int j = 0; j < IT; ++j) {
@@ -299,8 +293,8 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
         const unsigned long long k = S.key[s];
         const bool isb = s == 0 || (S.key[s - 1] >> lb) != (k >> lb);
         const bool isg = s == 0 || S.key[s - 1] != k;
-        if (isb) { bh = s; ++nb; }
-        if (isg) { gh = s; ++ng; }
+        if (isb) bh = s;
+        if (isg) gh = s;
         const uint32_t t = tagv[j];
         const uint32_t code = S.g[s];
         uint32_t r, g;
@@ -351,12 +345,10 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
             }
         }
     }
-    // bucket / group counts for statistics: block-reduced, sharded
-    const uint32_t nb_blk = blk_excl_sum(nb, S.red[0]) + nb;  // inclusive for the last thread
-    const uint32_t ng_blk = blk_excl_sum(ng, S.red[1]) + ng;
-    if (tid == PB_THREADS - 1) {
-        atomicAdd(&A.counts[p % NSHARD], (unsigned long long)nb_blk);
-        atomicAdd(&A.counts[NSHARD + p % NSHARD], (unsigned long long)ng_blk);
+    // bucket / group counts for statistics (block totals of the combined scan), sharded
+    if (tid == 0) {
+        atomicAdd(&A.counts[p % NSHARD], (unsigned long long)(blk_heads & 0xFFFFu));
+        atomicAdd(&A.counts[NSHARD + p % NSHARD], (unsigned long long)(blk_heads >> 16));
     }
 }
 
