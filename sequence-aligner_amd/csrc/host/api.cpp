@@ -1508,7 +1508,8 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint6
     uint64_t np = 0, cap_s = 0;
     rc = pair_stage(c, E, PI, false, true, nullptr, N, cnt, np, cap_s, items, n_multi);
     if (rc) return rc;
-    // partials grouped by the rank owning their lead: ascending (lead, trail)
+    // partials grouped by the rank owning their lead (one stable pass on the
+    // owner id; the owner's reduce sorts them)
     uint64_t *ok, *ok2; uint32_t *ov, *ov2; uint8_t *otmp; uint64_t *bounds;
     ENSURE(c->d_okeys, np, &ok);
     ENSURE(c->d_okeys2, np, &ok2);
@@ -1521,10 +1522,10 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint6
     {
         StageScope st(c, SA_STAGE_ORDER);
         HIPCHK(launch_make_order_keys((const uint32_t *)c->d_pf.p, (const uint32_t *)c->d_ps.p, nullptr, cnt->cursor,
-                                      cap_s, 2, idb, ok, ov, cnt->shard_off, c->stream));
-        HIPCHK(radix_sort(&ok, &ov, &ok2, &ov2, np, 0, 2 * idb, otmp, c->stream));
-        if (np) HIPCHK(launch_lead_bounds(ok, np, idb, (const uint32_t *)c->d_starts.p, (uint32_t)c->nranks, bounds,
-                                          c->stream));
+                                      cap_s, 3, idb, ok, ov, cnt->shard_off, c->stream,
+                                      (const uint32_t *)c->d_starts.p, (uint32_t)c->nranks));
+        HIPCHK(radix_sort(&ok, &ov, &ok2, &ov2, np, 0, std::max(c->log_ranks, 1), otmp, c->stream));
+        if (np) HIPCHK(launch_owner_bounds(ok, np, 0, (uint32_t)c->nranks, bounds, c->stream));
     }
     Counters hc;
     HIPCHK(hipMemcpyAsync(&hc, cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));

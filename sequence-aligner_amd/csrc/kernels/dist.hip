@@ -88,21 +88,6 @@ __global__ void owner_bounds_kernel(const uint64_t *keys, uint64_t n, int shift,
     bounds[o] = lo;
 }
 
-// partial pairs keyed (lead << idb | trail), ascending: bounds[o] = first entry
-// whose lead >= starts[o] (the first read of rank o)
-__global__ void lead_bounds_kernel(const uint64_t *keys, uint64_t n, int idb, const uint32_t *starts, uint32_t P,
-                                   uint64_t *bounds) {
-    const uint32_t o = threadIdx.x;
-    if (o > P) return;
-    const uint64_t s = starts[o];
-    uint64_t lo = 0, hi = n;
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if ((keys[mid] >> idb) < s) lo = mid + 1; else hi = mid;
-    }
-    bounds[o] = lo;
-}
-
 __global__ void gather_partials_kernel(const uint32_t *perm, uint64_t n, const uint32_t *fst, const uint32_t *snd,
                                        const uint32_t *cnt, uint32_t *of, uint32_t *os, uint32_t *oc) {
     const uint64_t i = (uint64_t)blockIdx.x * DT + threadIdx.x;
@@ -189,13 +174,6 @@ hipError_t launch_local_offsets(const uint32_t *rid, uint64_t n, uint32_t n_read
 hipError_t launch_owner_bounds(const uint64_t *keys, uint64_t n, int shift, uint32_t P, uint64_t *bounds,
                                hipStream_t s) {
     hipLaunchKernelGGL(owner_bounds_kernel, dim3(1), dim3(((P + 1 + 63) / 64) * 64), 0, s, keys, n, shift, P,
-                       bounds);
-    return hipGetLastError();
-}
-
-hipError_t launch_lead_bounds(const uint64_t *keys, uint64_t n, int idb, const uint32_t *starts, uint32_t P,
-                              uint64_t *bounds, hipStream_t s) {
-    hipLaunchKernelGGL(lead_bounds_kernel, dim3(1), dim3(((P + 1 + 63) / 64) * 64), 0, s, keys, n, idb, starts, P,
                        bounds);
     return hipGetLastError();
 }

@@ -619,7 +619,8 @@ __global__ void shard_offsets_kernel(const unsigned long long *cursor, unsigned 
 
 __global__ void make_order_keys_kernel(const uint32_t *fst, const uint32_t *snd, const uint64_t *rank,
                                        const unsigned long long *cursor, unsigned long long cap_s, int by_rank,
-                                       int idbits, uint64_t *keys, uint32_t *vals, const uint32_t *off) {
+                                       int idbits, uint64_t *keys, uint32_t *vals, const uint32_t *off,
+                                       const uint32_t *starts, uint32_t P) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // region-space index
     const uint32_t shard = (uint32_t)(i / cap_s);
     if (shard >= NSHARD) return;
@@ -629,21 +630,31 @@ __global__ void make_order_keys_kernel(const uint32_t *fst, const uint32_t *snd,
     // wide: lead descending then trail ascending; strict: first-occurrence rank
     const uint64_t top = (1ull << idbits) - 1;
     // by_rank 0: lead descending, trail ascending (wide canonical order);
-    // 1: first-occurrence rank (strict); 2: lead ascending (distributed send side)
-    keys[pos] = by_rank == 1 ? rank[i]
-              : by_rank == 2 ? (((uint64_t)fst[i] << idbits) | snd[i])
-                             : (((top - fst[i]) << idbits) | snd[i]);
+    // 1: first-occurrence rank (strict); 3: the rank owning the lead (distributed
+    // send side: starts[P + 1], largest o with starts[o] <= lead)
+    uint64_t key;
+    if (by_rank == 3) {
+        uint32_t lo = 0, hi = P;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (starts[mid] <= fst[i]) lo = mid; else hi = mid;
+        }
+        key = lo;
+    } else {
+        key = by_rank == 1 ? rank[i] : (((top - fst[i]) << idbits) | snd[i]);
+    }
+    keys[pos] = key;
     vals[pos] = (uint32_t)i;
 }
 
 hipError_t launch_make_order_keys(const uint32_t *fst, const uint32_t *snd, const uint64_t *rank,
                                   const unsigned long long *cursor, unsigned long long cap_s, int by_rank,
                                   int idbits, uint64_t *keys, uint32_t *vals, uint32_t *shard_off,
-                                  hipStream_t s) {
+                                  hipStream_t s, const uint32_t *starts, uint32_t P) {
     hipLaunchKernelGGL(shard_offsets_kernel, dim3(1), dim3(64), 0, s, cursor, cap_s, shard_off);
     const uint64_t tot = (uint64_t)NSHARD * cap_s;
     hipLaunchKernelGGL(make_order_keys_kernel, dim3((uint32_t)((tot + 255) / 256)), dim3(256), 0, s, fst, snd, rank,
-                       cursor, cap_s, by_rank, idbits, keys, vals, (const uint32_t *)shard_off);
+                       cursor, cap_s, by_rank, idbits, keys, vals, (const uint32_t *)shard_off, starts, P);
     return hipGetLastError();
 }
 

@@ -273,7 +273,7 @@ hipError_t launch_records_from_tables(const uint64_t *sk, const uint32_t *sv, ui
 hipError_t launch_make_order_keys(const uint32_t *fst, const uint32_t *snd, const uint64_t *rank,
                                   const unsigned long long *cursor, unsigned long long cap_s, int by_rank,
                                   int idbits, uint64_t *keys, uint32_t *vals, uint32_t *shard_off,
-                                  hipStream_t s);
+                                  hipStream_t s, const uint32_t *starts = nullptr, uint32_t P = 0);
 hipError_t launch_gather_pairs(const uint32_t *perm, uint64_t n, const uint32_t *fst, const uint32_t *snd,
                                const uint32_t *cnt, int32_t *lead, int32_t *trail, int32_t *count,
                                hipStream_t s);
@@ -329,8 +329,6 @@ hipError_t launch_prepare_received(uint64_t *recs, uint64_t n, const uint64_t *s
 hipError_t launch_local_offsets(const uint32_t *rid, uint64_t n, uint32_t n_reads, uint64_t *loff, hipStream_t s);
 hipError_t launch_owner_bounds(const uint64_t *keys, uint64_t n, int shift, uint32_t P, uint64_t *bounds,
                                hipStream_t s);
-hipError_t launch_lead_bounds(const uint64_t *keys, uint64_t n, int idb, const uint32_t *starts, uint32_t P,
-                              uint64_t *bounds, hipStream_t s);
 hipError_t launch_gather_partials(const uint32_t *perm, uint64_t n, const uint32_t *fst, const uint32_t *snd,
                                   const uint32_t *cnt, uint32_t *of, uint32_t *os, uint32_t *oc, hipStream_t s);
 hipError_t launch_reduce_keys(const uint32_t *fst, const uint32_t *snd, uint64_t n, int idb, uint64_t *keys,
