@@ -278,7 +278,7 @@ EmitParams emit_params(sa_ctx *c) {
     e.rkey = nullptr;
     e.rord = nullptr;
     e.pos_bits = 0;
-    e.occ_rid = e.occ_lr = nullptr;
+    e.occ_rl = nullptr;
     return e;
 }
 
@@ -309,7 +309,7 @@ int ensure_prepared(sa_ctx *c) {
 // for partitions too large for LDS.  Read ids come from rid[val] when given
 // (distributed mode), else from the occurrence offsets.
 int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, uint32_t *vals2, uint64_t n,
-                 const uint64_t *occ_off, uint32_t n_reads, uint32_t npr, const uint32_t *rid, const uint32_t *lr,
+                 const uint64_t *occ_off, uint32_t n_reads, uint32_t npr, const uint2 *rl,
                  const int32_t *len, bool strict, void *stmp, Counters *cnt, PartArgs &PA,
                  unsigned long long &big_buckets, int skip_bits = 0) {
     // keys: 8-byte records (mix32 << 32 | occurrence index); vals / vals2: u32
@@ -337,13 +337,12 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
     PA.sk = keys; PA.sv = nullptr; PA.start = pstart; PA.np = nparts; PA.lb = c->lb; PA.sort_bits = kbits - skip_bits - PB;
     PA.tagtab = (const uint8_t *)c->d_tagtab.p;
     PA.occ_off = occ_off;
-    PA.n_reads = n_reads; PA.npr = npr; PA.rid = rid;
-    PA.lr = lr;
+    PA.n_reads = n_reads; PA.npr = npr; PA.rl = rl;
     PA.len = len;
     PA.lbase = (const uint32_t *)c->d_lbase.p;
     PA.lrank = (const uint32_t *)c->d_lrank.p;
     PA.k = c->set.kmer_size;
-    PA.pos_bits = rid ? 0 : c->pos_bits;  // (occurrence indices + rid / lr tables)
+    PA.pos_bits = rl ? 0 : c->pos_bits;  // (occurrence indices + the {read, loc rank} table)
     PA.meta = (const uint2 *)c->d_meta.p;
     ENSURE(c->d_md, 3 * n + 3, &PA.lst);
     ENSURE(c->d_rec, n + 1, &PA.rec);
@@ -428,7 +427,7 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
                 HIPCHK(hipMemcpyAsync(vals + ps, v0, (size_t)pn * 4, hipMemcpyDeviceToDevice, c->stream));
             }
             B.n_occ = pn;
-            HIPCHK(build_buckets(keys2 + ps, vals + ps, pn, c->lb, tagtab, PA.occ_off, n_reads, npr, rid, B,
+            HIPCHK(build_buckets(keys2 + ps, vals + ps, pn, c->lb, tagtab, PA.occ_off, n_reads, npr, rl, B,
                                  bigtot + 4 * (size_t)bi, btmp, c->stream));
             if (strict) HIPCHK(build_strict_index(keys2 + ps, vals + ps, pn, c->lb, tagtab, B, c->stream));
             HIPCHK(launch_relayout_lists(B, ps, pn, bigtot + 4 * (size_t)bi, PA, strict, c->stream));
@@ -657,12 +656,10 @@ int device_build(sa_ctx *c, bool readback) {
     // mixed lengths without (read, pos) codes (too many reads, or strict ids):
     // the emit kernel also writes each occurrence's read and loc rank, so the
     // bucket build looks both up with one load each instead of a search
-    uint32_t *orid = nullptr, *olr = nullptr;
+    uint2 *orl = nullptr;
     if (c->uniform_npr == 0 && c->pos_bits == 0) {
-        ENSURE(c->d_rid, n + 1, &orid);
-        ENSURE(c->d_lr, n + 1, &olr);
-        E.occ_rid = orid;
-        E.occ_lr = olr;
+        ENSURE(c->d_rl, n + 1, &orl);
+        E.occ_rl = orl;
     }
     {
         StageScope st(c, SA_STAGE_EMIT);
@@ -674,7 +671,7 @@ int device_build(sa_ctx *c, bool readback) {
     PartArgs PA{};
     unsigned long long big_buckets = 0;
     rc = bucket_stage(c, keys, keys2, vals, vals2, n, (const uint64_t *)c->d_occ_off.p, nr, c->uniform_npr,
-                      orid, olr, (const int32_t *)c->d_len.p, strict, stmp, cnt, PA, big_buckets);
+                      orl, (const int32_t *)c->d_len.p, strict, stmp, cnt, PA, big_buckets);
     if (rc) return rc;
     if (strict) {
         // KmerData iteration rank of every bucket: replay its Trove layout over the
@@ -1071,7 +1068,7 @@ void sa_ctx_destroy(sa_ctx *c) {
                     &c->d_gmds, &c->d_gede, &c->d_ogid, &c->d_bkttmp, &c->d_mdidx, &c->d_edidx, &c->d_occidx,
                     &c->d_bnst, &c->d_brank, &c->d_bhash, &c->d_bfirst, &c->d_pf, &c->d_ps, &c->d_pc, &c->d_pr,
                     &c->d_ovl, &c->d_cnt, &c->d_okeys, &c->d_ovals, &c->d_okeys2, &c->d_ovals2, &c->d_osort,
-                    &c->d_lead, &c->d_trail, &c->d_count, &c->d_aln, &c->d_p1, &c->d_tb, &c->d_rkey, &c->d_rkey2, &c->d_rord, &c->d_rord2, &c->d_rtmp, &c->d_gocc, &c->d_seg, &c->d_rid, &c->d_loff, &c->d_starts, &c->d_bounds, &c->d_gcodes, &c->d_gwoff, &c->d_glen, &c->d_gbad, &c->d_psum, &c->d_pkeep, &c->d_ppos, &c->d_scan, &c->d_lr, &c->d_pstart, &c->d_biglist, &c->d_rec,
+                    &c->d_lead, &c->d_trail, &c->d_count, &c->d_aln, &c->d_p1, &c->d_tb, &c->d_rkey, &c->d_rkey2, &c->d_rord, &c->d_rord2, &c->d_rtmp, &c->d_gocc, &c->d_seg, &c->d_rl, &c->d_loff, &c->d_starts, &c->d_bounds, &c->d_gcodes, &c->d_gwoff, &c->d_glen, &c->d_gbad, &c->d_psum, &c->d_pkeep, &c->d_ppos, &c->d_scan, &c->d_pstart, &c->d_biglist, &c->d_rec,
                     &c->d_srec, &c->d_bnmd, &c->d_ishead, &c->d_bnst2, &c->d_tmd, &c->d_ted, &c->d_tmdi,
                     &c->d_tedi, &c->d_xrec, &c->d_tier, &c->d_ovlrp, &c->d_meta, &c->d_items, &c->d_bigtot, &c->d_hk0, &c->d_hk1, &c->d_hflag,
                     &c->d_hidx, &c->d_hpos, &c->d_htmp, &c->d_hist, &c->d_hovf, &c->d_hsmall,
@@ -1469,11 +1466,10 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint6
     HIPCHK(hipMemsetAsync(cnt, 0, sizeof(Counters), c->stream));
     // received records are in global occurrence order (sources in rank order,
     // each in occurrence order): local index i <-> i-th owned occurrence
-    uint32_t *rid, *lr, *vals, *vals2; uint64_t *loff, *keys2, *dseg; uint8_t *stmp;
+    uint2 *rl; uint32_t *vals, *vals2; uint64_t *loff, *keys2, *dseg; uint8_t *stmp;
     ENSURE(c->d_seg, seg.size(), &dseg);
     HIPCHK(hipMemcpyAsync(dseg, seg.data(), seg.size() * 8, hipMemcpyHostToDevice, c->stream));
-    ENSURE(c->d_rid, n, &rid);
-    ENSURE(c->d_lr, n, &lr);
+    ENSURE(c->d_rl, n, &rl);
     ENSURE(c->d_loff, (size_t)N + 1, &loff);
     ENSURE(c->d_vals, n, &vals);
     ENSURE(c->d_vals2, n, &vals2);
@@ -1487,12 +1483,12 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint6
         HIPCHK(launch_prepare_received(keys, n, dseg, (uint32_t)P, (const uint32_t *)c->d_starts.p,
                                        (const uint64_t *)c->d_gocc.p, c->gnpr,
                                        (const int32_t *)c->d_glen.p, (const uint32_t *)c->d_lbase.p,
-                                       (const uint32_t *)c->d_lrank.p, c->set.kmer_size, rid, lr, c->stream));
-        HIPCHK(launch_local_offsets(rid, n, N, loff, c->stream));
+                                       (const uint32_t *)c->d_lrank.p, c->set.kmer_size, rl, c->stream));
+        HIPCHK(launch_local_offsets(rl, n, N, loff, c->stream));
     }
     PartArgs PA{};
     unsigned long long big_buckets = 0;
-    rc = bucket_stage(c, keys, keys2, vals, vals2, n, loff, N, 0, rid, lr, nullptr, false, stmp, cnt, PA,
+    rc = bucket_stage(c, keys, keys2, vals, vals2, n, loff, N, 0, rl, nullptr, false, stmp, cnt, PA,
                       big_buckets, c->log_ranks);
     if (rc) return rc;
     PairIn PI{};

@@ -103,8 +103,8 @@ __global__ __launch_bounds__(BK_THREADS) void bk_partials_kernel(U4 *partial, ui
 }
 
 __device__ __forceinline__ uint32_t read_of(uint32_t g, const uint64_t *occ_off, uint32_t n_reads,
-                                            uint32_t npr, const uint32_t *rid) {
-    if (rid) return rid[g];  // occurrence table (distributed mode, mixed lengths)
+                                            uint32_t npr, const uint2 *rl) {
+    if (rl) return rl[g].x;  // occurrence table (distributed mode, mixed lengths)
     if (npr) return g / npr;
     uint32_t lo = 0, hi = n_reads;  // largest r with occ_off[r] <= g
     while (hi - lo > 1) {
@@ -117,7 +117,7 @@ __device__ __forceinline__ uint32_t read_of(uint32_t g, const uint64_t *occ_off,
 __global__ __launch_bounds__(BK_THREADS) void bk_down_kernel(const uint64_t *sk, const uint32_t *sv, uint64_t n,
                                                              int lb, const uint8_t *tagtab,
                                                              const uint64_t *occ_off, uint32_t n_reads,
-                                                             uint32_t npr, const uint32_t *rid, const U4 *partial,
+                                                             uint32_t npr, const uint2 *rl, const U4 *partial,
                                                              Buckets b) {
     __shared__ U4 lds4[4];
     const uint64_t base = (uint64_t)blockIdx.x * BK_TILE + (uint64_t)threadIdx.x * BK_ITEMS;
@@ -143,7 +143,7 @@ __global__ __launch_bounds__(BK_THREADS) void bk_down_kernel(const uint64_t *sk,
         const uint32_t bid = ex.x + F.bhead - 1;
         const uint32_t gid = ex.y + F.ghead - 1;
         const uint32_t g = sv[i];
-        const uint32_t r = read_of(g, occ_off, n_reads, npr, rid);
+        const uint32_t r = read_of(g, occ_off, n_reads, npr, rl);
         if (F.md) b.md_list[ex.z] = r;
         if (F.st) b.ed_list[ex.w] = r;
         if (F.en) b.ed_list[ex.w + F.st] = r;
@@ -168,7 +168,7 @@ size_t buckets_temp_bytes(uint64_t n) {
 
 hipError_t build_buckets(const uint64_t *skeys, const uint32_t *svals, uint64_t n, int lb,
                          const uint8_t *tagtab, const uint64_t *occ_off, uint32_t n_reads,
-                         uint32_t uniform_npr, const uint32_t *rid, Buckets &b,
+                         uint32_t uniform_npr, const uint2 *rl, Buckets &b,
                          uint32_t *totals_dev, void *tmp, hipStream_t s) {
     if (n == 0) return hipMemsetAsync(totals_dev, 0, 4 * sizeof(uint32_t), s);
     const uint64_t nb = (n + BK_TILE - 1) / BK_TILE;
@@ -176,7 +176,7 @@ hipError_t build_buckets(const uint64_t *skeys, const uint32_t *svals, uint64_t 
     hipLaunchKernelGGL(bk_reduce_kernel, dim3((uint32_t)nb), dim3(BK_THREADS), 0, s, skeys, n, lb, tagtab, partial);
     hipLaunchKernelGGL(bk_partials_kernel, dim3(1), dim3(BK_THREADS), 0, s, partial, (uint32_t)nb, totals_dev);
     hipLaunchKernelGGL(bk_down_kernel, dim3((uint32_t)nb), dim3(BK_THREADS), 0, s, skeys, svals, n, lb, tagtab,
-                       occ_off, n_reads, uniform_npr, rid, (const U4 *)partial, b);
+                       occ_off, n_reads, uniform_npr, rl, (const U4 *)partial, b);
     return hipGetLastError();
 }
 

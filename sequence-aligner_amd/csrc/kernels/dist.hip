@@ -29,12 +29,12 @@ __global__ void iota_kernel(uint32_t *v, uint64_t n) {
 // received 8-byte records (mix << 32 | occurrence index local to the source
 // rank): seg[s] = first record from source s (s < P, seg[P] = n), seg[P+1+s] =
 // the global occurrence index of source s's first k-mer, starts[s] its first
-// read.  rid[i] = read of the occurrence, lr[i] = its loc rank
-// (lrank[lbase[L - k] + pos]); the low word becomes i
+// read.  rl[i] = {read of the occurrence, its loc rank (lrank[lbase[L - k] +
+// pos])}; the low word becomes i
 __global__ void prepare_received_kernel(uint64_t *recs, uint64_t n, const uint64_t *seg, uint32_t P,
                                         const uint32_t *starts, const uint64_t *occ_off, uint32_t npr,
                                         const int32_t *len, const uint32_t *lbase, const uint32_t *lrank, int32_t k,
-                                        uint32_t *rid, uint32_t *lr) {
+                                        uint2 *rl) {
     const uint64_t i = (uint64_t)blockIdx.x * DT + threadIdx.x;
     if (i >= n) return;
     uint32_t s = 0, hi = P;  // the source whose segment holds i
@@ -58,20 +58,19 @@ __global__ void prepare_received_kernel(uint64_t *recs, uint64_t n, const uint64
         r = lo;
         pos = (uint32_t)(g - occ_off[r]);
     }
-    rid[i] = r;
-    lr[i] = lrank[lbase[len[r] - k] + pos];
+    rl[i] = make_uint2(r, lrank[lbase[(npr ? (int32_t)npr + k - 1 : len[r]) - k] + pos]);
     recs[i] = (rec & 0xFFFFFFFF00000000ull) | (uint32_t)i;
 }
 
-// loff[a] = first i with rid[i] >= a, for a in [0, n_reads] (rid ascending):
+// loff[a] = first i with rl[i].x >= a, for a in [0, n_reads] (reads ascending):
 // the local occurrences of read a are [loff[a], loff[a+1])
-__global__ void local_offsets_kernel(const uint32_t *rid, uint64_t n, uint32_t n_reads, uint64_t *loff) {
+__global__ void local_offsets_kernel(const uint2 *rl, uint64_t n, uint32_t n_reads, uint64_t *loff) {
     const uint64_t a = (uint64_t)blockIdx.x * DT + threadIdx.x;
     if (a > n_reads) return;
     uint64_t lo = 0, hi = n;
     while (lo < hi) {
         const uint64_t mid = (lo + hi) >> 1;
-        if (rid[mid] < a) lo = mid + 1; else hi = mid;
+        if (rl[mid].x < a) lo = mid + 1; else hi = mid;
     }
     loff[a] = lo;
 }
@@ -158,16 +157,16 @@ hipError_t launch_iota(uint32_t *v, uint64_t n, hipStream_t s) {
 
 hipError_t launch_prepare_received(uint64_t *recs, uint64_t n, const uint64_t *seg, uint32_t P,
                                    const uint32_t *starts, const uint64_t *occ_off, uint32_t npr, const int32_t *len,
-                                   const uint32_t *lbase, const uint32_t *lrank, int32_t k, uint32_t *rid,
-                                   uint32_t *lr, hipStream_t s) {
+                                   const uint32_t *lbase, const uint32_t *lrank, int32_t k, uint2 *rl,
+                                   hipStream_t s) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(prepare_received_kernel, grid_for(n), dim3(DT), 0, s, recs, n, seg, P, starts, occ_off, npr,
-                       len, lbase, lrank, k, rid, lr);
+                       len, lbase, lrank, k, rl);
     return hipGetLastError();
 }
 
-hipError_t launch_local_offsets(const uint32_t *rid, uint64_t n, uint32_t n_reads, uint64_t *loff, hipStream_t s) {
-    hipLaunchKernelGGL(local_offsets_kernel, grid_for((uint64_t)n_reads + 1), dim3(DT), 0, s, rid, n, n_reads, loff);
+hipError_t launch_local_offsets(const uint2 *rl, uint64_t n, uint32_t n_reads, uint64_t *loff, hipStream_t s) {
+    hipLaunchKernelGGL(local_offsets_kernel, grid_for((uint64_t)n_reads + 1), dim3(DT), 0, s, rl, n, n_reads, loff);
     return hipGetLastError();
 }
 

@@ -88,7 +88,7 @@ __global__ __launch_bounds__(256) void kmer_emit_kernel(DevReads r, EmitParams e
         }
         const uint32_t *w = r.codes + r.woff[rd];
         const uint64_t g0 = e.occ_off[rd];
-        const uint32_t *lr = e.occ_rid ? e.lrank + e.lbase[nk - 1] : nullptr;
+        const uint32_t *lr = e.occ_rl ? e.lrank + e.lbase[nk - 1] : nullptr;
         uint32_t kmin = 0xFFFFFFFFu;
         for (int32_t i = lane; i < nk; i += 64) {
             const uint32_t h = kmer_mix(w, i, shift);
@@ -98,10 +98,7 @@ __global__ __launch_bounds__(256) void kmer_emit_kernel(DevReads r, EmitParams e
             // needed, partition.hip)
             const uint32_t occ = e.pos_bits ? (rd << e.pos_bits) | (uint32_t)i : (uint32_t)(g0 + i);
             keys[g0 + i] = ((uint64_t)h << 32) | (uint64_t)occ;
-            if (e.occ_rid) {
-                e.occ_rid[g0 + i] = rd;
-                e.occ_lr[g0 + i] = lr[i];
-            }
+            if (e.occ_rl) e.occ_rl[g0 + i] = make_uint2(rd, lr[i]);
         }
         if (e.rkey) {
             // locality key: reads sharing their minimum k-mer overlap, so sorting

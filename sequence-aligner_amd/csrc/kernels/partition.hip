@@ -26,9 +26,7 @@
 
 namespace sa {
 
-__device__ __forceinline__ uint32_t read_of_g(uint32_t g, const uint64_t *occ_off, uint32_t n_reads, uint32_t npr,
-                                              const uint32_t *rid) {
-    if (rid) return rid[g];  // occurrence table (distributed mode, mixed lengths)
+__device__ __forceinline__ uint32_t read_of_g(uint32_t g, const uint64_t *occ_off, uint32_t n_reads, uint32_t npr) {
     if (npr) return g / npr;
     uint32_t lo = 0, hi = n_reads;  // largest r with occ_off[r] <= g
     while (hi - lo > 1) {
@@ -45,18 +43,23 @@ __device__ __forceinline__ uint64_t load_sk(const uint64_t *p) { return __builti
 // sort key (mix << lb | loc rank) and occurrence code of an 8-byte record: the
 // occurrence index g, or (pos_bits > 0: mixed read lengths) read << pos_bits |
 // pos, whose read meta {first occurrence, loc-rank base} gives g and the loc
-// rank with one load (instead of a search over the occurrence offsets)
-__device__ __forceinline__ unsigned long long record_key(uint64_t rec, const PartArgs &A, uint32_t &code) {
+// rank with one load (instead of a search over the occurrence offsets); with
+// an occurrence table (rl) its one 8-byte load gives the loc rank and the read
+// (rr, else untouched)
+__device__ __forceinline__ unsigned long long record_key(uint64_t rec, const PartArgs &A, uint32_t &code,
+                                                         uint32_t &rr) {
     code = (uint32_t)rec;
     const uint32_t g = code;
     uint32_t lr;
     if (A.pos_bits) {
         const uint32_t pos = code & ((1u << A.pos_bits) - 1u);
         lr = A.lrank[A.meta[code >> A.pos_bits].y + pos];
-    } else if (A.lr) {
-        lr = A.lr[g];
+    } else if (A.rl) {
+        const uint2 v = A.rl[g];
+        lr = v.y;
+        rr = v.x;
     } else {
-        const uint32_t r = read_of_g(g, A.occ_off, A.n_reads, A.npr, nullptr);
+        const uint32_t r = read_of_g(g, A.occ_off, A.n_reads, A.npr);
         const uint32_t pos = A.npr ? g - r * A.npr : g - (uint32_t)A.occ_off[r];
         const int32_t d = A.npr ? (int32_t)A.npr - 1 : A.len[r] - A.k;
         lr = A.lrank[A.lbase[d] + pos];
@@ -73,7 +76,8 @@ constexpr int PB_THREADS = 256;
 template <int CAP>
 struct PartShared {
     unsigned long long key[CAP];
-    uint32_t g[CAP];
+    uint32_t g[CAP];                 // occurrence code of load slot i
+    uint16_t oi[CAP];                // load slot of sorted item s (moves with the key)
     // the sort's digit counts are dead once the partition is sorted and the
     // per-item counts are only written after it: one region, and 16-bit counts
     // (<= 2 * CAP), so the 1,024-record block fits 18.5 KB -> 8 blocks per CU
@@ -85,14 +89,15 @@ struct PartShared {
         struct {
             uint16_t mdx[CAP + 2];   // exclusive md count (partition-local)
             uint16_t edx[CAP + 2];   // exclusive edge-role count
+            uint4 agg[4];            // per-wave inclusive aggregates of the combined block scan
+            uint2 aggu[4];
         };
     };
-    uint4 agg[4];                    // per-wave inclusive aggregates of the combined block scan
-    uint2 aggu[4];
 };
+// (with an occurrence table, a u32 read per load slot follows in dynamic LDS)
 static_assert(sizeof(PartShared<1024>) <= 20480, "1,024-record block must fit 8 per CU");
 
-// Stable LSD radix sort of the partition's (key, g) in LDS over key bits
+// Stable LSD radix sort of the partition's (key, load slot) in LDS over key bits
 // [0, bits): wave w owns elements [w*CAP/4, (w+1)*CAP/4) (slices of 64), ranks
 // come from a 64-lane ballot multisplit + wave-private counts, elements are held
 // in registers across the scatter.  Every wave derives its own scatter bases
@@ -111,7 +116,7 @@ __device__ __forceinline__ void lds_radix_sort(SH &S, uint32_t n, int bits) {
         for (int j = 0; j < SL; ++j) {
             const uint32_t i = w * SUB + j * 64 + lane;
             k[j] = i < n ? S.key[i] : 0ull;
-            gv[j] = i < n ? S.g[i] : 0u;
+            gv[j] = i < n ? S.oi[i] : 0u;
         }
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -163,7 +168,7 @@ __device__ __forceinline__ void lds_radix_sort(SH &S, uint32_t n, int bits) {
             if (i < n) {
                 const uint32_t pos = S.ofs[w][dg[j]] + rk[j];
                 S.key[pos] = k[j];
-                S.g[pos] = gv[j];
+                S.oi[pos] = (uint16_t)gv[j];
             }
         }
         __syncthreads();  // scatter complete; the counts may be cleared
@@ -175,7 +180,8 @@ __device__ __forceinline__ void lds_radix_sort(SH &S, uint32_t n, int bits) {
 // pass lists its overflow for the 4,096-record pass (mid2_list), and that one
 // lists the partitions above 4,096 for the global path (big_list).
 template <int CAP, bool STRICT>
-__device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t p, PartShared<CAP> &S) {
+__device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t p, PartShared<CAP> &S,
+                                               uint32_t *Sr) {
     constexpr int IT = CAP / PB_THREADS;
     const int tid = threadIdx.x;
     const uint32_t ps = A.start[p], pe = A.start[p + 1];
@@ -191,9 +197,11 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
     }
     // ---- load, then stable LDS radix sort on the key bits below the partition id
     for (uint32_t i = tid; i < n; i += PB_THREADS) {
-        uint32_t g;
-        S.key[i] = record_key(load_sk(A.sk + ps + i), A, g);
+        uint32_t g, r = 0;
+        S.key[i] = record_key(load_sk(A.sk + ps + i), A, g, r);
         S.g[i] = g;
+        S.oi[i] = (uint16_t)i;
+        if (Sr) Sr[i] = r;
     }
     __syncthreads();
     lds_radix_sort<CAP>(S, n, A.sort_bits);
@@ -296,14 +304,15 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
         if (isb) bh = s;
         if (isg) gh = s;
         const uint32_t t = tagv[j];
-        const uint32_t code = S.g[s];
+        const uint32_t slot = S.oi[s];
+        const uint32_t code = S.g[slot];
         uint32_t r, g;
         if (A.pos_bits) {  // read << pos_bits | pos (record_key)
             r = code >> A.pos_bits;
             g = A.meta[r].x + (code & ((1u << A.pos_bits) - 1u));
         } else {
             g = code;
-            r = read_of_g(g, A.occ_off, A.n_reads, A.npr, A.rid);
+            r = Sr ? Sr[slot] : read_of_g(g, A.occ_off, A.n_reads, A.npr);
         }
         const uint32_t st = (t & TAG_ST) ? 1u : 0u, en = (t & TAG_EN) ? 1u : 0u, md = (t & TAG_MD) ? 1u : 0u;
         // split point of the bucket [bh, nextb): its md entries end at c
@@ -323,7 +332,7 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
             uint32_t nst = 0, nmd = 0, nen = 0, st_tot = 0, md_tot = 0, gmin = 0xFFFFFFFFu;
             for (uint32_t q = bh; q < be; ++q) {
                 const uint32_t tq = A.tagtab[S.key[q] & lbm];
-                const uint32_t gq = S.g[q];
+                const uint32_t gq = S.g[S.oi[q]];
                 st_tot += (tq & TAG_ST) ? 1u : 0u;
                 md_tot += (tq & TAG_MD) ? 1u : 0u;
                 gmin = min(gmin, gq);
@@ -361,14 +370,15 @@ template <int CAP, bool STRICT>
 __global__ __launch_bounds__(PB_THREADS) void part_build_kernel(PartArgs A) {
     extern __shared__ __align__(16) uint8_t smem_raw[];
     PartShared<CAP> &S = *reinterpret_cast<PartShared<CAP> *>(smem_raw);
+    uint32_t *Sr = A.rl ? reinterpret_cast<uint32_t *>(smem_raw + sizeof(PartShared<CAP>)) : nullptr;
     if constexpr (CAP < 2048) {
-        part_build_one<CAP, STRICT>(A, blockIdx.x, S);
+        part_build_one<CAP, STRICT>(A, blockIdx.x, S, Sr);
     } else {
         const uint32_t *list = CAP >= 4096 ? A.mid2_list : A.mid_list;
         const uint32_t m = *(CAP >= 4096 ? A.mid2_n : A.mid_n);
         for (uint32_t i = blockIdx.x; i < m; i += gridDim.x) {
             __syncthreads();  // LDS of the previous partition fully consumed
-            part_build_one<CAP, STRICT>(A, list[i], S);
+            part_build_one<CAP, STRICT>(A, list[i], S, Sr);
         }
     }
 }
@@ -485,7 +495,7 @@ hipError_t launch_part_build(const PartArgs &a, bool strict, hipStream_t s) {
     if (!a.np) return hipSuccess;
 #define PB_LAUNCH(CAPV, GRID, ST)                                                                          \
     do {                                                                                                 \
-        const size_t lds = part_lds<CAPV>();                                                             \
+        const size_t lds = part_lds<CAPV>() + (a.rl ? 4 * (size_t)(CAPV) : 0);                           \
         (void)hipFuncSetAttribute((const void *)part_build_kernel<CAPV, ST>,                             \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                 \
         hipLaunchKernelGGL((part_build_kernel<CAPV, ST>), dim3(GRID), dim3(PB_THREADS), lds, s, a);     \
@@ -501,8 +511,8 @@ __global__ void convert_records_kernel(const uint64_t *rec8, uint32_t n, PartArg
                                        uint32_t *ovals) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    uint32_t code;
-    okeys[i] = record_key(rec8[i], A, code);
+    uint32_t code, r;
+    okeys[i] = record_key(rec8[i], A, code, r);
     // the global scan path indexes by occurrence: decode a (read, pos) code
     ovals[i] = A.pos_bits ? A.meta[code >> A.pos_bits].x + (code & ((1u << A.pos_bits) - 1u)) : code;
 }

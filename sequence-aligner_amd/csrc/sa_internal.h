@@ -34,9 +34,9 @@ struct EmitParams {
     uint64_t *rkey;            // [n] per-read locality key (min k-mer mix; nullable)
     uint32_t *rord;            // [n] read ids (sort payload for rkey)
     int32_t pos_bits;          // > 0: the record's low word is read << pos_bits | pos (mixed lengths)
-    // mixed lengths without pos_bits codes: per-occurrence read and loc rank
-    // tables (nullable), so the bucket build finds both with one load each
-    uint32_t *occ_rid, *occ_lr;
+    // mixed lengths without pos_bits codes: per-occurrence {read, loc rank}
+    // table (nullable), so the bucket build finds both with one load
+    uint2 *occ_rl;
 };
 
 // bijective 32-bit mix of the seqHash: equal mix <=> equal hash, so a bucket
@@ -202,7 +202,7 @@ hipError_t exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, uin
 size_t buckets_temp_bytes(uint64_t n);
 hipError_t build_buckets(const uint64_t *skeys, const uint32_t *svals, uint64_t n, int lb,
                          const uint8_t *tagtab, const uint64_t *occ_off, uint32_t n_reads,
-                         uint32_t uniform_npr, const uint32_t *rid, Buckets &b,
+                         uint32_t uniform_npr, const uint2 *rl, Buckets &b,
                          uint32_t *totals_dev, void *tmp, hipStream_t s);
 hipError_t build_strict_index(const uint64_t *skeys, const uint32_t *svals, uint64_t n, int lb,
                               const uint8_t *tagtab, Buckets &b, hipStream_t s);
@@ -228,11 +228,10 @@ struct PartArgs {
     const uint8_t *tagtab;
     const uint64_t *occ_off;
     uint32_t n_reads, npr;
-    const uint32_t *rid;         // read id by occurrence index (distributed mode, mixed lengths) or null
+    const uint2 *rl;             // {read, loc rank} by occurrence index (distributed mode, mixed lengths) or null
     // sk holds 8-byte records (mix32 << 32 | occurrence index); the loc rank is
-    // lr[g] when given (distributed mode, mixed lengths), else re-derived from
+    // rl[g].y when given (distributed mode, mixed lengths), else re-derived from
     // the read's length and the position (lrank[lbase[L - k] + pos])
-    const uint32_t *lr;
     const int32_t *len;
     const uint32_t *lbase, *lrank;
     int32_t k;
@@ -324,9 +323,9 @@ hipError_t launch_kmer_hist(const uint64_t *sorted, uint64_t n, uint32_t *flag, 
 hipError_t launch_iota(uint32_t *v, uint64_t n, hipStream_t s);
 hipError_t launch_prepare_received(uint64_t *recs, uint64_t n, const uint64_t *seg, uint32_t P,
                                    const uint32_t *starts, const uint64_t *occ_off, uint32_t npr, const int32_t *len,
-                                   const uint32_t *lbase, const uint32_t *lrank, int32_t k, uint32_t *rid,
-                                   uint32_t *lr, hipStream_t s);
-hipError_t launch_local_offsets(const uint32_t *rid, uint64_t n, uint32_t n_reads, uint64_t *loff, hipStream_t s);
+                                   const uint32_t *lbase, const uint32_t *lrank, int32_t k, uint2 *rl,
+                                   hipStream_t s);
+hipError_t launch_local_offsets(const uint2 *rl, uint64_t n, uint32_t n_reads, uint64_t *loff, hipStream_t s);
 hipError_t launch_owner_bounds(const uint64_t *keys, uint64_t n, int shift, uint32_t P, uint64_t *bounds,
                                hipStream_t s);
 hipError_t launch_gather_partials(const uint32_t *perm, uint64_t n, const uint32_t *fst, const uint32_t *snd,
