@@ -63,16 +63,15 @@ __global__ void prepare_received_kernel(uint64_t *recs, uint64_t n, const uint64
 }
 
 // loff[a] = first i with rl[i].x >= a, for a in [0, n_reads] (reads ascending):
-// the local occurrences of read a are [loff[a], loff[a+1])
+// the local occurrences of read a are [loff[a], loff[a+1]).  One pass over the
+// records: record i starts the reads (rl[i-1].x, rl[i].x] (usually one), the
+// last record closes the reads after it
 __global__ void local_offsets_kernel(const uint2 *rl, uint64_t n, uint32_t n_reads, uint64_t *loff) {
-    const uint64_t a = (uint64_t)blockIdx.x * DT + threadIdx.x;
-    if (a > n_reads) return;
-    uint64_t lo = 0, hi = n;
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (rl[mid].x < a) lo = mid + 1; else hi = mid;
-    }
-    loff[a] = lo;
+    const uint64_t i = (uint64_t)blockIdx.x * DT + threadIdx.x;
+    if (i > n) return;
+    const uint32_t prev = i == 0 ? 0u : rl[i - 1].x + 1u;  // first read not yet started
+    const uint32_t cur = i == n ? n_reads + 1u : rl[i].x + 1u;
+    for (uint32_t a = prev; a < cur; ++a) loff[a] = i;
 }
 
 // bounds[o] = first i with (keys[i] >> shift) >= o, o in [0, P]
@@ -166,7 +165,7 @@ hipError_t launch_prepare_received(uint64_t *recs, uint64_t n, const uint64_t *s
 }
 
 hipError_t launch_local_offsets(const uint2 *rl, uint64_t n, uint32_t n_reads, uint64_t *loff, hipStream_t s) {
-    hipLaunchKernelGGL(local_offsets_kernel, grid_for((uint64_t)n_reads + 1), dim3(DT), 0, s, rl, n, n_reads, loff);
+    hipLaunchKernelGGL(local_offsets_kernel, grid_for(n + 1), dim3(DT), 0, s, rl, n, n_reads, loff);
     return hipGetLastError();
 }
 
