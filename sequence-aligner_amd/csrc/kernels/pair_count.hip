@@ -47,8 +47,8 @@ __device__ __forceinline__ uint32_t pc_hash(uint32_t p) {
 }
 
 // Elements (role pairs) of a chunk are enumerated in windows of PC_WIN; eo[e]
-// = 1 + the occurrence holding element w0 + e, built from one marker per
-// occurrence start and an inclusive max-scan (pref is non-decreasing).
+// = 1 + the occurrence holding element w0 + e, filled by the thread owning the
+// occurrence (its element range is in its registers: no scan, one barrier).
 constexpr int PC_WIN = 2048;
 
 template <int TAB>
@@ -59,6 +59,8 @@ struct PcShared {
     uint4 rec[PC_CHUNK];       // per-occurrence partner ranges (partition.hip)
     uint16_t eo[PC_WIN];       // element -> occurrence (+1) of the current window
     uint32_t lds4[PC_THREADS / 64];
+    uint32_t emit4[2][PC_THREADS / 64];  // emission: per-wave kept counts (double-buffered)
+    uint32_t emit_base[2];
     uint32_t fill, overflow, out_base;
 };
 template <int TAB>
@@ -87,25 +89,6 @@ __device__ __forceinline__ uint32_t pc_block_excl_scan(uint32_t v, uint32_t *lds
     __syncthreads();
     *total = tot;
     return off + inc - v;
-}
-
-__device__ __forceinline__ uint32_t pc_block_excl_max(uint32_t v, uint32_t *lds4) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t inc = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t t = __shfl_up(inc, off, 64);
-        if (lane >= off) inc = max(inc, t);
-    }
-    uint32_t ex = __shfl_up(inc, 1, 64);
-    if (lane == 0) ex = 0;
-    if (lane == 63) lds4[w] = inc;
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < PC_THREADS / 64; ++i)
-        if (i < w) ex = max(ex, lds4[i]);
-    __syncthreads();
-    return ex;
 }
 
 template <bool STRICT, int TAB>
@@ -178,7 +161,7 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
     const uint32_t nocc = (uint32_t)(e.occ_off[a + 1] - g0);
     unsigned long long role_pairs = 0;
     unsigned long long x_over = ~0ull;  // role pairs enumerated when the table filled
-    __syncthreads();
+    // (the table initialisation is ordered before any insert by the chunk scan's barriers)
 
     for (uint32_t c0 = 0; c0 < nocc; c0 += PC_CHUNK) {
         const uint32_t cn = min((uint32_t)PC_CHUNK, nocc - c0);
@@ -202,10 +185,12 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
         for (int j = 0; j < PER; ++j) s += mytot[j];
         uint32_t total;
         uint32_t ex = pc_block_excl_scan(s, S.lds4, &total);
+        uint32_t myex[PER];
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
             const uint32_t oi = tid * PER + j;
             if (oi <= cn) S.pref[oi] = ex;
+            myex[j] = ex;
             ex += mytot[j];
         }
         if (tid == PC_THREADS - 1 && cn == PC_CHUNK) S.pref[PC_CHUNK] = total;
@@ -222,28 +207,11 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
                 if (x_over == ~0ull) x_over = role_pairs - total + w0;
                 break;
             }
-            static_assert(PC_WIN == 8 * PC_THREADS, "one 16-byte eo slice per thread");
-            reinterpret_cast<uint4 *>(S.eo)[tid] = make_uint4(0, 0, 0, 0);
-            __syncthreads();
-            for (uint32_t oi = tid; oi < cn; oi += PC_THREADS) {
-                const uint32_t s0 = S.pref[oi], s1 = S.pref[oi + 1];
-                if (s1 > s0) {
-                    if (s0 >= w0 && s0 < w0 + PC_WIN) S.eo[s0 - w0] = (uint16_t)(oi + 1);
-                    else if (s0 < w0 && s1 > w0) S.eo[0] = (uint16_t)(oi + 1);  // runs into the window
-                }
-            }
-            __syncthreads();
-            {   // inclusive max-scan of eo: 8 entries per thread, then across threads
-                const uint4 v = reinterpret_cast<const uint4 *>(S.eo)[tid];
-                uint32_t x[8] = {v.x & 0xFFFFu, v.x >> 16, v.y & 0xFFFFu, v.y >> 16,
-                                 v.z & 0xFFFFu, v.z >> 16, v.w & 0xFFFFu, v.w >> 16};
 #pragma unroll
-                for (int j = 1; j < 8; ++j) x[j] = max(x[j], x[j - 1]);
-                const uint32_t before = pc_block_excl_max(x[7], S.lds4);
-#pragma unroll
-                for (int j = 0; j < 8; ++j) x[j] = max(x[j], before);
-                reinterpret_cast<uint4 *>(S.eo)[tid] =
-                    make_uint4(x[0] | (x[1] << 16), x[2] | (x[3] << 16), x[4] | (x[5] << 16), x[6] | (x[7] << 16));
+            for (int j = 0; j < PER; ++j) {  // this thread's occurrences' elements inside the window
+                const uint32_t e0 = max(myex[j], w0), e1 = min(myex[j] + mytot[j], w0 + (uint32_t)PC_WIN);
+                const uint16_t v = (uint16_t)(tid * PER + j + 1);
+                for (uint32_t el = e0; el < e1; ++el) S.eo[el - w0] = v;
             }
             __syncthreads();
             const uint32_t wn = min((uint32_t)PC_WIN, total - w0);
@@ -302,6 +270,7 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
         __syncthreads();
     }
 
+    if (nocc == 0) __syncthreads();  // (no chunk barriers ordered the table initialisation)
     const uint32_t shard = blockIdx.x % NSHARD;
     if (tid == 0 && role_pairs) atomicAdd(&o.role_pairs[shard], role_pairs);  // recount tiers: a dummy counter
     if (tid == 0 && !S.overflow) atomicAdd(&o.distinct[shard], (unsigned long long)S.fill);
@@ -319,10 +288,12 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
         }
         return;
     }
-    // --- emit (a, partner, count[, rank]), 32 slots per thread at a time ---
+    // --- emit (a, partner, count[, rank]), 32 slots per thread at a time:
+    //     wave scans, one claim per block, two barriers per chunk
     constexpr int PER = TAB / PC_THREADS;
     constexpr int CH = PER < 32 ? PER : 32;
     const unsigned long long region = (unsigned long long)shard * o.cap_s;
+    const int lane = tid & 63, wvi = tid >> 6;
     for (int c0 = 0; c0 < PER; c0 += CH) {
         uint32_t keep = 0;
 #pragma unroll
@@ -332,13 +303,27 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
             if (S.key[sl] != PC_EMPTY && (p.emit_all || ((int32_t)c >= p.min_coll && (int32_t)c <= p.max_coll)))
                 keep |= 1u << j;
         }
-        uint32_t total;
-        const uint32_t ex = pc_block_excl_scan(__popc(keep), S.lds4, &total);
-        if (total == 0) continue;  // uniform: every thread sees the same total
-        if (tid == 0) S.out_base = (uint32_t)atomicAdd(&o.cursor[shard], (unsigned long long)total);
+        const int buf = (c0 / CH) & 1;  // slow readers of the previous chunk's counts are not overwritten
+        const uint32_t mine = __popc(keep);
+        uint32_t inc = mine;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t t = __shfl_up(inc, off, 64);
+            if (lane >= off) inc += t;
+        }
+        if (lane == 63) S.emit4[buf][wvi] = inc;
         __syncthreads();
-        const unsigned long long base = (unsigned long long)S.out_base + ex;
-        __syncthreads();  // out_base read before the next chunk's atomic overwrites it
+        uint32_t total = 0, ex = inc - mine;
+#pragma unroll
+        for (int q = 0; q < PC_THREADS / 64; ++q) {
+            const uint32_t v = S.emit4[buf][q];
+            total += v;
+            if (q < wvi) ex += v;
+        }
+        if (total == 0) continue;  // uniform: every thread sees the same total
+        if (tid == 0) S.emit_base[buf] = (uint32_t)atomicAdd(&o.cursor[shard], (unsigned long long)total);
+        __syncthreads();
+        const unsigned long long base = (unsigned long long)S.emit_base[buf] + ex;
         uint32_t k = 0;
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
