@@ -395,6 +395,7 @@ struct PcmShared {
     uint32_t pref[PC_CHUNK + 1];
     uint4 rec[PC_CHUNK];
     uint32_t aid[PC_CHUNK];    // read of each occurrence of the chunk
+    uint16_t eo[PC_WIN];       // element -> occurrence (+1) of the current window (as in pair_count_kernel)
     uint32_t lds4[PC_THREADS / 64];
     uint32_t fill, overflow, out_base;
 };
@@ -466,37 +467,40 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_multi_kernel(EmitParams
         for (int j = 0; j < PER; ++j) sum += mytot[j];
         uint32_t total;
         uint32_t ex = pc_block_excl_scan(sum, S.lds4, &total);
+        uint32_t myex[PER];
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
             const uint32_t oi = tid * PER + j;
             if (oi <= cn) S.pref[oi] = ex;
+            myex[j] = ex;
             ex += mytot[j];
         }
         if (tid == PC_THREADS - 1 && cn == PC_CHUNK) S.pref[PC_CHUNK] = total;
         role_pairs += total;
-        __syncthreads();
 
-        const uint32_t per = (total + PC_THREADS - 1) / PC_THREADS;
-        const uint32_t t0 = min(total, tid * per), t1 = min(total, t0 + per);
-        if (t0 < t1 && !S.overflow) {  // (an overflowed table: totals only, the reads are recounted)
-            uint32_t lo = 0, hi = cn;  // last oi with pref[oi] <= t0
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (S.pref[mid] <= t0) lo = mid; else hi = mid;
+        // lane-interleaved enumeration over windows, as in pair_count_kernel
+        for (uint32_t w0 = 0; w0 < total; w0 += PC_WIN) {
+            __syncthreads();  // pref / rec / aid written; the previous window's eo consumed
+            if (S.overflow) break;  // (an overflowed table: totals only, the reads are recounted)
+#pragma unroll
+            for (int j = 0; j < PER; ++j) {
+                const uint32_t e0 = max(myex[j], w0), e1 = min(myex[j] + mytot[j], w0 + (uint32_t)PC_WIN);
+                const uint16_t v = (uint16_t)(tid * PER + j + 1);
+                for (uint32_t el = e0; el < e1; ++el) S.eo[el - w0] = v;
             }
-            uint32_t oi = lo;
-            uint32_t base = S.pref[oi], nxt = S.pref[oi + 1];
-            for (uint32_t t = t0; t < t1; t += PC_BATCH) {
+            __syncthreads();
+            const uint32_t wn = min((uint32_t)PC_WIN, total - w0);
+            for (uint32_t e0 = 0; e0 < wn; e0 += PC_THREADS * PC_BATCH) {
                 uint32_t part[PC_BATCH], wv[PC_BATCH], own[PC_BATCH];
 #pragma unroll
                 for (int bb = 0; bb < PC_BATCH; ++bb) {
                     part[bb] = 0;
                     wv[bb] = 0;  // 0: no role pair in this slot
                     own[bb] = 0;
-                    const uint32_t tt = t + bb;
-                    if (tt < t1) {
-                        while (tt >= nxt) { ++oi; base = nxt; nxt = S.pref[oi + 1]; }
-                        const uint32_t off = tt - base;
+                    const uint32_t el = e0 + bb * PC_THREADS + tid;
+                    if (el < wn) {
+                        const uint32_t oi = (uint32_t)S.eo[el] - 1u;
+                        const uint32_t off = w0 + el - S.pref[oi];
                         const uint4 rc = S.rec[oi];
                         const uint32_t nE = rc.y & 0x3FFFFFFFu;
                         own[bb] = S.aid[oi];
