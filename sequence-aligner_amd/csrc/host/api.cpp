@@ -325,10 +325,24 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
     if (PB > 16 && (n >> 16) <= 900) PB = 16;
     const uint32_t nparts = 1u << PB;
     const int kbits = 32 + c->lb;  // LDS sort key: mix << lb | loc rank
+    uint2 *srl = nullptr;
     {
         StageScope st(c, SA_STAGE_SORT);
-        uint32_t *nv = nullptr, *nv2 = nullptr;  // key-only: the payload rides in the record
-        HIPCHK(radix_sort(&keys, &nv, &keys2, &nv2, n, 64 - skip_bits - PB, 64 - skip_bits, stmp, c->stream));
+        if (rl) {
+            // an occurrence table rides along as the sort's 8-byte value, so the
+            // bucket build reads each record's {read, loc rank} coalesced instead
+            // of gathering it (16-byte records through the two passes)
+            uint64_t *v0, *v1;
+            ENSURE(c->d_srl, n + 1, &v0);
+            ENSURE(c->d_srl2, n + 1, &v1);
+            if (n) HIPCHK(hipMemcpyAsync(v0, rl, n * 8, hipMemcpyDeviceToDevice, c->stream));
+            HIPCHK(radix_sort_kv64(&keys, &v0, &keys2, &v1, n, 64 - skip_bits - PB, 64 - skip_bits, stmp,
+                                   c->stream));
+            srl = (uint2 *)v0;
+        } else {
+            uint32_t *nv = nullptr, *nv2 = nullptr;  // key-only: the payload rides in the record
+            HIPCHK(radix_sort(&keys, &nv, &keys2, &nv2, n, 64 - skip_bits - PB, 64 - skip_bits, stmp, c->stream));
+        }
     }
     uint32_t *pstart, *biglist;
     ENSURE(c->d_pstart, nparts + 1, &pstart);
@@ -337,7 +351,7 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
     PA.sk = keys; PA.sv = nullptr; PA.start = pstart; PA.np = nparts; PA.lb = c->lb; PA.sort_bits = kbits - skip_bits - PB;
     PA.tagtab = (const uint8_t *)c->d_tagtab.p;
     PA.occ_off = occ_off;
-    PA.n_reads = n_reads; PA.npr = npr; PA.rl = rl;
+    PA.n_reads = n_reads; PA.npr = npr; PA.rl = rl; PA.srl = srl;
     PA.len = len;
     PA.lbase = (const uint32_t *)c->d_lbase.p;
     PA.lrank = (const uint32_t *)c->d_lrank.p;
@@ -1068,7 +1082,7 @@ void sa_ctx_destroy(sa_ctx *c) {
                     &c->d_gmds, &c->d_gede, &c->d_ogid, &c->d_bkttmp, &c->d_mdidx, &c->d_edidx, &c->d_occidx,
                     &c->d_bnst, &c->d_brank, &c->d_bhash, &c->d_bfirst, &c->d_pf, &c->d_ps, &c->d_pc, &c->d_pr,
                     &c->d_ovl, &c->d_cnt, &c->d_okeys, &c->d_ovals, &c->d_okeys2, &c->d_ovals2, &c->d_osort,
-                    &c->d_lead, &c->d_trail, &c->d_count, &c->d_aln, &c->d_p1, &c->d_tb, &c->d_rkey, &c->d_rkey2, &c->d_rord, &c->d_rord2, &c->d_rtmp, &c->d_gocc, &c->d_seg, &c->d_rl, &c->d_loff, &c->d_starts, &c->d_bounds, &c->d_gcodes, &c->d_gwoff, &c->d_glen, &c->d_gbad, &c->d_psum, &c->d_pkeep, &c->d_ppos, &c->d_scan, &c->d_pstart, &c->d_biglist, &c->d_rec,
+                    &c->d_lead, &c->d_trail, &c->d_count, &c->d_aln, &c->d_p1, &c->d_tb, &c->d_rkey, &c->d_rkey2, &c->d_rord, &c->d_rord2, &c->d_rtmp, &c->d_gocc, &c->d_seg, &c->d_rl, &c->d_srl, &c->d_srl2, &c->d_loff, &c->d_starts, &c->d_bounds, &c->d_gcodes, &c->d_gwoff, &c->d_glen, &c->d_gbad, &c->d_psum, &c->d_pkeep, &c->d_ppos, &c->d_scan, &c->d_pstart, &c->d_biglist, &c->d_rec,
                     &c->d_srec, &c->d_bnmd, &c->d_ishead, &c->d_bnst2, &c->d_tmd, &c->d_ted, &c->d_tmdi,
                     &c->d_tedi, &c->d_xrec, &c->d_tier, &c->d_ovlrp, &c->d_meta, &c->d_items, &c->d_bigtot, &c->d_hk0, &c->d_hk1, &c->d_hflag,
                     &c->d_hidx, &c->d_hpos, &c->d_htmp, &c->d_hist, &c->d_hovf, &c->d_hsmall,

@@ -44,18 +44,18 @@ __device__ __forceinline__ uint64_t load_sk(const uint64_t *p) { return __builti
 // occurrence index g, or (pos_bits > 0: mixed read lengths) read << pos_bits |
 // pos, whose read meta {first occurrence, loc-rank base} gives g and the loc
 // rank with one load (instead of a search over the occurrence offsets); with
-// an occurrence table (rl) its one 8-byte load gives the loc rank and the read
-// (rr, else untouched)
+// an occurrence table, the record's {read, loc rank} entry rlp gives the loc
+// rank and the read (rr, else untouched)
 __device__ __forceinline__ unsigned long long record_key(uint64_t rec, const PartArgs &A, uint32_t &code,
-                                                         uint32_t &rr) {
+                                                         uint32_t &rr, const uint2 *rlp) {
     code = (uint32_t)rec;
     const uint32_t g = code;
     uint32_t lr;
     if (A.pos_bits) {
         const uint32_t pos = code & ((1u << A.pos_bits) - 1u);
         lr = A.lrank[A.meta[code >> A.pos_bits].y + pos];
-    } else if (A.rl) {
-        const uint2 v = A.rl[g];
+    } else if (rlp) {
+        const uint2 v = *rlp;
         lr = v.y;
         rr = v.x;
     } else {
@@ -198,7 +198,9 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
     // ---- load, then stable LDS radix sort on the key bits below the partition id
     for (uint32_t i = tid; i < n; i += PB_THREADS) {
         uint32_t g, r = 0;
-        S.key[i] = record_key(load_sk(A.sk + ps + i), A, g, r);
+        const uint64_t rec = load_sk(A.sk + ps + i);
+        const uint2 *rlp = A.srl ? A.srl + ps + i : (A.rl ? A.rl + (uint32_t)rec : nullptr);
+        S.key[i] = record_key(rec, A, g, r, rlp);
         S.g[i] = g;
         S.oi[i] = (uint16_t)i;
         if (Sr) Sr[i] = r;
@@ -512,7 +514,7 @@ __global__ void convert_records_kernel(const uint64_t *rec8, uint32_t n, PartArg
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint32_t code, r;
-    okeys[i] = record_key(rec8[i], A, code, r);
+    okeys[i] = record_key(rec8[i], A, code, r, A.rl ? A.rl + (uint32_t)rec8[i] : nullptr);
     // the global scan path indexes by occurrence: decode a (read, pos) code
     ovals[i] = A.pos_bits ? A.meta[code >> A.pos_bits].x + (code & ((1u << A.pos_bits) - 1u)) : code;
 }

@@ -268,6 +268,107 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep_kernel(const uint64_t
     }
 }
 
+// 16-byte records (u64 key, u64 value): the tile is staged through LDS twice --
+// keys (with their digits), then the values in the same slots -- so the LDS
+// footprint stays that of a key-only tile (3 workgroups per CU, not 2)
+struct RsSharedKV {
+    unsigned long long buf[RS_TILE];  // staged keys, then staged values
+    uint8_t dig[RS_TILE];
+    uint32_t cnt[RS_WAVES][256];
+    uint32_t lofs[256];
+    uint32_t gofs[256];
+};
+
+__global__ __launch_bounds__(RS_THREADS) void rs_downsweep_kv64_kernel(const uint64_t *kin, const uint64_t *vin,
+                                                                       uint64_t *kout, uint64_t *vout, uint64_t n,
+                                                                       int shift, const uint32_t *hist,
+                                                                       uint32_t nblocks) {
+    extern __shared__ __align__(16) uint8_t rs_smem[];
+    RsSharedKV &S = *reinterpret_cast<RsSharedKV *>(rs_smem);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
+    for (int q = lane; q < 256; q += 64) S.cnt[w][q] = 0;
+    unsigned long long k[RS_SLICES], v[RS_SLICES];
+    uint32_t rk[RS_SLICES];
+    const uint64_t sub = base + (uint64_t)w * RS_SUB;
+#pragma unroll
+    for (int j = 0; j < RS_SLICES; ++j) {
+        const uint64_t i = sub + (uint64_t)j * 64 + lane;
+        k[j] = i < n ? rs_load_key(kin + i) : ~0ull;
+        v[j] = i < n ? rs_load_key(vin + i) : 0ull;
+    }
+#pragma unroll
+    for (int j = 0; j < RS_SLICES; ++j) {
+        const uint64_t i = sub + (uint64_t)j * 64 + lane;
+        const bool valid = i < n;
+        const uint32_t d = (uint32_t)(k[j] >> shift) & 255u;
+        const uint64_t peer = wave_peers(d, valid);
+        const uint32_t before = valid ? S.cnt[w][d] : 0u;
+        rk[j] = before + __popcll(peer & lt_mask);
+        __builtin_amdgcn_wave_barrier();
+        if (valid && (peer & lt_mask) == 0) S.cnt[w][d] = before + __popcll(peer);
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    {
+        uint32_t tot = 0;
+#pragma unroll
+        for (int q = 0; q < RS_WAVES; ++q) tot += S.cnt[q][tid];
+        uint32_t inc = tot;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t t = __shfl_up(inc, off, 64);
+            if (lane >= off) inc += t;
+        }
+        if (lane == 63) S.lofs[w] = inc;
+        __syncthreads();
+        uint32_t pre = 0;
+        for (int q = 0; q < w; ++q) pre += S.lofs[q];
+        __syncthreads();
+        const uint32_t lo = pre + inc - tot;
+        S.lofs[tid] = lo;
+        S.gofs[tid] = hist[(uint64_t)tid * nblocks + blockIdx.x];
+        uint32_t acc = lo;
+#pragma unroll
+        for (int q = 0; q < RS_WAVES; ++q) {
+            const uint32_t c = S.cnt[q][tid];
+            S.cnt[q][tid] = acc;
+            acc += c;
+        }
+    }
+    __syncthreads();
+    uint32_t pos[RS_SLICES];
+#pragma unroll
+    for (int j = 0; j < RS_SLICES; ++j) {
+        const uint64_t i = sub + (uint64_t)j * 64 + lane;
+        pos[j] = 0;
+        if (i < n) {
+            const uint32_t d = (uint32_t)(k[j] >> shift) & 255u;
+            pos[j] = S.cnt[w][d] + rk[j];
+            S.buf[pos[j]] = k[j];
+            S.dig[pos[j]] = (uint8_t)d;
+        }
+    }
+    __syncthreads();
+    const uint32_t nt = (uint32_t)min((uint64_t)RS_TILE, n - base);
+    for (uint32_t i = tid; i < nt; i += RS_THREADS) {
+        const uint32_t d = S.dig[i];
+        kout[S.gofs[d] + (i - S.lofs[d])] = S.buf[i];
+    }
+    __syncthreads();  // staged keys written out: the slots take the values
+#pragma unroll
+    for (int j = 0; j < RS_SLICES; ++j) {
+        const uint64_t i = sub + (uint64_t)j * 64 + lane;
+        if (i < n) S.buf[pos[j]] = v[j];
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < nt; i += RS_THREADS) {
+        const uint32_t d = S.dig[i];
+        vout[S.gofs[d] + (i - S.lofs[d])] = S.buf[i];
+    }
+}
+
 size_t radix_sort_temp_bytes(uint64_t n) {
     const uint64_t nb = (n + RS_TILE - 1) / RS_TILE;
     const uint64_t hist = 256 * (nb ? nb : 1);
@@ -295,14 +396,41 @@ hipError_t radix_sort(uint64_t **keys, uint32_t **vals, uint64_t **keys_alt, uin
         hipError_t e = exclusive_scan_u32(hist, hist, 256 * nb, nullptr, stmp, s);
         if (e != hipSuccess) return e;
         if (with_vals) {
-            hipLaunchKernelGGL(rs_downsweep_kernel<true>, dim3((uint32_t)nb), dim3(RS_THREADS), sizeof(RsShared<true>),
+            hipLaunchKernelGGL((rs_downsweep_kernel<true>), dim3((uint32_t)nb), dim3(RS_THREADS), sizeof(RsShared<true>),
                                s, *keys, *vals, *keys_alt, *vals_alt, n, shift, (const uint32_t *)hist, (uint32_t)nb);
             uint32_t *tv = *vals; *vals = *vals_alt; *vals_alt = tv;
         } else {
-            hipLaunchKernelGGL(rs_downsweep_kernel<false>, dim3((uint32_t)nb), dim3(RS_THREADS),
+            hipLaunchKernelGGL((rs_downsweep_kernel<false>), dim3((uint32_t)nb), dim3(RS_THREADS),
                                sizeof(RsShared<false>), s, *keys, nullptr, *keys_alt, nullptr, n, shift,
                                (const uint32_t *)hist, (uint32_t)nb);
         }
+        uint64_t *tk = *keys; *keys = *keys_alt; *keys_alt = tk;
+    }
+    return hipGetLastError();
+}
+
+// (key u64, value u64) pairs: 16-byte records (the sharded bucket build's
+// {slot | read, loc rank}); same passes as radix_sort
+hipError_t radix_sort_kv64(uint64_t **keys, uint64_t **vals, uint64_t **keys_alt, uint64_t **vals_alt, uint64_t n,
+                           int lo, int hi, void *tmp, hipStream_t s) {
+    if (n <= 1 || hi <= lo) return hipSuccess;
+    const uint64_t nb = (n + RS_TILE - 1) / RS_TILE;
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void *)rs_downsweep_kv64_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)sizeof(RsSharedKV));
+        attr_set = true;
+    }
+    uint32_t *hist = (uint32_t *)tmp;
+    void *stmp = (void *)(hist + 256 * nb);
+    for (int shift = lo; shift < hi; shift += 8) {
+        hipLaunchKernelGGL(rs_upsweep_kernel, dim3((uint32_t)nb), dim3(RS_THREADS), 0, s, *keys, n, shift, hist,
+                           (uint32_t)nb);
+        hipError_t e = exclusive_scan_u32(hist, hist, 256 * nb, nullptr, stmp, s);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(rs_downsweep_kv64_kernel, dim3((uint32_t)nb), dim3(RS_THREADS), sizeof(RsSharedKV), s,
+                           *keys, *vals, *keys_alt, *vals_alt, n, shift, (const uint32_t *)hist, (uint32_t)nb);
+        uint64_t *tv = *vals; *vals = *vals_alt; *vals_alt = tv;
         uint64_t *tk = *keys; *keys = *keys_alt; *keys_alt = tk;
     }
     return hipGetLastError();

@@ -191,6 +191,9 @@ hipError_t launch_kmer_emit(const DevReads &r, const EmitParams &p, uint64_t *ke
 size_t radix_sort_temp_bytes(uint64_t n);
 hipError_t radix_sort(uint64_t **keys, uint32_t **vals, uint64_t **keys_alt, uint32_t **vals_alt,
                       uint64_t n, int lo, int hi, void *tmp, hipStream_t s);
+// the same with 64-bit values (16-byte records)
+hipError_t radix_sort_kv64(uint64_t **keys, uint64_t **vals, uint64_t **keys_alt, uint64_t **vals_alt, uint64_t n,
+                           int lo, int hi, void *tmp, hipStream_t s);
 
 // exclusive scan of u32 (in place allowed), returns total in *total_dev
 size_t scan_temp_bytes(uint64_t n);
@@ -229,6 +232,7 @@ struct PartArgs {
     const uint64_t *occ_off;
     uint32_t n_reads, npr;
     const uint2 *rl;             // {read, loc rank} by occurrence index (distributed mode, mixed lengths) or null
+    const uint2 *srl;            // the same, sorted with the records (aligned with sk) or null
     // sk holds 8-byte records (mix32 << 32 | occurrence index); the loc rank is
     // rl[g].y when given (distributed mode, mixed lengths), else re-derived from
     // the read's length and the position (lrank[lbase[L - k] + pos])
