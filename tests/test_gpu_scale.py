@@ -8,6 +8,8 @@
   passes), which exercise the float32 loc comparison across read lengths
   (KmerTable.scala:65) and the per-length band width (BioLibs.scala:619-620).
 * README:164-175's sample record, pinned exactly.
+* configs[3]'s sharding at the bench size: the 100k-read workload over 4 and 8
+  virtual shards gives the single-device dispatch and .ovl exactly.
 """
 import os
 import sys
@@ -136,3 +138,28 @@ def test_many_partner_reads_recount_tiers(oracle_mod, n_edge):
     np.testing.assert_array_equal(trail, r.trail)
     assert (lead <= n_mid).sum() == n_mid * n_edge  # every middle read leads every edge read
     assert ov.stats()["role_pairs"] > 3 * n_mid * n_edge
+
+
+@pytest.mark.parametrize("shards", [4, 8])
+def test_bench_workload_sharded_matches_single(shards):
+    """The sharded path at the bench's full size: the 100k x 500 bp workload over
+    4 and 8 virtual shards gives the single-device dispatch and .ovl exactly
+    (records carry source-local occurrence indices, the occurrence table rides
+    through the partition sort, multi-read pair-count blocks, owner reduce)."""
+    b, o = bench.synth_workload(100000, 500, 2500000, 0.5, seed=1)
+    one = sao.Overlapper(kmer_size=15, id_mode=sao.SA_IDS_WIDE)
+    one.add_packed(b.tobytes(), o)
+    one.build()
+    one.align()
+    lead, trail, count = (np.array(x) for x in one.dispatch())
+    ovl = one.ovl()
+    one.close()
+    sh = sao.Overlapper(kmer_size=15, id_mode=sao.SA_IDS_WIDE, shards=shards)
+    sh.add_packed(b.tobytes(), o)
+    sh.build()
+    sh.align()
+    l2, t2, c2 = sh.dispatch()
+    np.testing.assert_array_equal(l2, lead)
+    np.testing.assert_array_equal(t2, trail)
+    np.testing.assert_array_equal(c2, count)
+    assert sh.ovl() == ovl
