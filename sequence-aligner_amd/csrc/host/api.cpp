@@ -884,13 +884,15 @@ int device_align(sa_ctx *c, bool readback) {
     const int G = wmax <= 15 ? 16 : (wmax <= 31 ? 32 : 64);
     const uint32_t rw_fit = (160u * 1024u / (256u * 4u) - 1u) | 1u;
     const uint32_t rw = std::min<uint32_t>((uint32_t)((maxL + 1 + 15) / 16) | 1u, rw_fit);
-    // The DP kernels hold the cost matrix as int8 bytes (HOXD70 spans -125..100).
+    // The DP kernels hold the cost matrix as int8 bytes (HOXD70 spans -125..100),
+    // or as int16 halves for other matrices (one extra select per lookup).
     // Every recurrence (BioLibs.scala:645-668, :725-764; :171-263 for the
     // quadratic aligner) is max-plus and linear in (costs, gO, gE) with 0, so
     // dividing all of them by their common divisor g scales every cell by 1/g
     // exactly: argmax, walk codes and the alignment are unchanged (a x10 HOXD
-    // matrix with gap costs -200 / -20 runs as HOXD70).
+    // matrix with gap costs -200 / -20 runs as HOXD70 in int8).
     int32_t cost[16], gap_open = c->set.gap_open, gap_extend = c->set.gap_extend;
+    int32_t cost_bits = 8;
     {
         auto gcd = [](int64_t a, int64_t b) { a = a < 0 ? -a : a; b = b < 0 ? -b : b; while (b) { int64_t t = a % b; a = b; b = t; } return a; };
         int64_t g = gcd(gap_open, gap_extend);
@@ -898,9 +900,10 @@ int device_align(sa_ctx *c, bool readback) {
         if (g <= 1) g = 1;
         for (int x = 0; x < 16; ++x) {
             cost[x] = (int32_t)(c->set.cost[x] / g);
-            if (cost[x] < -128 || cost[x] > 127)
+            if (cost[x] < -32768 || cost[x] > 32767)
                 return fail(c, SA_E_OVERFLOW, "cost matrix entries (divided by their common divisor with the gap "
-                                              "costs) must lie in [-128, 127]");
+                                              "costs) must lie in [-32768, 32767]");
+            if (cost[x] < -128 || cost[x] > 127) cost_bits = 16;
         }
         gap_open = (int32_t)(gap_open / g);
         gap_extend = (int32_t)(gap_extend / g);
@@ -915,6 +918,13 @@ int device_align(sa_ctx *c, bool readback) {
         return fail(c, SA_E_ARG, "SA_OPT_ALIGN_KERNEL=3 but a band or read exceeds the lane kernel");
     if (c->aligner == SA_ALIGNER_QUADRATIC && (c->set.gap_open > 0 || c->set.gap_extend > 0))
         return fail(c, SA_E_ARG, "--quadratic-align needs gap costs <= 0 (Project4.readArgs negates them)");
+    if (c->aligner == SA_ALIGNER_QUADRATIC) {
+        // its row argmax key packs (T << 5 | column): scores stay below 2^26
+        int64_t cmax = 0;
+        for (int x = 0; x < 16; ++x) cmax = std::max<int64_t>(cmax, cost[x]);
+        if (cmax * (int64_t)maxL >= (1ll << 26))
+            return fail(c, SA_E_OVERFLOW, "--quadratic-align: largest cost x read length reaches 2^26");
+    }
     const bool use_lane = c->align_kernel >= 2 || (c->align_kernel == 0 && lane_fits);
     const int32_t wmin = std::max(c->set.kmer_size, (int32_t)floor((double)((float)minL * omm)) + 1);
     const bool exact = wmin == 15 && wmax == 15 && lw == 16;  // every band exactly 16 cells wide
@@ -927,6 +937,7 @@ int device_align(sa_ctx *c, bool readback) {
     P.min_identity = c->set.min_identity;
     P.max_ignore = (float)c->set.max_ignore;
     memcpy(P.cost, cost, sizeof(P.cost));
+    P.cost_bits = cost_bits;
     P.rw = rw;
     Counters *cnt = (Counters *)c->d_cnt.p;
     DevAlignment *out;

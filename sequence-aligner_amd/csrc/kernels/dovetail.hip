@@ -73,10 +73,6 @@ __device__ __forceinline__ uint32_t win16(const uint32_t *w, int32_t p) {
     return (a << (2 * s)) | (w[(p >> 4) + 1] >> (32 - 2 * s));
 }
 
-__device__ __forceinline__ int32_t sext8(uint32_t packed, uint32_t idx) {
-    return (int32_t)(int8_t)(uint8_t)(packed >> (8 * idx));
-}
-
 // 64-bit argmax key: value desc, row asc, lane asc
 __device__ __forceinline__ unsigned long long amax_key(int32_t best, int32_t row, int lane) {
     return ((unsigned long long)(uint32_t)best << 32) | ((unsigned long long)(0xFFFFFu - (uint32_t)row) << 8) |
@@ -95,7 +91,7 @@ __device__ __forceinline__ unsigned long long group_max_u64(unsigned long long v
 
 __device__ __forceinline__ void set_err(int32_t *err, int32_t code) { atomicCAS(err, 0, code); }
 
-template <int G>
+template <int G, class C>
 __global__ __launch_bounds__(256) void dovetail_kernel(DevReads rd, const int32_t *lead, const int32_t *trail,
                                                        uint64_t npairs, AlignParams P, DevAlignment *out,
                                                        int32_t *err, unsigned long long *cells_total) {
@@ -134,9 +130,7 @@ __global__ __launch_bounds__(256) void dovetail_kernel(DevReads rd, const int32_
 
     // ---------------- phase 1: A vs B[0 .. w)   (BioLibs.scala:645-668) ------
     const int32_t bj = (ok && lane >= 1 && lane <= w) ? (int32_t)code_at(Bw, lane - 1) : 0;
-    uint32_t cb = 0;  // costs of (a, B[j-1]) for a = 0..3 as int8 bytes
-#pragma unroll
-    for (int x = 0; x < 4; ++x) cb |= ((uint32_t)(uint8_t)(int8_t)P.cost[x * 4 + bj]) << (8 * x);
+    const C cb = C::make(P.cost[0 * 4 + bj], P.cost[1 * 4 + bj], P.cost[2 * 4 + bj], P.cost[3 * 4 + bj]);  // (a, B[j-1])
     int32_t Mp = 0, Xp = 0, Yp = 0, Tp = 0;
     int32_t best = 0, brow = 0;
     uint32_t acc = 0, aw = 0;
@@ -144,7 +138,7 @@ __global__ __launch_bounds__(256) void dovetail_kernel(DevReads rd, const int32_
     for (int32_t i = 1; i <= rows1; ++i) {
         if (((i - 1) & 15) == 0) aw = (ok && i <= LA) ? Aw[(i - 1) >> 4] : 0u;
         const uint32_t ac = (aw >> (30 - 2 * ((i - 1) & 15))) & 3u;
-        const int32_t c = sext8(cb, ac);
+        const int32_t c = cb.at(ac << 3);
         const int32_t diag = shr_g<G, 1>(Tp, 0);
         // lane 0 is the boundary column j = 0: M = X = 0 and Y <= 0 there, so it
         // must feed 0 (not a computed cell) into the diagonal and the X scan
@@ -212,13 +206,9 @@ __global__ __launch_bounds__(256) void dovetail_kernel(DevReads rd, const int32_
         const int32_t pos = lane - zr - 1;
         if (col2 && pos >= 0 && pos < LB) bq = (int32_t)code_at(Bw, pos);
     }
-    uint32_t cpack[4];
+    C cpack[4];
 #pragma unroll
-    for (int x = 0; x < 4; ++x) {
-        cpack[x] = 0;
-#pragma unroll
-        for (int y = 0; y < 4; ++y) cpack[x] |= ((uint32_t)(uint8_t)(int8_t)P.cost[x * 4 + y]) << (8 * y);
-    }
+    for (int x = 0; x < 4; ++x) cpack[x] = C::make(P.cost[x * 4], P.cost[x * 4 + 1], P.cost[x * 4 + 2], P.cost[x * 4 + 3]);
     Mp = 0; Xp = 0; Yp = 0; Tp = 0;
     int32_t Qp = NEG;  // max(max(M,X)+gO, Y) of the previous row (feeds Y of lane k-1)
     best = 0; brow = 0; acc = 0;
@@ -236,8 +226,8 @@ __global__ __launch_bounds__(256) void dovetail_kernel(DevReads rd, const int32_
         }
         const uint32_t ac = (aw2 >> (30 - 2 * ((i - 1) & 15))) & 3u;
         const bool valid = row_ok && u >= 1 && j >= 1 && j <= LB;
-        const uint32_t cp = ac == 0 ? cpack[0] : (ac == 1 ? cpack[1] : (ac == 2 ? cpack[2] : cpack[3]));
-        const int32_t c = sext8(cp, (uint32_t)bq);
+        const C cp = ac == 0 ? cpack[0] : (ac == 1 ? cpack[1] : (ac == 2 ? cpack[2] : cpack[3]));
+        const int32_t c = cp.at((uint32_t)bq << 3);
         int32_t M = valid ? c + max(Tp, 0) : 0;
         const int32_t Ys = shl1_g<G>(Qp, NEG);
         int32_t Y = (valid && lane != w) ? gE + max(Ys, 0) : 0;
@@ -337,19 +327,25 @@ hipError_t launch_dovetail(const DevReads &r, const int32_t *lead, const int32_t
                            unsigned long long *cells, hipStream_t s) {
     if (!n) return hipSuccess;
     const size_t lds = (size_t)256 * p.rw * sizeof(uint32_t);  // (256/G groups) * G cols * rw
+#define SA_GROUP_LAUNCH(GV, C, BLOCKS)                                                                   \
+    do {                                                                                                 \
+        (void)hipFuncSetAttribute((const void *)dovetail_kernel<GV, C>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                  (int)lds);                                                             \
+        hipLaunchKernelGGL((dovetail_kernel<GV, C>), dim3(BLOCKS), dim3(256), lds, s, r, lead, trail, n, p, out, err, \
+                           cells);                                                                       \
+    } while (0)
+    const bool c16 = p.cost_bits == 16;  // int16 cost packs (sa_internal.h)
     if (group_lanes == 16) {
-        (void)hipFuncSetAttribute((const void *)dovetail_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(dovetail_kernel<16>, dim3((uint32_t)((n + 15) / 16)), dim3(256), lds, s, r, lead, trail, n,
-                           p, out, err, cells);
+        if (c16) SA_GROUP_LAUNCH(16, Cost16, (uint32_t)((n + 15) / 16));
+        else SA_GROUP_LAUNCH(16, Cost8, (uint32_t)((n + 15) / 16));
     } else if (group_lanes == 32) {
-        (void)hipFuncSetAttribute((const void *)dovetail_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(dovetail_kernel<32>, dim3((uint32_t)((n + 7) / 8)), dim3(256), lds, s, r, lead, trail, n,
-                           p, out, err, cells);
+        if (c16) SA_GROUP_LAUNCH(32, Cost16, (uint32_t)((n + 7) / 8));
+        else SA_GROUP_LAUNCH(32, Cost8, (uint32_t)((n + 7) / 8));
     } else {
-        (void)hipFuncSetAttribute((const void *)dovetail_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL(dovetail_kernel<64>, dim3((uint32_t)((n + 3) / 4)), dim3(256), lds, s, r, lead, trail, n,
-                           p, out, err, cells);
+        if (c16) SA_GROUP_LAUNCH(64, Cost16, (uint32_t)((n + 3) / 4));
+        else SA_GROUP_LAUNCH(64, Cost8, (uint32_t)((n + 3) / 4));
     }
+#undef SA_GROUP_LAUNCH
     return hipGetLastError();
 }
 

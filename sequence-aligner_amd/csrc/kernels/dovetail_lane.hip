@@ -26,10 +26,6 @@ namespace {
 // LW = band cells per row held in registers (w <= LW - 1): 16 for every read up
 // to ~750 bp at min identity 0.98 (the bench), 24 / 32 for longer reads
 
-__device__ __forceinline__ int32_t bfe_s8(uint32_t packed, uint32_t shift) {
-    return __builtin_amdgcn_sbfe((int32_t)packed, shift, 8);
-}
-
 __device__ __forceinline__ void set_err(int32_t *err, int32_t code) { atomicCAS(err, 0, code); }
 
 // A wave-uniform value copied into a VGPR the compiler cannot see through: on
@@ -63,14 +59,14 @@ struct Band {
 // (matches << 16 | errors).  MASKED rows test 1 <= j <= |B| per cell; EXACT
 // launches have w == LW - 1 for every pair (no per-lane column tests).
 // Q = max(max(M, X) + gO, Y) is kept clamped at 0: the next row's Y is gE + Q.
-template <int LW, bool MASKED, bool EXACT>
+template <int LW, bool MASKED, bool EXACT, class C>
 __device__ __forceinline__ void band_cell(Band<LW> &S, const int k, const int32_t u6, const int32_t jb, const int32_t LB,
-                                          const int32_t w, const uint32_t cp, const uint32_t eqsh, const int32_t gO,
+                                          const int32_t w, const C &cp, const uint32_t eqsh, const int32_t gO,
                                           const int32_t gE, const bool act, int32_t &Zl, int32_t &Xl, int32_t &Pl,
                                           int32_t &Cl) {
     const bool last = EXACT ? (k == LW - 1) : (k == LW - 1 || k == w);  // Y = 0 at k == width
     const int kn = k < LW - 1 ? k + 1 : k;
-    int32_t M = bfe_s8(cp, S.b8[k]) + S.Tk[k];
+    int32_t M = cp.at(S.b8[k]) + S.Tk[k];
     int32_t Y = last ? 0 : gE + S.Qk[kn];
     int32_t X = k == 0 ? 0 : gE + max(max(Zl, Xl), 0);
     if (MASKED) {
@@ -108,22 +104,22 @@ __device__ __forceinline__ void band_cell(Band<LW> &S, const int k, const int32_
 // One phase-2 row u, then advance the A / B windows one base.  Branch-free:
 // lanes past their last row (u > rows2) keep computing but no longer update the
 // argmax, and the window loads are unconditional (clamped to the read).
-template <int LW, bool MASKED, bool EXACT>
+template <int LW, bool MASKED, bool EXACT, class C>
 __device__ __forceinline__ void band_row(Band<LW> &S, const int32_t u, const int32_t rows2, const int32_t zr,
-                                         const int32_t LB, const int32_t w, const uint32_t c0, const uint32_t c1,
-                                         const uint32_t c2, const uint32_t c3,
+                                         const int32_t LB, const int32_t w, const C c0, const C c1,
+                                         const C c2, const C c3,
                                          const int32_t gO, const int32_t gE, const uint32_t *Aw, const int32_t awl,
                                          const uint32_t *Bw, const int32_t bwl, const uint32_t *dummy) {
     const uint32_t a8 = ((S.awd >> (30 - 2 * (S.ap & 15))) & 3u) << 3;
-    const uint32_t c01 = (a8 & 8) ? c1 : c0, c23 = (a8 & 8) ? c3 : c2;
-    const uint32_t cp = (a8 & 16) ? c23 : c01;
+    const C c01 = (a8 & 8) ? c1 : c0, c23 = (a8 & 8) ? c3 : c2;
+    const C cp = (a8 & 16) ? c23 : c01;
     const uint32_t eqsh = 16u << a8;
     const int32_t u6 = u << 6;
     const int32_t jb = u - zr - 1;  // j - 1 of column 0
     const bool act = u <= rows2;
     int32_t Zl = 0, Xl = 0, Pl = 0, Cl = 0;
 #pragma unroll
-    for (int k = 0; k < LW; ++k) band_cell<LW, MASKED, EXACT>(S, k, u6, jb, LB, w, cp, eqsh, gO, gE, act, Zl, Xl, Pl, Cl);
+    for (int k = 0; k < LW; ++k) band_cell<LW, MASKED, EXACT, C>(S, k, u6, jb, LB, w, cp, eqsh, gO, gE, act, Zl, Xl, Pl, Cl);
     // two-word windows: the word after the current one was loaded at least one
     // row earlier, so the loads issued here are not waited on until next row
     // Window words are fetched the row before a window crosses into them, so a
@@ -235,14 +231,14 @@ struct BandTb {
     uint32_t awd, bw, pa, pb;
 };
 
-template <int LW, bool MASKED, bool EXACT>
+template <int LW, bool MASKED, bool EXACT, class C>
 __device__ __forceinline__ void band_cell_tb(BandTb<LW> &S, const int k, const int32_t u6, const int32_t jb,
-                                             const int32_t LB, const int32_t w, const uint32_t cp, const int32_t gO,
+                                             const int32_t LB, const int32_t w, const C &cp, const int32_t gO,
                                              const int32_t gE, const bool act, const uint32_t c1, const uint32_t c2,
                                              const uint32_t c3, int32_t &Zl, int32_t &Xl) {
     const bool last = EXACT ? (k == LW - 1) : (k == LW - 1 || k == w);
     const int kn = k < LW - 1 ? k + 1 : k;
-    int32_t M = bfe_s8(cp, S.b8[k]) + S.Tk[k];
+    int32_t M = cp.at(S.b8[k]) + S.Tk[k];
     int32_t Y = last ? 0 : gE + S.Qk[kn];
     int32_t X = k == 0 ? 0 : gE + max(max(Zl, Xl), 0);
     if (MASKED) {
@@ -263,15 +259,15 @@ __device__ __forceinline__ void band_cell_tb(BandTb<LW> &S, const int k, const i
     Xl = X;
 }
 
-template <int LW, bool MASKED, bool EXACT>
+template <int LW, bool MASKED, bool EXACT, class C>
 __device__ __forceinline__ void band_row_tb(BandTb<LW> &S, const int32_t u, const int32_t rows2, const int32_t zr,
-                                            const int32_t LB, const int32_t w, const uint32_t c0, const uint32_t cq1,
-                                            const uint32_t cq2, const uint32_t cq3, const int32_t gO, const int32_t gE,
+                                            const int32_t LB, const int32_t w, const C c0, const C cq1,
+                                            const C cq2, const C cq3, const int32_t gO, const int32_t gE,
                                             const uint32_t *Aw, const int32_t awl, const uint32_t *Bw,
                                             const int32_t bwl, const uint32_t *dummy, uint32_t *tb, uint64_t nt) {
     const uint32_t a8 = ((S.awd >> (30 - 2 * (S.ap & 15))) & 3u) << 3;
-    const uint32_t c01 = (a8 & 8) ? cq1 : c0, c23 = (a8 & 8) ? cq3 : cq2;
-    const uint32_t cp = (a8 & 16) ? c23 : c01;
+    const C c01 = (a8 & 8) ? cq1 : c0, c23 = (a8 & 8) ? cq3 : cq2;
+    const C cp = (a8 & 16) ? c23 : c01;
     const int32_t u6 = u << 6;
     const int32_t jb = u - zr - 1;
     const bool act = u <= rows2;
@@ -280,7 +276,7 @@ __device__ __forceinline__ void band_row_tb(BandTb<LW> &S, const int32_t u, cons
                    k3 = in_vgpr((int32_t)(3u << sh));
     int32_t Zl = 0, Xl = 0;
 #pragma unroll
-    for (int k = 0; k < LW; ++k) band_cell_tb<LW, MASKED, EXACT>(S, k, u6, jb, LB, w, cp, gO, gE, act, k1, k2, k3, Zl, Xl);
+    for (int k = 0; k < LW; ++k) band_cell_tb<LW, MASKED, EXACT, C>(S, k, u6, jb, LB, w, cp, gO, gE, act, k1, k2, k3, Zl, Xl);
     if ((u & 15) == 15) {  // a full 16-row word per column: out, lane-interleaved
         uint32_t *base = tb + (uint64_t)(u >> 4) * LW * nt;
 #pragma unroll
@@ -313,7 +309,7 @@ __device__ __forceinline__ uint32_t win16_g(const uint32_t *w, int32_t p) {
 // backtrack and the dud test.  p1[pair] = (ds << 1 | dud) or a negative error;
 // rows2[pair] = phase-2 row count (0 when phase 2 does not run) -- the key the
 // host sorts by so each wave of the phase-2 kernel gets pairs of similar length.
-template <int LW, bool EXACT>
+template <int LW, bool EXACT, class C>
 __global__ __launch_bounds__(256) void dovetail_p1_kernel(DevReads rd, const int32_t *lead, const int32_t *trail,
                                                           uint64_t npairs, AlignParams P, int32_t *p1,
                                                           uint64_t *rows2_key, uint32_t *order, int32_t *err,
@@ -327,25 +323,22 @@ __global__ __launch_bounds__(256) void dovetail_p1_kernel(DevReads rd, const int
         if (q.status < 0) set_err(err, q.status);
     }
     const int32_t w = q.w;
-    // column j (1..w) costs for A base x = 0..3 against B[j-1], as int8 bytes
-    // column packs (byte x = cost(x, b)) as four scalars: selects over an array
-    // index would be lowered to an LDS table
+    // column j (1..w) costs for A base x = 0..3 against B[j-1] (cost packs);
+    // the four column packs as scalars: selects over an array index would be
+    // lowered to an LDS table
     auto colpack = [&](int bb) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int x = 0; x < 4; ++x) v |= ((uint32_t)(uint8_t)(int8_t)P.cost[x * 4 + bb]) << (8 * x);
-        return v;
+        return C::make(P.cost[0 * 4 + bb], P.cost[1 * 4 + bb], P.cost[2 * 4 + bb], P.cost[3 * 4 + bb]);
     };
-    const uint32_t cq0 = colpack(0), cq1 = colpack(1), cq2 = colpack(2), cq3 = colpack(3);
+    const C cq0 = colpack(0), cq1 = colpack(1), cq2 = colpack(2), cq3 = colpack(3);
     // B[0 .. LW - 1) covers every column j <= w <= LW - 1 (LB >= w, else status -5)
     const uint32_t bw0 = q.status == 0 ? gld(q.Bw, 0) : 0u;
     const uint32_t bw1 = (LW > 17 && q.status == 0 && q.LB > 16) ? gld(q.Bw, 1) : 0u;
-    uint32_t cb[LW - 1];
+    C cb[LW - 1];
 #pragma unroll
     for (int j = 1; j < LW; ++j) {
         const uint32_t bwj = (j - 1) < 16 ? bw0 : bw1;
         const uint32_t bj = (bwj >> (30 - 2 * ((j - 1) & 15))) & 3u;
-        const uint32_t c01 = (bj & 1) ? cq1 : cq0, c23 = (bj & 1) ? cq3 : cq2;
+        const C c01 = (bj & 1) ? cq1 : cq0, c23 = (bj & 1) ? cq3 : cq2;
         cb[j - 1] = (bj & 2) ? c23 : c01;
     }
     // row-0 state: every cell 0; Q = max(max(M, X) + gO, Y) feeds the next row's Y
@@ -374,7 +367,7 @@ __global__ __launch_bounds__(256) void dovetail_p1_kernel(DevReads rd, const int
         const int32_t self = (i << 1) | 1;
 #pragma unroll
         for (int j = 0; j < LW - 1; ++j) {
-            const int32_t M = bfe_s8(cb[j], a8) + Tdiag;
+            const int32_t M = cb[j].at(a8) + Tdiag;
             const int32_t Y = gE + Q[j];
             const int32_t X = gE + max(max(Zl, Xl), 0);
             const int32_t T = max(max(M, X), Y);
@@ -425,7 +418,7 @@ __global__ __launch_bounds__(256) void dovetail_p1_kernel(DevReads rd, const int
 
 // Phase 2 (BioLibs.scala:691-819) + Alignment/Overlap validity, one pair per
 // lane, pairs taken in the order `order` (grouped by phase-2 row count).
-template <int LW, bool EXACT>
+template <int LW, bool EXACT, class C>
 __global__ __launch_bounds__(256) void dovetail_p2_kernel(DevReads rd, const int32_t *lead, const int32_t *trail,
                                                           uint64_t npairs, AlignParams P, const int32_t *p1,
                                                           const uint32_t *order, DevAlignment *out, int32_t *err) {
@@ -458,12 +451,9 @@ __global__ __launch_bounds__(256) void dovetail_p2_kernel(DevReads rd, const int
     rmax = __builtin_amdgcn_readfirstlane(rmax);
     lo = __builtin_amdgcn_readfirstlane(lo);
     hi = __builtin_amdgcn_readfirstlane(hi);
-    uint32_t cpa[4];
+    C cpa[4];  // row packs: costs of A base x against B bases 0..3
 #pragma unroll
-    for (int x = 0; x < 4; ++x)
-        cpa[x] = (uint32_t)(uint8_t)(int8_t)P.cost[x * 4] | ((uint32_t)(uint8_t)(int8_t)P.cost[x * 4 + 1] << 8) |
-                 ((uint32_t)(uint8_t)(int8_t)P.cost[x * 4 + 2] << 16) |
-                 ((uint32_t)(uint8_t)(int8_t)P.cost[x * 4 + 3] << 24);
+    for (int x = 0; x < 4; ++x) cpa[x] = C::make(P.cost[x * 4], P.cost[x * 4 + 1], P.cost[x * 4 + 2], P.cost[x * 4 + 3]);
     Band<LW> S;
     const uint32_t bw0 = p2 ? gld(q.Bw, 0) : 0u;  // k - zr < LW: B[0 .. 32)
     const uint32_t bw1 = (LW > 16 && p2 && LB > 16) ? gld(q.Bw, 1) : 0u;
@@ -491,11 +481,11 @@ __global__ __launch_bounds__(256) void dovetail_p2_kernel(DevReads rd, const int
     __builtin_amdgcn_s_waitcnt(0);
     int32_t u = 1;
     const int32_t e1 = min(lo - 1, rmax), e2 = min(hi, rmax);
-    for (; u <= e1; ++u) band_row<LW, true, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl,
+    for (; u <= e1; ++u) band_row<LW, true, EXACT, C>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl,
                                                     q.Bw, bwl, rd.codes);
-    for (; u <= e2; ++u) band_row<LW, false, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw,
+    for (; u <= e2; ++u) band_row<LW, false, EXACT, C>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw,
                                                      awl, q.Bw, bwl, rd.codes);
-    for (; u <= rmax; ++u) band_row<LW, true, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl,
+    for (; u <= rmax; ++u) band_row<LW, true, EXACT, C>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl,
                                                     q.Bw, bwl, rd.codes);
 
     if (!have) return;
@@ -505,7 +495,7 @@ __global__ __launch_bounds__(256) void dovetail_p2_kernel(DevReads rd, const int
 // Phase 2 with stored traceback codes: same contract as dovetail_p2_kernel;
 // tb holds 16 columns x rw words for each of the nt lanes of this launch,
 // which covers pairs order[t0 .. t0 + nt).
-template <int LW, bool EXACT>
+template <int LW, bool EXACT, class C>
 __global__ __launch_bounds__(256) void dovetail_p2tb_kernel(DevReads rd, const int32_t *lead, const int32_t *trail,
                                                             uint64_t npairs, uint64_t t0, uint64_t nt, AlignParams P,
                                                             const int32_t *p1, const uint32_t *order,
@@ -539,12 +529,9 @@ __global__ __launch_bounds__(256) void dovetail_p2tb_kernel(DevReads rd, const i
     rmax = __builtin_amdgcn_readfirstlane(rmax);
     lo = __builtin_amdgcn_readfirstlane(lo);
     hi = __builtin_amdgcn_readfirstlane(hi);
-    uint32_t cpa[4];
+    C cpa[4];  // row packs: costs of A base x against B bases 0..3
 #pragma unroll
-    for (int x = 0; x < 4; ++x)
-        cpa[x] = (uint32_t)(uint8_t)(int8_t)P.cost[x * 4] | ((uint32_t)(uint8_t)(int8_t)P.cost[x * 4 + 1] << 8) |
-                 ((uint32_t)(uint8_t)(int8_t)P.cost[x * 4 + 2] << 16) |
-                 ((uint32_t)(uint8_t)(int8_t)P.cost[x * 4 + 3] << 24);
+    for (int x = 0; x < 4; ++x) cpa[x] = C::make(P.cost[x * 4], P.cost[x * 4 + 1], P.cost[x * 4 + 2], P.cost[x * 4 + 3]);
     BandTb<LW> S;
     const uint32_t bw0 = p2 ? gld(q.Bw, 0) : 0u;  // k - zr < LW: B[0 .. 32)
     const uint32_t bw1 = (LW > 16 && p2 && LB > 16) ? gld(q.Bw, 1) : 0u;
@@ -570,13 +557,13 @@ __global__ __launch_bounds__(256) void dovetail_p2tb_kernel(DevReads rd, const i
     int32_t u = 1;
     const int32_t e1 = min(lo - 1, rmax), e2 = min(hi, rmax);
     for (; u <= e1; ++u)
-        band_row_tb<LW, true, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl, q.Bw,
+        band_row_tb<LW, true, EXACT, C>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl, q.Bw,
                                  bwl, rd.codes, tb, nt);
     for (; u <= e2; ++u)
-        band_row_tb<LW, false, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl, q.Bw,
+        band_row_tb<LW, false, EXACT, C>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl, q.Bw,
                                   bwl, rd.codes, tb, nt);
     for (; u <= rmax; ++u)
-        band_row_tb<LW, true, EXACT>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl, q.Bw,
+        band_row_tb<LW, true, EXACT, C>(S, u, rows2, zr, LB, w, cpa[0], cpa[1], cpa[2], cpa[3], gO, gE, q.Aw, awl, q.Bw,
                                  bwl, rd.codes, tb, nt);
     if ((rmax & 15) != 15) {  // the last, partial row block
         uint32_t *base = tb + (uint64_t)(rmax >> 4) * LW * nt;
@@ -623,13 +610,19 @@ __global__ __launch_bounds__(256) void dovetail_p2tb_kernel(DevReads rd, const i
 }
 
 // LW = 16 (with the EXACT variant: every band exactly 16 cells), 24 or 32
-#define SA_LANE_DISPATCH(KERNEL, GRID, ...)                                                              \
-    do {                                                                                                 \
-        if (lw == 16 && exact) hipLaunchKernelGGL((KERNEL<16, true>), GRID, dim3(256), 0, s, __VA_ARGS__); \
-        else if (lw == 16) hipLaunchKernelGGL((KERNEL<16, false>), GRID, dim3(256), 0, s, __VA_ARGS__);     \
-        else if (lw == 24) hipLaunchKernelGGL((KERNEL<24, false>), GRID, dim3(256), 0, s, __VA_ARGS__);     \
-        else if (lw == 32) hipLaunchKernelGGL((KERNEL<32, false>), GRID, dim3(256), 0, s, __VA_ARGS__);     \
-        else return hipErrorInvalidValue;                                                                \
+#define SA_LANE_DISPATCH_C(KERNEL, C, GRID, ...)                                                            \
+    do {                                                                                                    \
+        if (lw == 16 && exact) hipLaunchKernelGGL((KERNEL<16, true, C>), GRID, dim3(256), 0, s, __VA_ARGS__); \
+        else if (lw == 16) hipLaunchKernelGGL((KERNEL<16, false, C>), GRID, dim3(256), 0, s, __VA_ARGS__);     \
+        else if (lw == 24) hipLaunchKernelGGL((KERNEL<24, false, C>), GRID, dim3(256), 0, s, __VA_ARGS__);     \
+        else if (lw == 32) hipLaunchKernelGGL((KERNEL<32, false, C>), GRID, dim3(256), 0, s, __VA_ARGS__);     \
+        else return hipErrorInvalidValue;                                                                   \
+    } while (0)
+// cost packs: int8 bytes unless the (reduced) matrix needs int16 halves
+#define SA_LANE_DISPATCH(KERNEL, GRID, ...)                                                                 \
+    do {                                                                                                    \
+        if (p.cost_bits == 16) SA_LANE_DISPATCH_C(KERNEL, Cost16, GRID, __VA_ARGS__);                       \
+        else SA_LANE_DISPATCH_C(KERNEL, Cost8, GRID, __VA_ARGS__);                                          \
     } while (0)
 
 int dovetail_lane_width(int32_t wmax) {

@@ -56,7 +56,7 @@ __device__ __forceinline__ uint32_t base_at(const uint32_t *w, int32_t p) {
 
 }  // namespace
 
-template <int S>
+template <int S, class C>
 __global__ __launch_bounds__(256) void local_dp_kernel(DevReads rd, const int32_t *lead, const int32_t *trail,
                                                        uint64_t p0, uint64_t np, AlignParams P, uint32_t wpl,
                                                        uint32_t *tb, int4 *lmax, int32_t *err,
@@ -84,19 +84,17 @@ __global__ __launch_bounds__(256) void local_dp_kernel(DevReads rd, const int32_
             const uint32_t *Bw = rd.codes + rd.woff[b];
             const int32_t gO = in_vgpr(P.gap_open), gE = in_vgpr(P.gap_extend);
             const int32_t nl = (LB + S - 1) / S;
-            // cost packs of my columns: byte x = cost(x, B[j-1]); columns past |B|
+            // cost packs of my columns: entry x = cost(x, B[j-1]); columns past |B|
             // get 0 (they can then never raise the lane's running best)
-            uint32_t cb[S];
+            C cb[S];
 #pragma unroll
             for (int s = 0; s < S; ++s) {
                 const int32_t pos = lane * S + s;
-                uint32_t v = 0;
+                cb[s] = C::make(0, 0, 0, 0);
                 if (pos < LB) {
                     const uint32_t bc = base_at(Bw, pos);
-#pragma unroll
-                    for (int x = 0; x < 4; ++x) v |= ((uint32_t)(uint8_t)(int8_t)P.cost[x * 4 + bc]) << (8 * x);
+                    cb[s] = C::make(P.cost[0 * 4 + bc], P.cost[1 * 4 + bc], P.cost[2 * 4 + bc], P.cost[3 * 4 + bc]);
                 }
-                cb[s] = v;
             }
             int32_t Pv[S], Qv[S];  // previous row: max(T, 0), max(max(M, X) + gO, Y, 0)
 #pragma unroll
@@ -130,7 +128,7 @@ __global__ __launch_bounds__(256) void local_dp_kernel(DevReads rd, const int32_
                     int32_t rk = INT32_MIN;  // row argmax key (T << 5 | 31 - s)
 #pragma unroll
                     for (int s = 0; s < S; ++s) {
-                        const int32_t c = __builtin_amdgcn_sbfe((int32_t)cb[s], a8, 8);
+                        const int32_t c = cb[s].at(a8);
                         const int32_t M = c + Pd;
                         const int32_t Y = gE + Qv[s];
                         const int32_t X = gE + R;
@@ -299,8 +297,12 @@ hipError_t launch_local_align(const DevReads &r, const int32_t *lead, const int3
     if (!np) return hipSuccess;
     const dim3 g1((uint32_t)((np + 3) / 4)), g2((uint32_t)((np + 255) / 256));
 #define SA_LOCAL(SS)                                                                                           \
-    hipLaunchKernelGGL(local_dp_kernel<SS>, g1, dim3(256), 0, s, r, lead, trail, p0, np, p, wpl, tb, lmax, err, \
-                       cells);                                                                                 \
+    if (p.cost_bits == 16)                                                                                     \
+        hipLaunchKernelGGL((local_dp_kernel<SS, Cost16>), g1, dim3(256), 0, s, r, lead, trail, p0, np, p, wpl, tb, \
+                           lmax, err, cells);                                                                  \
+    else                                                                                                       \
+        hipLaunchKernelGGL((local_dp_kernel<SS, Cost8>), g1, dim3(256), 0, s, r, lead, trail, p0, np, p, wpl, tb,  \
+                           lmax, err, cells);                                                                  \
     hipLaunchKernelGGL(local_walk_kernel<SS>, g2, dim3(256), 0, s, r, lead, trail, p0, np, p, wpl, tb, lmax, out)
     switch (stripe) {
     case 4: SA_LOCAL(4); break;

@@ -169,10 +169,34 @@ struct PairOut {
     uint32_t *overflow_n;
 };
 
+// Four alignment costs indexed by a 2-bit base code given as x8 = 8 * code.
+// Cost8: one word of int8 bytes (HOXD70 and every matrix whose entries fit a
+// byte after the common-divisor reduction); Cost16: two words of int16 halves
+// (any other matrix up to |cost| <= 32,767) -- one extra select per lookup.
+struct Cost8 {
+    uint32_t p;
+    __device__ __forceinline__ int32_t at(uint32_t x8) const { return __builtin_amdgcn_sbfe((int32_t)p, x8, 8); }
+    __device__ __forceinline__ static Cost8 make(int32_t c0, int32_t c1, int32_t c2, int32_t c3) {
+        return Cost8{(uint32_t)(c0 & 255) | ((uint32_t)(c1 & 255) << 8) | ((uint32_t)(c2 & 255) << 16) |
+                     ((uint32_t)(c3 & 255) << 24)};
+    }
+};
+struct Cost16 {
+    uint32_t lo, hi;
+    __device__ __forceinline__ int32_t at(uint32_t x8) const {
+        return __builtin_amdgcn_sbfe((int32_t)((x8 & 16) ? hi : lo), (x8 & 8) << 1, 16);
+    }
+    __device__ __forceinline__ static Cost16 make(int32_t c0, int32_t c1, int32_t c2, int32_t c3) {
+        return Cost16{(uint32_t)(c0 & 0xFFFF) | ((uint32_t)(c1 & 0xFFFF) << 16),
+                      (uint32_t)(c2 & 0xFFFF) | ((uint32_t)(c3 & 0xFFFF) << 16)};
+    }
+};
+
 struct AlignParams {
     int32_t k, gap_open, gap_extend, min_overlap;
     float one_minus_minid, min_identity, max_ignore;
     int32_t cost[16];
+    int32_t cost_bits;           // 8: Cost8 packs, 16: Cost16 packs (host: after the common-divisor reduction)
     uint32_t rw;                 // traceback words per column (odd)
 };
 

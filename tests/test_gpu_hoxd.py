@@ -5,8 +5,9 @@ Both aligners -- the banded dovetail DP (generateFastDovetailAlignmentSet) and
 --quadratic-align (generateLocalAlignmentSet) -- against the C oracle with:
 an asymmetric matrix, HOXD70 scaled x10 with x10 gap costs (run as HOXD70
 after the common-divisor reduction), and a matrix file with
-missing rows (readHOXD starts from a zeroed 4x4).  Costs that do not fit the
-kernels' 8-bit lanes after that reduction fail with SA_E_OVERFLOW.
+missing rows (readHOXD starts from a zeroed 4x4).  Costs that do not fit 8
+bits after that reduction run on int16 cost packs (every DP kernel: lane,
+lane-group and quadratic); beyond 16 bits they fail with SA_E_OVERFLOW.
 """
 import numpy as np
 import pytest
@@ -72,9 +73,32 @@ def test_matrix_file_with_missing_rows(oracle_mod, tmp_path, quadratic):
     check(oracle_mod, reads_for(13), cost, quadratic, kmer_size=12)
 
 
-def test_costs_beyond_int8_fail_exactly():
+@pytest.mark.parametrize("kernel", ["lane", "group", "quadratic"])
+def test_costs_beyond_int8(oracle_mod, kernel):
+    """A matrix whose reduced entries need 16 bits (gcd 1 with A:A = 1000):
+    the int16 cost packs of each DP kernel against the oracle."""
     cost = list(HOXD70)
-    cost[0] = 1000  # gcd with the rest is 1: 1000 does not fit the 8-bit cost lanes
+    cost[0] = 1000
+    cost[15] = -777
+    reads = reads_for(14)
+    st = dict(kmer_size=12)
+    quadratic = kernel == "quadratic"
+    r = oracle_mod.Run(reads=reads, settings=oracle_mod.default_settings(cost=cost, **st), quadratic=quadratic)
+    ov = sao.Overlapper(cost=cost, aligner=sao.SA_ALIGNER_QUADRATIC if quadratic else sao.SA_ALIGNER_LINEAR,
+                        align_kernel=1 if kernel == "group" else 0, **st)
+    ov.add_reads(reads)
+    ov.build()
+    ov.align()
+    al = ov.alignments()
+    assert len(al) == len(r.lead) > 100
+    for name in ALIGN_CMP:
+        np.testing.assert_array_equal(al[:, sao.ALIGN_FIELDS.index(name)], r.align_field(name), err_msg=name)
+    assert ov.ovl() == r.ovl
+
+
+def test_costs_beyond_int16_fail_exactly():
+    cost = list(HOXD70)
+    cost[0] = 40000  # gcd with the rest is 1: 40,000 does not fit the 16-bit cost packs
     ov = sao.Overlapper(cost=cost, kmer_size=12)
     ov.add_reads(reads_for(14))
     ov.build()
