@@ -972,8 +972,17 @@ int device_align(sa_ctx *c, bool readback) {
             ENSURE(c->d_ovals2, nd, &v1);
             ENSURE(c->d_osort, radix_sort_temp_bytes(nd), &tmp);
             const int32_t *dl = (const int32_t *)c->d_lead.p, *dt = (const int32_t *)c->d_trail.p;
-            HIPCHK(launch_dovetail_p1(AR, dl, dt, nd, P, lw, exact, p1, k0, v0, &cnt->err, cnt->cells,
-                                      c->stream));
+            // phase 1 two pairs per lane (packed 16-bit) when every score fits 16 bits
+            int64_t cmax = 0;
+            for (int x = 0; x < 16; ++x) cmax = std::max<int64_t>(cmax, P.cost[x]);
+            const bool x2 = lw == 16 && exact && P.cost_bits == 8 && P.gap_open <= 0 && P.gap_extend <= 0 &&
+                            -(int64_t)P.gap_open < 65536 && -(int64_t)P.gap_extend < 65536 &&
+                            cmax * (int64_t)maxL + 255 < 65536;
+            if (x2)
+                HIPCHK(launch_dovetail_p1x2(AR, dl, dt, nd, P, p1, k0, v0, &cnt->err, cnt->cells, c->stream));
+            else
+                HIPCHK(launch_dovetail_p1(AR, dl, dt, nd, P, lw, exact, p1, k0, v0, &cnt->err, cnt->cells,
+                                          c->stream));
             HIPCHK(radix_sort(&k0, &v0, &k1, &v1, nd, 0, 20, tmp, c->stream));
             if (c->align_kernel == 3) {  // path summaries forwarded per cell
                 HIPCHK(launch_dovetail_p2(AR, dl, dt, nd, P, lw, exact, p1, v0, out, &cnt->err, c->stream));

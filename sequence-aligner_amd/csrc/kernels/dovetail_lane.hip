@@ -416,6 +416,149 @@ __global__ __launch_bounds__(256) void dovetail_p1_kernel(DevReads rd, const int
     add_cells(cells, cells_total);
 }
 
+// Phase 1 with TWO pairs per lane in packed 16-bit halves (pair 2t in the low
+// half, 2t + 1 in the high half): v_pk_{add,sub,max}_u16 run both pairs' cells
+// in one instruction.  All values are kept saturated at 0 from below, which is
+// exact here: every recurrence takes max(.., 0) (or compares with a positive
+// maximum) before a negative value could matter -- T > 0 tests, M == T / X == T
+// when T > 0, best starts at 0 -- and the host launches this kernel only when
+// every score fits 16 bits (largest cost x |A| + 255 < 2^16), gap costs are
+// <= 0 and every band is exactly 16 cells (EXACT).  Costs are int8 bytes biased
+// by +128 so one v_perm_b32 per cell builds both pairs' (cost + 128).
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 pk(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+__device__ __forceinline__ uint32_t upk(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ u16x2 pk_max(u16x2 a, u16x2 b) { return __builtin_elementwise_max(a, b); }
+__device__ __forceinline__ u16x2 pk_subs(u16x2 a, u16x2 b) { return __builtin_elementwise_sub_sat(a, b); }
+// 0xFFFF in each half where x == 0 / where x > 0
+__device__ __forceinline__ uint32_t pk_is0(u16x2 x, u16x2 one) { return upk((u16x2)0 - pk_subs(one, x)); }
+__device__ __forceinline__ uint32_t pk_gt0(u16x2 x, u16x2 one) {
+    return upk((u16x2)0 - __builtin_elementwise_min(x, one));
+}
+__device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
+
+__global__ __launch_bounds__(256) void dovetail_p1x2_kernel(DevReads rd, const int32_t *lead, const int32_t *trail,
+                                                            uint64_t npairs, AlignParams P, int32_t *p1,
+                                                            uint64_t *rows2_key, uint32_t *order, int32_t *err,
+                                                            unsigned long long *cells_total) {
+    constexpr int LW = 16;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t pairA = 2 * t, pairB = 2 * t + 1;
+    const bool haveA = pairA < npairs, haveB = pairB < npairs;
+    LanePair qa{0, 0, 0, 0, 0, -100, rd.codes, rd.codes}, qb = qa;
+    if (haveA) {
+        qa = lane_pair<LW, true>(rd, lead, trail, pairA, P);
+        if (qa.status < 0) set_err(err, qa.status);
+    }
+    if (haveB) {
+        qb = lane_pair<LW, true>(rd, lead, trail, pairB, P);
+        if (qb.status < 0) set_err(err, qb.status);
+    }
+    // biased column packs: byte x = cost(x, b) + 128 for B base b of column j
+    auto colpack = [&](int bb) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int x = 0; x < 4; ++x) v |= (uint32_t)((P.cost[x * 4 + bb] + 128) & 255) << (8 * x);
+        return v;
+    };
+    const uint32_t cq0 = colpack(0), cq1 = colpack(1), cq2 = colpack(2), cq3 = colpack(3);
+    const uint32_t bwA = qa.status == 0 ? gld(qa.Bw, 0) : 0u, bwB = qb.status == 0 ? gld(qb.Bw, 0) : 0u;
+    uint32_t cbA[LW - 1], cbB[LW - 1];
+#pragma unroll
+    for (int j = 1; j < LW; ++j) {
+        const uint32_t ba = (bwA >> (30 - 2 * (j - 1))) & 3u, bb = (bwB >> (30 - 2 * (j - 1))) & 3u;
+        const uint32_t a01 = (ba & 1) ? cq1 : cq0, a23 = (ba & 1) ? cq3 : cq2;
+        const uint32_t b01 = (bb & 1) ? cq1 : cq0, b23 = (bb & 1) ? cq3 : cq2;
+        cbA[j - 1] = (ba & 2) ? a23 : a01;
+        cbB[j - 1] = (bb & 2) ? b23 : b01;
+    }
+    const u16x2 gO = pk((uint32_t)in_vgpr((int32_t)((uint32_t)(-P.gap_open) * 0x10001u)));
+    const u16x2 gE = pk((uint32_t)in_vgpr((int32_t)((uint32_t)(-P.gap_extend) * 0x10001u)));
+    const u16x2 bias = pk((uint32_t)in_vgpr((int32_t)0x00800080));
+    const u16x2 one = pk((uint32_t)in_vgpr((int32_t)0x00010001));
+    u16x2 Tc[LW - 1], Q[LW - 1];
+    uint32_t O[LW - 1];
+#pragma unroll
+    for (int j = 0; j < LW - 1; ++j) { Tc[j] = 0; Q[j] = 0; O[j] = 0x00010001u; }  // origin (row 0, col != 0)
+    u16x2 best = 0;
+    uint32_t borg = 0;
+    const int32_t rowsA = qa.status == 0 ? qa.LA : 0, rowsB = qb.status == 0 ? qb.LA : 0;
+    int32_t rmax = max(rowsA, rowsB);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) rmax = max(rmax, __shfl_xor(rmax, off, 64));
+    rmax = __builtin_amdgcn_readfirstlane(rmax);
+    const int32_t awlA = max((qa.LA + 15) / 16 - 1, 0), awlB = max((qb.LA + 15) / 16 - 1, 0);
+    uint32_t awA = qa.Aw[0], awnA = qa.Aw[min(1, awlA)];
+    uint32_t awB = qb.Aw[0], awnB = qb.Aw[min(1, awlB)];
+    __builtin_amdgcn_s_waitcnt(0);
+#pragma unroll 2
+    for (int32_t i = 1; i <= rmax; ++i) {
+        const uint32_t act = (i <= rowsA ? 0x0000FFFFu : 0u) | (i <= rowsB ? 0xFFFF0000u : 0u);
+        const uint32_t sh = 30 - 2 * ((i - 1) & 15);
+        const uint32_t aA = (awA >> sh) & 3u, aB = (awB >> sh) & 3u;
+        const uint32_t sel = aA | 0x00000C00u | ((4u + aB) << 16) | 0x0C000000u;  // [cA, 0, cB, 0]
+        u16x2 Tdiag = 0, Zl = 0, Xl = 0;
+        uint32_t Odiag = (uint32_t)((i - 1) << 1) * 0x10001u;
+        uint32_t Ol = (uint32_t)(i << 1) * 0x10001u;
+        const uint32_t self = (uint32_t)((i << 1) | 1) * 0x10001u;
+#pragma unroll
+        for (int j = 0; j < LW - 1; ++j) {
+            const u16x2 cpk = pk(__builtin_amdgcn_perm(cbB[j], cbA[j], sel));
+            const u16x2 M = pk_subs(Tdiag + cpk, bias);
+            const u16x2 Y = pk_subs(Q[j], gE);
+            const u16x2 X = pk_subs(pk_max(Zl, Xl), gE);
+            const u16x2 T = pk_max(pk_max(M, X), Y);
+            const uint32_t Oup = O[j];
+            const uint32_t mM = pk_is0(pk_subs(T, M), one), mX = pk_is0(pk_subs(T, X), one);
+            const uint32_t on = bsel(pk_gt0(T, one), bsel(mM, Odiag, bsel(mX, Ol, Oup)), self);
+            Tdiag = Tc[j];
+            Odiag = Oup;
+            Tc[j] = T;
+            Q[j] = pk_max(pk_subs(pk_max(M, X), gO), Y);
+            O[j] = on;
+            const uint32_t nb = pk_gt0(pk_subs(T, best), one) & act;  // first strict '>' in row-major order
+            best = pk(bsel(nb, upk(T), upk(best)));
+            borg = bsel(nb, on, borg);
+            Zl = pk_subs(pk_max(M, Y), gO);
+            Xl = X;
+            Ol = on;
+        }
+        awA = (i & 15) == 0 ? awnA : awA;
+        awB = (i & 15) == 0 ? awnB : awB;
+        awnA = gld(qa.Aw, min((i >> 4) + 1, awlA));
+        awnB = gld(qb.Aw, min((i >> 4) + 1, awlB));
+    }
+    unsigned long long cells = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const bool have = h ? haveB : haveA;
+        const LanePair &q = h ? qb : qa;
+        const uint64_t pair = h ? pairB : pairA;
+        if (!have) continue;
+        const int32_t bst = (int32_t)((upk(best) >> (16 * h)) & 0xFFFFu);
+        const int32_t org = (int32_t)((borg >> (16 * h)) & 0xFFFFu);
+        int32_t r = q.status, rows2 = 0;
+        if (r == 0) {
+            cells += (unsigned long long)q.LA * q.w;
+            if (bst <= 0) { r = -6; set_err(err, -6); }  // the reference walks off (0,0)
+            else {
+                r = org;  // (ds << 1) | dud
+                if (!(org & 1)) {
+                    const int32_t ds = org >> 1, zr = q.w / 2, dL = q.LA - ds;
+                    cells += (unsigned long long)(dL + 1) * (q.w + 1);
+                    const int32_t touched = max(q.w, min(q.LB, dL - zr + q.w));
+                    if (rd.bad[q.b] < touched) { r = -3; set_err(err, -3); }
+                    else rows2 = dL;
+                }
+            }
+        }
+        p1[pair] = r;
+        rows2_key[pair] = (uint64_t)(0xFFFFFu - (uint32_t)min(rows2, 0xFFFFF));
+        order[pair] = (uint32_t)pair;
+    }
+    add_cells(cells, cells_total);
+}
+
 // Phase 2 (BioLibs.scala:691-819) + Alignment/Overlap validity, one pair per
 // lane, pairs taken in the order `order` (grouped by phase-2 row count).
 template <int LW, bool EXACT, class C>
@@ -644,6 +787,16 @@ hipError_t launch_dovetail_p2(const DevReads &r, const int32_t *lead, const int3
     if (!n) return hipSuccess;
     const dim3 grid((uint32_t)((n + 255) / 256));
     SA_LANE_DISPATCH(dovetail_p2_kernel, grid, r, lead, trail, n, p, p1, order, out, err);
+    return hipGetLastError();
+}
+
+hipError_t launch_dovetail_p1x2(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
+                                const AlignParams &p, int32_t *p1, uint64_t *rows2_key, uint32_t *order, int32_t *err,
+                                unsigned long long *cells, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const uint64_t lanes = (n + 1) / 2;
+    hipLaunchKernelGGL(dovetail_p1x2_kernel, dim3((uint32_t)((lanes + 255) / 256)), dim3(256), 0, s, r, lead, trail,
+                       n, p, p1, rows2_key, order, err, cells);
     return hipGetLastError();
 }
 
