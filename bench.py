@@ -370,13 +370,15 @@ def main():
     VALU_PEAK = 256 * 4 * 32 * 2.4e9 / 1e12
     al_ms = astages["align"][0] / max(astages["align"][1], 1)
     cells_g = ast["dp_cells"] / P_here
-    valu = pmc_sum(rows, ("void sa::dovetail_p1_kernel<16, true>", "void sa::dovetail_p2tb_kernel<16, true>"),
-                   "SQ_INSTS_VALU_avg")
+    # at the bench shape both phases run two pairs per lane (packed 16-bit halves,
+    # DESIGN.md 4.6): one issue slot there does two cells' operation
+    valu = pmc_sum(rows, ("sa::dovetail_p1x2_kernel", "sa::dovetail_p2tbx2_kernel"), "SQ_INSTS_VALU_avg")
     valu_ach = valu * 64 / (al_ms * 1e-3) / 1e12 if valu is not None and al_ms > 0 else None
     roofline_align = {"bound": "valu", "unit": "T lane-ops/s", "peak": round(VALU_PEAK, 1),
                       "achieved": round(valu_ach, 2) if valu_ach is not None else None,
                       "frac": round(valu_ach / VALU_PEAK, 4) if valu_ach is not None else None,
-                      "kernel": "dovetail_p1<16> + dovetail_p2tb<16> (+ phase-2 pair regrouping sort)",
+                      "kernel": "dovetail_p1x2 + dovetail_p2tbx2 (+ phase-2 pair regrouping sort)",
+                      "gcups": round(cells_g / (al_ms * 1e-3) / 1e9, 1) if al_ms else None,
                       "launch_ms": round(al_ms, 4), "dp_cells_per_launch": int(cells_g),
                       "nominal_18_ops_per_cell": round(18.0 * cells_g / (al_ms * 1e-3) / 1e12, 2) if al_ms else None,
                       "valu_wave_insts_per_launch": int(valu) if valu is not None else None,

@@ -987,14 +987,21 @@ int device_align(sa_ctx *c, bool readback) {
             if (c->align_kernel == 3) {  // path summaries forwarded per cell
                 HIPCHK(launch_dovetail_p2(AR, dl, dt, nd, P, lw, exact, p1, v0, out, &cnt->err, c->stream));
             } else {  // 2-bit traceback codes in HBM + per-lane walk, in launches of <= 4 GiB of codes
-                const uint64_t per_lane = dovetail_tb_words(1, maxL, lw);
-                uint64_t chunk = std::max<uint64_t>(256, ((1ull << 30) / per_lane) & ~255ull);
-                chunk = std::min<uint64_t>(chunk, (nd + 255) & ~255ull);
+                // two pairs per lane as in phase 1 when the argmax row also fits (u << 4 | k in 16 bits)
+                const bool x2tb = x2 && maxL < 4096;
+                const uint64_t per_2 = x2tb ? dovetail_tbx2_words(2, maxL) : dovetail_tb_words(2, maxL, lw);
+                uint64_t chunk = std::max<uint64_t>(512, (2 * ((1ull << 30) / per_2)) & ~511ull);
+                chunk = std::min<uint64_t>(chunk, (nd + 511) & ~511ull);
                 uint32_t *tb;
-                ENSURE(c->d_tb, dovetail_tb_words(chunk, maxL, lw), &tb);
-                for (uint64_t t0 = 0; t0 < nd; t0 += chunk)
-                    HIPCHK(launch_dovetail_p2tb(AR, dl, dt, nd, t0, chunk, P, lw, exact, p1, v0, out, &cnt->err, tb,
-                                                c->stream));
+                ENSURE(c->d_tb, x2tb ? dovetail_tbx2_words(chunk, maxL) : dovetail_tb_words(chunk, maxL, lw), &tb);
+                for (uint64_t t0 = 0; t0 < nd; t0 += chunk) {
+                    if (x2tb)
+                        HIPCHK(launch_dovetail_p2tbx2(AR, dl, dt, nd, t0, chunk, P, p1, v0, out, &cnt->err, tb,
+                                                      c->stream));
+                    else
+                        HIPCHK(launch_dovetail_p2tb(AR, dl, dt, nd, t0, chunk, P, lw, exact, p1, v0, out, &cnt->err,
+                                                    tb, c->stream));
+                }
             }
         } else
             HIPCHK(launch_dovetail(AR, (const int32_t *)c->d_lead.p, (const int32_t *)c->d_trail.p, nd, P,

@@ -752,6 +752,241 @@ __global__ __launch_bounds__(256) void dovetail_p2tb_kernel(DevReads rd, const i
     finish_alignment(P, q, r1, ds, zr, S.best, S.bpos, bstop, bce, out + pair, err);
 }
 
+// Phase 2 with stored traceback codes, TWO pairs per lane in packed 16-bit
+// halves (pairs order[t0 + 2 tl] and order[t0 + 2 tl + 1]: adjacent in the
+// row-count order, so of similar length), same conditions and saturation
+// argument as dovetail_p1x2_kernel.  Each column word holds 8 rows of 2-bit
+// codes per pair (low half: the first pair), word (rb8, k) of lane tl at
+// (rb8 * 16 + k) * nl; the walks run per pair over the halves.
+struct BandX2 {
+    uint32_t sel[16];          // v_perm selector per column: [B code of pair 0, 0, 4 + B code of pair 1, 0]
+    u16x2 Tk[16], Qk[16];
+    uint32_t acc[16];
+    u16x2 best;
+    uint32_t bpos;
+    int32_t ap[2], bp[2];
+    uint32_t awd[2], pa[2], bw[2], pb[2];
+};
+
+__device__ __forceinline__ uint32_t x2_sel(uint32_t b0, uint32_t b1) {
+    return b0 | 0x00000C00u | ((4u + b1) << 16) | 0x0C000000u;
+}
+
+template <bool MASKED>
+__device__ __forceinline__ void band_row_x2(BandX2 &S, const int32_t u, const uint32_t act, const int32_t zr,
+                                            const int32_t LB0, const int32_t LB1, const uint32_t *cpa, const u16x2 gO,
+                                            const u16x2 gE, const u16x2 bias, const u16x2 one, const uint32_t two,
+                                            const uint32_t three, const LanePair &q0, const LanePair &q1,
+                                            const int32_t awl0, const int32_t awl1, const int32_t bwl0,
+                                            const int32_t bwl1, const uint32_t *dummy, uint32_t *tb, uint64_t nl) {
+    uint32_t cp[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const uint32_t a = (S.awd[h] >> (30 - 2 * (S.ap[h] & 15))) & 3u;
+        const uint32_t c01 = (a & 1) ? cpa[1] : cpa[0], c23 = (a & 1) ? cpa[3] : cpa[2];
+        cp[h] = (a & 2) ? c23 : c01;
+    }
+    const uint32_t u4 = (uint32_t)(u << 4) * 0x10001u;  // argmax cell (u << 4 | k) per half: u < 4096
+    const int32_t jb = u - zr - 1;
+    const int sh = 2 * (u & 7);
+    u16x2 Zl = 0, Xl = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const u16x2 cpk = pk(__builtin_amdgcn_perm(cp[1], cp[0], S.sel[k]));
+        u16x2 M = pk_subs(S.Tk[k] + cpk, bias);
+        u16x2 Y = k == 15 ? (u16x2)0 : pk_subs(S.Qk[k + 1], gE);
+        u16x2 X = k == 0 ? (u16x2)0 : pk_subs(pk_max(Zl, Xl), gE);
+        if (MASKED) {
+            const uint32_t v = ((uint32_t)(jb + k) < (uint32_t)LB0 ? 0x0000FFFFu : 0u) |
+                               ((uint32_t)(jb + k) < (uint32_t)LB1 ? 0xFFFF0000u : 0u);
+            M = pk(upk(M) & v);
+            X = pk(upk(X) & v);
+            Y = pk(upk(Y) & v);
+        }
+        const u16x2 T = pk_max(pk_max(M, X), Y);
+        const uint32_t mM = pk_is0(pk_subs(T, M), one), mX = pk_is0(pk_subs(T, X), one);
+        const uint32_t code = bsel(mM, upk(one), bsel(mX, two, three)) & pk_gt0(T, one);
+        S.acc[k] |= code << sh;
+        S.Tk[k] = T;
+        S.Qk[k] = pk_max(pk_subs(pk_max(M, X), gO), Y);
+        const uint32_t nb = pk_gt0(pk_subs(T, S.best), one) & act;  // first strict '>' in row-major order
+        S.best = pk(bsel(nb, upk(T), upk(S.best)));
+        S.bpos = bsel(nb, u4 | (uint32_t)k * 0x10001u, S.bpos);
+        Zl = pk_subs(pk_max(M, Y), gO);
+        Xl = X;
+    }
+    if ((u & 7) == 7) {  // 8 rows per half-word: out, lane-interleaved
+        uint32_t *base = tb + (uint64_t)(u >> 3) * 16 * nl;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            base[(uint64_t)k * nl] = S.acc[k];
+            S.acc[k] = 0;
+        }
+    }
+    uint32_t bnew[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const LanePair &q = h ? q1 : q0;
+        const int32_t awl = h ? awl1 : awl0, bwl = h ? bwl1 : bwl0, LB = h ? LB1 : LB0;
+        ++S.ap[h];
+        S.awd[h] = (S.ap[h] & 15) == 0 ? S.pa[h] : S.awd[h];
+        S.pa[h] = gld((((S.ap[h] + 1) & 15) == 0) ? q.Aw + min((S.ap[h] + 1) >> 4, awl) : dummy, 0);
+        bnew[h] = S.bp[h] < LB ? (S.bw[h] >> (30 - 2 * (S.bp[h] & 15))) & 3u : 0u;
+        ++S.bp[h];
+        S.bw[h] = (S.bp[h] & 15) == 0 ? S.pb[h] : S.bw[h];
+        S.pb[h] = gld((((S.bp[h] + 1) & 15) == 0) ? q.Bw + min((S.bp[h] + 1) >> 4, bwl) : dummy, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < 15; ++k) S.sel[k] = S.sel[k + 1];
+    S.sel[15] = x2_sel(bnew[0], bnew[1]);
+}
+
+__global__ __launch_bounds__(256) void dovetail_p2tbx2_kernel(DevReads rd, const int32_t *lead, const int32_t *trail,
+                                                              uint64_t npairs, uint64_t t0, uint64_t nt, AlignParams P,
+                                                              const int32_t *p1, const uint32_t *order,
+                                                              DevAlignment *out, int32_t *err, uint32_t *tbbuf) {
+    constexpr int LW = 16;
+    const uint64_t nl = (nt + 1) / 2;  // lanes of this launch
+    const uint64_t tl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool have[2];
+    uint64_t pair[2];
+    LanePair q[2];
+    int32_t r1[2], ds[2], rows2[2], LBh[2];
+    bool p2[2];
+    int32_t lo = 0, hi = 0x7fffffff, rmax = 0;
+    constexpr int32_t zr = (LW - 1) / 2;  // every band 16 cells (EXACT)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const uint64_t t = t0 + 2 * tl + h;
+        have[h] = tl < nl && 2 * tl + h < nt && t < npairs;
+        pair[h] = have[h] ? order[t] : 0;
+        q[h] = LanePair{0, 0, 0, 0, 0, -100, rd.codes, rd.codes};
+        r1[h] = -100;
+        if (have[h]) {
+            q[h] = lane_pair<LW, true>(rd, lead, trail, pair[h], P);
+            r1[h] = p1[pair[h]];
+        }
+        p2[h] = r1[h] >= 0 && !(r1[h] & 1);
+        ds[h] = r1[h] >= 0 ? r1[h] >> 1 : 0;
+        LBh[h] = q[h].LB;
+        rows2[h] = p2[h] ? q[h].LA - ds[h] : 0;
+        if (p2[h]) {
+            lo = max(lo, zr + 1);
+            hi = min(hi, LBh[h] + zr - (LW - 1));
+        }
+        rmax = max(rmax, rows2[h]);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        rmax = max(rmax, __shfl_xor(rmax, off, 64));
+        lo = max(lo, __shfl_xor(lo, off, 64));
+        hi = min(hi, __shfl_xor(hi, off, 64));
+    }
+    rmax = __builtin_amdgcn_readfirstlane(rmax);
+    lo = __builtin_amdgcn_readfirstlane(lo);
+    hi = __builtin_amdgcn_readfirstlane(hi);
+    uint32_t cpa[4];  // biased row packs: byte y = cost(x, y) + 128
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+        cpa[x] = 0;
+#pragma unroll
+        for (int y = 0; y < 4; ++y) cpa[x] |= (uint32_t)((P.cost[x * 4 + y] + 128) & 255) << (8 * y);
+    }
+    const u16x2 gO = pk((uint32_t)in_vgpr((int32_t)((uint32_t)(-P.gap_open) * 0x10001u)));
+    const u16x2 gE = pk((uint32_t)in_vgpr((int32_t)((uint32_t)(-P.gap_extend) * 0x10001u)));
+    const u16x2 bias = pk((uint32_t)in_vgpr((int32_t)0x00800080));
+    const u16x2 one = pk((uint32_t)in_vgpr((int32_t)0x00010001));
+    const uint32_t two = (uint32_t)in_vgpr((int32_t)0x00020002), three = (uint32_t)in_vgpr((int32_t)0x00030003);
+    BandX2 S;
+    uint32_t bw0[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) bw0[h] = p2[h] ? gld(q[h].Bw, 0) : 0u;  // k - zr < 16: B[0 .. 16)
+#pragma unroll
+    for (int k = 0; k < LW; ++k) {
+        const int32_t p = k - zr;
+        uint32_t b[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) b[h] = (p >= 0 && p < LBh[h]) ? (bw0[h] >> (30 - 2 * (p & 15))) & 3u : 0u;
+        S.sel[k] = x2_sel(b[0], b[1]);
+        S.Tk[k] = 0;
+        S.Qk[k] = 0;
+        S.acc[k] = 0;
+    }
+    S.best = 0;
+    S.bpos = 0;
+    int32_t awl[2], bwl[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        awl[h] = max((q[h].LA + 15) / 16 - 1, 0);
+        bwl[h] = max((LBh[h] + 15) / 16 - 1, 0);
+        S.bp[h] = LW - zr;
+        S.bw[h] = q[h].Bw[min(S.bp[h] >> 4, bwl[h])];
+        S.pb[h] = q[h].Bw[min((S.bp[h] >> 4) + 1, bwl[h])];
+        S.ap[h] = ds[h];
+        S.awd[h] = q[h].Aw[min(S.ap[h] >> 4, awl[h])];
+        S.pa[h] = q[h].Aw[min((S.ap[h] >> 4) + 1, awl[h])];
+    }
+    uint32_t *tb = tbbuf + tl;
+    __builtin_amdgcn_s_waitcnt(0);
+    int32_t u = 1;
+    const int32_t e1 = min(lo - 1, rmax), e2 = min(hi, rmax);
+#define X2_ROW(MASKED)                                                                                          \
+    band_row_x2<MASKED>(S, u, (u <= rows2[0] ? 0x0000FFFFu : 0u) | (u <= rows2[1] ? 0xFFFF0000u : 0u), zr, LBh[0], \
+                        LBh[1], cpa, gO, gE, bias, one, two, three, q[0], q[1], awl[0], awl[1], bwl[0], bwl[1],   \
+                        rd.codes, tb, nl)
+    for (; u <= e1; ++u) X2_ROW(true);
+    for (; u <= e2; ++u) X2_ROW(false);
+    for (; u <= rmax; ++u) X2_ROW(true);
+#undef X2_ROW
+    if ((rmax & 7) != 7) {  // the last, partial row block
+        uint32_t *base = tb + (uint64_t)(rmax >> 3) * 16 * nl;
+#pragma unroll
+        for (int k = 0; k < LW; ++k) base[(uint64_t)k * nl] = S.acc[k];
+    }
+    // ---- greedy walks from the argmaxes (BioLibs.scala:768-809) ------------
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (!have[h]) continue;
+        const int32_t best = (int32_t)((upk(S.best) >> (16 * h)) & 0xFFFFu);
+        const int32_t bp4 = (int32_t)((S.bpos >> (16 * h)) & 0xFFFFu);
+        const int32_t bpos = ((bp4 >> 4) << 6) | (bp4 & 15);
+        int32_t bstop = 0, bce = 0;
+        if (p2[h] && best > 0) {
+            int32_t uu = bpos >> 6, k = bpos & 63;
+            int32_t c = 0, e = 0;
+            uint32_t hw = (tb[((uint64_t)(uu >> 3) * LW + k) * nl] >> (16 * h)) & 0xFFFFu;
+            uint32_t code = (hw >> (2 * (uu & 7))) & 3u;
+            while (code != 0) {
+                if (code == 1) {
+                    // run of M codes in column k from row uu down, inside this half-word
+                    const int r = uu & 7;
+                    uint32_t x = hw ^ 0x5555u;
+                    x &= (r == 7) ? 0xFFFFu : ((1u << (2 * r + 2)) - 1u);
+                    const int32_t n = x == 0 ? r + 1 : r - ((31 - __clz(x)) >> 1);
+                    const int32_t i = uu + ds[h], j = k - zr + uu;
+                    const uint32_t shn = 32 - 2 * n;
+                    const uint32_t xa = win16_g(q[h].Aw, i - n), xb = win16_g(q[h].Bw, j - n);
+                    uint32_t d = (shn == 0) ? (xa ^ xb) : ((xa ^ xb) >> shn);
+                    d = (d | (d >> 1)) & 0x55555555u;
+                    const int32_t mism = __popc(d);
+                    c += n - mism;
+                    e += mism;
+                    uu -= n;
+                } else if (code == 2) {
+                    ++e; --k;
+                } else {
+                    ++e; --uu; ++k;
+                }
+                hw = (tb[((uint64_t)(uu >> 3) * LW + k) * nl] >> (16 * h)) & 0xFFFFu;
+                code = (hw >> (2 * (uu & 7))) & 3u;
+            }
+            bstop = (uu << 6) | k;
+            bce = (c << 16) | e;
+        }
+        finish_alignment(P, q[h], r1[h], ds[h], zr, best, bpos, bstop, bce, out + pair[h], err);
+    }
+}
+
 // LW = 16 (with the EXACT variant: every band exactly 16 cells), 24 or 32
 #define SA_LANE_DISPATCH_C(KERNEL, C, GRID, ...)                                                            \
     do {                                                                                                    \
@@ -797,6 +1032,22 @@ hipError_t launch_dovetail_p1x2(const DevReads &r, const int32_t *lead, const in
     const uint64_t lanes = (n + 1) / 2;
     hipLaunchKernelGGL(dovetail_p1x2_kernel, dim3((uint32_t)((lanes + 255) / 256)), dim3(256), 0, s, r, lead, trail,
                        n, p, p1, rows2_key, order, err, cells);
+    return hipGetLastError();
+}
+
+size_t dovetail_tbx2_words(uint64_t nt, int32_t max_len) {
+    const uint64_t rb8 = (uint64_t)(max_len + 1 + 7) / 8 + 1;
+    return rb8 * 16 * ((nt + 1) / 2);
+}
+
+hipError_t launch_dovetail_p2tbx2(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
+                                  uint64_t t0, uint64_t nt, const AlignParams &p, const int32_t *p1,
+                                  const uint32_t *order, DevAlignment *out, int32_t *err, uint32_t *tb,
+                                  hipStream_t s) {
+    if (!n || !nt) return hipSuccess;
+    const uint64_t lanes = (nt + 1) / 2;
+    hipLaunchKernelGGL(dovetail_p2tbx2_kernel, dim3((uint32_t)((lanes + 255) / 256)), dim3(256), 0, s, r, lead, trail,
+                       n, t0, nt, p, p1, order, out, err, tb);
     return hipGetLastError();
 }
 

@@ -328,6 +328,13 @@ hipError_t launch_dovetail_p2(const DevReads &r, const int32_t *lead, const int3
 // phase 2 with traceback codes in HBM: lanes t0 .. t0+nt of the order, nt
 // rounded up to 64; tb = dovetail_tb_words(nt, longest lead, lw) u32 words
 size_t dovetail_tb_words(uint64_t nt, int32_t max_len, int lw);
+// two pairs per lane (packed 16-bit; lw 16 EXACT, int8 costs, gaps <= 0, scores and
+// argmax rows within 16 bits): 8 rows of codes per pair per word
+size_t dovetail_tbx2_words(uint64_t nt, int32_t max_len);
+hipError_t launch_dovetail_p2tbx2(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
+                                  uint64_t t0, uint64_t nt, const AlignParams &p, const int32_t *p1,
+                                  const uint32_t *order, DevAlignment *out, int32_t *err, uint32_t *tb,
+                                  hipStream_t s);
 hipError_t launch_dovetail_p2tb(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
                                 uint64_t t0, uint64_t nt, const AlignParams &p, int lw, bool exact, const int32_t *p1,
                                 const uint32_t *order, DevAlignment *out, int32_t *err, uint32_t *tb,

@@ -105,3 +105,19 @@ def test_costs_beyond_int16_fail_exactly():
     with pytest.raises(sao.SAError) as e:
         ov.align()
     assert e.value.name == "SA_E_OVERFLOW"
+
+
+@pytest.mark.parametrize("cost", ["hoxd70", "near_16bit"])
+def test_two_pairs_per_lane_kernels(oracle_mod, cost):
+    """Reads of 467..500 bp (every band exactly 16 cells) with int8 costs: both
+    phases run two pairs per lane in packed 16-bit halves, pairs
+    of different trail lengths side by side.  'near_16bit' puts the largest
+    score (127 x 500 + bias) within 2,000 of the 16-bit limit."""
+    c = list(HOXD70)
+    if cost == "near_16bit":
+        c[0] = c[15] = 127
+        c[5] = c[10] = 113
+    rng = np.random.default_rng(21)
+    reads = H.mutate(H.synth_reads(200, 490, 4000, gc=0.45, seed=21, mixed=(470, 497)), rng, 3)
+    assert 467 <= min(map(len, reads)) and max(map(len, reads)) <= 500
+    check(oracle_mod, reads, c, False, kmer_size=12)
