@@ -436,6 +436,20 @@ __device__ __forceinline__ uint32_t pk_gt0(u16x2 x, u16x2 one) {
     return upk((u16x2)0 - __builtin_elementwise_min(x, one));
 }
 __device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
+// Issue costs measured on gfx950 (tools/valu_rate.hip, profiles/r02/valu_rate_v9.txt): v_add_u32,
+// v_sub_u32, v_and/or/xor_b32 and v_bitop3_b32 issue in ~2.5 cycles per wave per SIMD, every
+// v_pk_* op, v_max/min, v_perm_b32, v_bfi_b32 and v_lshl_or_b32 in ~4.4.  So: plain u32
+// add/sub wherever no half can carry or borrow, and selects as v_bitop3_b32 (S0 ? S1 : S2 is
+// truth table 0xCA; the compiler would pick v_bfi_b32).
+__device__ __forceinline__ uint32_t bsel3(uint32_t m, uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
+}
+// a - b per half where a >= b in both halves (no borrow crosses)
+__device__ __forceinline__ u16x2 pk_dif(u16x2 a, u16x2 b) { return pk(upk(a) - upk(b)); }
+// a + b per half where neither half reaches 2^16 (no carry crosses)
+__device__ __forceinline__ u16x2 pk_sum(u16x2 a, u16x2 b) { return pk(upk(a) + upk(b)); }
 
 __global__ __launch_bounds__(256) void dovetail_p1x2_kernel(DevReads rd, const int32_t *lead, const int32_t *trail,
                                                             uint64_t npairs, AlignParams P, int32_t *p1,
@@ -491,8 +505,7 @@ __global__ __launch_bounds__(256) void dovetail_p1x2_kernel(DevReads rd, const i
     uint32_t awA = qa.Aw[0], awnA = qa.Aw[min(1, awlA)];
     uint32_t awB = qb.Aw[0], awnB = qb.Aw[min(1, awlB)];
     __builtin_amdgcn_s_waitcnt(0);
-#pragma unroll 2
-    for (int32_t i = 1; i <= rmax; ++i) {
+    auto row = [&](const int32_t i) {
         const uint32_t act = (i <= rowsA ? 0x0000FFFFu : 0u) | (i <= rowsB ? 0xFFFF0000u : 0u);
         const uint32_t sh = 30 - 2 * ((i - 1) & 15);
         const uint32_t aA = (awA >> sh) & 3u, aB = (awB >> sh) & 3u;
@@ -504,21 +517,21 @@ __global__ __launch_bounds__(256) void dovetail_p1x2_kernel(DevReads rd, const i
 #pragma unroll
         for (int j = 0; j < LW - 1; ++j) {
             const u16x2 cpk = pk(__builtin_amdgcn_perm(cbB[j], cbA[j], sel));
-            const u16x2 M = pk_subs(Tdiag + cpk, bias);
+            const u16x2 M = pk_subs(pk_sum(Tdiag, cpk), bias);
             const u16x2 Y = pk_subs(Q[j], gE);
             const u16x2 X = pk_subs(pk_max(Zl, Xl), gE);
             const u16x2 T = pk_max(pk_max(M, X), Y);
             const uint32_t Oup = O[j];
-            const uint32_t mM = pk_is0(pk_subs(T, M), one), mX = pk_is0(pk_subs(T, X), one);
-            const uint32_t on = bsel(pk_gt0(T, one), bsel(mM, Odiag, bsel(mX, Ol, Oup)), self);
+            const uint32_t mM = pk_is0(pk_dif(T, M), one), mX = pk_is0(pk_dif(T, X), one);
+            const uint32_t on = bsel3(pk_gt0(T, one), bsel3(mM, Odiag, bsel3(mX, Ol, Oup)), self);
             Tdiag = Tc[j];
             Odiag = Oup;
             Tc[j] = T;
             Q[j] = pk_max(pk_subs(pk_max(M, X), gO), Y);
             O[j] = on;
             const uint32_t nb = pk_gt0(pk_subs(T, best), one) & act;  // first strict '>' in row-major order
-            best = pk(bsel(nb, upk(T), upk(best)));
-            borg = bsel(nb, on, borg);
+            best = pk(bsel3(nb, upk(T), upk(best)));
+            borg = bsel3(nb, on, borg);
             Zl = pk_subs(pk_max(M, Y), gO);
             Xl = X;
             Ol = on;
@@ -527,7 +540,13 @@ __global__ __launch_bounds__(256) void dovetail_p1x2_kernel(DevReads rd, const i
         awB = (i & 15) == 0 ? awnB : awB;
         awnA = gld(qa.Aw, min((i >> 4) + 1, awlA));
         awnB = gld(qb.Aw, min((i >> 4) + 1, awlB));
+    };
+    int32_t i = 1;
+    for (; i < rmax; i += 2) {  // two rows per iteration (by hand: #pragma unroll gives up here)
+        row(i);
+        row(i + 1);
     }
+    if (i == rmax) row(i);
     unsigned long long cells = 0;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -772,11 +791,22 @@ __device__ __forceinline__ uint32_t x2_sel(uint32_t b0, uint32_t b1) {
     return b0 | 0x00000C00u | ((4u + b1) << 16) | 0x0C000000u;
 }
 
+// after row u: every 8 rows the half-words go out, lane-interleaved
+__device__ __forceinline__ void store_x2(BandX2 &S, const int32_t u, uint32_t *tb, uint64_t nl) {
+    if ((u & 7) == 7) {
+        uint32_t *base = tb + (uint64_t)(u >> 3) * 16 * nl;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            base[(uint64_t)k * nl] = S.acc[k];
+            S.acc[k] = 0;
+        }
+    }
+}
+
 template <bool MASKED>
 __device__ __forceinline__ void band_row_x2(BandX2 &S, const int32_t u, const uint32_t act, const int32_t zr,
                                             const int32_t LB0, const int32_t LB1, const uint32_t *cpa, const u16x2 gO,
-                                            const u16x2 gE, const u16x2 bias, const u16x2 one, const uint32_t two,
-                                            const uint32_t three, const LanePair &q0, const LanePair &q1,
+                                            const u16x2 gE, const u16x2 bias, const u16x2 one, const LanePair &q0, const LanePair &q1,
                                             const int32_t awl0, const int32_t awl1, const int32_t bwl0,
                                             const int32_t bwl1, const uint32_t *dummy, uint32_t *tb, uint64_t nl) {
     uint32_t cp[2];
@@ -793,7 +823,7 @@ __device__ __forceinline__ void band_row_x2(BandX2 &S, const int32_t u, const ui
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         const u16x2 cpk = pk(__builtin_amdgcn_perm(cp[1], cp[0], S.sel[k]));
-        u16x2 M = pk_subs(S.Tk[k] + cpk, bias);
+        u16x2 M = pk_subs(pk_sum(S.Tk[k], cpk), bias);
         u16x2 Y = k == 15 ? (u16x2)0 : pk_subs(S.Qk[k + 1], gE);
         u16x2 X = k == 0 ? (u16x2)0 : pk_subs(pk_max(Zl, Xl), gE);
         if (MASKED) {
@@ -803,25 +833,20 @@ __device__ __forceinline__ void band_row_x2(BandX2 &S, const int32_t u, const ui
             X = pk(upk(X) & v);
             Y = pk(upk(Y) & v);
         }
-        const u16x2 T = pk_max(pk_max(M, X), Y);
-        const uint32_t mM = pk_is0(pk_subs(T, M), one), mX = pk_is0(pk_subs(T, X), one);
-        const uint32_t code = bsel(mM, upk(one), bsel(mX, two, three)) & pk_gt0(T, one);
+        const u16x2 MX = pk_max(M, X);
+        const u16x2 T = pk_max(MX, Y);
+        // [T > 0] + [M < T] + [max(M, X) < T]: 0 (T = 0: then M = X = Y = 0), 1 M, 2 X, 3 Y
+        const uint32_t code = upk(__builtin_elementwise_min(T, one)) +
+                              upk(__builtin_elementwise_min(pk_dif(T, M), one)) +
+                              upk(__builtin_elementwise_min(pk_dif(T, MX), one));
         S.acc[k] |= code << sh;
         S.Tk[k] = T;
-        S.Qk[k] = pk_max(pk_subs(pk_max(M, X), gO), Y);
+        S.Qk[k] = pk_max(pk_subs(MX, gO), Y);
         const uint32_t nb = pk_gt0(pk_subs(T, S.best), one) & act;  // first strict '>' in row-major order
-        S.best = pk(bsel(nb, upk(T), upk(S.best)));
-        S.bpos = bsel(nb, u4 | (uint32_t)k * 0x10001u, S.bpos);
+        S.best = pk(bsel3(nb, upk(T), upk(S.best)));
+        S.bpos = bsel3(nb, u4 | (uint32_t)k * 0x10001u, S.bpos);
         Zl = pk_subs(pk_max(M, Y), gO);
         Xl = X;
-    }
-    if ((u & 7) == 7) {  // 8 rows per half-word: out, lane-interleaved
-        uint32_t *base = tb + (uint64_t)(u >> 3) * 16 * nl;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            base[(uint64_t)k * nl] = S.acc[k];
-            S.acc[k] = 0;
-        }
     }
     uint32_t bnew[2];
 #pragma unroll
@@ -896,7 +921,6 @@ __global__ __launch_bounds__(256) void dovetail_p2tbx2_kernel(DevReads rd, const
     const u16x2 gE = pk((uint32_t)in_vgpr((int32_t)((uint32_t)(-P.gap_extend) * 0x10001u)));
     const u16x2 bias = pk((uint32_t)in_vgpr((int32_t)0x00800080));
     const u16x2 one = pk((uint32_t)in_vgpr((int32_t)0x00010001));
-    const uint32_t two = (uint32_t)in_vgpr((int32_t)0x00020002), three = (uint32_t)in_vgpr((int32_t)0x00030003);
     BandX2 S;
     uint32_t bw0[2];
 #pragma unroll
@@ -932,11 +956,19 @@ __global__ __launch_bounds__(256) void dovetail_p2tbx2_kernel(DevReads rd, const
     const int32_t e1 = min(lo - 1, rmax), e2 = min(hi, rmax);
 #define X2_ROW(MASKED)                                                                                          \
     band_row_x2<MASKED>(S, u, (u <= rows2[0] ? 0x0000FFFFu : 0u) | (u <= rows2[1] ? 0xFFFF0000u : 0u), zr, LBh[0], \
-                        LBh[1], cpa, gO, gE, bias, one, two, three, q[0], q[1], awl[0], awl[1], bwl[0], bwl[1],   \
+                        LBh[1], cpa, gO, gE, bias, one, q[0], q[1], awl[0], awl[1], bwl[0], bwl[1],   \
                         rd.codes, tb, nl)
-    for (; u <= e1; ++u) X2_ROW(true);
-    for (; u <= e2; ++u) X2_ROW(false);
-    for (; u <= rmax; ++u) X2_ROW(true);
+    for (; u <= e1; ++u) { X2_ROW(true); store_x2(S, u, tb, nl); }
+    if ((u & 1) && u <= e2) { X2_ROW(false); store_x2(S, u, tb, nl); ++u; }
+    for (; u < e2; u += 2) {  // two rows (even, odd) per iteration: one basic block
+        X2_ROW(false);
+        ++u;
+        X2_ROW(false);
+        store_x2(S, u, tb, nl);
+        --u;
+    }
+    for (; u <= e2; ++u) { X2_ROW(false); store_x2(S, u, tb, nl); }
+    for (; u <= rmax; ++u) { X2_ROW(true); store_x2(S, u, tb, nl); }
 #undef X2_ROW
     if ((rmax & 7) != 7) {  // the last, partial row block
         uint32_t *base = tb + (uint64_t)(rmax >> 3) * 16 * nl;
