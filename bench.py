@@ -110,6 +110,19 @@ def pmc_summary():
     return rows, os.path.relpath(files[-1], ROOT)
 
 
+def isa_mix():
+    """The aligner hot loops' VALU mix priced with measured issue costs
+    (newest profiles/<round>/isa_mix*.json, written by tools/isa_mix.py)."""
+    import glob
+
+    def natural(path):
+        return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", path)]
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "isa_mix*.json")), key=natural)
+    if not files:
+        return None, None
+    return json.load(open(files[-1])), os.path.relpath(files[-1], ROOT)
+
+
 def pmc_sum(rows, kernels, col):
     """Sum over the named kernels (name prefixes) of one counter's per-dispatch
     average; None if a kernel or the counter is missing."""
@@ -371,12 +384,27 @@ def main():
     al_ms = astages["align"][0] / max(astages["align"][1], 1)
     cells_g = ast["dp_cells"] / P_here
     # at the bench shape both phases run two pairs per lane (packed 16-bit halves,
-    # DESIGN.md 4.6): one issue slot there does two cells' operation
-    valu = pmc_sum(rows, ("sa::dovetail_p1x2_kernel", "sa::dovetail_p2tbx2_kernel"), "SQ_INSTS_VALU_avg")
+    # DESIGN.md 4.6): one issue slot there does two cells' operation.  The peak is
+    # the measured per-instruction issue cost (tools/valu_rate.hip: ~2.55 cycles per
+    # wave per SIMD for add/sub/bitwise/bitop3, ~4.35 for v_pk_*, max/min, perm, bfi)
+    # over the hot loops' static mix (tools/isa_mix.py): lane-ops/s the SIMDs can
+    # issue for THIS instruction mix; the 2-cycle figure stays beside it as nominal.
+    mix, mix_src = isa_mix()
+    kern = (("sa::dovetail_p1x2_kernel", "dovetail_p1x2"), ("sa::dovetail_p2tbx2_kernel", "dovetail_p2tbx2"))
+    valu_k = [pmc_sum(rows, (kn,), "SQ_INSTS_VALU_avg") for kn, _ in kern]
+    valu = sum(valu_k) if None not in valu_k else None
     valu_ach = valu * 64 / (al_ms * 1e-3) / 1e12 if valu is not None and al_ms > 0 else None
-    roofline_align = {"bound": "valu", "unit": "T lane-ops/s", "peak": round(VALU_PEAK, 1),
+    mix_peak = None
+    if valu is not None and mix and all(m in mix for _, m in kern):
+        cyc = sum(v * mix[m]["avg_cycles_per_valu"] for v, (_, m) in zip(valu_k, kern)) / valu
+        mix_peak = 1024 * 64 * 2.4e9 / cyc / 1e12
+    roofline_align = {"bound": "valu", "unit": "T lane-ops/s",
+                      "peak": round(mix_peak, 1) if mix_peak else None,
                       "achieved": round(valu_ach, 2) if valu_ach is not None else None,
-                      "frac": round(valu_ach / VALU_PEAK, 4) if valu_ach is not None else None,
+                      "frac": round(valu_ach / mix_peak, 4) if valu_ach is not None and mix_peak else None,
+                      "peak_nominal_2_cycles": round(VALU_PEAK, 1),
+                      "frac_nominal": round(valu_ach / VALU_PEAK, 4) if valu_ach is not None else None,
+                      "mix_source": mix_src,
                       "kernel": "dovetail_p1x2 + dovetail_p2tbx2 (+ phase-2 pair regrouping sort)",
                       "gcups": round(cells_g / (al_ms * 1e-3) / 1e9, 1) if al_ms else None,
                       "launch_ms": round(al_ms, 4), "dp_cells_per_launch": int(cells_g),
