@@ -103,6 +103,28 @@ struct StageScope {
     }
 };
 
+// the side stream (ctx.h) and its events, created on first use on the
+// context's (current) device
+hipError_t ensure_side(sa_ctx *c) {
+    if (c->side) return hipSuccess;
+    hipError_t e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+    for (hipEvent_t *ev : {&c->ev_fork, &c->ev_join, &c->ev_fork2, &c->ev_join2})
+        if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+    return e;
+}
+
+// fork: the side stream waits for everything queued on the main stream so far
+hipError_t fork_side(sa_ctx *c, hipEvent_t ev) {
+    hipError_t e = hipEventRecord(ev, c->stream);
+    return e == hipSuccess ? hipStreamWaitEvent(c->side, ev, 0) : e;
+}
+
+// join: the main stream waits for everything queued on the side stream so far
+hipError_t join_side(sa_ctx *c, hipEvent_t ev) {
+    hipError_t e = hipEventRecord(ev, c->side);
+    return e == hipSuccess ? hipStreamWaitEvent(c->stream, ev, 0) : e;
+}
+
 void resolve_timing(sa_ctx *c) {
     for (auto &p : c->pending) {
         float ms = 0.f;
@@ -311,7 +333,10 @@ int ensure_prepared(sa_ctx *c) {
 int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, uint32_t *vals2, uint64_t n,
                  const uint64_t *occ_off, uint32_t n_reads, uint32_t npr, const uint2 *rl,
                  const int32_t *len, bool strict, void *stmp, Counters *cnt, PartArgs &PA,
-                 unsigned long long &big_buckets, int skip_bits = 0) {
+                 unsigned long long &big_buckets, int skip_bits = 0, int phase = 0) {
+    // phase 0: everything; 1: sort + LDS tiers, no readback (the caller's
+    // first pair-count pass aborts on big_n); 2: only the global path of the
+    // partitions phase 1 listed (keys / PA as phase 1 left them)
     // keys: 8-byte records (mix32 << 32 | occurrence index); vals / vals2: u32
     // scratch for the big-partition path.  skip_bits: top bits of the mix every
     // record here shares (the owner rank's bits in distributed mode);
@@ -326,64 +351,75 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
     const uint32_t nparts = 1u << PB;
     const int kbits = 32 + c->lb;  // LDS sort key: mix << lb | loc rank
     uint2 *srl = nullptr;
-    {
-        StageScope st(c, SA_STAGE_SORT);
-        if (rl) {
-            // an occurrence table rides along as the sort's 8-byte value, so the
-            // bucket build reads each record's {read, loc rank} coalesced instead
-            // of gathering it (16-byte records through the two passes)
-            uint64_t *v0, *v1;
-            ENSURE(c->d_srl, n + 1, &v0);
-            ENSURE(c->d_srl2, n + 1, &v1);
-            if (n) HIPCHK(hipMemcpyAsync(v0, rl, n * 8, hipMemcpyDeviceToDevice, c->stream));
-            HIPCHK(radix_sort_kv64(&keys, &v0, &keys2, &v1, n, 64 - skip_bits - PB, 64 - skip_bits, stmp,
-                                   c->stream));
-            srl = (uint2 *)v0;
-        } else {
-            uint32_t *nv = nullptr, *nv2 = nullptr;  // key-only: the payload rides in the record
-            HIPCHK(radix_sort(&keys, &nv, &keys2, &nv2, n, 64 - skip_bits - PB, 64 - skip_bits, stmp, c->stream));
-        }
-    }
     uint32_t *pstart, *biglist;
     ENSURE(c->d_pstart, nparts + 1, &pstart);
     ENSURE(c->d_biglist, 3 * ((size_t)nparts + 1), &biglist);  // big list, mid list, mid2 list
-    PA = PartArgs{};
-    PA.sk = keys; PA.sv = nullptr; PA.start = pstart; PA.np = nparts; PA.lb = c->lb; PA.sort_bits = kbits - skip_bits - PB;
-    PA.tagtab = (const uint8_t *)c->d_tagtab.p;
-    PA.occ_off = occ_off;
-    PA.n_reads = n_reads; PA.npr = npr; PA.rl = rl; PA.srl = srl;
-    PA.len = len;
-    PA.lbase = (const uint32_t *)c->d_lbase.p;
-    PA.lrank = (const uint32_t *)c->d_lrank.p;
-    PA.k = c->set.kmer_size;
-    PA.pos_bits = rl ? 0 : c->pos_bits;  // (occurrence indices + the {read, loc rank} table)
-    PA.meta = (const uint2 *)c->d_meta.p;
-    ENSURE(c->d_md, 3 * n + 3, &PA.lst);
-    ENSURE(c->d_rec, n + 1, &PA.rec);
-    PA.xrec = nullptr;
-    PA.xrec_n = &cnt->xrec_n;
-    PA.big_list = biglist; PA.big_n = &cnt->big_n;
-    PA.mid_list = biglist + nparts + 1; PA.mid_n = &cnt->mid_n;
-    PA.mid2_list = biglist + 2 * ((size_t)nparts + 1); PA.mid2_n = &cnt->mid2_n;
-    PA.counts = cnt->bkt_counts;
-    if (strict) {
-        ENSURE(c->d_mdidx, 3 * n + 3, &PA.lidx);
-        ENSURE(c->d_srec, n + 1, &PA.srec);
-        ENSURE(c->d_bnst, n + 1, &PA.bkt_nst);
-        ENSURE(c->d_bnmd, n + 1, &PA.bkt_nmd);
-        ENSURE(c->d_bfirst, n + 1, &PA.bkt_first);
-        ENSURE(c->d_ishead, n + 1, &PA.is_head);
-        ENSURE(c->d_brank, n + 1, &c->bkt_rank_dev);
-        HIPCHK(hipMemsetAsync(PA.is_head, 0, n + 1, c->stream));
+    const uint8_t *tagtab = (const uint8_t *)c->d_tagtab.p;
+    if (phase != 2) {
+        {
+            StageScope st(c, SA_STAGE_SORT);
+            if (rl) {
+                // an occurrence table rides along as the sort's 8-byte value, so the
+                // bucket build reads each record's {read, loc rank} coalesced instead
+                // of gathering it (16-byte records through the two passes)
+                uint64_t *v0, *v1;
+                ENSURE(c->d_srl, n + 1, &v0);
+                ENSURE(c->d_srl2, n + 1, &v1);
+                if (n) HIPCHK(hipMemcpyAsync(v0, rl, n * 8, hipMemcpyDeviceToDevice, c->stream));
+                HIPCHK(radix_sort_kv64(&keys, &v0, &keys2, &v1, n, 64 - skip_bits - PB, 64 - skip_bits, stmp,
+                                       c->stream));
+                srl = (uint2 *)v0;
+            } else {
+                uint32_t *nv = nullptr, *nv2 = nullptr;  // key-only: the payload rides in the record
+                HIPCHK(radix_sort(&keys, &nv, &keys2, &nv2, n, 64 - skip_bits - PB, 64 - skip_bits, stmp, c->stream));
+            }
+        }
+        PA = PartArgs{};
+        PA.sk = keys; PA.sv = nullptr; PA.start = pstart; PA.np = nparts; PA.lb = c->lb; PA.sort_bits = kbits - skip_bits - PB;
+        PA.tagtab = (const uint8_t *)c->d_tagtab.p;
+        PA.occ_off = occ_off;
+        PA.n_reads = n_reads; PA.npr = npr; PA.rl = rl; PA.srl = srl;
+        PA.len = len;
+        PA.lbase = (const uint32_t *)c->d_lbase.p;
+        PA.lrank = (const uint32_t *)c->d_lrank.p;
+        PA.k = c->set.kmer_size;
+        PA.pos_bits = rl ? 0 : c->pos_bits;  // (occurrence indices + the {read, loc rank} table)
+        PA.meta = (const uint2 *)c->d_meta.p;
+        ENSURE(c->d_md, 3 * n + 3, &PA.lst);
+        ENSURE(c->d_rec, n + 1, &PA.rec);
+        PA.xrec = nullptr;
+        PA.xrec_n = &cnt->xrec_n;
+        PA.big_list = biglist; PA.big_n = &cnt->big_n;
+        PA.mid_list = biglist + nparts + 1; PA.mid_n = &cnt->mid_n;
+        PA.mid2_list = biglist + 2 * ((size_t)nparts + 1); PA.mid2_n = &cnt->mid2_n;
+        PA.counts = cnt->bkt_counts;
+        if (strict) {
+            ENSURE(c->d_mdidx, 3 * n + 3, &PA.lidx);
+            ENSURE(c->d_srec, n + 1, &PA.srec);
+            ENSURE(c->d_bnst, n + 1, &PA.bkt_nst);
+            ENSURE(c->d_bnmd, n + 1, &PA.bkt_nmd);
+            ENSURE(c->d_bfirst, n + 1, &PA.bkt_first);
+            ENSURE(c->d_ishead, n + 1, &PA.is_head);
+            ENSURE(c->d_brank, n + 1, &c->bkt_rank_dev);
+            HIPCHK(hipMemsetAsync(PA.is_head, 0, n + 1, c->stream));
+        }
+        HIPCHK(hipMemsetAsync(&cnt->mid_n, 0, 2 * sizeof(uint32_t), c->stream));  // mid_n, mid2_n
+        {
+            // the bounds kernel lists the partitions above 1,024 records; their
+            // 2,048 / 4,096-record tiers (~1 % of partitions, a few blocks' latency)
+            // run on the side stream beside the 1,024-record pass
+            StageScope st(c, SA_STAGE_BUCKETS);
+            HIPCHK(launch_part_starts(PA, n, 64 - skip_bits - PB, c->stream));
+            HIPCHK(ensure_side(c));
+            HIPCHK(fork_side(c, c->ev_fork2));
+            HIPCHK(launch_part_build(PA, strict, 2048, c->side));
+            HIPCHK(launch_part_build(PA, strict, 4096, c->side));
+            HIPCHK(launch_part_build(PA, strict, 1024, c->stream));
+            HIPCHK(join_side(c, c->ev_join2));
+        }
+        if (phase == 1) return SA_OK;
     }
-    const uint8_t *tagtab = PA.tagtab;
     uint32_t big_n = 0;
-    HIPCHK(hipMemsetAsync(&cnt->mid_n, 0, 2 * sizeof(uint32_t), c->stream));  // mid_n, mid2_n
-    {
-        StageScope st(c, SA_STAGE_BUCKETS);
-        HIPCHK(launch_part_starts(keys, n, 64 - skip_bits - PB, pstart, nparts, c->stream));
-        HIPCHK(launch_part_build(PA, strict, c->stream));
-    }
     HIPCHK(hipMemcpyAsync(&big_n, &cnt->big_n, 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     big_buckets = 0;
@@ -466,7 +502,10 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
 // entries in the NSHARD output regions of cap_s_out entries each.
 int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bool emit_all,
                const uint32_t *read_order, uint32_t n_items, Counters *cnt, uint64_t &np, uint64_t &cap_s_out,
-               const uint32_t *item_start = nullptr, uint32_t n_multi = 0) {
+               const uint32_t *item_start = nullptr, uint32_t n_multi = 0, const uint32_t *abort_flag = nullptr,
+               bool *aborted = nullptr) {
+    // abort_flag (device): the first pass exits when it is set (big partitions
+    // still to build, bucket_stage phase 1); *aborted then tells the caller
     // ---- pair counting -------------------------------------------------
     PairParams P;
     P.min_coll = c->set.min_collisions;
@@ -479,6 +518,8 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
     P.n_items = n_items;
     P.xcd_swizzle = read_order ? 1 : 0;
     P.table = 256;
+    P.abort = abort_flag;
+    if (aborted) *aborted = false;
     if (c->pair_cap == 0) c->pair_cap = std::max<uint64_t>(1 << 16, (uint64_t)n_items * (P.emit_all ? 64 : 24));
     // output regions: NSHARD x cap_s entries (a block appends to region blockIdx % NSHARD)
     unsigned long long cur[NSHARD];
@@ -517,7 +558,14 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
         }
         HIPCHK(hipMemcpyAsync(cur, cnt->cursor, sizeof(cur), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipMemcpyAsync(&ovn, &cnt->overflow_n, 4, hipMemcpyDeviceToHost, c->stream));
+        uint32_t abv = 0;
+        if (P.abort) HIPCHK(hipMemcpyAsync(&abv, P.abort, 4, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
+        if (abv) {
+            *aborted = true;
+            return SA_OK;
+        }
+        P.abort = nullptr;
         // Reads whose 256-slot table overflowed (> 192 partners) are recounted
         // one per block in bigger tables: 2,048 slots unless their partner count
         // -- extrapolated from how fast the first pass filled -- is far beyond it,
@@ -549,6 +597,7 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
             ENSURE(c->d_ovl, items.size() + 3, &fl);  // at most one failure per item
             HIPCHK(hipMemcpy(tl, items.data(), items.size() * 4, hipMemcpyHostToDevice));
             PairParams PT = P;
+            PT.abort = nullptr;
             PT.table = table;
             PT.split = split;
             PT.coded = 1;
@@ -678,15 +727,25 @@ int device_build(sa_ctx *c, bool readback) {
     {
         StageScope st(c, SA_STAGE_EMIT);
         HIPCHK(launch_kmer_emit(R, E, keys, vals, c->stream));
-        // reads in locality order (overlapping reads adjacent) for pair_count
-        HIPCHK(radix_sort(&rk0, &ro0, &rk1, &ro1, nr, 0, 32, rtmp, c->stream));
     }
+    // reads in locality order (overlapping reads adjacent) for pair_count: by
+    // the top 16 bits of their minimum k-mer mix (reads sharing it stay
+    // adjacent; two radix passes of a 100k-key sort are launch-bound), on the
+    // side stream beside the partition sort and the bucket build
+    HIPCHK(ensure_side(c));
+    HIPCHK(fork_side(c, c->ev_fork));
+    HIPCHK(radix_sort(&rk0, &ro0, &rk1, &ro1, nr, 16, 32, rtmp, c->side));
+    HIPCHK(hipEventRecord(c->ev_join, c->side));
     const uint32_t *read_order = ro0;
     PartArgs PA{};
     unsigned long long big_buckets = 0;
+    // wide ids: no readback between the bucket build and the pair counter (its
+    // first pass aborts if a partition needs the global path, see below)
+    const int bphase = strict ? 0 : 1;
     rc = bucket_stage(c, keys, keys2, vals, vals2, n, (const uint64_t *)c->d_occ_off.p, nr, c->uniform_npr,
-                      orl, (const int32_t *)c->d_len.p, strict, stmp, cnt, PA, big_buckets);
+                      orl, (const int32_t *)c->d_len.p, strict, stmp, cnt, PA, big_buckets, 0, bphase);
     if (rc) return rc;
+    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
     if (strict) {
         // KmerData iteration rank of every bucket: replay its Trove layout over the
         // distinct hashes in first-occurrence order (KmerTable.scala:45-50).  A
@@ -735,8 +794,18 @@ int device_build(sa_ctx *c, bool readback) {
     }
 
     uint64_t np = 0, cap_s = 0;
-    rc = pair_stage(c, E, PI, strict, strict || c->keep_pairs, read_order, nr, cnt, np, cap_s);
+    bool aborted = false;
+    rc = pair_stage(c, E, PI, strict, strict || c->keep_pairs, read_order, nr, cnt, np, cap_s, nullptr, 0,
+                    bphase == 1 ? &cnt->big_n : nullptr, &aborted);
     if (rc) return rc;
+    if (aborted) {  // partitions above 4,096 records (high-copy repeats): build them, count again
+        rc = bucket_stage(c, keys, keys2, vals, vals2, n, (const uint64_t *)c->d_occ_off.p, nr, c->uniform_npr,
+                          orl, (const int32_t *)c->d_len.p, strict, stmp, cnt, PA, big_buckets, 0, 2);
+        if (rc) return rc;
+        PI.xrec = PA.xrec;
+        rc = pair_stage(c, E, PI, strict, strict || c->keep_pairs, read_order, nr, cnt, np, cap_s);
+        if (rc) return rc;
+    }
     const bool emit_all = strict || c->keep_pairs;
 
     // ---- ordering --------------------------------------------------------
@@ -1118,6 +1187,12 @@ void sa_ctx_destroy(sa_ctx *c) {
         if (b->p) (void)hipFree(b->p);
     for (auto &p : c->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+    if (c->side) {
+        (void)hipStreamSynchronize(c->side);
+        (void)hipStreamDestroy(c->side);
+    }
+    for (hipEvent_t e : {c->ev_fork, c->ev_join, c->ev_fork2, c->ev_join2})
+        if (e) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }

@@ -57,6 +57,11 @@ struct sa_ctx {
     sa_settings set{};
     int device = 0;
     hipStream_t stream = nullptr;
+    // second stream for work that overlaps the main chain (the read-order sort
+    // beside the partition sort, the 2,048 / 4,096-record bucket tiers beside
+    // the 1,024-record pass) and its fork / join events; created on first use
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_fork2 = nullptr, ev_join2 = nullptr;
     std::string err;
     // reads (host)
     std::vector<char> bases;

@@ -139,6 +139,7 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
         bid = (blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);
     }
     if (bid >= p.n_items) return;  // whole block: before any barrier
+    if (p.abort && *p.abort) return;
     // recount tiers take codes (read << 6 | residue class); the first pass reads
     uint32_t a, residue;
     if (p.coded) {

@@ -187,11 +187,10 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
     const uint32_t ps = A.start[p], pe = A.start[p + 1];
     const uint32_t n = pe - ps;
     if (n == 0) return;
-    if (n > (uint32_t)CAP) {
+    if (n > (uint32_t)CAP) {  // (the bounds kernel listed the partitions above 1,024)
         if (tid == 0) {
             if (CAP >= 4096) A.big_list[atomicAdd(A.big_n, 1u)] = p;
             else if (CAP >= 2048) A.mid2_list[atomicAdd(A.mid2_n, 1u)] = p;
-            else A.mid_list[atomicAdd(A.mid_n, 1u)] = p;
         }
         return;
     }
@@ -473,27 +472,39 @@ __global__ void records_from_tables_kernel(const uint64_t *sk, const uint32_t *s
 // search per partition over the sorted records -- log2(n) cached loads each
 // instead of a pass over all n records plus a serial suffix-min fill.  (Bits
 // above the partition id -- the owner rank's in distributed mode -- are the
-// same for every key and masked off.)
+// same for every key and masked off.)  Thread p also finds start[p + 1] (the
+// two searches interleaved) and lists the partitions above 1,024 records, so
+// the 2,048 / 4,096-record tiers need not wait for the 1,024-record pass: they
+// run beside it on a second stream.
 __global__ void part_bounds_kernel(const uint64_t *sk, uint64_t n, int shift, uint32_t mask, uint32_t np,
-                                   uint32_t *start) {
+                                   uint32_t *start, uint32_t *mid_list, uint32_t *mid_n) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p > np) return;
-    uint64_t lo = 0, hi = n;
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (((uint32_t)(sk[mid] >> shift) & mask) < p) lo = mid + 1; else hi = mid;
+    const bool two = p < np;
+    uint64_t lo = 0, hi = n, lo1 = 0, hi1 = two ? n : 0;
+    while (lo < hi || lo1 < hi1) {
+        if (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (((uint32_t)(sk[mid] >> shift) & mask) < p) lo = mid + 1; else hi = mid;
+        }
+        if (lo1 < hi1) {
+            const uint64_t mid = (lo1 + hi1) >> 1;
+            if (((uint32_t)(sk[mid] >> shift) & mask) < p + 1) lo1 = mid + 1; else hi1 = mid;
+        }
     }
     start[p] = (uint32_t)lo;
+    if (two && lo1 - lo > 1024u) mid_list[atomicAdd(mid_n, 1u)] = p;
 }
 
-hipError_t launch_part_starts(const uint64_t *sk, uint64_t n, int shift, uint32_t *start, uint32_t np,
-                              hipStream_t s) {
-    hipLaunchKernelGGL(part_bounds_kernel, dim3((np + 1 + 255) / 256), dim3(256), 0, s, sk, n, shift, np - 1, np,
-                       start);
+hipError_t launch_part_starts(const PartArgs &a, uint64_t n, int shift, hipStream_t s) {
+    hipLaunchKernelGGL(part_bounds_kernel, dim3((a.np + 1 + 255) / 256), dim3(256), 0, s, a.sk, n, shift, a.np - 1,
+                       a.np, const_cast<uint32_t *>(a.start), a.mid_list, a.mid_n);
     return hipGetLastError();
 }
 
-hipError_t launch_part_build(const PartArgs &a, bool strict, hipStream_t s) {
+// one tier of the bucket build: CAP 1,024 over every partition, 2,048 / 4,096
+// over the lists the bounds kernel / the 2,048 tier made
+hipError_t launch_part_build(const PartArgs &a, bool strict, int cap, hipStream_t s) {
     if (!a.np) return hipSuccess;
 #define PB_LAUNCH(CAPV, GRID, ST)                                                                          \
     do {                                                                                                 \
@@ -503,8 +514,13 @@ hipError_t launch_part_build(const PartArgs &a, bool strict, hipStream_t s) {
         hipLaunchKernelGGL((part_build_kernel<CAPV, ST>), dim3(GRID), dim3(PB_THREADS), lds, s, a);     \
     } while (0)
     const uint32_t mid_grid = a.np < 1024u ? a.np : 1024u;
-    if (strict) { PB_LAUNCH(1024, a.np, true); PB_LAUNCH(2048, mid_grid, true); PB_LAUNCH(4096, mid_grid, true); }
-    else { PB_LAUNCH(1024, a.np, false); PB_LAUNCH(2048, mid_grid, false); PB_LAUNCH(4096, mid_grid, false); }
+    if (cap == 1024) {
+        if (strict) PB_LAUNCH(1024, a.np, true); else PB_LAUNCH(1024, a.np, false);
+    } else if (cap == 2048) {
+        if (strict) PB_LAUNCH(2048, mid_grid, true); else PB_LAUNCH(2048, mid_grid, false);
+    } else {
+        if (strict) PB_LAUNCH(4096, mid_grid, true); else PB_LAUNCH(4096, mid_grid, false);
+    }
 #undef PB_LAUNCH
     return hipGetLastError();
 }

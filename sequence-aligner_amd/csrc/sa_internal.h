@@ -148,6 +148,10 @@ struct PairParams {
     uint32_t n_items;      // reads (x split) to process; blocks beyond it exit
     int32_t xcd_swizzle;   // 1: XCD-contiguous block -> item map (grid % 8 == 0)
     int32_t table;         // LDS hash slots per read: 256 (first pass) or 2048
+    // non-null: every block exits at once when *abort != 0 -- the first pass is
+    // launched before the host has read back whether any partition needs the
+    // global bucket path (big_n); if one did, the pass is discarded and re-run
+    const uint32_t *abort;
 };
 
 // Device-wide counters are sharded NSHARD ways (shard = blockIdx % NSHARD) and
@@ -281,9 +285,8 @@ struct PartArgs {
     uint32_t *bkt_nst, *bkt_nmd, *bkt_first;  // at bucket head sorted positions
     uint8_t *is_head;            // [n] head flags
 };
-hipError_t launch_part_starts(const uint64_t *sk, uint64_t n, int shift, uint32_t *start, uint32_t np,
-                              hipStream_t s);
-hipError_t launch_part_build(const PartArgs &a, bool strict, hipStream_t s);
+hipError_t launch_part_starts(const PartArgs &a, uint64_t n, int shift, hipStream_t s);
+hipError_t launch_part_build(const PartArgs &a, bool strict, int cap, hipStream_t s);
 // 8-byte records of one big partition -> (mix << lb | locrank, g) for the global scan path
 hipError_t launch_convert_records(const uint64_t *rec8, uint32_t n, const PartArgs &a, uint64_t *okeys,
                                   uint32_t *ovals, hipStream_t s);
