@@ -71,12 +71,7 @@ struct PcSharedStrict {
 
 __device__ __forceinline__ uint32_t pc_block_excl_scan(uint32_t v, uint32_t *lds4, uint32_t *total) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t inc = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t t = __shfl_up(inc, off, 64);
-        if (lane >= off) inc += t;
-    }
+    const uint32_t inc = wave_incl_add(v);
     if (lane == 63) lds4[w] = inc;
     __syncthreads();
     uint32_t off = 0, tot = 0;
@@ -306,12 +301,7 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
         }
         const int buf = (c0 / CH) & 1;  // slow readers of the previous chunk's counts are not overwritten
         const uint32_t mine = __popc(keep);
-        uint32_t inc = mine;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t t = __shfl_up(inc, off, 64);
-            if (lane >= off) inc += t;
-        }
+        const uint32_t inc = wave_incl_add(mine);
         if (lane == 63) S.emit4[buf][wvi] = inc;
         __syncthreads();
         uint32_t total = 0, ex = inc - mine;

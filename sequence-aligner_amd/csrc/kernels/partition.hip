@@ -148,13 +148,7 @@ __device__ __forceinline__ void lds_radix_sort(SH &S, uint32_t n, int bits) {
                 if (q < w) { mine[0] += c.x; mine[1] += c.y; mine[2] += c.z; mine[3] += c.w; }
             }
             const uint32_t lsum = tot[0] + tot[1] + tot[2] + tot[3];
-            uint32_t inc = lsum;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const uint32_t t = __shfl_up(inc, off, 64);
-                if (lane >= off) inc += t;
-            }
-            uint32_t acc = inc - lsum;  // digits below 4 * lane, all waves
+            uint32_t acc = wave_incl_add(lsum) - lsum;  // digits below 4 * lane, all waves
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 S.ofs[w][4 * lane + i] = (uint16_t)(acc + mine[i]);
@@ -229,28 +223,36 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
             if (gh) { last_gh = s; ++n_gh; if (first_gh == 0xFFFFFFFFu) first_gh = s; }
         }
     }
-    // one combined block scan (wave shuffles, one barrier): exclusive sums of
-    // (md | edge << 16) and (bucket heads | group heads << 16), exclusive prefix
-    // max of the last bucket / group head, exclusive suffix min of the first
-    // group / bucket head (element 0 is always a head; counts < 2^16)
+    // one combined block scan (one barrier): exclusive sums of (md | edge << 16)
+    // and (bucket heads | group heads << 16) as DPP add-scans; the exclusive
+    // prefix max of the last bucket / group head and the exclusive suffix min
+    // of the first group / bucket head are each one lane's value -- the nearest
+    // lane below / above holding a head (head positions grow with the lane) --
+    // found by ballot and fetched with one bpermute (element 0 is always a
+    // head; counts < 2^16)
     uint32_t sme = md_c | (ed_c << 16), shd = n_bh | (n_gh << 16);
-    uint32_t mbh = last_bh, mgh = last_gh, ugh = first_gh, ubh = first_bh;
     const uint32_t sme0 = sme;
     const int lane = tid & 63, wv = tid >> 6;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t a1 = __shfl_up(sme, off, 64), a2 = __shfl_up(shd, off, 64);
-        const uint32_t a3 = __shfl_up(mbh, off, 64), a4 = __shfl_up(mgh, off, 64);
-        const uint32_t a5 = __shfl_down(ugh, off, 64), a6 = __shfl_down(ubh, off, 64);
-        if (lane >= off) { sme += a1; shd += a2; mbh = max(mbh, a3); mgh = max(mgh, a4); }
-        if (lane + off < 64) { ugh = min(ugh, a5); ubh = min(ubh, a6); }
-    }
+    sme = wave_incl_add(sme);
+    shd = wave_incl_add(shd);
+    const uint64_t bb = __ballot(n_bh != 0), bg = __ballot(n_gh != 0);
+    const uint64_t below = (1ull << lane) - 1ull, above = ~below << 1;  // lanes < lane, lanes > lane
+    // (63 - clz / ctz of an empty mask select an out-of-wave lane: masked below)
+    const int lbb = 63 - __clzll(bb & below), lbg = 63 - __clzll(bg & below);
+    const int lab = __ffsll((long long)(bb & above)) - 1, lag = __ffsll((long long)(bg & above)) - 1;
+    uint32_t xbh = (uint32_t)__shfl((int)last_bh, lbb & 63, 64), xgh = (uint32_t)__shfl((int)last_gh, lbg & 63, 64);
+    uint32_t xubh = (uint32_t)__shfl((int)first_bh, lab & 63, 64), xugh = (uint32_t)__shfl((int)first_gh, lag & 63, 64);
+    if (!(bb & below)) xbh = 0;
+    if (!(bg & below)) xgh = 0;
+    if (!(bb & above)) xubh = 0xFFFFFFFFu;
+    if (!(bg & above)) xugh = 0xFFFFFFFFu;
+    // wave aggregates: the highest / lowest lane holding a head
+    const uint32_t mbh = bb ? (uint32_t)__builtin_amdgcn_readlane((int)last_bh, 63 - __clzll(bb)) : 0u;
+    const uint32_t mgh = bg ? (uint32_t)__builtin_amdgcn_readlane((int)last_gh, 63 - __clzll(bg)) : 0u;
+    const uint32_t ubh = bb ? (uint32_t)__builtin_amdgcn_readlane((int)first_bh, __ffsll((long long)bb) - 1) : 0xFFFFFFFFu;
+    const uint32_t ugh = bg ? (uint32_t)__builtin_amdgcn_readlane((int)first_gh, __ffsll((long long)bg) - 1) : 0xFFFFFFFFu;
     if (lane == 63) S.agg[wv] = make_uint4(sme, shd, mbh, mgh);
     if (lane == 0) S.aggu[wv] = make_uint2(ugh, ubh);
-    uint32_t xbh = __shfl_up(mbh, 1, 64), xgh = __shfl_up(mgh, 1, 64);
-    uint32_t xugh = __shfl_down(ugh, 1, 64), xubh = __shfl_down(ubh, 1, 64);
-    if (lane == 0) { xbh = 0; xgh = 0; }
-    if (lane == 63) { xugh = 0xFFFFFFFFu; xubh = 0xFFFFFFFFu; }
     sme -= sme0;
     __syncthreads();
     uint32_t blk_heads = 0;

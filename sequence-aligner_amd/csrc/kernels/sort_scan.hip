@@ -13,12 +13,8 @@ constexpr int SC_ITEMS = 8;
 constexpr int SC_TILE = SC_THREADS * SC_ITEMS;
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t t = __shfl_up(v, off, 64);
-        if (lane >= off) v += t;
-    }
-    return v;
+    (void)lane;
+    return wave_incl_add(v);
 }
 
 // Block-wide exclusive scan of one value per thread (256 threads); returns the
@@ -223,12 +219,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep_kernel(const uint64_t
 #pragma unroll
         for (int q = 0; q < RS_WAVES; ++q) tot += S.cnt[q][tid];
         // block exclusive scan of tot over the 256 digits
-        uint32_t inc = tot;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t t = __shfl_up(inc, off, 64);
-            if (lane >= off) inc += t;
-        }
+        const uint32_t inc = wave_incl_add(tot);
         if (lane == 63) S.lofs[w] = inc;  // temporarily: wave sums
         __syncthreads();
         uint32_t pre = 0;
@@ -315,12 +306,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep_kv64_kernel(const uin
         uint32_t tot = 0;
 #pragma unroll
         for (int q = 0; q < RS_WAVES; ++q) tot += S.cnt[q][tid];
-        uint32_t inc = tot;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t t = __shfl_up(inc, off, 64);
-            if (lane >= off) inc += t;
-        }
+        const uint32_t inc = wave_incl_add(tot);
         if (lane == 63) S.lofs[w] = inc;
         __syncthreads();
         uint32_t pre = 0;

@@ -68,6 +68,20 @@ __device__ __forceinline__ uint32_t kmer_mix(const uint32_t *w, int32_t p, int s
     return mix32(x);
 }
 
+// Inclusive add-scan over the 64 lanes of a wave in DPP moves (row_shr 1, 2, 4,
+// 8 within each row of 16, then row_bcast 15 / 31 across rows): VALU only, where
+// a __shfl_up ladder is six dependent ds_bpermute round trips through the LDS
+// pipe.  Lanes whose DPP source is outside the row keep `old` = 0.
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15, rows 1, 3
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31, rows 2, 3
+    return v;
+}
+
 // ---- partner lists and per-occurrence records ------------------------------
 // Every bucket owns one slice of the combined partner list `lst` (read index
 // per entry), laid out around a split point c:
