@@ -379,6 +379,7 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
         PA.tagtab = (const uint8_t *)c->d_tagtab.p;
         PA.occ_off = occ_off;
         PA.n_reads = n_reads; PA.npr = npr; PA.rl = rl; PA.srl = srl;
+            PA.npr_magic = npr >= 2 ? ~0ull / npr + 1 : 0;
         PA.len = len;
         PA.lbase = (const uint32_t *)c->d_lbase.p;
         PA.lrank = (const uint32_t *)c->d_lrank.p;

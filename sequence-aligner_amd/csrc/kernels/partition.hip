@@ -26,8 +26,14 @@
 
 namespace sa {
 
-__device__ __forceinline__ uint32_t read_of_g(uint32_t g, const uint64_t *occ_off, uint32_t n_reads, uint32_t npr) {
-    if (npr) return g / npr;
+// read of occurrence g.  Uniform lengths: floor(g / npr) as the high word of
+// g * M, M = floor((2^64 - 1) / npr) + 1 (PartArgs::npr_magic, host-side): M =
+// 2^64 / npr + e with 0 <= e < 1, so g * M / 2^64 = g / npr + (< 2^-32), which
+// never reaches the next integer for g, npr < 2^32 -- a few multiplies instead
+// of the ~35-instruction integer-division expansion, twice per record
+__device__ __forceinline__ uint32_t read_of_g(uint32_t g, const uint64_t *occ_off, uint32_t n_reads, uint32_t npr,
+                                              uint64_t npr_magic) {
+    if (npr) return npr == 1 ? g : (uint32_t)__umul64hi((unsigned long long)g, (unsigned long long)npr_magic);
     uint32_t lo = 0, hi = n_reads;  // largest r with occ_off[r] <= g
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -59,7 +65,7 @@ __device__ __forceinline__ unsigned long long record_key(uint64_t rec, const Par
         lr = v.y;
         rr = v.x;
     } else {
-        const uint32_t r = read_of_g(g, A.occ_off, A.n_reads, A.npr);
+        const uint32_t r = read_of_g(g, A.occ_off, A.n_reads, A.npr, A.npr_magic);
         const uint32_t pos = A.npr ? g - r * A.npr : g - (uint32_t)A.occ_off[r];
         const int32_t d = A.npr ? (int32_t)A.npr - 1 : A.len[r] - A.k;
         lr = A.lrank[A.lbase[d] + pos];
@@ -109,6 +115,10 @@ __device__ __forceinline__ void lds_radix_sort(SH &S, uint32_t n, int bits) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     for (int shift = 0; shift < bits; shift += 8) {
+        // digit width of this pass: the last one ranks only the bits that are
+        // left (25-bit keys: 8 + 8 + 8 + 1 ballots, not 32)
+        const int nbits = bits - shift < 8 ? bits - shift : 8;
+        const uint32_t dmask = (1u << nbits) - 1u;
         reinterpret_cast<uint4 *>(S.cnt[w])[lane] = make_uint4(0, 0, 0, 0);
         unsigned long long k[SL];
         uint32_t gv[SL], rk[SL], dg[SL];
@@ -123,11 +133,12 @@ __device__ __forceinline__ void lds_radix_sort(SH &S, uint32_t n, int bits) {
         for (int j = 0; j < SL; ++j) {
             const uint32_t i = w * SUB + j * 64 + lane;
             const bool valid = i < n;
-            const uint32_t d = (uint32_t)(k[j] >> shift) & 255u;
+            const uint32_t d = (uint32_t)(k[j] >> shift) & dmask;
             dg[j] = d;
             uint64_t peer = __ballot(valid);
 #pragma unroll
             for (int b = 0; b < 8; ++b) {
+                if (b >= nbits) break;  // uniform
                 const bool bit = (d >> b) & 1u;
                 const uint64_t bb = __ballot(bit);
                 peer &= bit ? bb : ~bb;
@@ -315,7 +326,7 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
             g = A.meta[r].x + (code & ((1u << A.pos_bits) - 1u));
         } else {
             g = code;
-            r = Sr ? Sr[slot] : read_of_g(g, A.occ_off, A.n_reads, A.npr);
+            r = Sr ? Sr[slot] : read_of_g(g, A.occ_off, A.n_reads, A.npr, A.npr_magic);
         }
         const uint32_t st = (t & TAG_ST) ? 1u : 0u, en = (t & TAG_EN) ? 1u : 0u, md = (t & TAG_MD) ? 1u : 0u;
         // split point of the bucket [bh, nextb): its md entries end at c

@@ -273,6 +273,7 @@ struct PartArgs {
     const uint8_t *tagtab;
     const uint64_t *occ_off;
     uint32_t n_reads, npr;
+    uint64_t npr_magic;          // floor((2^64 - 1) / npr) + 1 (npr >= 2): read_of_g's division
     const uint2 *rl;             // {read, loc rank} by occurrence index (distributed mode, mixed lengths) or null
     const uint2 *srl;            // the same, sorted with the records (aligned with sk) or null
     // sk holds 8-byte records (mix32 << 32 | occurrence index); the loc rank is
