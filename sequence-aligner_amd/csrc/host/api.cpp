@@ -294,6 +294,7 @@ EmitParams emit_params(sa_ctx *c) {
     e.m = c->m;
     e.lb = c->lb;
     e.occ_off = (const uint64_t *)c->d_occ_off.p;
+    e.npr = c->uniform_npr;
     e.lbase = (const uint32_t *)c->d_lbase.p;
     e.lrank = (const uint32_t *)c->d_lrank.p;
     e.maxd = c->maxd;
@@ -1612,6 +1613,7 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint6
     PI.rec = PA.rec; PI.xrec = PA.xrec; PI.lst = PA.lst;
     EmitParams E = emit_params(c);
     E.occ_off = loff;  // occurrences of read a on this rank: [loff[a], loff[a+1])
+    E.npr = 0;
     // every global read has ~1/P of its occurrences here: blocks take ranges of
     // reads with ~PCM_TARGET local occurrences (pair_count.hip, multi-read blocks)
     const uint32_t n_multi = (uint32_t)((n + PCM_TARGET - 1) / PCM_TARGET) + 1;

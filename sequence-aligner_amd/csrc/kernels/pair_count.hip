@@ -153,8 +153,9 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
     }
     if (tid == 0) { S.fill = 0; S.overflow = 0; }
 
-    const uint64_t g0 = e.occ_off[a];
-    const uint32_t nocc = (uint32_t)(e.occ_off[a + 1] - g0);
+    // (uniform lengths: no dependent offset load before the record loads)
+    const uint64_t g0 = e.npr ? (uint64_t)a * e.npr : e.occ_off[a];
+    const uint32_t nocc = e.npr ? e.npr : (uint32_t)(e.occ_off[a + 1] - g0);
     unsigned long long role_pairs = 0;
     unsigned long long x_over = ~0ull;  // role pairs enumerated when the table filled
     // (the table initialisation is ordered before any insert by the chunk scan's barriers)

@@ -200,14 +200,35 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
         return;
     }
     // ---- load, then stable LDS radix sort on the key bits below the partition id
-    for (uint32_t i = tid; i < n; i += PB_THREADS) {
-        uint32_t g, r = 0;
-        const uint64_t rec = load_sk(A.sk + ps + i);
-        const uint2 *rlp = A.srl ? A.srl + ps + i : (A.rl ? A.rl + (uint32_t)rec : nullptr);
-        S.key[i] = record_key(rec, A, g, r, rlp);
-        S.g[i] = g;
-        S.oi[i] = (uint16_t)i;
-        if (Sr) Sr[i] = r;
+    //      (all of a thread's record loads are issued before any is used, so a
+    //      block waits one HBM latency here, not one per record)
+    {
+        uint64_t recs[IT];
+#pragma unroll
+        for (int j = 0; j < IT; ++j) {
+            const uint32_t i = tid + j * PB_THREADS;
+            recs[j] = load_sk(A.sk + ps + (i < n ? i : n - 1));
+        }
+        // (keys of the clamped slots too: their loc-rank gathers issue together)
+        unsigned long long kk[IT];
+        uint32_t gg[IT], rr[IT];
+#pragma unroll
+        for (int j = 0; j < IT; ++j) {
+            const uint32_t i = tid + j * PB_THREADS, ic = i < n ? i : n - 1;
+            rr[j] = 0;
+            const uint2 *rlp = A.srl ? A.srl + ps + ic : (A.rl ? A.rl + (uint32_t)recs[j] : nullptr);
+            kk[j] = record_key(recs[j], A, gg[j], rr[j], rlp);
+        }
+#pragma unroll
+        for (int j = 0; j < IT; ++j) {
+            const uint32_t i = tid + j * PB_THREADS;
+            if (i < n) {
+                S.key[i] = kk[j];
+                S.g[i] = gg[j];
+                S.oi[i] = (uint16_t)i;
+                if (Sr) Sr[i] = rr[j];
+            }
+        }
     }
     __syncthreads();
     lds_radix_sort<CAP>(S, n, A.sort_bits);

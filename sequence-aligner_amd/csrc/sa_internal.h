@@ -28,6 +28,7 @@ struct EmitParams {
     int32_t m;                 // min(16, k): hashed window (ObjectStore.scala:52)
     int32_t lb;                // locrank bits in the sort key
     const uint64_t *occ_off;   // [n+1] first occurrence index of each read
+    uint32_t npr;              // > 0: every read has npr k-mers (occ_off[r] = r * npr)
     const uint32_t *lbase;     // [maxd+1] offset of denominator d = L-k in lrank
     const uint32_t *lrank;     // rank of float32 i/d among all distinct locs
     int32_t maxd;
