@@ -505,7 +505,12 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
 int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bool emit_all,
                const uint32_t *read_order, uint32_t n_items, Counters *cnt, uint64_t &np, uint64_t &cap_s_out,
                const uint32_t *item_start = nullptr, uint32_t n_multi = 0, const uint32_t *abort_flag = nullptr,
-               bool *aborted = nullptr) {
+               bool *aborted = nullptr, bool *per_read = nullptr, uint64_t *distinct_ub = nullptr) {
+    // per_read (in: allowed; out: used): the first pass writes each read's
+    // dispatched pairs, trail-ascending, into a fixed region of PC_RREG slots
+    // (wide ids, dispatched pairs only, one device); a read whose table
+    // overflows needs the recount tiers, so the pass is then re-run in the
+    // shared-region mode.  distinct_ub: distinct pairs counted (>= dispatched)
     // abort_flag (device): the first pass exits when it is set (big partitions
     // still to build, bucket_stage phase 1); *aborted then tells the caller
     // ---- pair counting -------------------------------------------------
@@ -522,6 +527,14 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
     P.table = 256;
     P.abort = abort_flag;
     if (aborted) *aborted = false;
+    P.per_read = per_read && *per_read ? 1 : 0;
+    if (per_read) *per_read = false;
+    uint2 *rreg = nullptr;
+    uint32_t *rcnt = nullptr;
+    if (P.per_read) {
+        ENSURE(c->d_rreg, (uint64_t)n_items * PC_RREG, &rreg);
+        ENSURE(c->d_rcnt, (uint64_t)n_items + 1, &rcnt);
+    }
     if (c->pair_cap == 0) c->pair_cap = std::max<uint64_t>(1 << 16, (uint64_t)n_items * (P.emit_all ? 64 : 24));
     // output regions: NSHARD x cap_s entries (a block appends to region blockIdx % NSHARD)
     unsigned long long cur[NSHARD];
@@ -544,6 +557,10 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
         O.role_pairs = cnt->role_pairs;
         O.overflow_n = &cnt->overflow_n;
         O.distinct = cnt->distinct;
+        O.rreg = rreg;
+        O.rcnt = rcnt;
+        // (cursor, role pairs, dummy, distinct: a pass re-run after an abort or
+        // in the shared-region mode counts from zero)
         HIPCHK(hipMemsetAsync(cnt->cursor, 0, 4 * NSHARD * sizeof(unsigned long long), c->stream));
         HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(uint32_t), c->stream));
         {
@@ -562,12 +579,26 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
         HIPCHK(hipMemcpyAsync(&ovn, &cnt->overflow_n, 4, hipMemcpyDeviceToHost, c->stream));
         uint32_t abv = 0;
         if (P.abort) HIPCHK(hipMemcpyAsync(&abv, P.abort, 4, hipMemcpyDeviceToHost, c->stream));
+        unsigned long long dist_h[NSHARD];
+        if (P.per_read) HIPCHK(hipMemcpyAsync(dist_h, cnt->distinct, sizeof(dist_h), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         if (abv) {
             *aborted = true;
             return SA_OK;
         }
         P.abort = nullptr;
+        if (P.per_read) {
+            if (ovn == 0) {
+                *per_read = true;
+                if (distinct_ub) *distinct_ub = shard_sum(dist_h);
+                np = 0;
+                cap_s_out = cap_s;
+                return SA_OK;
+            }
+            P.per_read = 0;  // overflowed reads: count again in the shared regions
+            --attempt;
+            continue;
+        }
         // Reads whose 256-slot table overflowed (> 192 partners) are recounted
         // one per block in bigger tables: 2,048 slots unless their partner count
         // -- extrapolated from how fast the first pass filled -- is far beyond it,
@@ -797,44 +828,68 @@ int device_build(sa_ctx *c, bool readback) {
 
     uint64_t np = 0, cap_s = 0;
     bool aborted = false;
-    rc = pair_stage(c, E, PI, strict, strict || c->keep_pairs, read_order, nr, cnt, np, cap_s, nullptr, 0,
-                    bphase == 1 ? &cnt->big_n : nullptr, &aborted);
+    const bool emit_all = strict || c->keep_pairs;
+    // dispatched pairs straight into per-read regions (pair_stage) when the
+    // regions stay within 4 GB: the lead-descending order is then a scan and
+    // a copy instead of a 34-bit radix sort
+    const bool per_read_ok = !emit_all && (uint64_t)nr * PC_RREG * sizeof(uint2) <= (4ull << 30);
+    bool per_read = per_read_ok;
+    uint64_t np_ub = 0;
+    rc = pair_stage(c, E, PI, strict, emit_all, read_order, nr, cnt, np, cap_s, nullptr, 0,
+                    bphase == 1 ? &cnt->big_n : nullptr, &aborted, &per_read, &np_ub);
     if (rc) return rc;
     if (aborted) {  // partitions above 4,096 records (high-copy repeats): build them, count again
         rc = bucket_stage(c, keys, keys2, vals, vals2, n, (const uint64_t *)c->d_occ_off.p, nr, c->uniform_npr,
                           orl, (const int32_t *)c->d_len.p, strict, stmp, cnt, PA, big_buckets, 0, 2);
         if (rc) return rc;
         PI.xrec = PA.xrec;
-        rc = pair_stage(c, E, PI, strict, strict || c->keep_pairs, read_order, nr, cnt, np, cap_s);
+        per_read = per_read_ok;
+        rc = pair_stage(c, E, PI, strict, emit_all, read_order, nr, cnt, np, cap_s, nullptr, 0, nullptr, nullptr,
+                        &per_read, &np_ub);
         if (rc) return rc;
     }
-    const bool emit_all = strict || c->keep_pairs;
 
     // ---- ordering --------------------------------------------------------
-    uint64_t *ok, *ok2; uint32_t *ov, *ov2; uint8_t *otmp;
-    ENSURE(c->d_okeys, np, &ok);
-    ENSURE(c->d_okeys2, np, &ok2);
-    ENSURE(c->d_ovals, np, &ov);
-    ENSURE(c->d_ovals2, np, &ov2);
-    ENSURE(c->d_osort, radix_sort_temp_bytes(np), &otmp);
     int32_t *dlead, *dtrail, *dcount;
-    ENSURE(c->d_lead, np, &dlead);
-    ENSURE(c->d_trail, np, &dtrail);
-    ENSURE(c->d_count, np, &dcount);
-    {
+    if (per_read) {
+        uint32_t *rex; uint8_t *stmp2;
+        ENSURE(c->d_lead, np_ub, &dlead);
+        ENSURE(c->d_trail, np_ub, &dtrail);
+        ENSURE(c->d_count, np_ub, &dcount);
+        ENSURE(c->d_rex, (uint64_t)nr + 1, &rex);
+        ENSURE(c->d_osort, scan_temp_bytes(nr), &stmp2);
+        const uint32_t *rcnt = (const uint32_t *)c->d_rcnt.p;
         StageScope st(c, SA_STAGE_ORDER);
-        const int idb = bits_for(nr ? nr - 1 : 0);
-        HIPCHK(launch_make_order_keys((const uint32_t *)c->d_pf.p, (const uint32_t *)c->d_ps.p,
-                                      (const uint64_t *)c->d_pr.p, cnt->cursor, cap_s, strict ? 1 : 0, idb, ok, ov,
-                                      cnt->shard_off, c->stream));
-        const int hi = strict ? 64 : 2 * idb;
-        HIPCHK(radix_sort(&ok, &ov, &ok2, &ov2, np, 0, hi, otmp, c->stream));
-        HIPCHK(launch_gather_pairs(ov, np, (const uint32_t *)c->d_pf.p, (const uint32_t *)c->d_ps.p,
-                                   (const uint32_t *)c->d_pc.p, dlead, dtrail, dcount, c->stream));
+        HIPCHK(exclusive_scan_u32(rcnt, rex, nr, &cnt->rtotal, stmp2, c->stream));
+        HIPCHK(launch_copy_read_regions((const uint2 *)c->d_rreg.p, rcnt, rex, &cnt->rtotal, nr, dlead, dtrail,
+                                        dcount, c->stream));
+    }
+    uint64_t *ok, *ok2; uint32_t *ov, *ov2; uint8_t *otmp;
+    if (!per_read) {
+        ENSURE(c->d_okeys, np, &ok);
+        ENSURE(c->d_okeys2, np, &ok2);
+        ENSURE(c->d_ovals, np, &ov);
+        ENSURE(c->d_ovals2, np, &ov2);
+        ENSURE(c->d_osort, radix_sort_temp_bytes(np), &otmp);
+        ENSURE(c->d_lead, np, &dlead);
+        ENSURE(c->d_trail, np, &dtrail);
+        ENSURE(c->d_count, np, &dcount);
+        {
+            StageScope st(c, SA_STAGE_ORDER);
+            const int idb = bits_for(nr ? nr - 1 : 0);
+            HIPCHK(launch_make_order_keys((const uint32_t *)c->d_pf.p, (const uint32_t *)c->d_ps.p,
+                                          (const uint64_t *)c->d_pr.p, cnt->cursor, cap_s, strict ? 1 : 0, idb, ok, ov,
+                                          cnt->shard_off, c->stream));
+            const int hi = strict ? 64 : 2 * idb;
+            HIPCHK(radix_sort(&ok, &ov, &ok2, &ov2, np, 0, hi, otmp, c->stream));
+            HIPCHK(launch_gather_pairs(ov, np, (const uint32_t *)c->d_pf.p, (const uint32_t *)c->d_ps.p,
+                                       (const uint32_t *)c->d_pc.p, dlead, dtrail, dcount, c->stream));
+        }
     }
     Counters hc;
     HIPCHK(hipMemcpyAsync(&hc, cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    if (per_read) np = hc.rtotal;
     resolve_timing(c);
     c->stats = sa_stats{};
     c->stats.kmers = n;
@@ -1184,7 +1239,7 @@ void sa_ctx_destroy(sa_ctx *c) {
                     &c->d_srec, &c->d_bnmd, &c->d_ishead, &c->d_bnst2, &c->d_tmd, &c->d_ted, &c->d_tmdi,
                     &c->d_tedi, &c->d_xrec, &c->d_tier, &c->d_ovlrp, &c->d_meta, &c->d_items, &c->d_bigtot, &c->d_hk0, &c->d_hk1, &c->d_hflag,
                     &c->d_hidx, &c->d_hpos, &c->d_htmp, &c->d_hist, &c->d_hovf, &c->d_hsmall,
-                    &c->d_ltb, &c->d_lmax};
+                    &c->d_ltb, &c->d_lmax, &c->d_rreg, &c->d_rcnt, &c->d_rex};
     for (DBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto &p : c->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }

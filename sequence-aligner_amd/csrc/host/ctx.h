@@ -36,6 +36,7 @@ struct Counters {
     uint32_t mid_n;
     uint32_t mid2_n;
     uint32_t xrec_n;     // escape records written (big partitions)
+    uint32_t rtotal;     // per-read pair mode: dispatched pairs (scan total)
     uint32_t shard_off[NSHARD + 2];
 };
 
@@ -94,6 +95,7 @@ struct sa_ctx {
     DBuf d_okeys, d_ovals, d_okeys2, d_ovals2, d_osort;
     DBuf d_lead, d_trail, d_count, d_aln, d_p1, d_tb, d_ltb, d_lmax;
     DBuf d_rkey, d_rkey2, d_rord, d_rord2, d_rtmp;
+    DBuf d_rreg, d_rcnt, d_rex;  // per-read pair regions, counts, their exclusive scan
     uint64_t pair_cap = 0;
     uint64_t n_disp = 0;
     // distributed mode (sa_dist_*): this rank's slice of a global read set

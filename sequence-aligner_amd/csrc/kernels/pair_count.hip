@@ -273,6 +273,7 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
     if (tid == 0 && !S.overflow) atomicAdd(&o.distinct[shard], (unsigned long long)S.fill);
     if (S.overflow) {  // recounted by the next tier: this read's class only
         if (tid == 0) {
+            if (p.per_read) o.rcnt[a] = 0;  // (the host re-runs the pass in region mode)
             const uint32_t at = atomicAdd(o.overflow_n, 1u);
             o.overflow_list[at] = (a << 6) | residue;
             // its distinct partners, extrapolated from the fill rate (FILL_MAX
@@ -282,6 +283,27 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
                 const unsigned long long est = (unsigned long long)(TAB * 3 / 4) * role_pairs / (x ? x : 1);
                 o.overflow_rp[at] = est > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)est;
             }
+        }
+        return;
+    }
+    if (p.per_read) {
+        // --- per-read region (TAB = 256: one slot per thread): compact the
+        //     kept keys in LDS, rank each by its trail among them (<= 192,
+        //     distinct), store at its rank -- the region is trail-ascending
+        if constexpr (TAB == PC_THREADS) {
+            const uint32_t kk = S.key[tid], kc = S.cnt[tid];
+            const bool keep = kk != PC_EMPTY && (int32_t)kc >= p.min_coll && (int32_t)kc <= p.max_coll;
+            uint32_t m;
+            const uint32_t ex = pc_block_excl_scan(keep ? 1u : 0u, S.lds4, &m);
+            uint32_t *ck = reinterpret_cast<uint32_t *>(S.rec);  // enumeration state is dead
+            if (keep) ck[ex] = kk;
+            __syncthreads();
+            if (keep) {
+                uint32_t r = 0;
+                for (uint32_t i = 0; i < m; ++i) r += ck[i] < kk ? 1u : 0u;
+                o.rreg[(uint64_t)a * PC_RREG + r] = make_uint2(kk, kc);
+            }
+            if (tid == 0) o.rcnt[a] = m;
         }
         return;
     }
@@ -647,6 +669,32 @@ __global__ void gather_pairs_kernel(const uint32_t *perm, uint64_t n, const uint
     lead[i] = (int32_t)fst[j] + 1;  // reference ids are 1-based
     trail[i] = (int32_t)snd[j] + 1;
     count[i] = (int32_t)cnt[j];
+}
+
+// one wave per read: its region's entries to their place in the lead-descending
+// dispatch list, offset = (sum of the counts of reads above it) = total - ex - cnt
+__global__ void copy_read_regions_kernel(const uint2 *rreg, const uint32_t *rcnt, const uint32_t *ex,
+                                         const uint32_t *total, uint32_t n_reads, int32_t *lead, int32_t *trail,
+                                         int32_t *count) {
+    const uint32_t a = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (a >= n_reads) return;
+    const uint32_t m = rcnt[a];
+    const uint32_t off = *total - ex[a] - m;
+    for (uint32_t j = threadIdx.x & 63u; j < m; j += 64) {
+        const uint2 v = rreg[(uint64_t)a * PC_RREG + j];
+        lead[off + j] = (int32_t)a + 1;  // reference ids are 1-based
+        trail[off + j] = (int32_t)v.x + 1;
+        count[off + j] = (int32_t)v.y;
+    }
+}
+
+hipError_t launch_copy_read_regions(const uint2 *rreg, const uint32_t *rcnt, const uint32_t *ex,
+                                    const uint32_t *total, uint32_t n_reads, int32_t *lead, int32_t *trail,
+                                    int32_t *count, hipStream_t s) {
+    if (!n_reads) return hipSuccess;
+    hipLaunchKernelGGL(copy_read_regions_kernel, dim3((n_reads + 3) / 4), dim3(256), 0, s, rreg, rcnt, ex, total,
+                       n_reads, lead, trail, count);
+    return hipGetLastError();
 }
 
 hipError_t launch_gather_pairs(const uint32_t *perm, uint64_t n, const uint32_t *fst, const uint32_t *snd,

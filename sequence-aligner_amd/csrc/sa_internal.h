@@ -167,6 +167,7 @@ struct PairParams {
     // launched before the host has read back whether any partition needs the
     // global bucket path (big_n); if one did, the pass is discarded and re-run
     const uint32_t *abort;
+    int32_t per_read;      // 1: emit into PairOut::rreg / rcnt (first pass, wide ids, dispatched pairs only)
 };
 
 // Device-wide counters are sharded NSHARD ways (shard = blockIdx % NSHARD) and
@@ -186,7 +187,13 @@ struct PairOut {
     uint32_t *overflow_list;     // (read << 6 | residue) of the blocks whose LDS table overflowed
     uint32_t *overflow_rp;       // their role-pair totals (nullable)
     uint32_t *overflow_n;
+    // per-read mode (PairParams::per_read): read a's kept pairs, trail
+    // ascending, at rreg[a * PC_RREG ..] and their number at rcnt[a]; the
+    // dispatch order (lead descending) is then one scan + one copy, no sort
+    uint2 *rreg;                 // {trail, count}
+    uint32_t *rcnt;
 };
+constexpr uint32_t PC_RREG = 192;  // = the first pass's fill limit (256 slots at 3/4)
 
 // Four alignment costs indexed by a 2-bit base code given as x8 = 8 * code.
 // Cost8: one word of int8 bytes (HOXD70 and every matrix whose entries fit a
@@ -320,6 +327,11 @@ hipError_t launch_make_order_keys(const uint32_t *fst, const uint32_t *snd, cons
                                   const unsigned long long *cursor, unsigned long long cap_s, int by_rank,
                                   int idbits, uint64_t *keys, uint32_t *vals, uint32_t *shard_off,
                                   hipStream_t s, const uint32_t *starts = nullptr, uint32_t P = 0);
+// per-read mode: the dispatch list (lead descending, trail ascending) from the
+// per-read regions; ex = exclusive scan of rcnt, total = its sum
+hipError_t launch_copy_read_regions(const uint2 *rreg, const uint32_t *rcnt, const uint32_t *ex,
+                                    const uint32_t *total, uint32_t n_reads, int32_t *lead, int32_t *trail,
+                                    int32_t *count, hipStream_t s);
 hipError_t launch_gather_pairs(const uint32_t *perm, uint64_t n, const uint32_t *fst, const uint32_t *snd,
                                const uint32_t *cnt, int32_t *lead, int32_t *trail, int32_t *count,
                                hipStream_t s);
