@@ -113,6 +113,18 @@ hipError_t ensure_side(sa_ctx *c) {
     return e;
 }
 
+// the pinned counter copy (ctx.h), allocated on first use
+int pinned_counters(sa_ctx *c, Counters **out) {
+    if (!c->hcnt) {
+        void *p = nullptr;
+        hipError_t e = hipHostMalloc(&p, sizeof(Counters), hipHostMallocDefault);
+        if (e != hipSuccess) return fail(c, SA_E_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+        c->hcnt = (Counters *)p;
+    }
+    *out = c->hcnt;
+    return SA_OK;
+}
+
 // fork: the side stream waits for everything queued on the main stream so far
 hipError_t fork_side(sa_ctx *c, hipEvent_t ev) {
     hipError_t e = hipEventRecord(ev, c->stream);
@@ -575,13 +587,17 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
                                          c->stream));
             }
         }
-        HIPCHK(hipMemcpyAsync(cur, cnt->cursor, sizeof(cur), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipMemcpyAsync(&ovn, &cnt->overflow_n, 4, hipMemcpyDeviceToHost, c->stream));
-        uint32_t abv = 0;
-        if (P.abort) HIPCHK(hipMemcpyAsync(&abv, P.abort, 4, hipMemcpyDeviceToHost, c->stream));
-        unsigned long long dist_h[NSHARD];
-        if (P.per_read) HIPCHK(hipMemcpyAsync(dist_h, cnt->distinct, sizeof(dist_h), hipMemcpyDeviceToHost, c->stream));
+        // one pinned copy of the counters: cursors, overflow count, distinct
+        // pairs and the abort flag (P.abort is cnt->big_n)
+        Counters *hp;
+        if (int rc_p = pinned_counters(c, &hp)) return rc_p;
+        HIPCHK(hipMemcpyAsync(hp, cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
+        memcpy(cur, hp->cursor, sizeof(cur));
+        ovn = hp->overflow_n;
+        const uint32_t abv = P.abort ? hp->big_n : 0u;
+        unsigned long long dist_h[NSHARD];
+        memcpy(dist_h, hp->distinct, sizeof(dist_h));
         if (abv) {
             *aborted = true;
             return SA_OK;
@@ -886,9 +902,11 @@ int device_build(sa_ctx *c, bool readback) {
                                        (const uint32_t *)c->d_pc.p, dlead, dtrail, dcount, c->stream));
         }
     }
-    Counters hc;
-    HIPCHK(hipMemcpyAsync(&hc, cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+    Counters *hp;
+    if ((rc = pinned_counters(c, &hp))) return rc;
+    HIPCHK(hipMemcpyAsync(hp, cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    const Counters hc = *hp;
     if (per_read) np = hc.rtotal;
     resolve_timing(c);
     c->stats = sa_stats{};
@@ -1244,6 +1262,7 @@ void sa_ctx_destroy(sa_ctx *c) {
         if (b->p) (void)hipFree(b->p);
     for (auto &p : c->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+    if (c->hcnt) (void)hipHostFree(c->hcnt);
     if (c->side) {
         (void)hipStreamSynchronize(c->side);
         (void)hipStreamDestroy(c->side);

@@ -63,6 +63,9 @@ struct sa_ctx {
     // the 1,024-record pass) and its fork / join events; created on first use
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_fork2 = nullptr, ev_join2 = nullptr;
+    // pinned host copy of the device counters: each build's readbacks are one
+    // DMA each (a pageable copy stages through a driver buffer)
+    sa::Counters *hcnt = nullptr;
     std::string err;
     // reads (host)
     std::vector<char> bases;
