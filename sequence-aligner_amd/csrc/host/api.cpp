@@ -729,7 +729,10 @@ int device_build(sa_ctx *c, bool readback) {
     uint8_t *stmp8;
     ENSURE(c->d_sorttmp, std::max(radix_sort_temp_bytes(n), buckets_temp_bytes(n)), &stmp8);
     stmp = stmp8;
-    {
+    // reads of <= 1,024 bases: packing and emission in one kernel (pack_emit.hip),
+    // timed as the emit stage
+    const bool fused = c->maxL <= 1024;
+    if (!fused) {
         StageScope st(c, SA_STAGE_PACK);
         HIPCHK(launch_pack_reads(R, c->stream));
     }
@@ -775,7 +778,8 @@ int device_build(sa_ctx *c, bool readback) {
     }
     {
         StageScope st(c, SA_STAGE_EMIT);
-        HIPCHK(launch_kmer_emit(R, E, keys, vals, c->stream));
+        if (fused) HIPCHK(launch_pack_emit(R, E, keys, c->stream));
+        else HIPCHK(launch_kmer_emit(R, E, keys, vals, c->stream));
     }
     // reads in locality order (overlapping reads adjacent) for pair_count: by
     // the top 16 bits of their minimum k-mer mix (reads sharing it stay

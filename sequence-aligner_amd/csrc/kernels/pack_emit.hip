@@ -109,6 +109,85 @@ __global__ __launch_bounds__(256) void kmer_emit_kernel(DevReads r, EmitParams e
     }
 }
 
+// Packing and emission in one pass for reads of <= 1,024 bases (<= 64 words):
+// lane q packs word q as pack_reads_kernel does, keeps it in a register, and
+// the k-mer windows are assembled from the wave's words with two lane shuffles
+// -- no second launch, no reload of the packed words.  Records, locality keys
+// and occurrence tables are exactly kmer_emit_kernel's.
+__global__ __launch_bounds__(256) void pack_emit_kernel(DevReads r, EmitParams e, uint64_t *keys) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    const int shift = 32 - 2 * e.m;
+    for (uint32_t rd = wave; rd < r.n; rd += nwaves) {
+        const uint64_t b0 = r.boff[rd];
+        const int32_t L = (int32_t)(r.boff[rd + 1] - b0);
+        const int32_t nw = (L + 15) >> 4;  // <= 64 (host-checked)
+        int32_t first_bad = INT32_MAX;
+        uint32_t word = 0;
+        if ((int32_t)lane < nw) {
+            const int32_t p0 = (int32_t)lane << 4;
+            const uint64_t a = b0 + (uint64_t)p0;
+            const uint32_t *wp = reinterpret_cast<const uint32_t *>(r.ascii + (a & ~3ull));
+            const uint32_t sh = (uint32_t)(a & 3u);
+            uint32_t d[5];
+#pragma unroll
+            for (int j = 0; j < 5; ++j) d[j] = wp[j];
+            const int32_t valid = min(16, L - p0);
+            uint32_t badm = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t x = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
+                uint32_t bm;
+                const uint32_t c = codes4(x, bm);
+#pragma unroll
+                for (int b = 0; b < 4; ++b) word |= ((c >> (2 * b)) & 3u) << (30 - 2 * (4 * j + b));
+                badm |= bm << (4 * j);
+            }
+            const uint32_t vmask = valid >= 16 ? 0xFFFFu : ((1u << valid) - 1u);
+            word &= valid >= 16 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> (2 * valid));
+            badm &= vmask;
+            if (badm) first_bad = p0 + (int32_t)__builtin_ctz(badm);
+            r.codes[r.woff[rd] + lane] = word;
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            const int32_t o = __shfl_xor(first_bad, off, 64);
+            first_bad = o < first_bad ? o : first_bad;
+        }
+        if (lane == 0) r.bad[rd] = first_bad;
+        // ---- emission (kmer_emit_kernel's records)
+        const int32_t nk = L - e.k + 1;
+        if (nk <= 0) {
+            if (e.rkey && lane == 0) { e.rkey[rd] = 0xFFFFFFFFu; e.rord[rd] = rd; }
+            continue;
+        }
+        const uint64_t g0 = e.npr ? (uint64_t)rd * e.npr : e.occ_off[rd];
+        const uint32_t *lr = e.occ_rl ? e.lrank + e.lbase[nk - 1] : nullptr;
+        uint32_t kmin = 0xFFFFFFFFu;
+        for (int32_t i0 = 0; i0 < nk; i0 += 64) {  // wave-uniform trip count: every lane
+            // takes part in the shuffles (a bpermute from an inactive lane reads nothing)
+            const int32_t i = i0 + (int32_t)lane;
+            // window16 from the wave's words: word i >> 4 and the next one (a
+            // lane past the read's words only feeds bits the hash shifts out)
+            const int q = (i >> 4) & 63, s2 = i & 15;
+            const uint32_t wa = (uint32_t)__shfl((int)word, q, 64), wb = (uint32_t)__shfl((int)word, (q + 1) & 63, 64);
+            if (i >= nk) continue;
+            uint32_t x = s2 == 0 ? wa : ((wa << (2 * s2)) | (wb >> (32 - 2 * s2)));
+            x = shift == 32 ? 0u : (x >> shift);
+            x ^= (x >> 1) & 0x55555555u;
+            const uint32_t h = mix32(x);
+            kmin = min(kmin, h);
+            const uint32_t occ = e.pos_bits ? (rd << e.pos_bits) | (uint32_t)i : (uint32_t)(g0 + i);
+            keys[g0 + i] = ((uint64_t)h << 32) | (uint64_t)occ;
+            if (e.occ_rl) e.occ_rl[g0 + i] = make_uint2(rd, lr[i]);
+        }
+        if (e.rkey) {
+            for (int off = 32; off > 0; off >>= 1) kmin = min(kmin, (uint32_t)__shfl_xor(kmin, off, 64));
+            if (lane == 0) { e.rkey[rd] = kmin; e.rord[rd] = rd; }
+        }
+    }
+}
+
 static uint32_t grid_for_waves(uint64_t waves) {
     uint64_t blocks = (waves + 3) / 4;
     if (blocks > 8192) blocks = 8192;
@@ -125,6 +204,12 @@ hipError_t launch_kmer_emit(const DevReads &r, const EmitParams &p, uint64_t *ke
                             hipStream_t s) {
     if (r.n == 0) return hipSuccess;
     hipLaunchKernelGGL(kmer_emit_kernel, dim3(grid_for_waves(r.n)), dim3(256), 0, s, r, p, keys, vals);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_emit(const DevReads &r, const EmitParams &p, uint64_t *keys, hipStream_t s) {
+    if (r.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(pack_emit_kernel, dim3(grid_for_waves(r.n)), dim3(256), 0, s, r, p, keys);
     return hipGetLastError();
 }
 

@@ -232,6 +232,8 @@ struct DevAlignment {            // mirrors sa_alignment
 
 // ---- launchers (kernels/*.hip) ------------------------------------------
 hipError_t launch_pack_reads(const DevReads &r, hipStream_t s);
+// pack + emit in one pass (reads of <= 1,024 bases)
+hipError_t launch_pack_emit(const DevReads &r, const EmitParams &p, uint64_t *keys, hipStream_t s);
 hipError_t launch_kmer_emit(const DevReads &r, const EmitParams &p, uint64_t *keys, uint32_t *vals,
                             hipStream_t s);
 
