@@ -9,6 +9,15 @@ sys.path.insert(0, os.path.join(ROOT, "sequence-aligner_amd"))
 import bench  # noqa: E402  (synthetic workload helpers)
 import saoverlap as sao  # noqa: E402
 
+# optional: hold a device buffer of SPACER_GB before the first context, so
+# its arrays land elsewhere in VRAM (placement probe)
+spacer_gb = float(os.environ.get("SPACER_GB", "0"))
+if spacer_gb > 0:
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    sp = ctypes.c_void_p()
+    assert hip.hipMalloc(ctypes.byref(sp), ctypes.c_size_t(int(spacer_gb * (1 << 30)))) == 0
+    print("spacer %.1f GB at 0x%x" % (spacer_gb, sp.value), flush=True)
 n, L = 100000, 500
 bases, offsets = bench.synth_workload(n, L, n * L // 20, 0.5, seed=1)
 keep = []
