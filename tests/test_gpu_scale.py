@@ -163,3 +163,21 @@ def test_bench_workload_sharded_matches_single(shards):
     np.testing.assert_array_equal(t2, trail)
     np.testing.assert_array_equal(c2, count)
     assert sh.ovl() == ovl
+
+
+@pytest.mark.parametrize("min_len", [None, 300])
+def test_per_read_regions_match_shared_regions(min_len):
+    """Dispatched pairs written into per-read regions (one scan + one copy, no
+    sort; wide ids, keep_pairs off) equal the shared-region path's dispatch
+    (every distinct pair kept, radix-sorted), for uniform and mixed lengths."""
+    b, o = bench.synth_workload(20000, 500, 500000, 0.5, seed=3, min_len=min_len)
+    out = []
+    for kp in (False, True):
+        ov = sao.Overlapper(kmer_size=15, id_mode=sao.SA_IDS_WIDE, keep_pairs=kp)
+        ov.add_packed(b.tobytes(), o)
+        ov.build()
+        out.append([np.array(x) for x in ov.dispatch()])
+        ov.close()
+    assert len(out[0][0]) > 10000
+    for x, y in zip(*out):
+        np.testing.assert_array_equal(x, y)
