@@ -21,6 +21,11 @@ if spacer_gb > 0:
 n, L = 100000, 500
 bases, offsets = bench.synth_workload(n, L, n * L // 20, 0.5, seed=1)
 keep = []
+# optional: DUMMY_CTX=1 creates one context (its streams) that never builds
+# before the measured ones (queue probe)
+if os.environ.get("DUMMY_CTX") == "1":
+    keep.append(sao.Overlapper(timing=True, kmer_size=15, id_mode=sao.SA_IDS_WIDE))
+    print("dummy context", flush=True)
 for i in range(int(sys.argv[1]) if len(sys.argv) > 1 else 6):
     ov = sao.Overlapper(timing=True, kmer_size=15, id_mode=sao.SA_IDS_WIDE)
     ov.add_packed(bases.tobytes(), offsets)
