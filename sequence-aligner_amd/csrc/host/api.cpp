@@ -852,7 +852,8 @@ int device_build(sa_ctx *c, bool readback) {
     // dispatched pairs straight into per-read regions (pair_stage) when the
     // regions stay within 4 GB: the lead-descending order is then a scan and
     // a copy instead of a 34-bit radix sort
-    const bool per_read_ok = !emit_all && (uint64_t)nr * PC_RREG * sizeof(uint2) <= (4ull << 30);
+    const bool per_read_ok = !emit_all && (uint64_t)nr * PC_RREG * sizeof(uint2) <= (4ull << 30) &&
+                             !(c->pr_off_gen == c->reads_gen && c->pr_off_k == c->set.kmer_size);
     bool per_read = per_read_ok;
     uint64_t np_ub = 0;
     rc = pair_stage(c, E, PI, strict, emit_all, read_order, nr, cnt, np, cap_s, nullptr, 0,
@@ -867,6 +868,10 @@ int device_build(sa_ctx *c, bool readback) {
         rc = pair_stage(c, E, PI, strict, emit_all, read_order, nr, cnt, np, cap_s, nullptr, 0, nullptr, nullptr,
                         &per_read, &np_ub);
         if (rc) return rc;
+    }
+    if (per_read_ok && !per_read) {  // overflowed: remember it for this read set
+        c->pr_off_gen = c->reads_gen;
+        c->pr_off_k = c->set.kmer_size;
     }
 
     // ---- ordering --------------------------------------------------------

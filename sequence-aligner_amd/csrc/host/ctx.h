@@ -66,6 +66,11 @@ struct sa_ctx {
     // pinned host copy of the device counters: each build's readbacks are one
     // DMA each (a pageable copy stages through a driver buffer)
     sa::Counters *hcnt = nullptr;
+    // per-read pair regions overflowed for this read set and k (a read with
+    // more than 192 partners): later builds skip the mode instead of paying
+    // the re-run of the first pass every time
+    uint64_t pr_off_gen = ~0ull;
+    int pr_off_k = 0;
     std::string err;
     // reads (host)
     std::vector<char> bases;
