@@ -93,16 +93,38 @@ def synth_workload(n_reads, read_len, genome_len, gc, seed, shard=0, min_len=Non
     return out, offsets
 
 
-def pmc_summary():
-    """Per-kernel counter averages of the newest committed PMC summary
-    (profiles/<round>/pmc_summary*.csv, written by tools/pmc_summary.py from
-    separate rocprofv3 --pmc passes of this bench, tools_profile.sh)."""
+DEFAULT_WORKLOAD = "n100000_L500_k15"
+
+
+def workload_tag(reads, read_len, min_len, k, gc=0.50, shards=1):
+    """Key of a PMC summary: the workload its rocprofv3 passes ran (reads, read
+    length(s), k, and GC / virtual shards when not the default)."""
+    t = "n%d_L%s_k%d" % (reads, "%d" % read_len if min_len is None else "%d-%d" % (min_len, read_len), k)
+    if abs(gc - 0.50) > 1e-9:
+        t += "_gc%g" % gc
+    if shards > 1:
+        t += "_s%d" % shards
+    return t
+
+
+def pmc_summary(tag):
+    """Per-kernel counter averages of the newest committed PMC summary of THIS
+    workload: profiles/<round>/pmc_summary*__<tag>.csv (tools_profile.sh /
+    tools_slice_prof.sh write them from separate rocprofv3 --pmc passes of this
+    bench).  Summaries without a tag are the default bench workload's
+    (rounds 1-2).  No summary of the workload -> ({}, None): the traffic and
+    VALU fields are then null rather than another workload's counters."""
     import csv
     import glob
 
     def natural(path):  # r02 after r01, pmc_summary_v9 < pmc_summary_v10
         return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", path)]
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary*.csv")), key=natural)
+
+    def tag_of(path):
+        base = os.path.basename(path)[:-4]
+        return base.split("__", 1)[1] if "__" in base else DEFAULT_WORKLOAD
+    files = sorted((f for f in glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary*.csv")) if tag_of(f) == tag),
+                   key=natural)
     if not files:
         return {}, None
     with open(files[-1]) as f:
@@ -246,6 +268,7 @@ def main():
     if mode in ("process", "virtual"):  # one shard's reads (the per-GPU byte model)
         offsets = np.concatenate([[0], np.cumsum(synth_lengths(args.reads, args.len, args.min_len, 1, 0))])
     build_step = ov.device_build
+    tag = workload_tag(args.reads, args.len, args.min_len, args.k, args.gc, args.shards if mode == "virtual" else 1)
 
     def barrier():
         if dist is not None:
@@ -271,10 +294,22 @@ def main():
 
     # ---- hash stage (configs[1]) ------------------------------------------
     note("inputs ready (%d reads)" % (len(offsets) - 1))
+    ov.sync()
+    t0 = time.perf_counter()
     build_step()  # allocations happen here, outside the timed region
+    ov.sync()
+    t_first = max_over_ranks(time.perf_counter() - t0)
     note("first build done")
-    for _ in range(args.warmup):
+    # the first build after the allocations: what a single CLI run pays
+    # (nothing is remembered between builds of one read set), then warm-up
+    t_second = None
+    for i in range(args.warmup):
+        ov.sync()
+        t0 = time.perf_counter()
         build_step()
+        ov.sync()
+        if i == 0:
+            t_second = max_over_ranks(time.perf_counter() - t0)
     ov.reset_stage_times()
     xb0 = ov.exchanged_bytes()
     barrier()
@@ -347,7 +382,7 @@ def main():
     pairs_g = st["pairs"] / P_here
     bases_g = float(offsets[-1])
     step_bytes = bases_g / 4.0 + 32.0 * kmers_g + 16.0 * pairs_g
-    rows, pmc_src = pmc_summary()
+    rows, pmc_src = pmc_summary(tag)
     ms_step = t_build / args.steps * 1e3
 
     def roof(bytes_, ms, kernels, name):
@@ -398,12 +433,15 @@ def main():
     if valu is not None and mix and all(m in mix for _, m in kern):
         cyc = sum(v * mix[m]["avg_cycles_per_valu"] for v, (_, m) in zip(valu_k, kern)) / valu
         mix_peak = 1024 * 64 * 2.4e9 / cyc / 1e12
+    # frac leads with the nominal gfx950 VALU peak (2 cycles per wave64 op); the
+    # mix-weighted peak (measured issue costs of the kernels' own instruction
+    # mix) is kept beside it
     roofline_align = {"bound": "valu", "unit": "T lane-ops/s",
-                      "peak": round(mix_peak, 1) if mix_peak else None,
+                      "peak": round(VALU_PEAK, 1),
                       "achieved": round(valu_ach, 2) if valu_ach is not None else None,
-                      "frac": round(valu_ach / mix_peak, 4) if valu_ach is not None and mix_peak else None,
-                      "peak_nominal_2_cycles": round(VALU_PEAK, 1),
-                      "frac_nominal": round(valu_ach / VALU_PEAK, 4) if valu_ach is not None else None,
+                      "frac": round(valu_ach / VALU_PEAK, 4) if valu_ach is not None else None,
+                      "peak_mix_weighted": round(mix_peak, 1) if mix_peak else None,
+                      "frac_mix_weighted": round(valu_ach / mix_peak, 4) if valu_ach is not None and mix_peak else None,
                       "mix_source": mix_src,
                       "kernel": "dovetail_p1x2 + dovetail_p2tbx2 (+ phase-2 pair regrouping sort)",
                       "gcups": round(cells_g / (al_ms * 1e-3) / 1e9, 1) if al_ms else None,
@@ -517,6 +555,8 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 3),
+            "first_build_ms": {"incl_allocation": round(t_first * 1e3, 3),
+                               "second": round(t_second * 1e3, 3) if t_second is not None else None},
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -527,7 +567,7 @@ def main():
                                        "%d" % args.len if args.min_len is None else
                                        "%d-%d" % (args.min_len, args.len)), args.k),
                        "reads_per_gpu": args.reads, "read_len": args.len, "min_len": args.min_len, "k": args.k,
-                       "genome_bp_per_gpu": G, "ids": "wide",
+                       "genome_bp_per_gpu": G, "ids": "wide", "pmc_key": tag,
                        "parallelism": {"rank": "rccl-a2a, one process per GPU", "process":
                                        "rccl-a2a, one process over %d devices" % n_gpus,
                                        "virtual": "%d virtual shards on one GPU" % args.shards,

@@ -170,8 +170,14 @@ typedef struct sa_stats {
     uint64_t ovl_records;      /* valid overlaps */
     uint64_t dp_cells;         /* DP cells evaluated (phase 1 + phase 2) */
     int32_t id_mode;           /* resolved mode (STRICT or WIDE) */
-    int32_t reserved;
+    int32_t flags;             /* SA_STATS_* bits of the last build (was `reserved`, always 0) */
 } sa_stats;
+/* the build kept each read's dispatched pairs in its own region (wide ids,
+ * dispatched pairs only): the lead-descending order is a scan + copy */
+#define SA_STATS_PER_READ_REGIONS 1
+/* some reads had more distinct partners than the first pass's table: they were
+ * recounted by the larger tiers (KmerTable.scala:85-149 semantics unchanged) */
+#define SA_STATS_RECOUNTED 2
 int sa_get_stats(const sa_ctx *ctx, sa_stats *out);
 
 /* Per-stage device time accumulated since the last reset (SA_OPT_TIMING). */

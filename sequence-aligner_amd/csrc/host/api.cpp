@@ -521,8 +521,10 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
     // per_read (in: allowed; out: used): the first pass writes each read's
     // dispatched pairs, trail-ascending, into a fixed region of PC_RREG slots
     // (wide ids, dispatched pairs only, one device); a read whose table
-    // overflows needs the recount tiers, so the pass is then re-run in the
-    // shared-region mode.  distinct_ub: distinct pairs counted (>= dispatched)
+    // overflows is recounted by the tiers below into the shared regions (np
+    // entries), and only those reads' pairs are sorted afterwards (device_build).
+    // distinct_ub: an upper bound of the dispatched pairs (first-pass distinct
+    // pairs + the tiers' kept pairs)
     // abort_flag (device): the first pass exits when it is set (big partitions
     // still to build, bucket_stage phase 1); *aborted then tells the caller
     // ---- pair counting -------------------------------------------------
@@ -603,17 +605,13 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
             return SA_OK;
         }
         P.abort = nullptr;
-        if (P.per_read) {
-            if (ovn == 0) {
-                *per_read = true;
-                if (distinct_ub) *distinct_ub = shard_sum(dist_h);
-                np = 0;
-                cap_s_out = cap_s;
-                return SA_OK;
-            }
-            P.per_read = 0;  // overflowed reads: count again in the shared regions
-            --attempt;
-            continue;
+        const uint64_t first_distinct = shard_sum(dist_h);
+        if (P.per_read && ovn == 0) {
+            *per_read = true;
+            if (distinct_ub) *distinct_ub = first_distinct;
+            np = 0;
+            cap_s_out = cap_s;
+            return SA_OK;
         }
         // Reads whose 256-slot table overflowed (> 192 partners) are recounted
         // one per block in bigger tables: 2,048 slots unless their partner count
@@ -647,6 +645,7 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
             HIPCHK(hipMemcpy(tl, items.data(), items.size() * 4, hipMemcpyHostToDevice));
             PairParams PT = P;
             PT.abort = nullptr;
+            PT.per_read = 0;  // the tiers emit into the shared regions
             PT.table = table;
             PT.split = split;
             PT.coded = 1;
@@ -691,7 +690,15 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
         if (!failed.empty() && cur_max() <= cap_s)
             return fail(c, SA_E_OVERFLOW, strict ? "a read has more than 98,304 distinct partners"
                                                  : "a read has more than 786,432 distinct partners");
-        if (cur_max() <= cap_s) break;
+        if (cur_max() <= cap_s) {
+            if (P.per_read) {  // regions kept; the recounted reads' pairs are in the shared regions
+                *per_read = true;
+                uint64_t ns = 0;
+                for (auto v : cur) ns += v;
+                if (distinct_ub) *distinct_ub = first_distinct + ns;
+            }
+            break;
+        }
         cap_s = cur_max() + cur_max() / 4 + 1024;  // grow and recount
         c->pair_cap = cap_s * NSHARD;
         if (attempt == 3) return fail(c, SA_E_OVERFLOW, "pair output did not fit");
@@ -851,9 +858,8 @@ int device_build(sa_ctx *c, bool readback) {
     const bool emit_all = strict || c->keep_pairs;
     // dispatched pairs straight into per-read regions (pair_stage) when the
     // regions stay within 4 GB: the lead-descending order is then a scan and
-    // a copy instead of a 34-bit radix sort
-    const bool per_read_ok = !emit_all && (uint64_t)nr * PC_RREG * sizeof(uint2) <= (4ull << 30) &&
-                             !(c->pr_off_gen == c->reads_gen && c->pr_off_k == c->set.kmer_size);
+    // a copy instead of a 34-bit radix sort (of the recounted reads' pairs only)
+    const bool per_read_ok = !emit_all && (uint64_t)nr * PC_RREG * sizeof(uint2) <= (4ull << 30);
     bool per_read = per_read_ok;
     uint64_t np_ub = 0;
     rc = pair_stage(c, E, PI, strict, emit_all, read_order, nr, cnt, np, cap_s, nullptr, 0,
@@ -869,27 +875,55 @@ int device_build(sa_ctx *c, bool readback) {
                         &per_read, &np_ub);
         if (rc) return rc;
     }
-    if (per_read_ok && !per_read) {  // overflowed: remember it for this read set
-        c->pr_off_gen = c->reads_gen;
-        c->pr_off_k = c->set.kmer_size;
-    }
+    c->recounted = per_read ? np : 0;
+    c->used_per_read = per_read;
 
     // ---- ordering --------------------------------------------------------
     int32_t *dlead, *dtrail, *dcount;
+    uint64_t *ok, *ok2; uint32_t *ov, *ov2; uint8_t *otmp;
     if (per_read) {
         uint32_t *rex; uint8_t *stmp2;
         ENSURE(c->d_lead, np_ub, &dlead);
         ENSURE(c->d_trail, np_ub, &dtrail);
         ENSURE(c->d_count, np_ub, &dcount);
         ENSURE(c->d_rex, (uint64_t)nr + 1, &rex);
-        ENSURE(c->d_osort, scan_temp_bytes(nr), &stmp2);
-        const uint32_t *rcnt = (const uint32_t *)c->d_rcnt.p;
+        uint32_t *rcnt = (uint32_t *)c->d_rcnt.p;
         StageScope st(c, SA_STAGE_ORDER);
+        // reads the tiers recounted (np pairs in the shared regions, their
+        // regions empty): those pairs sorted lead-descending / trail-ascending,
+        // each such read's segment start into rsh[read] (+1) and its length
+        // into rcnt[read]; the copy then takes those reads from the segments
+        const int32_t *sl = nullptr, *stl = nullptr, *scn = nullptr;
+        uint32_t *rsh = nullptr;
+        if (np) {
+            int32_t *shl, *sht, *shc;
+            ENSURE(c->d_okeys, np, &ok);
+            ENSURE(c->d_okeys2, np, &ok2);
+            ENSURE(c->d_ovals, np, &ov);
+            ENSURE(c->d_ovals2, np, &ov2);
+            ENSURE(c->d_osort, std::max(radix_sort_temp_bytes(np), scan_temp_bytes(nr)), &otmp);
+            ENSURE(c->d_shl, np, &shl);
+            ENSURE(c->d_sht, np, &sht);
+            ENSURE(c->d_shc, np, &shc);
+            ENSURE(c->d_rsh, nr, &rsh);
+            const int idb = bits_for(nr ? nr - 1 : 0);
+            HIPCHK(launch_make_order_keys((const uint32_t *)c->d_pf.p, (const uint32_t *)c->d_ps.p, nullptr,
+                                          cnt->cursor, cap_s, 0, idb, ok, ov, cnt->shard_off, c->stream));
+            HIPCHK(radix_sort(&ok, &ov, &ok2, &ov2, np, 0, 2 * idb, otmp, c->stream));
+            HIPCHK(launch_gather_pairs(ov, np, (const uint32_t *)c->d_pf.p, (const uint32_t *)c->d_ps.p,
+                                       (const uint32_t *)c->d_pc.p, shl, sht, shc, c->stream));
+            HIPCHK(hipMemsetAsync(rsh, 0, (size_t)nr * 4, c->stream));
+            HIPCHK(launch_mark_segments(shl, np, rsh, rcnt, c->stream));
+            sl = shl; stl = sht; scn = shc;
+            stmp2 = otmp;
+        } else {
+            ENSURE(c->d_osort, scan_temp_bytes(nr), &stmp2);
+        }
+        (void)sl;
         HIPCHK(exclusive_scan_u32(rcnt, rex, nr, &cnt->rtotal, stmp2, c->stream));
-        HIPCHK(launch_copy_read_regions((const uint2 *)c->d_rreg.p, rcnt, rex, &cnt->rtotal, nr, dlead, dtrail,
-                                        dcount, c->stream));
+        HIPCHK(launch_copy_read_regions((const uint2 *)c->d_rreg.p, rcnt, rex, &cnt->rtotal, nr, rsh, stl, scn,
+                                        dlead, dtrail, dcount, c->stream));
     }
-    uint64_t *ok, *ok2; uint32_t *ov, *ov2; uint8_t *otmp;
     if (!per_read) {
         ENSURE(c->d_okeys, np, &ok);
         ENSURE(c->d_okeys2, np, &ok2);
@@ -924,6 +958,7 @@ int device_build(sa_ctx *c, bool readback) {
     c->stats.role_pairs = shard_sum(hc.role_pairs);
     c->stats.pairs = shard_sum(hc.distinct);
     c->stats.id_mode = c->mode;
+    c->stats.flags = (per_read ? SA_STATS_PER_READ_REGIONS : 0) | (hc.overflow_n || c->recounted ? SA_STATS_RECOUNTED : 0);
 
     c->lead.clear(); c->trail.clear(); c->count.clear();
     c->pfst.clear(); c->psnd.clear(); c->pcnt.clear();
@@ -1266,7 +1301,8 @@ void sa_ctx_destroy(sa_ctx *c) {
                     &c->d_srec, &c->d_bnmd, &c->d_ishead, &c->d_bnst2, &c->d_tmd, &c->d_ted, &c->d_tmdi,
                     &c->d_tedi, &c->d_xrec, &c->d_tier, &c->d_ovlrp, &c->d_meta, &c->d_items, &c->d_bigtot, &c->d_hk0, &c->d_hk1, &c->d_hflag,
                     &c->d_hidx, &c->d_hpos, &c->d_htmp, &c->d_hist, &c->d_hovf, &c->d_hsmall,
-                    &c->d_ltb, &c->d_lmax, &c->d_rreg, &c->d_rcnt, &c->d_rex};
+                    &c->d_ltb, &c->d_lmax, &c->d_rreg, &c->d_rcnt, &c->d_rex,
+                    &c->d_shl, &c->d_sht, &c->d_shc, &c->d_rsh};
     for (DBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto &p : c->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }

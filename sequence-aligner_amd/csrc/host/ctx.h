@@ -66,11 +66,6 @@ struct sa_ctx {
     // pinned host copy of the device counters: each build's readbacks are one
     // DMA each (a pageable copy stages through a driver buffer)
     sa::Counters *hcnt = nullptr;
-    // per-read pair regions overflowed for this read set and k (a read with
-    // more than 192 partners): later builds skip the mode instead of paying
-    // the re-run of the first pass every time
-    uint64_t pr_off_gen = ~0ull;
-    int pr_off_k = 0;
     std::string err;
     // reads (host)
     std::vector<char> bases;
@@ -104,6 +99,11 @@ struct sa_ctx {
     DBuf d_lead, d_trail, d_count, d_aln, d_p1, d_tb, d_ltb, d_lmax;
     DBuf d_rkey, d_rkey2, d_rord, d_rord2, d_rtmp;
     DBuf d_rreg, d_rcnt, d_rex;  // per-read pair regions, counts, their exclusive scan
+    // per-read mode: the recounted reads' pairs sorted (lead, trail, count) and
+    // each such read's segment start + 1 (0: the read's pairs are in its region)
+    DBuf d_shl, d_sht, d_shc, d_rsh;
+    uint64_t recounted = 0;      // last build: dispatched pairs of reads recounted by the tiers (per-read mode)
+    bool used_per_read = false;  // last build used the per-read regions
     uint64_t pair_cap = 0;
     uint64_t n_disp = 0;
     // distributed mode (sa_dist_*): this rank's slice of a global read set

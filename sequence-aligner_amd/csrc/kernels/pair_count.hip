@@ -273,7 +273,7 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
     if (tid == 0 && !S.overflow) atomicAdd(&o.distinct[shard], (unsigned long long)S.fill);
     if (S.overflow) {  // recounted by the next tier: this read's class only
         if (tid == 0) {
-            if (p.per_read) o.rcnt[a] = 0;  // (the host re-runs the pass in region mode)
+            if (p.per_read) o.rcnt[a] = 0;  // (the recount tiers emit its pairs into the shared regions)
             const uint32_t at = atomicAdd(o.overflow_n, 1u);
             o.overflow_list[at] = (a << 6) | residue;
             // its distinct partners, extrapolated from the fill rate (FILL_MAX
@@ -672,14 +672,26 @@ __global__ void gather_pairs_kernel(const uint32_t *perm, uint64_t n, const uint
 }
 
 // one wave per read: its region's entries to their place in the lead-descending
-// dispatch list, offset = (sum of the counts of reads above it) = total - ex - cnt
+// dispatch list, offset = (sum of the counts of reads above it) = total - ex - cnt;
+// a read the recount tiers handled (rsh[a] != 0) copies its segment of the
+// sorted shared list instead
 __global__ void copy_read_regions_kernel(const uint2 *rreg, const uint32_t *rcnt, const uint32_t *ex,
-                                         const uint32_t *total, uint32_t n_reads, int32_t *lead, int32_t *trail,
-                                         int32_t *count) {
+                                         const uint32_t *total, uint32_t n_reads, const uint32_t *rsh,
+                                         const int32_t *sh_trail, const int32_t *sh_count, int32_t *lead,
+                                         int32_t *trail, int32_t *count) {
     const uint32_t a = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (a >= n_reads) return;
     const uint32_t m = rcnt[a];
     const uint32_t off = *total - ex[a] - m;
+    const uint32_t h = rsh ? rsh[a] : 0u;
+    if (h) {
+        for (uint32_t j = threadIdx.x & 63u; j < m; j += 64) {
+            lead[off + j] = (int32_t)a + 1;
+            trail[off + j] = sh_trail[h - 1 + j];  // (already 1-based)
+            count[off + j] = sh_count[h - 1 + j];
+        }
+        return;
+    }
     for (uint32_t j = threadIdx.x & 63u; j < m; j += 64) {
         const uint2 v = rreg[(uint64_t)a * PC_RREG + j];
         lead[off + j] = (int32_t)a + 1;  // reference ids are 1-based
@@ -689,11 +701,32 @@ __global__ void copy_read_regions_kernel(const uint2 *rreg, const uint32_t *rcnt
 }
 
 hipError_t launch_copy_read_regions(const uint2 *rreg, const uint32_t *rcnt, const uint32_t *ex,
-                                    const uint32_t *total, uint32_t n_reads, int32_t *lead, int32_t *trail,
+                                    const uint32_t *total, uint32_t n_reads, const uint32_t *rsh,
+                                    const int32_t *sh_trail, const int32_t *sh_count, int32_t *lead, int32_t *trail,
                                     int32_t *count, hipStream_t s) {
     if (!n_reads) return hipSuccess;
     hipLaunchKernelGGL(copy_read_regions_kernel, dim3((n_reads + 3) / 4), dim3(256), 0, s, rreg, rcnt, ex, total,
-                       n_reads, lead, trail, count);
+                       n_reads, rsh, sh_trail, sh_count, lead, trail, count);
+    return hipGetLastError();
+}
+
+// segment heads first (rsh = 1 + start), then the tails read them (rcnt = length)
+__global__ void mark_heads_kernel(const int32_t *lead, uint64_t n, uint32_t *rsh) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (i == 0 || lead[i - 1] != lead[i]) rsh[lead[i] - 1] = (uint32_t)i + 1u;
+}
+__global__ void mark_tails_kernel(const int32_t *lead, uint64_t n, const uint32_t *rsh, uint32_t *rcnt) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (i + 1 == n || lead[i + 1] != lead[i]) rcnt[lead[i] - 1] = (uint32_t)i + 2u - rsh[lead[i] - 1];
+}
+
+hipError_t launch_mark_segments(const int32_t *lead, uint64_t n, uint32_t *rsh, uint32_t *rcnt, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const dim3 grid((uint32_t)((n + 255) / 256));
+    hipLaunchKernelGGL(mark_heads_kernel, grid, dim3(256), 0, s, lead, n, rsh);
+    hipLaunchKernelGGL(mark_tails_kernel, grid, dim3(256), 0, s, lead, n, (const uint32_t *)rsh, rcnt);
     return hipGetLastError();
 }
 

@@ -330,10 +330,16 @@ hipError_t launch_make_order_keys(const uint32_t *fst, const uint32_t *snd, cons
                                   int idbits, uint64_t *keys, uint32_t *vals, uint32_t *shard_off,
                                   hipStream_t s, const uint32_t *starts = nullptr, uint32_t P = 0);
 // per-read mode: the dispatch list (lead descending, trail ascending) from the
-// per-read regions; ex = exclusive scan of rcnt, total = its sum
+// per-read regions; ex = exclusive scan of rcnt, total = its sum.  Reads the
+// recount tiers handled take their pairs from the sorted shared list instead:
+// rsh[read] = 1 + its segment's start in (sh_trail, sh_count) (0: region)
 hipError_t launch_copy_read_regions(const uint2 *rreg, const uint32_t *rcnt, const uint32_t *ex,
-                                    const uint32_t *total, uint32_t n_reads, int32_t *lead, int32_t *trail,
+                                    const uint32_t *total, uint32_t n_reads, const uint32_t *rsh,
+                                    const int32_t *sh_trail, const int32_t *sh_count, int32_t *lead, int32_t *trail,
                                     int32_t *count, hipStream_t s);
+// segments of a lead-descending (1-based) lead list: rsh[lead - 1] = 1 + start,
+// rcnt[lead - 1] = length
+hipError_t launch_mark_segments(const int32_t *lead, uint64_t n, uint32_t *rsh, uint32_t *rcnt, hipStream_t s);
 hipError_t launch_gather_pairs(const uint32_t *perm, uint64_t n, const uint32_t *fst, const uint32_t *snd,
                                const uint32_t *cnt, int32_t *lead, int32_t *trail, int32_t *count,
                                hipStream_t s);

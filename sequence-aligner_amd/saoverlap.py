@@ -24,6 +24,7 @@ LIB_PATH = os.environ.get("SA_OVERLAP_LIB") or os.path.join(HERE, "build", "libs
 SA_IDS_AUTO, SA_IDS_STRICT, SA_IDS_WIDE = 0, 1, 2
 SA_OPT_KEEP_PAIRS, SA_OPT_TIMING, SA_OPT_ALIGN_KERNEL, SA_OPT_ALIGNER, SA_OPT_LOCAL_BATCH_MB = 1, 2, 3, 4, 5
 SA_ALIGNER_LINEAR, SA_ALIGNER_QUADRATIC = 0, 1   # --linear-align / --quadratic-align
+SA_STATS_PER_READ_REGIONS, SA_STATS_RECOUNTED = 1, 2    # sa_stats.flags bits of the last build
 ALIGN_AUTO, ALIGN_GROUP, ALIGN_LANE, ALIGN_LANE_SUMMARY = 0, 1, 2, 3
 STAGES = ("pack", "emit", "sort", "buckets", "pairs", "order", "align", "exchange")
 ERRORS = {-1: "SA_E_ARG", -2: "SA_E_INPUT", -3: "SA_E_NON_ACGT", -4: "SA_E_ID_RANGE", -5: "SA_E_SHORT_READ",
@@ -52,7 +53,7 @@ class Settings(C.Structure):
 class Stats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("kmers", "buckets", "role_pairs", "pairs", "dispatched", "aligned",
                                            "ovl_records", "dp_cells")] + [("id_mode", C.c_int32),
-                                                                          ("reserved", C.c_int32)]
+                                                                          ("flags", C.c_int32)]
 
 
 ALIGN_FIELDS = ("lead", "trail", "start_i", "start_j", "end_i", "end_j", "correct", "error", "ahg", "bhg",
@@ -287,7 +288,7 @@ class Overlapper:
     def stats(self):
         st = Stats()
         self._chk(lib().sa_get_stats(self.h, C.byref(st)))
-        return {f[0]: getattr(st, f[0]) for f in Stats._fields_ if f[0] != "reserved"}
+        return {f[0]: getattr(st, f[0]) for f in Stats._fields_}
 
     def stage_times(self):
         ms = (C.c_double * len(STAGES))()

@@ -138,6 +138,8 @@ def test_many_partner_reads_recount_tiers(oracle_mod, n_edge):
     np.testing.assert_array_equal(trail, r.trail)
     assert (lead <= n_mid).sum() == n_mid * n_edge  # every middle read leads every edge read
     assert ov.stats()["role_pairs"] > 3 * n_mid * n_edge
+    # the edge reads kept their per-read regions; only the middle reads were recounted
+    assert ov.stats()["flags"] & 3 == sao.SA_STATS_PER_READ_REGIONS | sao.SA_STATS_RECOUNTED
 
 
 @pytest.mark.parametrize("shards", [4, 8])
@@ -177,7 +179,43 @@ def test_per_read_regions_match_shared_regions(min_len):
         ov.add_packed(b.tobytes(), o)
         ov.build()
         out.append([np.array(x) for x in ov.dispatch()])
+        # the per-read mode really ran (and only without keep_pairs)
+        assert bool(ov.stats()["flags"] & sao.SA_STATS_PER_READ_REGIONS) == (not kp)
         ov.close()
     assert len(out[0][0]) > 10000
     for x, y in zip(*out):
         np.testing.assert_array_equal(x, y)
+
+
+def test_per_read_regions_with_recounted_reads_twice():
+    """A read set where some reads overflow the first pass's table (> 192
+    partners): 20k ordinary reads plus 1,200 reads sharing a motif (40 middle
+    reads x 1,160 edge reads, so each middle read has > 1,000 partners).  Only
+    the overflowed reads are recounted (their pairs sorted into the shared
+    list), the rest keep their per-read regions; built twice on one context,
+    both dispatches equal the keep_pairs (shared-region, sorted) path."""
+    b, o = bench.synth_workload(20000, 500, 500000, 0.5, seed=5)
+    reads = [b[int(o[i]):int(o[i + 1])].tobytes().decode() for i in range(len(o) - 1)]
+    rng = np.random.default_rng(7)
+    motif = "".join("ACGT"[x] for x in rng.integers(0, 4, 17))
+    for i in range(1200):
+        s_ = "".join("ACGT"[x] for x in rng.integers(0, 4, 120))
+        p_ = 55 if i < 40 else 5
+        reads.append(s_[:p_] + motif + s_[p_ + 17:])
+    st = dict(kmer_size=15, min_collisions=3, id_mode=sao.SA_IDS_WIDE)
+    ref = sao.Overlapper(keep_pairs=True, **st)
+    ref.add_reads(reads)
+    ref.build()
+    want = [np.array(x) for x in ref.dispatch()]
+    assert not ref.stats()["flags"] & sao.SA_STATS_PER_READ_REGIONS
+    ref.close()
+    ov = sao.Overlapper(**st)
+    ov.add_reads(reads)
+    for _ in range(2):
+        ov.build()
+        assert ov.stats()["flags"] & 3 == sao.SA_STATS_PER_READ_REGIONS | sao.SA_STATS_RECOUNTED
+        got = [np.array(x) for x in ov.dispatch()]
+        for x, y in zip(got, want):
+            np.testing.assert_array_equal(x, y)
+    assert len(want[0]) > 40 * 1000
+    ov.close()

@@ -85,7 +85,34 @@ static void run_w8(void *) { hipLaunchKernelGGL(stream_write<8>, grid_of(g.n), d
 static void run_w16(void *) { hipLaunchKernelGGL(stream_write<16>, grid_of(g.n), dim3(256), 0, 0, g.n, (Rec<16> *)g.out); }
 static void run_g4(void *) { hipLaunchKernelGGL(gather, grid_of(g.n), dim3(256), 0, 0, g.idx, g.n, g.src, g.sink); }
 
-int main() {
+int main(int argc, char **argv) {
+    // argv[1] = "big N": only the 8-byte scatter section at N items (round 3:
+    // does the per-store cost grow with the target array -- TLB reach -- at
+    // configs[3]'s per-GPU slice, N = 607.5M, 4.86 GB?)
+    if (argc > 2 && argv[1][0] == 'b') {
+        const uint64_t n = strtoull(argv[2], nullptr, 10);
+        uint32_t *idx, *sink;
+        void *out;
+        CHK(hipMalloc(&idx, n * 4));
+        CHK(hipMalloc(&out, 8 * n));
+        CHK(hipMalloc(&sink, 64));
+        CHK(hipMemset(out, 0, 8 * n));
+        g.idx = idx; g.n = n; g.out = out; g.sink = sink; g.src = (const uint32_t *)out;
+        const float w = time_it(run_w8, 0, 3);
+        printf("n=%llu coalesced write 8B: %.3f ms (%.2f ns/item x1000)\n", (unsigned long long)n, w, w * 1e3 / (n / 1e6));
+        hipLaunchKernelGGL(make_idx, grid_of(n), dim3(256), 0, 0, idx, n, n, 0u);
+        const float s = time_it(run_s8, 0, 3);
+        printf("scatter 8B over %.0f MB: %.3f ms (%.3f ms per 48.6M)\n", 8.0 * n / 1e6, s, s * 48.6e6 / n);
+        for (uint64_t win_mb : {2ull, 32ull, 256ull, 1024ull}) {
+            const uint32_t ws = (uint32_t)(win_mb * 1000000ull / 8);
+            if (ws >= n) continue;
+            hipLaunchKernelGGL(make_idx, grid_of(n), dim3(256), 0, 0, idx, n, n, ws);
+            const float t = time_it(run_s8, 0, 3);
+            printf("  windowed %4llu MB: %.3f ms (%.3f ms per 48.6M)\n", (unsigned long long)win_mb, t, t * 48.6e6 / n);
+        }
+        CHK(hipFree(idx)); CHK(hipFree(out)); CHK(hipFree(sink));
+        return 0;
+    }
     const uint64_t n = 48600000ull;  // k-mer occurrences at the bench shape
     uint32_t *idx, *sink;
     void *out;

@@ -2,7 +2,8 @@
 # Kernel statistics and PMC passes over a short bench run (one counter group per
 # pass, as MI355X_MICROARCH.md prescribes: FETCH_SIZE and WRITE_SIZE cannot
 # share a pass).  Outputs under gpurun_out/; copy the summaries worth keeping
-# into profiles/<round>/ (pmc_summary.csv is what bench.py's traffic fields read).
+# into profiles/<round>/ (pmc_summary*__<workload>.csv is what bench.py's
+# traffic / VALU fields read; the default bench workload is n100000_L500_k15).
 set -u
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
@@ -26,4 +27,4 @@ pass lds SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE
 # shape; one LDS pass over it gives that DP kernel's bank-conflict rate
 BENCH="$BENCH --align-kernel 1" pass lds_group SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE
 pass sq SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY
-python3 $R/tools/pmc_summary.py $R/gpurun_out $R/gpurun_out/pmc_summary.csv
+python3 $R/tools/pmc_summary.py $R/gpurun_out $R/gpurun_out/pmc_summary__n100000_L500_k15.csv
