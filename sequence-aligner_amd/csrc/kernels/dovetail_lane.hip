@@ -441,10 +441,11 @@ __device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t a, uint32_t b) { r
 // v_pk_* op, v_max/min, v_perm_b32, v_bfi_b32 and v_lshl_or_b32 in ~4.4.  So: plain u32
 // add/sub wherever no half can carry or borrow, and selects as v_bitop3_b32 (S0 ? S1 : S2 is
 // truth table 0xCA; the compiler would pick v_bfi_b32).
+// (the builtin, not inline asm: an asm statement bounds the scheduling region,
+// which left dependent packed ops back to back, each pair split by a hazard
+// s_nop -- 146 of them in the phase-2 row loop)
 __device__ __forceinline__ uint32_t bsel3(uint32_t m, uint32_t a, uint32_t b) {
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(r) : "v"(m), "v"(a), "v"(b));
-    return r;
+    return __builtin_amdgcn_bitop3_b32(m, a, b, 0xCA);
 }
 // a - b per half where a >= b in both halves (no borrow crosses)
 __device__ __forceinline__ u16x2 pk_dif(u16x2 a, u16x2 b) { return pk(upk(a) - upk(b)); }

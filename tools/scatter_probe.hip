@@ -45,6 +45,82 @@ __global__ void scatter(const uint32_t *idx, uint64_t n, Rec<B> *out) {
     out[idx[i]] = r;
 }
 
+__global__ void scatter_nt8(const uint32_t *idx, uint64_t n, uint64_t *out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    __builtin_nontemporal_store((uint64_t)i * 3u, out + idx[i]);
+}
+__global__ void scatter4(const uint32_t *idx, uint64_t n, uint32_t *out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[idx[i]] = (uint32_t)i;
+}
+
+// per-block cursor claims: lane b < nbins of every block adds 16 to cursor
+// (b, block % nshard) and keeps the old value (the staged-scatter design's
+// atomics: one claim per bin and partition)
+__global__ void claim_kernel(unsigned long long *cur, uint32_t nbins, uint32_t nshard, uint32_t *sink) {
+    const uint32_t b = threadIdx.x;
+    if (b < nbins) {
+        const unsigned long long old = atomicAdd(&cur[(uint64_t)b * nshard + blockIdx.x % nshard], 16ull);
+        if (old == 0xFFFFFFFFFFull) sink[0] = (uint32_t)old;
+    }
+}
+
+// Staged scatter (the round-3 bucket-build design): block b owns items
+// [b*ipb, (b+1)*ipb) (one partition), bins them by g >> wshift in LDS, claims
+// one run per bin from cursor (bin, b % ns), writes {g, value} there (region
+// capacity cap; overflow -> direct store); then stage_scatter walks the
+// regions bin-major so the stores in flight land in about one bin's span.
+__global__ void stage_kernel(const uint32_t *idx, uint64_t n, uint32_t ipb, int wshift, uint32_t nbins, uint32_t ns,
+                             uint64_t cap, unsigned long long *cur, uint32_t *sg, uint64_t *sv, uint64_t *out) {
+    __shared__ uint32_t cnt[256];
+    __shared__ uint64_t base[256];
+    const uint64_t b0 = (uint64_t)blockIdx.x * ipb;
+    if (threadIdx.x < nbins) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t gv[4], bn[4], rk[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint64_t i = b0 + threadIdx.x + j * 256;
+        bn[j] = 0xFFFFFFFFu;
+        if (threadIdx.x + j * 256 < ipb && i < n) {
+            gv[j] = idx[i];
+            bn[j] = gv[j] >> wshift;
+            rk[j] = atomicAdd(&cnt[bn[j]], 1u);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < nbins && cnt[threadIdx.x])
+        base[threadIdx.x] = atomicAdd(&cur[(uint64_t)threadIdx.x * ns + blockIdx.x % ns], (unsigned long long)cnt[threadIdx.x]);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (bn[j] == 0xFFFFFFFFu) continue;
+        const uint64_t pos = base[bn[j]] + rk[j];
+        const uint64_t v = (uint64_t)gv[j] * 3u;
+        if (pos < cap) {
+            const uint64_t at = ((uint64_t)bn[j] * ns + blockIdx.x % ns) * cap + pos;
+            sg[at] = gv[j];
+            sv[at] = v;
+        } else {
+            out[gv[j]] = v;
+        }
+    }
+}
+__global__ void stage_scatter(const unsigned long long *cur, uint32_t nregions, uint64_t cap, const uint32_t *sg,
+                              const uint64_t *sv, uint64_t *out) {
+    const uint64_t chunks = (cap + 1023) / 1024;
+    const uint64_t r = blockIdx.x / chunks, c = blockIdx.x % chunks;
+    if (r >= nregions) return;
+    const uint64_t m = min((uint64_t)cur[r], cap);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint64_t q = c * 1024 + j * 256 + threadIdx.x;
+        if (q < m) out[sg[r * cap + q]] = sv[r * cap + q];
+    }
+}
+
 template <int B>
 __global__ void stream_write(uint64_t n, Rec<B> *out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -83,12 +159,107 @@ static void run_s8(void *) { hipLaunchKernelGGL(scatter<8>, grid_of(g.n), dim3(2
 static void run_s16(void *) { hipLaunchKernelGGL(scatter<16>, grid_of(g.n), dim3(256), 0, 0, g.idx, g.n, (Rec<16> *)g.out); }
 static void run_w8(void *) { hipLaunchKernelGGL(stream_write<8>, grid_of(g.n), dim3(256), 0, 0, g.n, (Rec<8> *)g.out); }
 static void run_w16(void *) { hipLaunchKernelGGL(stream_write<16>, grid_of(g.n), dim3(256), 0, 0, g.n, (Rec<16> *)g.out); }
+static void run_nt8(void *) { hipLaunchKernelGGL(scatter_nt8, grid_of(g.n), dim3(256), 0, 0, g.idx, g.n, (uint64_t *)g.out); }
+static void run_s4(void *) { hipLaunchKernelGGL(scatter4, grid_of(g.n), dim3(256), 0, 0, g.idx, g.n, (uint32_t *)g.out); }
 static void run_g4(void *) { hipLaunchKernelGGL(gather, grid_of(g.n), dim3(256), 0, 0, g.idx, g.n, g.src, g.sink); }
 
 int main(int argc, char **argv) {
     // argv[1] = "big N": only the 8-byte scatter section at N items (round 3:
     // does the per-store cost grow with the target array -- TLB reach -- at
     // configs[3]'s per-GPU slice, N = 607.5M, 4.86 GB?)
+    // argv[1] = "stage N IPB WSHIFT NSHARD": direct vs staged scatter of N random
+    // targets (a permutation-like map into N 8-byte slots)
+    if (argc > 5 && argv[1][0] == 's' && argv[1][1] == 't') {
+        const uint64_t n = strtoull(argv[2], nullptr, 10);
+        const uint32_t ipb = (uint32_t)strtoul(argv[3], nullptr, 10);
+        const int wshift = atoi(argv[4]);
+        const uint32_t ns = (uint32_t)strtoul(argv[5], nullptr, 10);
+        const uint32_t nbins = (uint32_t)((n + (1ull << wshift) - 1) >> wshift);
+        const uint64_t per = ((1ull << wshift) + ns - 1) / ns;
+        const uint64_t cap = per + per / 50 + 1024;
+        uint32_t *idx, *sg;
+        uint64_t *out, *sv;
+        unsigned long long *cur;
+        CHK(hipMalloc(&idx, n * 4));
+        CHK(hipMalloc(&out, n * 8));
+        CHK(hipMalloc(&sg, (size_t)nbins * ns * cap * 4));
+        CHK(hipMalloc(&sv, (size_t)nbins * ns * cap * 8));
+        CHK(hipMalloc(&cur, (size_t)nbins * ns * 8));
+        hipLaunchKernelGGL(make_idx, grid_of(n), dim3(256), 0, 0, idx, n, n, 0u);
+        g.idx = idx; g.n = n; g.out = out;
+        const float d = time_it(run_s8, 0, 3);
+        hipEvent_t a, b, c;
+        CHK(hipEventCreate(&a)); CHK(hipEventCreate(&b)); CHK(hipEventCreate(&c));
+        const uint32_t nblk = (uint32_t)((n + ipb - 1) / ipb);
+        const uint32_t nreg = nbins * ns;
+        const uint32_t sgrid = (uint32_t)(nreg * ((cap + 1023) / 1024));
+        float t1 = 0, t2 = 0;
+        for (int rep = 0; rep < 4; ++rep) {
+            CHK(hipMemset(cur, 0, (size_t)nreg * 8));
+            CHK(hipEventRecord(a));
+            hipLaunchKernelGGL(stage_kernel, dim3(nblk), dim3(256), 0, 0, idx, n, ipb, wshift, nbins, ns, cap, cur, sg, sv,
+                               out);
+            CHK(hipEventRecord(b));
+            hipLaunchKernelGGL(stage_scatter, dim3(sgrid), dim3(256), 0, 0, cur, nreg, cap, sg, sv, out);
+            CHK(hipEventRecord(c));
+            CHK(hipEventSynchronize(c));
+            float x, y;
+            CHK(hipEventElapsedTime(&x, a, b));
+            CHK(hipEventElapsedTime(&y, b, c));
+            if (rep) { t1 += x; t2 += y; }
+        }
+        printf("n=%llu direct %.3f ms | staged (ipb %u, bins %u x %u shards, %.0f MB each): stage %.3f + scatter %.3f = %.3f ms\n",
+               (unsigned long long)n, d, ipb, nbins, ns, 8.0 * (1ull << wshift) / 1e6, t1 / 3, t2 / 3, (t1 + t2) / 3);
+        return 0;
+    }
+    // argv[1] = "atom NBLOCKS NBINS NSHARD"
+    if (argc > 4 && argv[1][0] == 'a') {
+        const uint32_t nb = (uint32_t)strtoul(argv[2], nullptr, 10), nbins = (uint32_t)strtoul(argv[3], nullptr, 10),
+                       ns = (uint32_t)strtoul(argv[4], nullptr, 10);
+        unsigned long long *cur;
+        uint32_t *sink;
+        CHK(hipMalloc(&cur, (size_t)nbins * ns * 8));
+        CHK(hipMalloc(&sink, 64));
+        CHK(hipMemset(cur, 0, (size_t)nbins * ns * 8));
+        hipEvent_t a, b;
+        CHK(hipEventCreate(&a)); CHK(hipEventCreate(&b));
+        hipLaunchKernelGGL(claim_kernel, dim3(nb), dim3(256), 0, 0, cur, nbins, ns, sink);
+        CHK(hipDeviceSynchronize());
+        CHK(hipEventRecord(a));
+        for (int r = 0; r < 3; ++r) hipLaunchKernelGGL(claim_kernel, dim3(nb), dim3(256), 0, 0, cur, nbins, ns, sink);
+        CHK(hipEventRecord(b));
+        CHK(hipEventSynchronize(b));
+        float ms = 0;
+        CHK(hipEventElapsedTime(&ms, a, b));
+        printf("claims: %u blocks x %u bins over %u shards: %.3f ms\n", nb, nbins, ns, ms / 3);
+        return 0;
+    }
+    // argv[1] = "span N SPAN_MB ALLOC_MB": N random 8-byte stores into the first
+    // SPAN_MB of an ALLOC_MB array (does the cost follow the items, the span
+    // they land in, or the allocation?)
+    if (argc > 4 && argv[1][0] == 's') {
+        const uint64_t n = strtoull(argv[2], nullptr, 10);
+        const uint64_t span = strtoull(argv[3], nullptr, 10) * 1000000ull / 8;
+        const uint64_t alloc = strtoull(argv[4], nullptr, 10) * 1000000ull;
+        uint32_t *idx, *sink;
+        void *out;
+        CHK(hipMalloc(&idx, n * 4));
+        CHK(hipMalloc(&out, alloc));
+        CHK(hipMalloc(&sink, 64));
+        CHK(hipMemset(out, 0, alloc));
+        g.idx = idx; g.n = n; g.out = out; g.sink = sink; g.src = (const uint32_t *)out;
+        hipLaunchKernelGGL(make_idx, grid_of(n), dim3(256), 0, 0, idx, n, span, 0u);
+        const float s = time_it(run_s8, 0, 3);
+        printf("n=%llu span %.0f MB alloc %.0f MB: %.3f ms (%.3f ms per 48.6M)\n", (unsigned long long)n,
+               8.0 * span / 1e6, alloc / 1e6, s, s * 48.6e6 / n);
+        const float s2 = time_it(run_nt8, 0, 3);
+        printf("   non-temporal 8B: %.3f ms (%.3f ms per 48.6M)\n", s2, s2 * 48.6e6 / n);
+        // the same slots as 4-byte words (a 4-byte record array of the same count: half the span)
+        const float s3 = time_it(run_s4, 0, 3);
+        printf("   4B words over %.0f MB: %.3f ms (%.3f ms per 48.6M)\n", 4.0 * span / 1e6, s3, s3 * 48.6e6 / n);
+        CHK(hipFree(idx)); CHK(hipFree(out)); CHK(hipFree(sink));
+        return 0;
+    }
     if (argc > 2 && argv[1][0] == 'b') {
         const uint64_t n = strtoull(argv[2], nullptr, 10);
         uint32_t *idx, *sink;
