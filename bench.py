@@ -469,6 +469,11 @@ def main():
         t0 = time.perf_counter()
         r = oracle.Run(packed=(b_s.tobytes(), o_s), settings=s, wide=True, skip_align=True)
         t_cpu = time.perf_counter() - t0
+        # the same hash stage on all of this job's cores (OpenMP restatement:
+        # per-thread PairData maps over hash bins, merged by lead; same pairs)
+        t0 = time.perf_counter()
+        r_mt = oracle.Run(packed=(b_s.tobytes(), o_s), settings=s, wide=True, skip_align=True, threads=cores_all)
+        t_cpu_mt = time.perf_counter() - t0
         # role pairs of the sample counted exactly as the GPU counts them
         ovs = sao.Overlapper(kmer_size=args.k, id_mode=sao.SA_IDS_WIDE)
         ovs.add_packed(b_s.tobytes(), o_s)
@@ -477,6 +482,8 @@ def main():
         lead_s, trail_s, _ = ovs.dispatch()
         assert np.array_equal(r.lead, lead_s) and np.array_equal(r.trail, trail_s), \
             "CPU/GPU dispatch mismatch on the baseline sample"
+        assert np.array_equal(r_mt.lead, lead_s) and np.array_equal(r_mt.trail, trail_s) and \
+            r_mt.role_pairs == rp_s, "all-core CPU / GPU hash stage mismatch on the baseline sample"
         # aligner: the same dispatch (first pairs of it), 1 thread and all threads,
         # each tuple checked against the GPU's
         ovs.align()
@@ -498,6 +505,11 @@ def main():
                          "(KmerTable.calcPairData + calcDispatchData restated in C, one thread: the reference's "
                          "KmerTable is single-writer), %.1f s; dispatch equal to the GPU's"
                          % (n_s, args.len, G_s, args.k, t_cpu),
+               "all_cores": {"value": round(rp_s / t_cpu_mt, 1), "cores": cores_all, "s": round(t_cpu_mt, 2),
+                             "sample": "the same sample and stage on %d OpenMP threads (this job's CPU share): "
+                                       "per-thread PairData maps over hash bins merged by lead "
+                                       "(oracle orc_run_wide_mt); dispatch and role pairs equal to the GPU's"
+                                       % cores_all},
                "cpu_model": cpu_model(), "nproc": os.cpu_count(),
                "align": {"unit": "aligned read-pairs/s", "kind": "port",
                          "value_1_thread": round(na1 / t_a1, 1), "value_all_threads": round(naa / t_aa, 1),

@@ -53,6 +53,7 @@ def lib():
         L.orc_num_reads.argtypes = [C.c_void_p]
         L.orc_num_reads.restype = C.c_uint32
         L.orc_run.argtypes = [C.c_void_p, P(Settings), C.c_int]
+        L.orc_run_wide_mt.argtypes = [C.c_void_p, P(Settings), C.c_int, P(C.c_uint64)]
         for fn in ("orc_num_kmers", "orc_num_buckets", "orc_num_pairs", "orc_num_dispatch"):
             getattr(L, fn).argtypes = [C.c_void_p]
             getattr(L, fn).restype = C.c_size_t
@@ -105,7 +106,10 @@ class Run:
     """Result of one calc-overlaps run of the oracle."""
 
     def __init__(self, reads=None, fasta=None, settings=None, wide=False, keep_kmers=False, skip_align=False,
-                 packed=None, quadratic=False):
+                 packed=None, quadratic=False, threads=None):
+        """threads (wide + skip_align only): the all-core hash stage
+        (orc_run_wide_mt) on that many OpenMP threads (0 = all); self.role_pairs
+        is then the role pairs it visited."""
         L = lib()
         h = C.c_void_p()
         if packed is not None:
@@ -125,8 +129,15 @@ class Run:
             raise OracleError(rc)
         self.settings = settings or default_settings()
         try:
-            rc = L.orc_run(h, C.byref(self.settings), (1 if wide else 0) | (2 if skip_align else 0) |
-                         (4 if quadratic else 0))
+            if threads is not None:
+                if not (wide and skip_align and not keep_kmers):
+                    raise ValueError("threads= runs the wide-id hash stage only")
+                rp = C.c_uint64(0)
+                rc = L.orc_run_wide_mt(h, C.byref(self.settings), int(threads), C.byref(rp))
+                self.role_pairs = int(rp.value)
+            else:
+                rc = L.orc_run(h, C.byref(self.settings), (1 if wide else 0) | (2 if skip_align else 0) |
+                             (4 if quadratic else 0))
             self.rc = rc
             self.n_reads = L.orc_num_reads(h)
             if keep_kmers:

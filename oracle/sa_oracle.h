@@ -81,6 +81,10 @@ uint32_t orc_num_reads(const orc_ctx *c);
  * `--quadratic-align` (generateLocalAlignmentSet, BioLibs.scala:267-368) instead
  * of the banded dovetail aligner. */
 int orc_run(orc_ctx *c, const orc_settings *s, int flags);
+/* Wide-id hash stage only (flags 1 | 2 of orc_run) on `threads` OpenMP threads
+ * (0 = all): same pairs / dispatch; role pairs visited -> *role_pairs.  The
+ * all-core CPU baseline of the hash stage (bench.py). */
+int orc_run_wide_mt(orc_ctx *c, const orc_settings *s, int threads, uint64_t *role_pairs);
 
 /* Results of orc_run (arrays owned by ctx, valid until destroy/next run). */
 size_t orc_num_kmers(const orc_ctx *c);

@@ -47,6 +47,23 @@ def test_small_random_matches_literal(oracle_mod):
         assert r.ovl.decode() == out
 
 
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_all_core_hash_stage_equals_single_thread(oracle_mod, threads):
+    """The all-core CPU baseline of the hash stage (orc_run_wide_mt: per-thread
+    PairData maps over hash bins, merged by lead) gives the single-threaded
+    restatement's PairData counts and wide dispatch exactly, for uniform and
+    mixed lengths (float32 cross-length loc comparisons)."""
+    for mixed, k in ((None, 15), ((60, 160), 12)):
+        reads = H.synth_reads(900, 160, 12000, gc=0.45, seed=11 + threads, mixed=mixed)
+        s = oracle_mod.default_settings(kmer_size=k, min_collisions=3)
+        r1 = oracle_mod.Run(reads=reads, settings=s, wide=True, skip_align=True)
+        r2 = oracle_mod.Run(reads=reads, settings=s, wide=True, skip_align=True, threads=threads)
+        assert len(r1.lead) > 100
+        for a in ("pair_fst", "pair_snd", "pair_cnt", "lead", "trail"):
+            np.testing.assert_array_equal(getattr(r1, a), getattr(r2, a))
+        assert r2.role_pairs > len(r1.pair_fst)
+
+
 def test_hoxd1_equals_default_matrix(oracle_mod):
     """amos/HOXD1.txt (readHOXD format) == defaultHOXD (BioLibs.scala:122-140)."""
     rows = [l.split(",") for l in open(os.path.join(GOLD, "HOXD1.txt")).read().strip().split("\n")[1:]]
