@@ -216,6 +216,8 @@ def main():
                     help="SA_OPT_ALIGN_KERNEL: 0 auto, 1 lane-group (LDS), 2 lane-per-pair")
     ap.add_argument("--replicas", action="store_true", help="torchrun: independent per-rank datasets, no exchange")
     ap.add_argument("--shards", type=int, default=1, help="virtual shards on one GPU (sharded path, device copies)")
+    ap.add_argument("--serial-shards", action="store_true",
+                    help="virtual shards: run the shards one after another (clean per-shard stage times)")
     ap.add_argument("--check-shards", type=int, default=0,
                     help="single mode: afterwards rebuild the same reads over S virtual shards and require the "
                          "identical dispatch (a size-independent parity property at full size)")
@@ -257,7 +259,7 @@ def main():
         ov.add_packed(bases.tobytes(), offsets)
     elif mode in ("process", "virtual"):
         P = n_gpus if mode == "process" else args.shards
-        ov = sao.Overlapper(gpus=n_gpus, shards=P, **common)
+        ov = sao.Overlapper(gpus=n_gpus, shards=P, serial_shards=args.serial_shards, **common)
         for r in range(P):  # the same reads the torchrun ranks would hold, in rank order
             b_r, o_r = synth_workload(args.reads, args.len, G * P, args.gc, seed=1, shard=r, min_len=args.min_len)
             ov.add_packed(b_r.tobytes(), o_r)

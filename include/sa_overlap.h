@@ -147,7 +147,9 @@ enum sa_option {
                                 a band or read does not fit it); 3 lane-per-pair with
                                 per-cell path summaries instead of stored codes */
     SA_OPT_ALIGNER = 4,      /* enum sa_aligner: which reference aligner sa_align runs */
-    SA_OPT_LOCAL_BATCH_MB = 5 /* quadratic aligner: MiB of traceback codes per launch (16384) */
+    SA_OPT_LOCAL_BATCH_MB = 5, /* quadratic aligner: MiB of traceback codes per launch (16384) */
+    SA_OPT_SERIAL_SHARDS = 6   /* sharded context: run the shards' compute one after another
+                                  (measurement: clean per-shard stage times on one device) */
 };
 
 /* Project4's fdAlign switch (Project4.scala:187-192, :585-604).

@@ -1299,7 +1299,7 @@ void sa_ctx_destroy(sa_ctx *c) {
                     &c->d_ovl, &c->d_cnt, &c->d_okeys, &c->d_ovals, &c->d_okeys2, &c->d_ovals2, &c->d_osort,
                     &c->d_lead, &c->d_trail, &c->d_count, &c->d_aln, &c->d_p1, &c->d_tb, &c->d_rkey, &c->d_rkey2, &c->d_rord, &c->d_rord2, &c->d_rtmp, &c->d_gocc, &c->d_seg, &c->d_rl, &c->d_srl, &c->d_srl2, &c->d_loff, &c->d_starts, &c->d_bounds, &c->d_gcodes, &c->d_gwoff, &c->d_glen, &c->d_gbad, &c->d_psum, &c->d_pkeep, &c->d_ppos, &c->d_scan, &c->d_pstart, &c->d_biglist, &c->d_rec,
                     &c->d_srec, &c->d_bnmd, &c->d_ishead, &c->d_bnst2, &c->d_tmd, &c->d_ted, &c->d_tmdi,
-                    &c->d_tedi, &c->d_xrec, &c->d_tier, &c->d_ovlrp, &c->d_meta, &c->d_items, &c->d_bigtot, &c->d_hk0, &c->d_hk1, &c->d_hflag,
+                    &c->d_tedi, &c->d_xrec, &c->d_tier, &c->d_ovlrp, &c->d_meta, &c->d_items, &c->d_lr, &c->d_bigtot, &c->d_hk0, &c->d_hk1, &c->d_hflag,
                     &c->d_hidx, &c->d_hpos, &c->d_htmp, &c->d_hist, &c->d_hovf, &c->d_hsmall,
                     &c->d_ltb, &c->d_lmax, &c->d_rreg, &c->d_rcnt, &c->d_rex,
                     &c->d_shl, &c->d_sht, &c->d_shc, &c->d_rsh};
@@ -1520,6 +1520,9 @@ int sa_set_option(sa_ctx *c, int option, int64_t value) {
         if (value < 1) return fail(c, SA_E_ARG, "SA_OPT_LOCAL_BATCH_MB must be >= 1");
         c->local_batch_bytes = (uint64_t)value << 20;
         break;
+    case SA_OPT_SERIAL_SHARDS:
+        if (!c->multi) return fail(c, SA_E_ARG, "SA_OPT_SERIAL_SHARDS needs a sharded context");
+        return multi_set_option(c, option, value);
     default: return fail(c, SA_E_ARG, "unknown option");
     }
     return c->multi ? multi_set_option(c, option, value) : SA_OK;
@@ -1804,9 +1807,61 @@ int sa_dist_reduce(sa_ctx *c, const void *fst, const void *snd, const void *cnt_
     ENSURE(c->d_psum, n, &sum);
     ENSURE(c->d_pkeep, n, &keep);
     ENSURE(c->d_ppos, n, &pos);
-    ENSURE(c->d_scan, scan_temp_bytes(n), &scan);
+    const uint32_t lbase = c->dstarts[c->rank], nl = c->dstarts[c->rank + 1] - lbase;
+    ENSURE(c->d_scan, scan_temp_bytes(std::max<uint64_t>(n, nl)), &scan);
     HIPCHK(hipMemsetAsync(cnt->distinct, 0, sizeof(cnt->distinct), c->stream));
     HIPCHK(hipMemsetAsync(cnt->totals, 0, sizeof(cnt->totals), c->stream));
+    HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(cnt->overflow_n), c->stream));
+    // this rank's leads: per-lead segments of the received partials, summed and
+    // filtered in LDS (one wave per lead), then one scan + one copy in lead-
+    // descending order; a lead with more than 192 distinct partners (high-copy
+    // repeats) falls back to the (lead, trail) radix sort below
+    {
+        uint32_t *lr;
+        uint2 *seg = (uint2 *)ok;
+        ENSURE(c->d_lr, 5 * ((size_t)nl + 1), &lr);
+        uint32_t *lcnt = lr, *loff = lr + ((size_t)nl + 1), *lcur = lr + 2 * ((size_t)nl + 1),
+                 *kcnt = lr + 3 * ((size_t)nl + 1), *kex = lr + 4 * ((size_t)nl + 1);
+        uint8_t *scan2 = scan;
+        Counters *hp;
+        if (int rc_ = pinned_counters(c, &hp)) return rc_;
+        {
+            StageScope st(c, SA_STAGE_ORDER);
+            HIPCHK(launch_lead_reduce((const uint32_t *)fst, (const uint32_t *)snd, (const uint32_t *)cnt_in, n, lbase,
+                                      nl, c->set.min_collisions, c->set.max_collisions, lcnt, loff, lcur, seg, kcnt,
+                                      cnt->distinct, &cnt->overflow_n, scan2, &cnt->totals[1], c->stream));
+            HIPCHK(exclusive_scan_u32(kcnt, kex, nl, &cnt->totals[0], scan2, c->stream));
+        }
+        HIPCHK(hipMemcpyAsync(hp, cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (nl && hp->overflow_n == 0) {
+            const uint32_t nd = hp->totals[0];
+            const unsigned long long ndist = shard_sum(hp->distinct);
+            int32_t *dlead, *dtrail, *dcount;
+            ENSURE(c->d_lead, nd, &dlead);
+            ENSURE(c->d_trail, nd, &dtrail);
+            ENSURE(c->d_count, nd, &dcount);
+            {
+                StageScope st(c, SA_STAGE_ORDER);
+                HIPCHK(launch_lead_copy(seg, loff, kcnt, kex, &cnt->totals[0], nl, lbase, dlead, dtrail, dcount,
+                                        c->stream));
+            }
+            HIPCHK(hipStreamSynchronize(c->stream));
+            resolve_timing(c);
+            c->n_disp = nd;
+            c->lead.clear(); c->trail.clear(); c->count.clear();
+            c->pfst.clear(); c->psnd.clear(); c->pcnt.clear();
+            c->stats.pairs = ndist;
+            c->stats.dispatched = nd;
+            c->stats.id_mode = SA_IDS_WIDE;
+            c->mode = SA_IDS_WIDE;
+            c->built = true;
+            c->aligned = false;
+            return SA_OK;
+        }
+        HIPCHK(hipMemsetAsync(cnt->distinct, 0, sizeof(cnt->distinct), c->stream));
+        HIPCHK(hipMemsetAsync(cnt->totals, 0, sizeof(cnt->totals), c->stream));
+    }
     {
         StageScope st(c, SA_STAGE_ORDER);
         HIPCHK(launch_reduce_keys((const uint32_t *)fst, (const uint32_t *)snd, n, idb, ok, ov, c->stream));

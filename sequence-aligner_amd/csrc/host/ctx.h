@@ -118,6 +118,7 @@ struct sa_ctx {
     uint32_t *part_perm = nullptr;   // their ascending-lead order (region-space indices)
     DBuf d_gocc, d_seg, d_rl, d_srl, d_srl2, d_loff, d_starts, d_bounds, d_gcodes, d_gwoff, d_glen, d_gbad, d_psum, d_pkeep, d_ppos;
     DBuf d_scan, d_bigtot, d_items;
+    DBuf d_lr;                       // owner-side reduce by lead: counts, offsets, cursors, kept, kept scan
     // k-mer table statistics (sa_kmer_histogram)
     DBuf d_hk0, d_hk1, d_hflag, d_hidx, d_hpos, d_htmp, d_hist, d_hovf, d_hsmall;
     std::vector<uint64_t> hsize, hcount;

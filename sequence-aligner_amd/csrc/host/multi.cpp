@@ -65,6 +65,7 @@ struct sa_multi {
     uint64_t dist_gen = ~0ull;      // reads generation the shards hold
     bool reads_gathered = false;    // packed reads all-gathered for alignment
     bool sharded = false;           // the last build ran sharded
+    bool serial = false;            // SA_OPT_SERIAL_SHARDS: shard compute one after another
     DBuf gcodes, gbad;              // virtual shards: one all-gathered copy on the device
     double x_ms = 0;                // exchange wall time (SA_STAGE_EXCHANGE)
     uint64_t x_n = 0, x_bytes = 0;
@@ -111,8 +112,11 @@ int for_shards(sa_ctx *c, F f) {
         rcs[i] = f(s);
         if (rcs[i] && s.err.empty()) s.err = s.child ? sa_last_error(s.child) : "";
     };
-    if (m->sh.size() == 1) {
-        run(0);
+    if (m->sh.size() == 1 || m->serial) {
+        for (size_t i = 0; i < m->sh.size(); ++i) {
+            run(i);
+            if (m->serial && m->sh[i].child) (void)sa_sync(m->sh[i].child);
+        }
     } else {
         std::vector<std::thread> th;
         for (size_t i = 0; i < m->sh.size(); ++i) th.emplace_back(run, i);
@@ -138,7 +142,16 @@ struct Plan {
     std::vector<uint64_t> soff, scnt, roff, rcnt;
 };
 
-int exchange(sa_ctx *c, std::vector<Plan> &pl, size_t elem) {
+// One exchange of several arrays that share a plan's counts and offsets
+// (parts[a] = array a's send / recv buffers per local shard): every send and
+// receive of every array goes into ONE RCCL group, so the arrays travel
+// together instead of one group (and one wait) per array.
+struct Part {
+    std::vector<const void *> send;
+    std::vector<void *> recv;
+};
+
+int exchange_parts(sa_ctx *c, std::vector<Plan> &pl, const std::vector<Part> &parts, size_t elem) {
     sa_multi *m = c->multi;
     const auto t0 = std::chrono::steady_clock::now();
     uint64_t moved = 0;
@@ -146,36 +159,38 @@ int exchange(sa_ctx *c, std::vector<Plan> &pl, size_t elem) {
         // RCCL point-to-point: over xGMI every pair of MI355X has its own link,
         // so the P - 1 sends of a shard proceed in parallel (no ring)
         ncclResult_t r = ncclGroupStart();
-        for (size_t l = 0; l < m->sh.size() && r == ncclSuccess; ++l) {
-            Shard &s = m->sh[l];
-            for (int q = 0; q < m->P && r == ncclSuccess; ++q) {
-                if (pl[l].scnt[q]) {
-                    r = ncclSend((const char *)pl[l].send + pl[l].soff[q] * elem, pl[l].scnt[q] * elem, ncclUint8, q,
-                                 s.comm, s.xs);
-                    if (q != s.rank) moved += pl[l].scnt[q] * elem;
+        for (const Part &pa : parts)
+            for (size_t l = 0; l < m->sh.size() && r == ncclSuccess; ++l) {
+                Shard &s = m->sh[l];
+                for (int q = 0; q < m->P && r == ncclSuccess; ++q) {
+                    if (pl[l].scnt[q]) {
+                        r = ncclSend((const char *)pa.send[l] + pl[l].soff[q] * elem, pl[l].scnt[q] * elem, ncclUint8,
+                                     q, s.comm, s.xs);
+                        if (q != s.rank) moved += pl[l].scnt[q] * elem;
+                    }
+                    if (r == ncclSuccess && pl[l].rcnt[q])
+                        r = ncclRecv((char *)pa.recv[l] + pl[l].roff[q] * elem, pl[l].rcnt[q] * elem, ncclUint8, q,
+                                     s.comm, s.xs);
                 }
-                if (r == ncclSuccess && pl[l].rcnt[q])
-                    r = ncclRecv((char *)pl[l].recv + pl[l].roff[q] * elem, pl[l].rcnt[q] * elem, ncclUint8, q,
-                                 s.comm, s.xs);
             }
-        }
         const ncclResult_t r2 = ncclGroupEnd();
         if (r != ncclSuccess || r2 != ncclSuccess)
             return set_err(c, SA_E_RCCL, std::string("RCCL send/recv: ") +
                                              ncclGetErrorString(r != ncclSuccess ? r : r2));
     } else {
         // virtual shards, all in this process on one device: device copies
-        for (size_t q = 0; q < m->sh.size(); ++q)
-            for (size_t l = 0; l < m->sh.size(); ++l) {
-                const uint64_t n = pl[l].scnt[q];
-                if (n != pl[q].rcnt[l]) return set_err(c, SA_E_STATE, "exchange counts disagree");
-                if (!n) continue;
-                if (hipMemcpyAsync((char *)pl[q].recv + pl[q].roff[l] * elem,
-                                   (const char *)pl[l].send + pl[l].soff[q] * elem, n * elem, hipMemcpyDeviceToDevice,
-                                   m->sh[q].xs) != hipSuccess)
-                    return set_err(c, SA_E_HIP, "exchange copy");
-                if (q != l) moved += n * elem;
-            }
+        for (const Part &pa : parts)
+            for (size_t q = 0; q < m->sh.size(); ++q)
+                for (size_t l = 0; l < m->sh.size(); ++l) {
+                    const uint64_t n = pl[l].scnt[q];
+                    if (n != pl[q].rcnt[l]) return set_err(c, SA_E_STATE, "exchange counts disagree");
+                    if (!n) continue;
+                    if (hipMemcpyAsync((char *)pa.recv[q] + pl[q].roff[l] * elem,
+                                       (const char *)pa.send[l] + pl[l].soff[q] * elem, n * elem,
+                                       hipMemcpyDeviceToDevice, m->sh[q].xs) != hipSuccess)
+                        return set_err(c, SA_E_HIP, "exchange copy");
+                    if (q != l) moved += n * elem;
+                }
     }
     for (Shard &s : m->sh) {
         (void)hipSetDevice(s.device);
@@ -185,6 +200,15 @@ int exchange(sa_ctx *c, std::vector<Plan> &pl, size_t elem) {
     m->x_n += 1;
     m->x_bytes += moved;
     return SA_OK;
+}
+
+int exchange(sa_ctx *c, std::vector<Plan> &pl, size_t elem) {
+    std::vector<Part> parts(1);
+    for (const Plan &p : pl) {
+        parts[0].send.push_back(p.send);
+        parts[0].recv.push_back(p.recv);
+    }
+    return exchange_parts(c, pl, parts, elem);
 }
 
 // per-peer element counts: cnt[l][q] (shard l -> q) becomes rcnt[l][q] (q -> l)
@@ -391,15 +415,16 @@ int multi_build(sa_ctx *c, bool readback, int (*single_build)(sa_ctx *, bool)) {
         pl[l].scnt = s.cnt; pl[l].soff = prefix(s.cnt);
         pl[l].rcnt = s.rcnt; pl[l].roff = prefix(s.rcnt);
     }
+    // (lead, trail, count) arrays in one RCCL group
     DBuf Shard::*src[3] = {&Shard::pf, &Shard::ps, &Shard::pc};
     DBuf Shard::*dst[3] = {&Shard::qf, &Shard::qs, &Shard::qc};
-    for (int a = 0; a < 3; ++a) {
+    std::vector<Part> parts(3);
+    for (int a = 0; a < 3; ++a)
         for (size_t l = 0; l < m->sh.size(); ++l) {
-            pl[l].send = (m->sh[l].*src[a]).p;
-            pl[l].recv = (m->sh[l].*dst[a]).p;
+            parts[a].send.push_back((m->sh[l].*src[a]).p);
+            parts[a].recv.push_back((m->sh[l].*dst[a]).p);
         }
-        if ((rc = exchange(c, pl, 4))) return rc;
-    }
+    if ((rc = exchange_parts(c, pl, parts, 4))) return rc;
     // ---- reduce + filter: this shard's leads
     rc = for_shards(c, [&](Shard &s) { return sa_dist_reduce(s.child, s.qf.p, s.qs.p, s.qc.p, s.n_recv); });
     if (rc) return rc;
@@ -610,6 +635,10 @@ bool multi_rank_mode(const sa_ctx *c) { return c->multi && c->multi->rank_mode; 
 int multi_rank(const sa_ctx *c) { return c->multi && c->multi->rank_mode ? c->multi->sh[0].rank : 0; }
 
 int multi_set_option(sa_ctx *c, int option, int64_t value) {
+    if (option == SA_OPT_SERIAL_SHARDS) {
+        c->multi->serial = value != 0;
+        return SA_OK;
+    }
     for (Shard &s : c->multi->sh) {
         int rc = sa_set_option(s.child, option, value);
         if (rc) return set_err(c, rc, sa_last_error(s.child));

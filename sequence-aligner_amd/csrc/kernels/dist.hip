@@ -146,7 +146,194 @@ __global__ void reduce_compact_kernel(const uint64_t *skeys, uint64_t n, int idb
     count[p] = (int32_t)sum[i];
 }
 
+// ---- owner-side reduce by lead (replaces the (lead, trail) radix sort) ----
+// received partials (fst = global lead, snd, cnt) -> per-lead segments ->
+// per-lead LDS aggregation (sum, [min, max] filter, trail-ascending rank) ->
+// lead-descending copy.  A lead with more than 192 distinct partners sets
+// *overflow and the caller falls back to the sort.
+// Partials arrive clustered by the sender's pair-count blocks (a few leads
+// each, interleaved), so per-partial global atomics on the lead counters
+// serialise on the same addresses.  A tile of LT partials is first counted in
+// an LDS table keyed by lead (LT_SLOTS slots, linear probing); each distinct
+// lead then takes one global atomic for the whole tile (a lead whose probe
+// run fails falls back to its own global atomic).  PLACE = false: counts
+// only (lcnt); true: every partial gets its position in its lead's segment
+// (loff + tile base + its rank among the tile's partials of that lead).
+constexpr int LT_THREADS = 256, LT_PER = 8, LT = LT_THREADS * LT_PER, LT_SLOTS = 1024;
+
+template <bool PLACE>
+__global__ __launch_bounds__(LT_THREADS) void lead_tile_kernel(const uint32_t *fst, const uint32_t *snd,
+                                                               const uint32_t *cnt, uint64_t n, uint32_t base,
+                                                               uint32_t *lcnt, const uint32_t *loff, uint32_t *lcur,
+                                                               uint2 *seg) {
+    __shared__ uint32_t key[LT_SLOTS], num[LT_SLOTS];
+    for (int j = threadIdx.x; j < LT_SLOTS; j += LT_THREADS) { key[j] = 0xFFFFFFFFu; num[j] = 0; }
+    __syncthreads();
+    const uint64_t t0 = (uint64_t)blockIdx.x * LT;
+    uint32_t l[LT_PER], slot[LT_PER], rk[LT_PER];
+#pragma unroll
+    for (int j = 0; j < LT_PER; ++j) {
+        const uint64_t i = t0 + (uint64_t)j * LT_THREADS + threadIdx.x;
+        l[j] = i < n ? fst[i] - base : 0xFFFFFFFFu;
+        slot[j] = 0xFFFFFFFFu;
+        if (l[j] == 0xFFFFFFFFu) continue;
+        uint32_t h = (l[j] * 0x9E3779B1u) >> 22;  // 10 bits: LT_SLOTS
+        for (int probe = 0; probe < 32; ++probe) {
+            uint32_t old = ((volatile uint32_t *)key)[h];
+            if (old == 0xFFFFFFFFu) old = atomicCAS(&key[h], 0xFFFFFFFFu, l[j]);
+            if (old == 0xFFFFFFFFu || old == l[j]) {
+                slot[j] = h;
+                rk[j] = atomicAdd(&num[h], 1u);
+                break;
+            }
+            h = (h + 1) & (LT_SLOTS - 1);
+        }
+    }
+    __syncthreads();
+    // one global atomic per distinct lead of the tile
+    for (int j = threadIdx.x; j < LT_SLOTS; j += LT_THREADS) {
+        const uint32_t k = key[j];
+        if (k == 0xFFFFFFFFu) continue;
+        if (PLACE) num[j] = atomicAdd(&lcur[k], num[j]);  // the tile's base within the lead's segment
+        else atomicAdd(&lcnt[k], num[j]);
+    }
+    if (!PLACE) {
+#pragma unroll
+        for (int j = 0; j < LT_PER; ++j)
+            if (l[j] != 0xFFFFFFFFu && slot[j] == 0xFFFFFFFFu) atomicAdd(&lcnt[l[j]], 1u);
+        return;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < LT_PER; ++j) {
+        if (l[j] == 0xFFFFFFFFu) continue;
+        const uint64_t i = t0 + (uint64_t)j * LT_THREADS + threadIdx.x;
+        const uint32_t at = slot[j] != 0xFFFFFFFFu ? num[slot[j]] + rk[j] : atomicAdd(&lcur[l[j]], 1u);
+        seg[loff[l[j]] + at] = make_uint2(snd[i], cnt[i]);
+    }
+}
+
+constexpr int LR_SLOTS = 256, LR_FILL = 192;
+constexpr uint32_t LR_EMPTY = 0xFFFFFFFFu;
+
+// one wave per lead: partials into a wave-private 256-slot table (trail ->
+// count sum), then the kept entries compacted, ranked by trail and written
+// back over the start of the lead's own segment; kcnt[l] = kept, distinct
+// pairs counted (KmerTable.calcDispatchData's filter, :155-187)
+__global__ __launch_bounds__(256) void lead_reduce_kernel(uint2 *seg, const uint32_t *loff, uint32_t nl, int32_t min_c,
+                                                          int32_t max_c, uint32_t *kcnt,
+                                                          unsigned long long *distinct, uint32_t *overflow) {
+    __shared__ uint32_t key[4][LR_SLOTS], val[4][LR_SLOTS];
+    __shared__ uint2 kept[4][LR_FILL];
+    __shared__ uint32_t nd_blk;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t l = blockIdx.x * 4 + w;
+    if (threadIdx.x == 0) nd_blk = 0;
+    for (int j = lane; j < LR_SLOTS; j += 64) { key[w][j] = LR_EMPTY; val[w][j] = 0; }
+    __syncthreads();
+    uint32_t nd = 0;
+    if (l < nl) {
+        const uint32_t s0 = loff[l], m = loff[l + 1] - s0;
+        bool ovf = false;
+        for (uint32_t j = lane; j < m; j += 64) {
+            const uint2 v = seg[s0 + j];
+            uint32_t h = (v.x * 0x9E3779B1u) >> 24;
+            int probe = 0;
+            for (; probe < 64; ++probe) {
+                uint32_t old = ((volatile uint32_t *)key[w])[h];
+                if (old == LR_EMPTY) old = atomicCAS(&key[w][h], LR_EMPTY, v.x);
+                if (old == LR_EMPTY || old == v.x) { atomicAdd(&val[w][h], v.y); break; }
+                h = (h + 1) & (LR_SLOTS - 1);
+            }
+            if (probe == 64) ovf = true;
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        // this lane's 4 slots: distinct keys, kept ones compacted by wave prefix
+        uint32_t kk[4], kc[4], kp = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            kk[q] = key[w][lane * 4 + q];
+            kc[q] = val[w][lane * 4 + q];
+            if (kk[q] != LR_EMPTY) {
+                ++nd;
+                if ((int32_t)kc[q] >= min_c && (int32_t)kc[q] <= max_c) kp |= 1u << q;
+            }
+        }
+        const uint32_t tot_nd = (uint32_t)__shfl((int)wave_incl_add(nd), 63, 64);
+        if (tot_nd > LR_FILL || __any(ovf)) {
+            if (lane == 0) atomicOr(overflow, 1u);
+            if (lane == 0) kcnt[l] = 0;
+        } else {
+            const uint32_t mine = __popc(kp);
+            const uint32_t ex = wave_incl_add(mine) - mine;
+            const uint32_t k = (uint32_t)__shfl((int)(ex + mine), 63, 64);
+            uint32_t at = ex;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (kp & (1u << q)) kept[w][at++] = make_uint2(kk[q], kc[q]);
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+            for (uint32_t j = lane; j < k; j += 64) {
+                const uint2 e = kept[w][j];
+                uint32_t r = 0;
+                for (uint32_t q = 0; q < k; ++q) r += kept[w][q].x < e.x ? 1u : 0u;
+                seg[s0 + r] = e;  // (the segment's partials are all consumed)
+            }
+            if (lane == 0) kcnt[l] = k;
+        }
+        if (lane == 0) atomicAdd(&nd_blk, tot_nd);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && nd_blk) atomicAdd(&distinct[blockIdx.x % NSHARD], (unsigned long long)nd_blk);
+}
+
+// lead-descending dispatch: lead l's kept entries go to total - kex[l] - kcnt[l]
+__global__ void lead_copy_kernel(const uint2 *seg, const uint32_t *loff, const uint32_t *kcnt, const uint32_t *kex,
+                                 const uint32_t *total, uint32_t nl, uint32_t base, int32_t *lead, int32_t *trail,
+                                 int32_t *count) {
+    const uint32_t l = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (l >= nl) return;
+    const uint32_t m = kcnt[l], off = *total - kex[l] - m, s0 = loff[l];
+    for (uint32_t j = threadIdx.x & 63u; j < m; j += 64) {
+        const uint2 e = seg[s0 + j];
+        lead[off + j] = (int32_t)(base + l) + 1;  // 1-based ids downstream
+        trail[off + j] = (int32_t)e.x + 1;
+        count[off + j] = (int32_t)e.y;
+    }
+}
+
 }  // namespace
+
+hipError_t launch_lead_reduce(const uint32_t *fst, const uint32_t *snd, const uint32_t *cnt, uint64_t n, uint32_t base,
+                              uint32_t nl, int32_t min_c, int32_t max_c, uint32_t *lcnt, uint32_t *loff, uint32_t *lcur,
+                              uint2 *seg, uint32_t *kcnt, unsigned long long *distinct, uint32_t *overflow,
+                              void *scan_tmp, uint32_t *total_dev, hipStream_t s) {
+    if (!nl) return hipSuccess;
+    hipError_t e;
+    if ((e = hipMemsetAsync(lcnt, 0, (size_t)nl * 4, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(lcur, 0, (size_t)nl * 4, s)) != hipSuccess) return e;
+    const dim3 tiles((uint32_t)((n + LT - 1) / LT));
+    if (n) hipLaunchKernelGGL(lead_tile_kernel<false>, tiles, dim3(LT_THREADS), 0, s, fst, snd, cnt, n, base, lcnt,
+                              (const uint32_t *)nullptr, lcur, (uint2 *)nullptr);
+    if ((e = exclusive_scan_u32(lcnt, loff, nl, total_dev, scan_tmp, s)) != hipSuccess) return e;
+    // loff[nl] = n (the scan leaves nl entries)
+    if ((e = hipMemcpyAsync(loff + nl, total_dev, 4, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+    if (n) hipLaunchKernelGGL(lead_tile_kernel<true>, tiles, dim3(LT_THREADS), 0, s, fst, snd, cnt, n, base, lcnt,
+                              (const uint32_t *)loff, lcur, seg);
+    hipLaunchKernelGGL(lead_reduce_kernel, dim3((nl + 3) / 4), dim3(256), 0, s, seg, loff, nl, min_c, max_c, kcnt,
+                       distinct, overflow);
+    return hipGetLastError();
+}
+
+hipError_t launch_lead_copy(const uint2 *seg, const uint32_t *loff, const uint32_t *kcnt, const uint32_t *kex,
+                            const uint32_t *total, uint32_t nl, uint32_t base, int32_t *lead, int32_t *trail,
+                            int32_t *count, hipStream_t s) {
+    if (!nl) return hipSuccess;
+    hipLaunchKernelGGL(lead_copy_kernel, dim3((nl + 3) / 4), dim3(256), 0, s, seg, loff, kcnt, kex, total, nl, base,
+                       lead, trail, count);
+    return hipGetLastError();
+}
 
 hipError_t launch_iota(uint32_t *v, uint64_t n, hipStream_t s) {
     if (!n) return hipSuccess;
