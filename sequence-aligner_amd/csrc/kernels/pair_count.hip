@@ -51,24 +51,37 @@ __device__ __forceinline__ uint32_t pc_hash(uint32_t p) {
 // occurrence (its element range is in its registers: no scan, one barrier).
 constexpr int PC_WIN = 2048;
 
+// Per-table block shape.  The 16,384-slot tier holds 128 KB of table, so only
+// one block fits a CU: it runs 1,024 threads (16 waves to hide the partner
+// gathers, not 4), 1,024-occurrence chunks and 4,096-element windows (4
+// partner loads in flight per thread); the smaller tables keep 256 threads.
+template <int TAB> struct PcShape {
+    static constexpr int NT = TAB >= PC_TAB_HUGE ? 1024 : PC_THREADS;
+    static constexpr int CHUNK = TAB >= PC_TAB_HUGE ? 1024 : PC_CHUNK;
+    static constexpr int WIN = TAB >= PC_TAB_HUGE ? 4096 : PC_WIN;
+    static constexpr int BATCH = TAB >= PC_TAB_HUGE ? 4 : PC_BATCH;
+};
+
 template <int TAB>
 struct PcShared {
+    static constexpr int NT = PcShape<TAB>::NT, CHUNK = PcShape<TAB>::CHUNK;
     uint32_t key[TAB];
     uint32_t cnt[TAB];
-    uint32_t pref[PC_CHUNK + 1];
-    uint4 rec[PC_CHUNK];       // per-occurrence partner ranges (partition.hip)
-    uint16_t eo[PC_WIN];       // element -> occurrence (+1) of the current window
-    uint32_t lds4[PC_THREADS / 64];
-    uint32_t emit4[2][PC_THREADS / 64];  // emission: per-wave kept counts (double-buffered)
+    uint32_t pref[CHUNK + 1];
+    uint4 rec[CHUNK];          // per-occurrence partner ranges (partition.hip)
+    uint16_t eo[PcShape<TAB>::WIN];  // element -> occurrence (+1) of the current window
+    uint32_t lds4[NT / 64];
+    uint32_t emit4[2][NT / 64];  // emission: per-wave kept counts (double-buffered)
     uint32_t emit_base[2];
     uint32_t fill, overflow, out_base;
 };
 template <int TAB>
 struct PcSharedStrict {
     unsigned long long rank[TAB];
-    uint4 srec[PC_CHUNK];      // {bucket head pos, own_e, own_m, 0}
+    uint4 srec[PcShape<TAB>::CHUNK];  // {bucket head pos, own_e, own_m, 0}
 };
 
+template <int NT = PC_THREADS>
 __device__ __forceinline__ uint32_t pc_block_excl_scan(uint32_t v, uint32_t *lds4, uint32_t *total) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t inc = wave_incl_add(v);
@@ -76,7 +89,7 @@ __device__ __forceinline__ uint32_t pc_block_excl_scan(uint32_t v, uint32_t *lds
     __syncthreads();
     uint32_t off = 0, tot = 0;
 #pragma unroll
-    for (int i = 0; i < PC_THREADS / 64; ++i) {
+    for (int i = 0; i < NT / 64; ++i) {
         const uint32_t x = lds4[i];
         if (i < w) off += x;
         tot += x;
@@ -119,12 +132,14 @@ __device__ __forceinline__ void pc_insert(PcShared<TAB> &S, PcSharedStrict<TAB> 
 }
 
 template <bool STRICT, int TAB>
-__global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, PairIn in, PairParams p, PairOut o,
+__global__ __launch_bounds__(PcShape<TAB>::NT) void pair_count_kernel(EmitParams e, PairIn in, PairParams p, PairOut o,
                                                                 const uint32_t *read_list) {
     extern __shared__ __align__(16) uint8_t smem[];
     PcShared<TAB> &S = *reinterpret_cast<PcShared<TAB> *>(smem);
     PcSharedStrict<TAB> &X =
         *reinterpret_cast<PcSharedStrict<TAB> *>(smem + ((sizeof(PcShared<TAB>) + 15) & ~size_t(15)));
+    constexpr int NT = PcShape<TAB>::NT, CHUNK = PcShape<TAB>::CHUNK, WIN = PcShape<TAB>::WIN,
+                  BATCH = PcShape<TAB>::BATCH;
     const int tid = threadIdx.x;
     const uint32_t split = (uint32_t)p.split;
     uint32_t bid = blockIdx.x;
@@ -146,7 +161,7 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
         residue = 0;
     }
 
-    for (int i = tid; i < TAB; i += PC_THREADS) {
+    for (int i = tid; i < TAB; i += NT) {
         S.key[i] = PC_EMPTY;
         S.cnt[i] = 0;
         if constexpr (STRICT) X.rank[i] = ~0ull;
@@ -160,10 +175,10 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
     unsigned long long x_over = ~0ull;  // role pairs enumerated when the table filled
     // (the table initialisation is ordered before any insert by the chunk scan's barriers)
 
-    for (uint32_t c0 = 0; c0 < nocc; c0 += PC_CHUNK) {
-        const uint32_t cn = min((uint32_t)PC_CHUNK, nocc - c0);
+    for (uint32_t c0 = 0; c0 < nocc; c0 += CHUNK) {
+        const uint32_t cn = min((uint32_t)CHUNK, nocc - c0);
         // --- per-occurrence partner ranges: one 8-byte record each
-        constexpr int PER = PC_CHUNK / PC_THREADS;
+        constexpr int PER = CHUNK / NT;
         uint32_t mytot[PER];
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
@@ -181,7 +196,7 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
 #pragma unroll
         for (int j = 0; j < PER; ++j) s += mytot[j];
         uint32_t total;
-        uint32_t ex = pc_block_excl_scan(s, S.lds4, &total);
+        uint32_t ex = pc_block_excl_scan<NT>(s, S.lds4, &total);
         uint32_t myex[PER];
 #pragma unroll
         for (int j = 0; j < PER; ++j) {
@@ -190,13 +205,13 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
             myex[j] = ex;
             ex += mytot[j];
         }
-        if (tid == PC_THREADS - 1 && cn == PC_CHUNK) S.pref[PC_CHUNK] = total;
+        if (tid == NT - 1 && cn == CHUNK) S.pref[CHUNK] = total;
         role_pairs += total;
 
         // --- lane-interleaved enumeration: consecutive lanes take consecutive
         //     elements, so a wave's partner loads walk one occurrence's list range
         //     (a few cache lines per instruction, not 64)
-        for (uint32_t w0 = 0; w0 < total; w0 += PC_WIN) {
+        for (uint32_t w0 = 0; w0 < total; w0 += WIN) {
             __syncthreads();  // pref / rec written; the previous window's eo consumed
             // an overflowed table is recounted by the next tier: skip the rest of
             // the enumeration (the chunk totals -- role pairs -- are still summed)
@@ -206,21 +221,21 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
             }
 #pragma unroll
             for (int j = 0; j < PER; ++j) {  // this thread's occurrences' elements inside the window
-                const uint32_t e0 = max(myex[j], w0), e1 = min(myex[j] + mytot[j], w0 + (uint32_t)PC_WIN);
+                const uint32_t e0 = max(myex[j], w0), e1 = min(myex[j] + mytot[j], w0 + (uint32_t)WIN);
                 const uint16_t v = (uint16_t)(tid * PER + j + 1);
                 for (uint32_t el = e0; el < e1; ++el) S.eo[el - w0] = v;
             }
             __syncthreads();
-            const uint32_t wn = min((uint32_t)PC_WIN, total - w0);
-            for (uint32_t e0 = 0; e0 < wn; e0 += PC_THREADS * PC_BATCH) {
-                uint32_t part[PC_BATCH], wv[PC_BATCH];
-                unsigned long long rk[PC_BATCH];
+            const uint32_t wn = min((uint32_t)WIN, total - w0);
+            for (uint32_t e0 = 0; e0 < wn; e0 += NT * BATCH) {
+                uint32_t part[BATCH], wv[BATCH];
+                unsigned long long rk[BATCH];
 #pragma unroll
-                for (int bb = 0; bb < PC_BATCH; ++bb) {
+                for (int bb = 0; bb < BATCH; ++bb) {
                     part[bb] = a;  // "same read" = skip
                     wv[bb] = 0;
                     rk[bb] = 0;
-                    const uint32_t el = e0 + bb * PC_THREADS + tid;
+                    const uint32_t el = e0 + bb * NT + tid;
                     if (el < wn) {
                         const uint32_t oi = (uint32_t)S.eo[el] - 1u;
                         const uint32_t off = w0 + el - S.pref[oi];
@@ -255,7 +270,7 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
                     }
                 }
 #pragma unroll
-                for (int bb = 0; bb < PC_BATCH; ++bb) {
+                for (int bb = 0; bb < BATCH; ++bb) {
                     const uint32_t partner = part[bb];
                     if (partner == a) continue;                 // same read (KmerTable.scala:61-63)
                     if (split > 1 && (partner % split) != residue) continue;
@@ -290,11 +305,11 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
         // --- per-read region (TAB = 256: one slot per thread): compact the
         //     kept keys in LDS, rank each by its trail among them (<= 192,
         //     distinct), store at its rank -- the region is trail-ascending
-        if constexpr (TAB == PC_THREADS) {
+        if constexpr (TAB == NT) {
             const uint32_t kk = S.key[tid], kc = S.cnt[tid];
             const bool keep = kk != PC_EMPTY && (int32_t)kc >= p.min_coll && (int32_t)kc <= p.max_coll;
             uint32_t m;
-            const uint32_t ex = pc_block_excl_scan(keep ? 1u : 0u, S.lds4, &m);
+            const uint32_t ex = pc_block_excl_scan<NT>(keep ? 1u : 0u, S.lds4, &m);
             uint32_t *ck = reinterpret_cast<uint32_t *>(S.rec);  // enumeration state is dead
             if (keep) ck[ex] = kk;
             __syncthreads();
@@ -309,7 +324,7 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
     }
     // --- emit (a, partner, count[, rank]), 32 slots per thread at a time:
     //     wave scans, one claim per block, two barriers per chunk
-    constexpr int PER = TAB / PC_THREADS;
+    constexpr int PER = TAB / NT;
     constexpr int CH = PER < 32 ? PER : 32;
     const unsigned long long region = (unsigned long long)shard * o.cap_s;
     const int lane = tid & 63, wvi = tid >> 6;
@@ -329,7 +344,7 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_kernel(EmitParams e, Pa
         __syncthreads();
         uint32_t total = 0, ex = inc - mine;
 #pragma unroll
-        for (int q = 0; q < PC_THREADS / 64; ++q) {
+        for (int q = 0; q < NT / 64; ++q) {
             const uint32_t v = S.emit4[buf][q];
             total += v;
             if (q < wvi) ex += v;
@@ -370,7 +385,7 @@ static void pc_launch(const EmitParams &e, const PairIn &in, const PairParams &p
     const size_t lds = pc_lds_bytes<TAB>(STRICT);
     (void)hipFuncSetAttribute((const void *)pair_count_kernel<STRICT, TAB>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((pair_count_kernel<STRICT, TAB>), dim3(n_blocks), dim3(PC_THREADS), lds, s, e, in, p, o,
+    hipLaunchKernelGGL((pair_count_kernel<STRICT, TAB>), dim3(n_blocks), dim3(PcShape<TAB>::NT), lds, s, e, in, p, o,
                        read_list);
 }
 
