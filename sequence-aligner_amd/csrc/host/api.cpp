@@ -629,10 +629,14 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
             HIPCHK(hipMemcpy(codes.data(), O.overflow_list, (size_t)ovn * 4, hipMemcpyDeviceToHost));
             if (O.overflow_rp) HIPCHK(hipMemcpy(rps.data(), O.overflow_rp, (size_t)ovn * 4, hipMemcpyDeviceToHost));
             for (uint32_t i = 0; i < ovn; ++i)
-                // rps: the partner estimate; it over-reads reads whose partners
-                // recur (found early, met again later), so only a clear excess
-                // skips the 2,048-slot tier (whose overflow stops early anyway)
-                (strict || rps[i] <= 4u * 1536u ? q_big : q_huge).push_back(codes[i]);
+                // rps: the partner estimate, a linear extrapolation of the
+                // first pass's fill rate -- partners are met early and then
+                // recur, so it over-reads (estimate >= partners).  Past 1.5x the
+                // 2,048-slot table's 1,536 a read goes straight to 16,384 slots:
+                // on configs[4]'s k = 12 shape (~3,900 partners per read) 86 % of
+                // the reads the 2,048-slot tier took filled it and were re-run
+                // anyway (57 ms of 221 ms of pair counting, 1M reads)
+                (strict || rps[i] <= 1536u * 3u / 2u ? q_big : q_huge).push_back(codes[i]);
         }
         // one tier over host-side items; returns its failures (codes)
         auto run_tier = [&](int table, int split, const std::vector<uint32_t> &items,

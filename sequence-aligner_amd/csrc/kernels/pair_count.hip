@@ -74,6 +74,7 @@ struct PcShared {
     uint32_t emit4[2][NT / 64];  // emission: per-wave kept counts (double-buffered)
     uint32_t emit_base[2];
     uint32_t fill, overflow, out_base;
+    uint32_t xfill;            // role-pair index (within the read) of the insert that filled the table
 };
 template <int TAB>
 struct PcSharedStrict {
@@ -101,7 +102,7 @@ __device__ __forceinline__ uint32_t pc_block_excl_scan(uint32_t v, uint32_t *lds
 
 template <bool STRICT, int TAB>
 __device__ __forceinline__ void pc_insert(PcShared<TAB> &S, PcSharedStrict<TAB> &X, uint32_t partner, uint32_t w,
-                                          unsigned long long rank) {
+                                          unsigned long long rank, uint32_t eidx) {
     constexpr uint32_t FILL_MAX = TAB * 3 / 4;
     uint32_t slot = pc_hash<TAB>(partner);
     // probe runs are bounded: at <= 3/4 load they average < 9 slots, and a run
@@ -121,7 +122,10 @@ __device__ __forceinline__ void pc_insert(PcShared<TAB> &S, PcSharedStrict<TAB> 
         uint32_t old = ((volatile uint32_t *)S.key)[slot];
         if (old == PC_EMPTY) old = atomicCAS(&S.key[slot], PC_EMPTY, partner);
         if (old == PC_EMPTY || old == partner) {
-            if (old == PC_EMPTY && atomicAdd(&S.fill, 1u) >= FILL_MAX) S.overflow = 1;
+            if (old == PC_EMPTY && atomicAdd(&S.fill, 1u) >= FILL_MAX) {
+                S.overflow = 1;
+                atomicMin(&S.xfill, eidx);
+            }
             atomicAdd(&S.cnt[slot], w);
             if constexpr (STRICT) atomicMin(&X.rank[slot], rank);
             return;
@@ -166,7 +170,7 @@ __global__ __launch_bounds__(PcShape<TAB>::NT) void pair_count_kernel(EmitParams
         S.cnt[i] = 0;
         if constexpr (STRICT) X.rank[i] = ~0ull;
     }
-    if (tid == 0) { S.fill = 0; S.overflow = 0; }
+    if (tid == 0) { S.fill = 0; S.overflow = 0; S.xfill = 0xFFFFFFFFu; }
 
     // (uniform lengths: no dependent offset load before the record loads)
     const uint64_t g0 = e.npr ? (uint64_t)a * e.npr : e.occ_off[a];
@@ -274,7 +278,8 @@ __global__ __launch_bounds__(PcShape<TAB>::NT) void pair_count_kernel(EmitParams
                     const uint32_t partner = part[bb];
                     if (partner == a) continue;                 // same read (KmerTable.scala:61-63)
                     if (split > 1 && (partner % split) != residue) continue;
-                    pc_insert<STRICT, TAB>(S, X, partner, wv[bb], rk[bb]);
+                    pc_insert<STRICT, TAB>(S, X, partner, wv[bb], rk[bb],
+                                           (uint32_t)min(role_pairs - total + w0 + e0 + bb * NT + tid, 0xFFFFFFFEull));
                 }
                 if (S.overflow) break;
             }
@@ -292,9 +297,12 @@ __global__ __launch_bounds__(PcShape<TAB>::NT) void pair_count_kernel(EmitParams
             const uint32_t at = atomicAdd(o.overflow_n, 1u);
             o.overflow_list[at] = (a << 6) | residue;
             // its distinct partners, extrapolated from the fill rate (FILL_MAX
-            // partners in the first x_over role pairs): the host picks the tier
+            // partners in the first xfill role pairs -- the index of the insert
+            // that filled the table; else the window where it was seen full):
+            // the host picks the tier
             if (o.overflow_rp) {
-                const unsigned long long x = x_over == ~0ull || x_over == 0 ? role_pairs : x_over;
+                const unsigned long long x = S.xfill != 0xFFFFFFFFu ? (unsigned long long)S.xfill + 1
+                                             : x_over == ~0ull || x_over == 0 ? role_pairs : x_over;
                 const unsigned long long est = (unsigned long long)(TAB * 3 / 4) * role_pairs / (x ? x : 1);
                 o.overflow_rp[at] = est > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)est;
             }
