@@ -148,8 +148,11 @@ enum sa_option {
                                 per-cell path summaries instead of stored codes */
     SA_OPT_ALIGNER = 4,      /* enum sa_aligner: which reference aligner sa_align runs */
     SA_OPT_LOCAL_BATCH_MB = 5, /* quadratic aligner: MiB of traceback codes per launch (16384) */
-    SA_OPT_SERIAL_SHARDS = 6   /* sharded context: run the shards' compute one after another
+    SA_OPT_SERIAL_SHARDS = 6,  /* sharded context: run the shards' compute one after another
                                   (measurement: clean per-shard stage times on one device) */
+    SA_OPT_LAUNCH_SLICE = 7    /* pair counter: at most this many workgroups per launch (0 =
+                                  default: lists are sliced only where a dispatch's 32-bit
+                                  work-item count would wrap; a test hook for that path) */
 };
 
 /* Project4's fdAlign switch (Project4.scala:187-192, :585-604).

@@ -542,6 +542,7 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
     P.abort = abort_flag;
     if (aborted) *aborted = false;
     P.per_read = per_read && *per_read ? 1 : 0;
+    P.max_blocks = c->launch_slice;
     if (per_read) *per_read = false;
     uint2 *rreg = nullptr;
     uint32_t *rcnt = nullptr;
@@ -605,6 +606,7 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
             return SA_OK;
         }
         P.abort = nullptr;
+        c->first_overflow = ovn;  // reads the first pass handed to the recount tiers
         const uint64_t first_distinct = shard_sum(dist_h);
         if (P.per_read && ovn == 0) {
             *per_read = true;
@@ -639,9 +641,10 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
                 (strict || rps[i] <= 1536u * 3u / 2u ? q_big : q_huge).push_back(codes[i]);
         }
         // one tier over host-side items; returns its failures (codes)
-        auto run_tier = [&](int table, int split, const std::vector<uint32_t> &items,
-                            std::vector<uint32_t> &failed) -> int {
+        auto run_tier = [&](int table, int split, const std::vector<uint32_t> &items, std::vector<uint32_t> &failed,
+                            std::vector<uint32_t> *fest = nullptr) -> int {
             failed.clear();
+            if (fest) fest->clear();
             if (items.empty() || cur_max() > cap_s) return SA_OK;
             uint32_t *tl, *fl;
             ENSURE(c->d_tier, items.size(), &tl);
@@ -659,6 +662,11 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
             OT.role_pairs = cnt->role_pairs_dummy;
             OT.overflow_list = fl;
             OT.overflow_rp = nullptr;
+            uint32_t *fe = nullptr;
+            if (fest) {  // the failures' partner estimates (this class's partners)
+                ENSURE(c->d_ovlrp, items.size() + 3, &fe);
+                OT.overflow_rp = fe;
+            }
             HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(uint32_t), c->stream));
             {
                 StageScope st(c, SA_STAGE_PAIRS);
@@ -670,6 +678,10 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
             HIPCHK(hipStreamSynchronize(c->stream));
             failed.resize(nf);
             if (nf) HIPCHK(hipMemcpy(failed.data(), fl, (size_t)nf * 4, hipMemcpyDeviceToHost));
+            if (fest) {
+                fest->resize(nf);
+                if (nf) HIPCHK(hipMemcpy(fest->data(), fe, (size_t)nf * 4, hipMemcpyDeviceToHost));
+            }
             return SA_OK;
         };
         // the failed classes of a tier at split s, refined into f sub-classes
@@ -686,10 +698,32 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
         if (strict) {
             if ((rc_t = run_tier(2048, 64, refine(failed, 1, 64), failed))) return rc_t;
         } else {
-            q_huge.insert(q_huge.end(), failed.begin(), failed.end());
-            if ((rc_t = run_tier(16384, 1, q_huge, failed))) return rc_t;
-            if ((rc_t = run_tier(16384, 8, refine(failed, 1, 8), failed))) return rc_t;
-            if ((rc_t = run_tier(16384, 64, refine(failed, 8, 8), failed))) return rc_t;
+            // 16,384 slots (12,288 partners) per block; a read that overflows is
+            // recounted in partner-residue classes (split s: partners with
+            // partner % s == residue, each class re-enumerating the read), as
+            // many as its partner estimate from the overflowed 16,384-slot
+            // pass asks for (12,288 partners found in the first x role pairs;
+            // that sample is large enough to trust -- the first pass's is not:
+            // classes chosen from it ran 1M k=12 reads 172 -> 219 ms):
+            // configs[4]'s k = 12 slice has ~24k partners per read -> 2-4
+            // classes, not 8; a class that still overflows is refined again
+            std::vector<uint32_t> lv[7];  // split 1, 2, 4, ..., 64
+            lv[0] = q_huge;
+            lv[0].insert(lv[0].end(), failed.begin(), failed.end());  // the 2,048-slot tier's overflow
+            failed.clear();
+            for (int e = 0; e <= 6; ++e) {
+                std::vector<uint32_t> fest;
+                if ((rc_t = run_tier(16384, 1 << e, lv[e], failed, &fest))) return rc_t;
+                if (failed.empty() || e == 6) continue;
+                for (size_t i = 0; i < failed.size(); ++i) {
+                    // classes so that each holds <= 12,288 of this class's
+                    // estimated partners (at least 2x finer, at most 64 in all)
+                    int ne = e + 1;
+                    while (ne < 6 && (uint64_t)fest[i] > (uint64_t)12288u << (ne - e)) ++ne;
+                    for (uint32_t j = 0; j < (1u << (ne - e)); ++j) lv[ne].push_back(failed[i] + (1u << e) * j);
+                }
+                failed.clear();
+            }
         }
         if (!failed.empty() && cur_max() <= cap_s)
             return fail(c, SA_E_OVERFLOW, strict ? "a read has more than 98,304 distinct partners"
@@ -962,7 +996,7 @@ int device_build(sa_ctx *c, bool readback) {
     c->stats.role_pairs = shard_sum(hc.role_pairs);
     c->stats.pairs = shard_sum(hc.distinct);
     c->stats.id_mode = c->mode;
-    c->stats.flags = (per_read ? SA_STATS_PER_READ_REGIONS : 0) | (hc.overflow_n || c->recounted ? SA_STATS_RECOUNTED : 0);
+    c->stats.flags = (per_read ? SA_STATS_PER_READ_REGIONS : 0) | (c->first_overflow ? SA_STATS_RECOUNTED : 0);
 
     c->lead.clear(); c->trail.clear(); c->count.clear();
     c->pfst.clear(); c->psnd.clear(); c->pcnt.clear();
@@ -1523,6 +1557,10 @@ int sa_set_option(sa_ctx *c, int option, int64_t value) {
     case SA_OPT_LOCAL_BATCH_MB:
         if (value < 1) return fail(c, SA_E_ARG, "SA_OPT_LOCAL_BATCH_MB must be >= 1");
         c->local_batch_bytes = (uint64_t)value << 20;
+        break;
+    case SA_OPT_LAUNCH_SLICE:
+        if (value < 0 || value > 0x7FFFFFFF) return fail(c, SA_E_ARG, "SA_OPT_LAUNCH_SLICE must be 0..2^31-1");
+        c->launch_slice = (uint32_t)value;
         break;
     case SA_OPT_SERIAL_SHARDS:
         if (!c->multi) return fail(c, SA_E_ARG, "SA_OPT_SERIAL_SHARDS needs a sharded context");

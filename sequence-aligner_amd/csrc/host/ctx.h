@@ -103,6 +103,7 @@ struct sa_ctx {
     // each such read's segment start + 1 (0: the read's pairs are in its region)
     DBuf d_shl, d_sht, d_shc, d_rsh;
     uint64_t recounted = 0;      // last build: dispatched pairs of reads recounted by the tiers (per-read mode)
+    uint32_t first_overflow = 0; // last build: reads whose first-pass table overflowed (recounted)
     bool used_per_read = false;  // last build used the per-read regions
     uint64_t pair_cap = 0;
     uint64_t n_disp = 0;
@@ -125,6 +126,7 @@ struct sa_ctx {
     // options / state
     bool keep_pairs = false, timing = false;
     int align_kernel = 0;  // SA_OPT_ALIGN_KERNEL
+    uint32_t launch_slice = 0;  // SA_OPT_LAUNCH_SLICE (0: only when a grid would pass 2^31 work-items)
     int aligner = SA_ALIGNER_LINEAR;  // SA_OPT_ALIGNER (--linear-align / --quadratic-align)
     uint64_t local_batch_bytes = 16ull << 30;  // traceback-code budget of one quadratic launch
     bool built = false, aligned = false;

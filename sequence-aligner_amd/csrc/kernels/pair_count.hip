@@ -388,29 +388,47 @@ static size_t pc_lds_bytes(bool strict) {
 size_t pair_count_lds_bytes(bool strict) { return pc_lds_bytes<PC_TAB_BIG>(strict); }
 
 template <bool STRICT, int TAB>
-static void pc_launch(const EmitParams &e, const PairIn &in, const PairParams &p, PairOut &o,
-                      const uint32_t *read_list, uint32_t n_blocks, hipStream_t s) {
+static hipError_t pc_launch(const EmitParams &e, const PairIn &in, const PairParams &p, PairOut &o,
+                            const uint32_t *read_list, uint32_t n_blocks, hipStream_t s) {
     const size_t lds = pc_lds_bytes<TAB>(STRICT);
     (void)hipFuncSetAttribute((const void *)pair_count_kernel<STRICT, TAB>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((pair_count_kernel<STRICT, TAB>), dim3(n_blocks), dim3(PcShape<TAB>::NT), lds, s, e, in, p, o,
-                       read_list);
+    // a dispatch's grid is counted in work-items with 32 bits: 6.25M reads at
+    // 1,024 threads (configs[4]'s slice in the 16,384-slot tier) would wrap it.
+    // Larger item lists go in slices of the list (the XCD-contiguous swizzle
+    // is a schedule only, so the slices drop it)
+    constexpr uint32_t NT = PcShape<TAB>::NT;
+    uint32_t max_blocks = (0x80000000u / NT) & ~7u;
+    if (p.max_blocks && p.max_blocks < max_blocks) max_blocks = p.max_blocks;
+    if (n_blocks <= max_blocks) {
+        hipLaunchKernelGGL((pair_count_kernel<STRICT, TAB>), dim3(n_blocks), dim3(NT), lds, s, e, in, p, o, read_list);
+        return hipGetLastError();
+    }
+    if (!read_list) return hipErrorInvalidValue;  // (every large launch walks an item list)
+    for (uint32_t b0 = 0; b0 < n_blocks && b0 < p.n_items; b0 += max_blocks) {
+        PairParams q = p;
+        q.xcd_swizzle = 0;
+        q.n_items = min(p.n_items - b0, max_blocks);
+        hipLaunchKernelGGL((pair_count_kernel<STRICT, TAB>), dim3(q.n_items), dim3(NT), lds, s, e, in, q, o,
+                           read_list + b0);
+        const hipError_t er = hipGetLastError();
+        if (er != hipSuccess) return er;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_pair_count(const EmitParams &e, const PairIn &in, const PairParams &p, PairOut &o,
                              const uint32_t *read_list, uint32_t n_blocks, hipStream_t s) {
     if (n_blocks == 0) return hipSuccess;
     if (p.strict) {
-        if (p.table == PC_TAB_SMALL) pc_launch<true, PC_TAB_SMALL>(e, in, p, o, read_list, n_blocks, s);
-        else if (p.table == PC_TAB_BIG) pc_launch<true, PC_TAB_BIG>(e, in, p, o, read_list, n_blocks, s);
-        else return hipErrorInvalidValue;  // strict ids stop at 2,048 slots (then split)
-    } else {
-        if (p.table == PC_TAB_SMALL) pc_launch<false, PC_TAB_SMALL>(e, in, p, o, read_list, n_blocks, s);
-        else if (p.table == PC_TAB_BIG) pc_launch<false, PC_TAB_BIG>(e, in, p, o, read_list, n_blocks, s);
-        else if (p.table == PC_TAB_HUGE) pc_launch<false, PC_TAB_HUGE>(e, in, p, o, read_list, n_blocks, s);
-        else return hipErrorInvalidValue;
+        if (p.table == PC_TAB_SMALL) return pc_launch<true, PC_TAB_SMALL>(e, in, p, o, read_list, n_blocks, s);
+        if (p.table == PC_TAB_BIG) return pc_launch<true, PC_TAB_BIG>(e, in, p, o, read_list, n_blocks, s);
+        return hipErrorInvalidValue;  // strict ids stop at 2,048 slots (then split)
     }
-    return hipGetLastError();
+    if (p.table == PC_TAB_SMALL) return pc_launch<false, PC_TAB_SMALL>(e, in, p, o, read_list, n_blocks, s);
+    if (p.table == PC_TAB_BIG) return pc_launch<false, PC_TAB_BIG>(e, in, p, o, read_list, n_blocks, s);
+    if (p.table == PC_TAB_HUGE) return pc_launch<false, PC_TAB_HUGE>(e, in, p, o, read_list, n_blocks, s);
+    return hipErrorInvalidValue;
 }
 
 // ---------------------------------------------------------------------------

@@ -168,6 +168,7 @@ struct PairParams {
     // global bucket path (big_n); if one did, the pass is discarded and re-run
     const uint32_t *abort;
     int32_t per_read;      // 1: emit into PairOut::rreg / rcnt (first pass, wide ids, dispatched pairs only)
+    uint32_t max_blocks;   // > 0: at most this many blocks per launch (item lists are sliced; tests)
 };
 
 // Device-wide counters are sharded NSHARD ways (shard = blockIdx % NSHARD) and

@@ -140,6 +140,17 @@ def test_many_partner_reads_recount_tiers(oracle_mod, n_edge):
     assert ov.stats()["role_pairs"] > 3 * n_mid * n_edge
     # the edge reads kept their per-read regions; only the middle reads were recounted
     assert ov.stats()["flags"] & 3 == sao.SA_STATS_PER_READ_REGIONS | sao.SA_STATS_RECOUNTED
+    # item lists sliced into launches of 3 workgroups (the path taken where a
+    # dispatch's 32-bit work-item count would wrap: configs[4]'s 6.25M-read
+    # slice in the 1,024-thread tier and its residue classes): same dispatch
+    sl = sao.Overlapper(id_mode=sao.SA_IDS_WIDE, launch_slice=3, **st)
+    sl.add_reads(reads)
+    sl.build()
+    l2, t2, c2 = sl.dispatch()
+    np.testing.assert_array_equal(l2, lead)
+    np.testing.assert_array_equal(t2, trail)
+    np.testing.assert_array_equal(c2, count)
+    sl.close()
 
 
 @pytest.mark.parametrize("shards", [4, 8])
