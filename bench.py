@@ -216,6 +216,8 @@ def main():
                     help="SA_OPT_ALIGN_KERNEL: 0 auto, 1 lane-group (LDS), 2 lane-per-pair")
     ap.add_argument("--replicas", action="store_true", help="torchrun: independent per-rank datasets, no exchange")
     ap.add_argument("--shards", type=int, default=1, help="virtual shards on one GPU (sharded path, device copies)")
+    ap.add_argument("--dispatch-hash", action="store_true",
+                    help="add a checksum of the dispatch list (lead, trail, count) to the line (cross-build checks)")
     ap.add_argument("--serial-shards", action="store_true",
                     help="virtual shards: run the shards one after another (clean per-shard stage times)")
     ap.add_argument("--check-shards", type=int, default=0,
@@ -541,6 +543,13 @@ def main():
                    "ovl_records": g_ovl.count(b"{OVL"), "ovl_identical": g_ovl == rc0.ovl}
 
     note("aligner timed")
+    dhash = None
+    if args.dispatch_hash:
+        ld, tr, ct = (np.asarray(x, dtype=np.uint64) for x in ov.dispatch())
+        w = np.arange(1, len(ld) + 1, dtype=np.uint64)
+        with np.errstate(over="ignore"):
+            dhash = "%016x" % int(np.bitwise_xor.reduce((ld * np.uint64(0x9E3779B97F4A7C15) + tr * np.uint64(
+                0xC2B2AE3D27D4EB4F) + ct * np.uint64(0x165667B19E3779F9)) * w) if len(ld) else 0)
     # ---- full-size parity property: S virtual shards == one device ----------
     check = None
     if args.check_shards > 1 and mode == "single":
@@ -602,6 +611,7 @@ def main():
             "cpu_baseline": cpu,
             "config0": config0,
             "check_shards": check,
+            "dispatch_hash": dhash,
         }
         print(json.dumps(line), flush=True)
     ov.close()
