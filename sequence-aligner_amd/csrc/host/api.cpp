@@ -1855,15 +1855,16 @@ int sa_dist_reduce(sa_ctx *c, const void *fst, const void *snd, const void *cnt_
     HIPCHK(hipMemsetAsync(cnt->totals, 0, sizeof(cnt->totals), c->stream));
     HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(cnt->overflow_n), c->stream));
     // this rank's leads: per-lead segments of the received partials, summed and
-    // filtered in LDS (one wave per lead), then one scan + one copy in lead-
-    // descending order; a lead with more than 192 distinct partners (high-copy
-    // repeats) falls back to the (lead, trail) radix sort below
+    // filtered in LDS (one wave per lead; one block for a lead with more than
+    // 192 distinct partners), then one scan + one copy in lead-descending
+    // order; a lead with more than 3,072 (high-copy repeats) falls back to the
+    // (lead, trail) radix sort below
     {
         uint32_t *lr;
         uint2 *seg = (uint2 *)ok;
-        ENSURE(c->d_lr, 5 * ((size_t)nl + 1), &lr);
+        ENSURE(c->d_lr, 6 * ((size_t)nl + 1), &lr);
         uint32_t *lcnt = lr, *loff = lr + ((size_t)nl + 1), *lcur = lr + 2 * ((size_t)nl + 1),
-                 *kcnt = lr + 3 * ((size_t)nl + 1), *kex = lr + 4 * ((size_t)nl + 1);
+                 *kcnt = lr + 3 * ((size_t)nl + 1), *kex = lr + 4 * ((size_t)nl + 1), *big = lr + 5 * ((size_t)nl + 1);
         uint8_t *scan2 = scan;
         Counters *hp;
         if (int rc_ = pinned_counters(c, &hp)) return rc_;
@@ -1871,7 +1872,7 @@ int sa_dist_reduce(sa_ctx *c, const void *fst, const void *snd, const void *cnt_
             StageScope st(c, SA_STAGE_ORDER);
             HIPCHK(launch_lead_reduce((const uint32_t *)fst, (const uint32_t *)snd, (const uint32_t *)cnt_in, n, lbase,
                                       nl, c->set.min_collisions, c->set.max_collisions, lcnt, loff, lcur, seg, kcnt,
-                                      cnt->distinct, &cnt->overflow_n, scan2, &cnt->totals[1], c->stream));
+                                      cnt->distinct, &cnt->overflow_n, big, scan2, &cnt->totals[1], c->stream));
             HIPCHK(exclusive_scan_u32(kcnt, kex, nl, &cnt->totals[0], scan2, c->stream));
         }
         HIPCHK(hipMemcpyAsync(hp, cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));

@@ -222,7 +222,8 @@ constexpr uint32_t LR_EMPTY = 0xFFFFFFFFu;
 // pairs counted (KmerTable.calcDispatchData's filter, :155-187)
 __global__ __launch_bounds__(256) void lead_reduce_kernel(uint2 *seg, const uint32_t *loff, uint32_t nl, int32_t min_c,
                                                           int32_t max_c, uint32_t *kcnt,
-                                                          unsigned long long *distinct, uint32_t *overflow) {
+                                                          unsigned long long *distinct, uint32_t *big_list,
+                                                          uint32_t *big_n) {
     __shared__ uint32_t key[4][LR_SLOTS], val[4][LR_SLOTS];
     __shared__ uint2 kept[4][LR_FILL];
     __shared__ uint32_t nd_blk;
@@ -262,8 +263,12 @@ __global__ __launch_bounds__(256) void lead_reduce_kernel(uint2 *seg, const uint
         }
         const uint32_t tot_nd = (uint32_t)__shfl((int)wave_incl_add(nd), 63, 64);
         if (tot_nd > LR_FILL || __any(ovf)) {
-            if (lane == 0) atomicOr(overflow, 1u);
-            if (lane == 0) kcnt[l] = 0;
+            // a lead with more partners than the wave table (high-copy repeats):
+            // listed for the block-per-lead pass (lead_reduce_big_kernel)
+            if (lane == 0) {
+                kcnt[l] = 0;
+                big_list[atomicAdd(big_n, 1u)] = l;
+            }
         } else {
             const uint32_t mine = __popc(kp);
             const uint32_t ex = wave_incl_add(mine) - mine;
@@ -280,12 +285,75 @@ __global__ __launch_bounds__(256) void lead_reduce_kernel(uint2 *seg, const uint
                 for (uint32_t q = 0; q < k; ++q) r += kept[w][q].x < e.x ? 1u : 0u;
                 seg[s0 + r] = e;  // (the segment's partials are all consumed)
             }
-            if (lane == 0) kcnt[l] = k;
+            if (lane == 0) {
+                kcnt[l] = k;
+                atomicAdd(&nd_blk, tot_nd);  // (a listed lead is counted by the block pass)
+            }
         }
-        if (lane == 0) atomicAdd(&nd_blk, tot_nd);
     }
     __syncthreads();
     if (threadIdx.x == 0 && nd_blk) atomicAdd(&distinct[blockIdx.x % NSHARD], (unsigned long long)nd_blk);
+}
+
+// the listed leads, one 256-thread block each (a fixed grid walks the list):
+// a 4,096-slot table (3,072 partners) summed and filtered as above, the kept
+// entries ranked by trail over the block; beyond 3,072 partners *overflow
+// sends the caller to the sort
+constexpr int LRB_SLOTS = 4096, LRB_FILL = 3072;
+
+__global__ __launch_bounds__(256) void lead_reduce_big_kernel(uint2 *seg, const uint32_t *loff, const uint32_t *big_list,
+                                                              const uint32_t *big_n, int32_t min_c, int32_t max_c,
+                                                              uint32_t *kcnt, unsigned long long *distinct,
+                                                              uint32_t *overflow) {
+    __shared__ uint32_t key[LRB_SLOTS], val[LRB_SLOTS];
+    __shared__ uint2 kept[LRB_FILL];
+    __shared__ uint32_t fill, bad, nk;
+    const uint32_t nb = *big_n;
+    for (uint32_t it = blockIdx.x; it < nb; it += gridDim.x) {
+        __syncthreads();  // the previous lead's LDS consumed
+        for (int j = threadIdx.x; j < LRB_SLOTS; j += 256) { key[j] = LR_EMPTY; val[j] = 0; }
+        if (threadIdx.x == 0) { fill = 0; bad = 0; nk = 0; }
+        __syncthreads();
+        const uint32_t l = big_list[it];
+        const uint32_t s0 = loff[l], m = loff[l + 1] - s0;
+        for (uint32_t j = threadIdx.x; j < m; j += 256) {
+            const uint2 v = seg[s0 + j];
+            uint32_t h = (v.x * 0x9E3779B1u) >> 20;  // 12 bits: LRB_SLOTS
+            int probe = 0;
+            for (; probe < 256; ++probe) {
+                uint32_t old = ((volatile uint32_t *)key)[h];
+                if (old == LR_EMPTY) old = atomicCAS(&key[h], LR_EMPTY, v.x);
+                if (old == LR_EMPTY || old == v.x) {
+                    if (old == LR_EMPTY && atomicAdd(&fill, 1u) >= LRB_FILL) bad = 1;
+                    atomicAdd(&val[h], v.y);
+                    break;
+                }
+                h = (h + 1) & (LRB_SLOTS - 1);
+            }
+            if (probe == 256) bad = 1;
+        }
+        __syncthreads();
+        if (bad) {
+            if (threadIdx.x == 0) atomicOr(overflow, 1u);
+            continue;
+        }
+        for (int j = threadIdx.x; j < LRB_SLOTS; j += 256) {
+            const uint32_t k = key[j], c = val[j];
+            if (k != LR_EMPTY && (int32_t)c >= min_c && (int32_t)c <= max_c) kept[atomicAdd(&nk, 1u)] = make_uint2(k, c);
+        }
+        __syncthreads();
+        const uint32_t k = nk;
+        for (uint32_t j = threadIdx.x; j < k; j += 256) {
+            const uint2 e = kept[j];
+            uint32_t r = 0;
+            for (uint32_t q = 0; q < k; ++q) r += kept[q].x < e.x ? 1u : 0u;
+            seg[s0 + r] = e;  // (every partial of the segment was read before the barrier)
+        }
+        if (threadIdx.x == 0) {
+            kcnt[l] = k;
+            atomicAdd(&distinct[blockIdx.x % NSHARD], (unsigned long long)fill);
+        }
+    }
 }
 
 // lead-descending dispatch: lead l's kept entries go to total - kex[l] - kcnt[l]
@@ -308,7 +376,7 @@ __global__ void lead_copy_kernel(const uint2 *seg, const uint32_t *loff, const u
 hipError_t launch_lead_reduce(const uint32_t *fst, const uint32_t *snd, const uint32_t *cnt, uint64_t n, uint32_t base,
                               uint32_t nl, int32_t min_c, int32_t max_c, uint32_t *lcnt, uint32_t *loff, uint32_t *lcur,
                               uint2 *seg, uint32_t *kcnt, unsigned long long *distinct, uint32_t *overflow,
-                              void *scan_tmp, uint32_t *total_dev, hipStream_t s) {
+                              uint32_t *big, void *scan_tmp, uint32_t *total_dev, hipStream_t s) {
     if (!nl) return hipSuccess;
     hipError_t e;
     if ((e = hipMemsetAsync(lcnt, 0, (size_t)nl * 4, s)) != hipSuccess) return e;
@@ -321,8 +389,11 @@ hipError_t launch_lead_reduce(const uint32_t *fst, const uint32_t *snd, const ui
     if ((e = hipMemcpyAsync(loff + nl, total_dev, 4, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
     if (n) hipLaunchKernelGGL(lead_tile_kernel<true>, tiles, dim3(LT_THREADS), 0, s, fst, snd, cnt, n, base, lcnt,
                               (const uint32_t *)loff, lcur, seg);
+    if ((e = hipMemsetAsync(big, 0, 4, s)) != hipSuccess) return e;
     hipLaunchKernelGGL(lead_reduce_kernel, dim3((nl + 3) / 4), dim3(256), 0, s, seg, loff, nl, min_c, max_c, kcnt,
-                       distinct, overflow);
+                       distinct, big + 1, big);
+    hipLaunchKernelGGL(lead_reduce_big_kernel, dim3(256), dim3(256), 0, s, seg, loff, (const uint32_t *)(big + 1),
+                       (const uint32_t *)big, min_c, max_c, kcnt, distinct, overflow);
     return hipGetLastError();
 }
 
