@@ -1083,6 +1083,8 @@ int device_build(sa_ctx *c, bool readback) {
     return SA_OK;
 }
 
+int host_results(sa_ctx *c);
+
 int device_align(sa_ctx *c, bool readback) {
     if (!c->built) return fail(c, SA_E_STATE, "sa_align before sa_build_candidates");
     const uint64_t nd = c->n_disp;
@@ -1240,6 +1242,7 @@ int device_align(sa_ctx *c, bool readback) {
     HIPCHK(hipStreamSynchronize(c->stream));
     resolve_timing(c);
     c->stats.aligned = nd;
+    c->stats.ovl_records = 0;  // (set when the records are formatted: host_results)
     c->stats.dp_cells = shard_sum(cells_s);
     if (err) {
         const char *msg = err == SA_E_NON_ACGT ? "non-ACGT base in an aligned region (HOXD MatchError)"
@@ -1248,24 +1251,35 @@ int device_align(sa_ctx *c, bool readback) {
                         : "alignment limit exceeded";
         return fail(c, err, msg);
     }
-    if (readback) {
-        c->alns.resize(nd);
-        if (nd) HIPCHK(hipMemcpy(c->alns.data(), out, nd * sizeof(sa_alignment), hipMemcpyDeviceToHost));
-        uint64_t rec = 0;
-        c->ovl.clear();
-        char buf[160];
-        for (uint64_t i = 0; i < nd; ++i) {
-            const sa_alignment &a = c->alns[i];
-            if (!(a.flags & SA_ALN_OVL_VALID)) continue;
-            const int ra = (a.flags & SA_ALN_DUD) ? 0 : a.lead, rb = (a.flags & SA_ALN_DUD) ? 0 : a.trail;
-            const int m = snprintf(buf, sizeof(buf), "{OVL\nadj:N\nrds:%d,%d\nscr:0\nahg:%d\nbhg:%d\n}\n", ra, rb,
-                                   a.ahg, a.bhg);
-            c->ovl.append(buf, (size_t)m);
-            ++rec;
-        }
-        c->stats.ovl_records = rec;
-    }
     c->aligned = true;
+    c->host_valid = false;
+    if (readback) return host_results(c);
+    return SA_OK;
+}
+
+// alignments read back and the .ovl records formatted (calcOverlaps,
+// Project4.scala:795-825; Overlap.print, ObjectStore.scala:127-135) for the
+// last alignment, once: sa_align does it at once, after sa_device_align the
+// getters / writer do it on first use (never a previous run's records)
+int host_results(sa_ctx *c) {
+    if (c->host_valid) return SA_OK;
+    const uint64_t nd = c->n_disp;
+    c->alns.resize(nd);
+    if (nd) HIPCHK(hipMemcpy(c->alns.data(), c->d_aln.p, nd * sizeof(sa_alignment), hipMemcpyDeviceToHost));
+    uint64_t rec = 0;
+    c->ovl.clear();
+    char buf[160];
+    for (uint64_t i = 0; i < nd; ++i) {
+        const sa_alignment &a = c->alns[i];
+        if (!(a.flags & SA_ALN_OVL_VALID)) continue;
+        const int ra = (a.flags & SA_ALN_DUD) ? 0 : a.lead, rb = (a.flags & SA_ALN_DUD) ? 0 : a.trail;
+        const int m = snprintf(buf, sizeof(buf), "{OVL\nadj:N\nrds:%d,%d\nscr:0\nahg:%d\nbhg:%d\n}\n", ra, rb,
+                               a.ahg, a.bhg);
+        c->ovl.append(buf, (size_t)m);
+        ++rec;
+    }
+    c->stats.ovl_records = rec;
+    c->host_valid = true;
     return SA_OK;
 }
 
@@ -1500,14 +1514,8 @@ int sa_device_align(sa_ctx *c) {
 int sa_get_alignments(sa_ctx *c, const sa_alignment **out, size_t *n) {
     if (!c || !out || !n) return SA_E_ARG;
     if (!c->aligned) return fail(c, SA_E_STATE, "no alignments");
-    if (multi_sharded(c)) {
-        int rc = multi_alignments(c);
-        if (rc) return rc;
-    } else if (c->alns.size() != c->n_disp) {
-        c->alns.resize(c->n_disp);
-        if (c->n_disp)
-            HIPCHK(hipMemcpy(c->alns.data(), c->d_aln.p, c->n_disp * sizeof(sa_alignment), hipMemcpyDeviceToHost));
-    }
+    const int rc = multi_sharded(c) ? multi_host_results(c) : host_results(c);
+    if (rc) return rc;
     *out = c->alns.data();
     *n = c->alns.size();
     return SA_OK;
@@ -1516,6 +1524,8 @@ int sa_get_alignments(sa_ctx *c, const sa_alignment **out, size_t *n) {
 int sa_get_ovl(sa_ctx *c, const char **text, size_t *len) {
     if (!c || !text || !len) return SA_E_ARG;
     if (!c->aligned) return fail(c, SA_E_STATE, "no alignments");
+    const int rc = multi_sharded(c) ? multi_host_results(c) : host_results(c);
+    if (rc) return rc;
     *text = c->ovl.data();
     *len = c->ovl.size();
     return SA_OK;
@@ -1523,14 +1533,25 @@ int sa_get_ovl(sa_ctx *c, const char **text, size_t *len) {
 
 int sa_write_ovl(sa_ctx *c, const char *path) {
     if (!c) return SA_E_ARG;
-    if (!c->aligned) return fail(c, SA_E_STATE, "no alignments");
     const std::string *text = &c->ovl;
     std::string all;
-    if (multi_rank_mode(c)) {  // collective: rank 0 writes every rank's records
-        int rc = multi_gather_ovl(c, all);
+    if (multi_rank_mode(c)) {
+        // collective: rank 0 writes every rank's records.  Every rank takes part
+        // in the status exchange whatever its own state, so one rank that has
+        // not aligned fails them all instead of leaving the others blocked in
+        // the gather; records after sa_device_align are formatted first
+        int rc = c->aligned ? multi_host_results(c) : SA_E_STATE;
+        const int rc_all = multi_all_ok(c, rc == SA_OK);
+        if (rc_all) return rc_all;
+        if (rc) return fail(c, rc, "no alignments");
+        rc = multi_gather_ovl(c, all);
         if (rc) return rc;
         if (multi_rank(c) != 0) return SA_OK;
         text = &all;
+    } else {
+        if (!c->aligned) return fail(c, SA_E_STATE, "no alignments");
+        const int rc = multi_sharded(c) ? multi_host_results(c) : host_results(c);
+        if (rc) return rc;
     }
     FILE *f = path ? fopen(path, "wb") : stdout;  // the file is deleted and recreated (Project4.scala:797-805)
     if (!f) return fail(c, SA_E_INPUT, std::string("cannot write ") + path);

@@ -130,6 +130,7 @@ struct sa_ctx {
     int aligner = SA_ALIGNER_LINEAR;  // SA_OPT_ALIGNER (--linear-align / --quadratic-align)
     uint64_t local_batch_bytes = 16ull << 30;  // traceback-code budget of one quadratic launch
     bool built = false, aligned = false;
+    bool host_valid = false;  // alns / ovl hold the last alignment's results (sa_align or first use)
     // results (host)
     std::vector<int32_t> lead, trail, count;
     std::vector<int32_t> pfst, psnd, pcnt;
@@ -155,7 +156,8 @@ void multi_destroy(sa_ctx *c);
 int multi_build(sa_ctx *c, bool readback, int (*single_build)(sa_ctx *, bool));
 int multi_dispatch(sa_ctx *c);
 int multi_align(sa_ctx *c, bool readback, int (*single_align)(sa_ctx *, bool));
-int multi_alignments(sa_ctx *c);
+int multi_host_results(sa_ctx *c);
+int multi_all_ok(sa_ctx *c, bool ok);
 int multi_gather_ovl(sa_ctx *c, std::string &all);
 int multi_set_option(sa_ctx *c, int option, int64_t value);
 void multi_stage_times(const sa_ctx *c, double *ms, uint64_t *n);

@@ -558,38 +558,51 @@ int multi_align(sa_ctx *c, bool readback, int (*single_align)(sa_ctx *, bool)) {
     }
     c->alns.clear();
     c->ovl.clear();
-    if (readback) {
-        std::vector<std::vector<sa_alignment>> A(m->sh.size());
-        std::vector<std::string> O(m->sh.size());
-        for (size_t i = 0; i < m->sh.size(); ++i) {
-            const sa_alignment *p;
-            size_t n;
-            if ((rc = sa_get_alignments(m->sh[i].child, &p, &n))) return set_err(c, rc, sa_last_error(m->sh[i].child));
-            A[i].assign(p, p + n);
-            const char *t;
-            size_t tl;
-            if ((rc = sa_get_ovl(m->sh[i].child, &t, &tl))) return set_err(c, rc, sa_last_error(m->sh[i].child));
-            O[i].assign(t, tl);
-        }
-        concat_desc(c, c->alns, A);
-        for (size_t i = O.size(); i-- > 0;) c->ovl += O[i];
-    }
     c->aligned = true;
-    return SA_OK;
+    c->host_valid = false;
+    return readback ? multi_host_results(c) : SA_OK;
 }
 
-int multi_alignments(sa_ctx *c) {
+// every local shard's alignments and .ovl records (read back and formatted by
+// the shard on first use), concatenated in descending shard order
+int multi_host_results(sa_ctx *c) {
+    if (c->host_valid) return SA_OK;
     sa_multi *m = c->multi;
-    if (c->alns.size() == c->stats.aligned) return SA_OK;
     std::vector<std::vector<sa_alignment>> A(m->sh.size());
+    std::vector<std::string> O(m->sh.size());
+    uint64_t recs = 0;
     for (size_t i = 0; i < m->sh.size(); ++i) {
+        (void)hipSetDevice(m->sh[i].device);
         const sa_alignment *p;
         size_t n;
         int rc = sa_get_alignments(m->sh[i].child, &p, &n);
         if (rc) return set_err(c, rc, sa_last_error(m->sh[i].child));
         A[i].assign(p, p + n);
+        const char *t;
+        size_t tl;
+        if ((rc = sa_get_ovl(m->sh[i].child, &t, &tl))) return set_err(c, rc, sa_last_error(m->sh[i].child));
+        O[i].assign(t, tl);
+        sa_stats st;
+        sa_get_stats(m->sh[i].child, &st);
+        recs += st.ovl_records;
     }
     concat_desc(c, c->alns, A);
+    c->ovl.clear();
+    for (size_t i = O.size(); i-- > 0;) c->ovl += O[i];
+    c->stats.ovl_records = recs;
+    c->host_valid = true;
+    return SA_OK;
+}
+
+// rank mode, collective: every rank learns whether every rank is ok
+int multi_all_ok(sa_ctx *c, bool ok) {
+    sa_multi *m = c->multi;
+    Shard &s = m->sh[0];
+    s.cnt.assign(m->P, ok ? 1 : 0);
+    int rc = exchange_counts(c);
+    if (rc) return rc;
+    for (int q = 0; q < m->P; ++q)
+        if (!s.rcnt[q]) return set_err(c, SA_E_STATE, "rank " + std::to_string(q) + " has no alignments to write");
     return SA_OK;
 }
 

@@ -116,12 +116,45 @@ def test_rank_mode_one_rank_rccl(tmp_path):
     ov = sao.Overlapper(rank=0, nranks=1, rccl_id=uid, **st)
     ov.add_reads(reads)
     ov.build()
+    # the collective writer fails on every rank (here: the only one) when a
+    # rank has not aligned, instead of blocking in the gather
+    with pytest.raises(sao.SAError) as ei:
+        ov.write_ovl(str(tmp_path / "none.ovl"))
+    assert ei.value.name == "SA_E_STATE"
     ov.build()
     ov.align()
     assert_same(ov, ref)
     path = str(tmp_path / "r.ovl")
     ov.write_ovl(path)
     assert open(path, "rb").read() == ref.ovl()
+    # after a device-only align the writer formats this run's records (not
+    # an earlier run's, and not an empty file)
+    ov.device_align()
+    path2 = str(tmp_path / "r2.ovl")
+    ov.write_ovl(path2)
+    assert open(path2, "rb").read() == ref.ovl()
+
+
+@pytest.mark.parametrize("shards", [1, 4])
+def test_device_align_then_results(shards):
+    """sa_device_align leaves the records on the device; the getters read them
+    back on first use and never return a previous run's (the quadratic
+    aligner run in between gives different alignments)."""
+    reads, st = workload(101)
+    ov = sao.Overlapper(shards=shards, **st) if shards > 1 else sao.Overlapper(**st)
+    ov.add_reads(reads)
+    ov.build()
+    ov.align()
+    want_aln, want_ovl = ov.alignments(), ov.ovl()
+    ov.set_aligner(sao.SA_ALIGNER_QUADRATIC)
+    ov.align()
+    quad_ovl = ov.ovl()
+    ov.set_aligner(sao.SA_ALIGNER_LINEAR)
+    ov.device_align()
+    assert ov.ovl() == want_ovl
+    np.testing.assert_array_equal(ov.alignments(), want_aln)
+    assert ov.stats()["ovl_records"] == want_ovl.count(b"{OVL")
+    assert len(quad_ovl) > 0
 
 
 def test_multi_gpu_context_if_available():
