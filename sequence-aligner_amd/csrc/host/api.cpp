@@ -346,7 +346,7 @@ int ensure_prepared(sa_ctx *c) {
 int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, uint32_t *vals2, uint64_t n,
                  const uint64_t *occ_off, uint32_t n_reads, uint32_t npr, const uint2 *rl,
                  const int32_t *len, bool strict, void *stmp, Counters *cnt, PartArgs &PA,
-                 unsigned long long &big_buckets, int skip_bits = 0, int phase = 0) {
+                 unsigned long long &big_buckets, int skip_bits = 0, int phase = 0, const uint32_t *pv = nullptr) {
     // phase 0: everything; 1: sort + LDS tiers, no readback (the caller's
     // first pair-count pass aborts on big_n); 2: only the global path of the
     // partitions phase 1 listed (keys / PA as phase 1 left them)
@@ -364,6 +364,7 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
     const uint32_t nparts = 1u << PB;
     const int kbits = 32 + c->lb;  // LDS sort key: mix << lb | loc rank
     uint2 *srl = nullptr;
+    const uint32_t *spv = nullptr;
     uint32_t *pstart, *biglist;
     ENSURE(c->d_pstart, nparts + 1, &pstart);
     ENSURE(c->d_biglist, 3 * ((size_t)nparts + 1), &biglist);  // big list, mid list, mid2 list
@@ -371,7 +372,15 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
     if (phase != 2) {
         {
             StageScope st(c, SA_STAGE_SORT);
-            if (rl) {
+            if (pv) {
+                // the occurrence table packed into 4 bytes (read << lb | loc rank)
+                // rides along as the sort's value: 12-byte records through the
+                // passes instead of 16 (vals / vals2 are free until the global path)
+                uint32_t *v0 = vals, *v1 = vals2;
+                if (n) HIPCHK(hipMemcpyAsync(v0, pv, n * 4, hipMemcpyDeviceToDevice, c->stream));
+                HIPCHK(radix_sort(&keys, &v0, &keys2, &v1, n, 64 - skip_bits - PB, 64 - skip_bits, stmp, c->stream));
+                spv = v0;
+            } else if (rl) {
                 // an occurrence table rides along as the sort's 8-byte value, so the
                 // bucket build reads each record's {read, loc rank} coalesced instead
                 // of gathering it (16-byte records through the two passes)
@@ -391,13 +400,13 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
         PA.sk = keys; PA.sv = nullptr; PA.start = pstart; PA.np = nparts; PA.lb = c->lb; PA.sort_bits = kbits - skip_bits - PB;
         PA.tagtab = (const uint8_t *)c->d_tagtab.p;
         PA.occ_off = occ_off;
-        PA.n_reads = n_reads; PA.npr = npr; PA.rl = rl; PA.srl = srl;
+        PA.n_reads = n_reads; PA.npr = npr; PA.rl = rl; PA.srl = srl; PA.pv = pv; PA.spv = spv;
             PA.npr_magic = npr >= 2 ? ~0ull / npr + 1 : 0;
         PA.len = len;
         PA.lbase = (const uint32_t *)c->d_lbase.p;
         PA.lrank = (const uint32_t *)c->d_lrank.p;
         PA.k = c->set.kmer_size;
-        PA.pos_bits = rl ? 0 : c->pos_bits;  // (occurrence indices + the {read, loc rank} table)
+        PA.pos_bits = rl || pv ? 0 : c->pos_bits;  // (occurrence indices + the {read, loc rank} table)
         PA.meta = (const uint2 *)c->d_meta.p;
         ENSURE(c->d_md, 3 * n + 3, &PA.lst);
         ENSURE(c->d_rec, n + 1, &PA.rec);
@@ -1773,6 +1782,10 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint6
     ENSURE(c->d_seg, seg.size(), &dseg);
     HIPCHK(hipMemcpyAsync(dseg, seg.data(), seg.size() * 8, hipMemcpyHostToDevice, c->stream));
     ENSURE(c->d_rl, n, &rl);
+    // reads and loc ranks fit 4 bytes (e.g. 800k global reads of 500 bp: 20 + 9
+    // bits): the occurrence table is packed, 12-byte records in the partition sort
+    const bool packed = bits_for(N ? N - 1 : 0) + c->lb <= 32;
+    uint32_t *pv = packed ? (uint32_t *)rl : nullptr;
     ENSURE(c->d_loff, (size_t)N + 1, &loff);
     ENSURE(c->d_vals, n, &vals);
     ENSURE(c->d_vals2, n, &vals2);
@@ -1786,13 +1799,14 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint6
         HIPCHK(launch_prepare_received(keys, n, dseg, (uint32_t)P, (const uint32_t *)c->d_starts.p,
                                        (const uint64_t *)c->d_gocc.p, c->gnpr,
                                        (const int32_t *)c->d_glen.p, (const uint32_t *)c->d_lbase.p,
-                                       (const uint32_t *)c->d_lrank.p, c->set.kmer_size, rl, c->stream));
-        HIPCHK(launch_local_offsets(rl, n, N, loff, c->stream));
+                                       (const uint32_t *)c->d_lrank.p, c->set.kmer_size, packed ? nullptr : rl, pv,
+                                       c->lb, c->stream));
+        HIPCHK(launch_local_offsets(packed ? nullptr : rl, pv, c->lb, n, N, loff, c->stream));
     }
     PartArgs PA{};
     unsigned long long big_buckets = 0;
-    rc = bucket_stage(c, keys, keys2, vals, vals2, n, loff, N, 0, rl, nullptr, false, stmp, cnt, PA,
-                      big_buckets, c->log_ranks);
+    rc = bucket_stage(c, keys, keys2, vals, vals2, n, loff, N, 0, packed ? nullptr : rl, nullptr, false, stmp, cnt,
+                      PA, big_buckets, c->log_ranks, 0, pv);
     if (rc) return rc;
     PairIn PI{};
     PI.rec = PA.rec; PI.xrec = PA.xrec; PI.lst = PA.lst;

@@ -34,7 +34,7 @@ __global__ void iota_kernel(uint32_t *v, uint64_t n) {
 __global__ void prepare_received_kernel(uint64_t *recs, uint64_t n, const uint64_t *seg, uint32_t P,
                                         const uint32_t *starts, const uint64_t *occ_off, uint32_t npr,
                                         const int32_t *len, const uint32_t *lbase, const uint32_t *lrank, int32_t k,
-                                        uint2 *rl) {
+                                        uint2 *rl, uint32_t *pv, int lb) {
     const uint64_t i = (uint64_t)blockIdx.x * DT + threadIdx.x;
     if (i >= n) return;
     uint32_t s = 0, hi = P;  // the source whose segment holds i
@@ -58,7 +58,9 @@ __global__ void prepare_received_kernel(uint64_t *recs, uint64_t n, const uint64
         r = lo;
         pos = (uint32_t)(g - occ_off[r]);
     }
-    rl[i] = make_uint2(r, lrank[lbase[(npr ? (int32_t)npr + k - 1 : len[r]) - k] + pos]);
+    const uint32_t lr = lrank[lbase[(npr ? (int32_t)npr + k - 1 : len[r]) - k] + pos];
+    if (pv) pv[i] = (r << lb) | lr;
+    else rl[i] = make_uint2(r, lr);
     recs[i] = (rec & 0xFFFFFFFF00000000ull) | (uint32_t)i;
 }
 
@@ -66,11 +68,13 @@ __global__ void prepare_received_kernel(uint64_t *recs, uint64_t n, const uint64
 // the local occurrences of read a are [loff[a], loff[a+1]).  One pass over the
 // records: record i starts the reads (rl[i-1].x, rl[i].x] (usually one), the
 // last record closes the reads after it
-__global__ void local_offsets_kernel(const uint2 *rl, uint64_t n, uint32_t n_reads, uint64_t *loff) {
+__global__ void local_offsets_kernel(const uint2 *rl, const uint32_t *pv, int lb, uint64_t n, uint32_t n_reads,
+                                     uint64_t *loff) {
     const uint64_t i = (uint64_t)blockIdx.x * DT + threadIdx.x;
     if (i > n) return;
-    const uint32_t prev = i == 0 ? 0u : rl[i - 1].x + 1u;  // first read not yet started
-    const uint32_t cur = i == n ? n_reads + 1u : rl[i].x + 1u;
+    auto read_of = [&](uint64_t j) { return pv ? pv[j] >> lb : rl[j].x; };
+    const uint32_t prev = i == 0 ? 0u : read_of(i - 1) + 1u;  // first read not yet started
+    const uint32_t cur = i == n ? n_reads + 1u : read_of(i) + 1u;
     for (uint32_t a = prev; a < cur; ++a) loff[a] = i;
 }
 
@@ -415,15 +419,16 @@ hipError_t launch_iota(uint32_t *v, uint64_t n, hipStream_t s) {
 hipError_t launch_prepare_received(uint64_t *recs, uint64_t n, const uint64_t *seg, uint32_t P,
                                    const uint32_t *starts, const uint64_t *occ_off, uint32_t npr, const int32_t *len,
                                    const uint32_t *lbase, const uint32_t *lrank, int32_t k, uint2 *rl,
-                                   hipStream_t s) {
+                                   uint32_t *pv, int lb, hipStream_t s) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(prepare_received_kernel, grid_for(n), dim3(DT), 0, s, recs, n, seg, P, starts, occ_off, npr,
-                       len, lbase, lrank, k, rl);
+                       len, lbase, lrank, k, rl, pv, lb);
     return hipGetLastError();
 }
 
-hipError_t launch_local_offsets(const uint2 *rl, uint64_t n, uint32_t n_reads, uint64_t *loff, hipStream_t s) {
-    hipLaunchKernelGGL(local_offsets_kernel, grid_for(n + 1), dim3(DT), 0, s, rl, n, n_reads, loff);
+hipError_t launch_local_offsets(const uint2 *rl, const uint32_t *pv, int lb, uint64_t n, uint32_t n_reads,
+                                uint64_t *loff, hipStream_t s) {
+    hipLaunchKernelGGL(local_offsets_kernel, grid_for(n + 1), dim3(DT), 0, s, rl, pv, lb, n, n_reads, loff);
     return hipGetLastError();
 }
 

@@ -53,13 +53,17 @@ __device__ __forceinline__ uint64_t load_sk(const uint64_t *p) { return __builti
 // an occurrence table, the record's {read, loc rank} entry rlp gives the loc
 // rank and the read (rr, else untouched)
 __device__ __forceinline__ unsigned long long record_key(uint64_t rec, const PartArgs &A, uint32_t &code,
-                                                         uint32_t &rr, const uint2 *rlp) {
+                                                         uint32_t &rr, const uint2 *rlp, const uint32_t *pvp) {
     code = (uint32_t)rec;
     const uint32_t g = code;
     uint32_t lr;
     if (A.pos_bits) {
         const uint32_t pos = code & ((1u << A.pos_bits) - 1u);
         lr = A.lrank[A.meta[code >> A.pos_bits].y + pos];
+    } else if (pvp) {  // packed read << lb | loc rank
+        const uint32_t v = *pvp;
+        lr = v & ((1u << A.lb) - 1u);
+        rr = v >> A.lb;
     } else if (rlp) {
         const uint2 v = *rlp;
         lr = v.y;
@@ -217,7 +221,8 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
             const uint32_t i = tid + j * PB_THREADS, ic = i < n ? i : n - 1;
             rr[j] = 0;
             const uint2 *rlp = A.srl ? A.srl + ps + ic : (A.rl ? A.rl + (uint32_t)recs[j] : nullptr);
-            kk[j] = record_key(recs[j], A, gg[j], rr[j], rlp);
+            const uint32_t *pvp = A.spv ? A.spv + ps + ic : (A.pv ? A.pv + (uint32_t)recs[j] : nullptr);
+            kk[j] = record_key(recs[j], A, gg[j], rr[j], rlp, pvp);
         }
 #pragma unroll
         for (int j = 0; j < IT; ++j) {
@@ -405,7 +410,7 @@ template <int CAP, bool STRICT>
 __global__ __launch_bounds__(PB_THREADS) void part_build_kernel(PartArgs A) {
     extern __shared__ __align__(16) uint8_t smem_raw[];
     PartShared<CAP> &S = *reinterpret_cast<PartShared<CAP> *>(smem_raw);
-    uint32_t *Sr = A.rl ? reinterpret_cast<uint32_t *>(smem_raw + sizeof(PartShared<CAP>)) : nullptr;
+    uint32_t *Sr = A.rl || A.pv ? reinterpret_cast<uint32_t *>(smem_raw + sizeof(PartShared<CAP>)) : nullptr;
     if constexpr (CAP < 2048) {
         part_build_one<CAP, STRICT>(A, blockIdx.x, S, Sr);
     } else {
@@ -542,7 +547,7 @@ hipError_t launch_part_build(const PartArgs &a, bool strict, int cap, hipStream_
     if (!a.np) return hipSuccess;
 #define PB_LAUNCH(CAPV, GRID, ST)                                                                          \
     do {                                                                                                 \
-        const size_t lds = part_lds<CAPV>() + (a.rl ? 4 * (size_t)(CAPV) : 0);                           \
+        const size_t lds = part_lds<CAPV>() + (a.rl || a.pv ? 4 * (size_t)(CAPV) : 0);                   \
         (void)hipFuncSetAttribute((const void *)part_build_kernel<CAPV, ST>,                             \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                 \
         hipLaunchKernelGGL((part_build_kernel<CAPV, ST>), dim3(GRID), dim3(PB_THREADS), lds, s, a);     \
@@ -564,7 +569,8 @@ __global__ void convert_records_kernel(const uint64_t *rec8, uint32_t n, PartArg
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint32_t code, r;
-    okeys[i] = record_key(rec8[i], A, code, r, A.rl ? A.rl + (uint32_t)rec8[i] : nullptr);
+    okeys[i] = record_key(rec8[i], A, code, r, A.rl ? A.rl + (uint32_t)rec8[i] : nullptr,
+                          A.pv ? A.pv + (uint32_t)rec8[i] : nullptr);
     // the global scan path indexes by occurrence: decode a (read, pos) code
     ovals[i] = A.pos_bits ? A.meta[code >> A.pos_bits].x + (code & ((1u << A.pos_bits) - 1u)) : code;
 }

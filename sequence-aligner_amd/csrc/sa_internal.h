@@ -287,6 +287,10 @@ struct PartArgs {
     uint64_t npr_magic;          // floor((2^64 - 1) / npr) + 1 (npr >= 2): read_of_g's division
     const uint2 *rl;             // {read, loc rank} by occurrence index (distributed mode, mixed lengths) or null
     const uint2 *srl;            // the same, sorted with the records (aligned with sk) or null
+    // or packed into 4 bytes when read bits + lb <= 32 (12-byte records through
+    // the partition sort instead of 16): read << lb | loc rank, by occurrence
+    // index (pv) and sorted with the records (spv)
+    const uint32_t *pv, *spv;
     // sk holds 8-byte records (mix32 << 32 | occurrence index); the loc rank is
     // rl[g].y when given (distributed mode, mixed lengths), else re-derived from
     // the read's length and the position (lrank[lbase[L - k] + pos])
@@ -401,11 +405,13 @@ hipError_t launch_kmer_hist(const uint64_t *sorted, uint64_t n, uint32_t *flag, 
 
 // distributed (multi-GPU) glue, dist.hip
 hipError_t launch_iota(uint32_t *v, uint64_t n, hipStream_t s);
+// rl[i] = {read, loc rank}; or, with pv, pv[i] = read << lb | loc rank
 hipError_t launch_prepare_received(uint64_t *recs, uint64_t n, const uint64_t *seg, uint32_t P,
                                    const uint32_t *starts, const uint64_t *occ_off, uint32_t npr, const int32_t *len,
                                    const uint32_t *lbase, const uint32_t *lrank, int32_t k, uint2 *rl,
-                                   hipStream_t s);
-hipError_t launch_local_offsets(const uint2 *rl, uint64_t n, uint32_t n_reads, uint64_t *loff, hipStream_t s);
+                                   uint32_t *pv, int lb, hipStream_t s);
+hipError_t launch_local_offsets(const uint2 *rl, const uint32_t *pv, int lb, uint64_t n, uint32_t n_reads,
+                                uint64_t *loff, hipStream_t s);
 hipError_t launch_owner_bounds(const uint64_t *keys, uint64_t n, int shift, uint32_t P, uint64_t *bounds,
                                hipStream_t s);
 hipError_t launch_gather_partials(const uint32_t *perm, uint64_t n, const uint32_t *fst, const uint32_t *snd,
