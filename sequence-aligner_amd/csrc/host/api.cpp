@@ -1720,13 +1720,16 @@ int sa_dist_emit(sa_ctx *c, void *send_recs, uint64_t *counts) {
     uint64_t *keys, *keys2; uint8_t *stmp;
     ENSURE(c->d_keys, n, &keys);
     ENSURE(c->d_sorttmp, std::max(radix_sort_temp_bytes(n), buckets_temp_bytes(n)), &stmp);
-    {
+    // reads of <= 1,024 bases: packing and emission in one kernel, as on one device
+    const bool fused = c->maxL <= 1024;
+    if (!fused) {
         StageScope st(c, SA_STAGE_PACK);
         HIPCHK(launch_pack_reads(R, c->stream));
     }
     {
         StageScope st(c, SA_STAGE_EMIT);
-        HIPCHK(launch_kmer_emit(R, E, keys, nullptr, c->stream));
+        if (fused) HIPCHK(launch_pack_emit(R, E, keys, c->stream));
+        else HIPCHK(launch_kmer_emit(R, E, keys, nullptr, c->stream));
     }
     // owner = top log2(P) bits of the mixed hash: one stable radix pass groups
     // the 8-byte records by owner and keeps them in occurrence order within each

@@ -31,23 +31,33 @@ __global__ void iota_kernel(uint32_t *v, uint64_t n) {
 // the global occurrence index of source s's first k-mer, starts[s] its first
 // read.  rl[i] = {read of the occurrence, its loc rank (lrank[lbase[L - k] +
 // pos])}; the low word becomes i
-__global__ void prepare_received_kernel(uint64_t *recs, uint64_t n, const uint64_t *seg, uint32_t P,
-                                        const uint32_t *starts, const uint64_t *occ_off, uint32_t npr,
-                                        const int32_t *len, const uint32_t *lbase, const uint32_t *lrank, int32_t k,
-                                        uint2 *rl, uint32_t *pv, int lb) {
+__global__ void prepare_received_kernel(uint64_t *recs, uint64_t n, const uint64_t *__restrict__ seg, uint32_t P,
+                                        const uint32_t *__restrict__ starts, const uint64_t *occ_off, uint32_t npr,
+                                        const int32_t *len, const uint32_t *__restrict__ lbase,
+                                        const uint32_t *lrank, int32_t k, uint2 *rl, uint32_t *pv, int lb,
+                                        unsigned long long npr_magic) {
     const uint64_t i = (uint64_t)blockIdx.x * DT + threadIdx.x;
     if (i >= n) return;
-    uint32_t s = 0, hi = P;  // the source whose segment holds i
+    // the source whose segment holds i: searched once per wave on its first
+    // record (wave-uniform: scalar loads, no dependent vector round trips),
+    // then stepped forward by the few lanes past a segment boundary
+    const uint64_t i0 = (uint64_t)blockIdx.x * DT + (threadIdx.x & ~63u);
+    uint32_t s = 0, hi = P;
     while (hi - s > 1) {
         const uint32_t mid = (s + hi) >> 1;
-        if (seg[mid] <= i) s = mid; else hi = mid;
+        if (seg[mid] <= i0) s = mid; else hi = mid;
     }
+    s = (uint32_t)__builtin_amdgcn_readfirstlane((int)s);
+    while (s + 1 < P && seg[s + 1] <= i) ++s;
     const uint64_t rec = recs[i];
     const uint32_t local = (uint32_t)rec;
     uint32_t r, pos;
     if (npr) {
-        r = starts[s] + local / npr;
-        pos = local % npr;
+        // local / npr as the high word of local * magic (magic = floor((2^64 - 1) /
+        // npr) + 1: exact for local, npr < 2^32; partition.hip read_of_g)
+        const uint32_t q = npr == 1 ? local : (uint32_t)__umul64hi((unsigned long long)local, npr_magic);
+        r = starts[s] + q;
+        pos = local - q * npr;
     } else {
         const uint64_t g = seg[P + 1 + s] + local;
         uint32_t lo = starts[s], up = starts[s + 1];  // largest r with occ_off[r] <= g
@@ -58,7 +68,7 @@ __global__ void prepare_received_kernel(uint64_t *recs, uint64_t n, const uint64
         r = lo;
         pos = (uint32_t)(g - occ_off[r]);
     }
-    const uint32_t lr = lrank[lbase[(npr ? (int32_t)npr + k - 1 : len[r]) - k] + pos];
+    const uint32_t lr = lrank[(npr ? lbase[npr - 1] : lbase[len[r] - k]) + pos];
     if (pv) pv[i] = (r << lb) | lr;
     else rl[i] = make_uint2(r, lr);
     recs[i] = (rec & 0xFFFFFFFF00000000ull) | (uint32_t)i;
@@ -422,7 +432,7 @@ hipError_t launch_prepare_received(uint64_t *recs, uint64_t n, const uint64_t *s
                                    uint32_t *pv, int lb, hipStream_t s) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(prepare_received_kernel, grid_for(n), dim3(DT), 0, s, recs, n, seg, P, starts, occ_off, npr,
-                       len, lbase, lrank, k, rl, pv, lb);
+                       len, lbase, lrank, k, rl, pv, lb, npr >= 2 ? ~0ull / npr + 1 : 0ull);
     return hipGetLastError();
 }
 
