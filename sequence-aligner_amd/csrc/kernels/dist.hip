@@ -193,7 +193,7 @@ __global__ __launch_bounds__(LT_THREADS) void lead_tile_kernel(const uint32_t *f
         if (l[j] == 0xFFFFFFFFu) continue;
         uint32_t h = (l[j] * 0x9E3779B1u) >> 22;  // 10 bits: LT_SLOTS
         for (int probe = 0; probe < 32; ++probe) {
-            uint32_t old = ((volatile uint32_t *)key)[h];
+            uint32_t old = lds_relaxed(&key[h]);
             if (old == 0xFFFFFFFFu) old = atomicCAS(&key[h], 0xFFFFFFFFu, l[j]);
             if (old == 0xFFFFFFFFu || old == l[j]) {
                 slot[j] = h;
@@ -255,7 +255,7 @@ __global__ __launch_bounds__(256) void lead_reduce_kernel(uint2 *seg, const uint
             uint32_t h = (v.x * 0x9E3779B1u) >> 24;
             int probe = 0;
             for (; probe < 64; ++probe) {
-                uint32_t old = ((volatile uint32_t *)key[w])[h];
+                uint32_t old = lds_relaxed(&key[w][h]);
                 if (old == LR_EMPTY) old = atomicCAS(&key[w][h], LR_EMPTY, v.x);
                 if (old == LR_EMPTY || old == v.x) { atomicAdd(&val[w][h], v.y); break; }
                 h = (h + 1) & (LR_SLOTS - 1);
@@ -335,7 +335,7 @@ __global__ __launch_bounds__(256) void lead_reduce_big_kernel(uint2 *seg, const 
             uint32_t h = (v.x * 0x9E3779B1u) >> 20;  // 12 bits: LRB_SLOTS
             int probe = 0;
             for (; probe < 256; ++probe) {
-                uint32_t old = ((volatile uint32_t *)key)[h];
+                uint32_t old = lds_relaxed(&key[h]);
                 if (old == LR_EMPTY) old = atomicCAS(&key[h], LR_EMPTY, v.x);
                 if (old == LR_EMPTY || old == v.x) {
                     if (old == LR_EMPTY && atomicAdd(&fill, 1u) >= LRB_FILL) bad = 1;

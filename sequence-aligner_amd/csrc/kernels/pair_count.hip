@@ -114,12 +114,12 @@ __device__ __forceinline__ void pc_insert(PcShared<TAB> &S, PcSharedStrict<TAB> 
     constexpr int PMAX = TAB / 4 < PC_PROBE_MAX ? TAB / 4 : PC_PROBE_MAX;
     for (int probe = 0; probe < PMAX; ++probe) {
         if constexpr (TAB >= PC_TAB_BIG)
-            if ((probe & 15) == 15 && ((volatile uint32_t *)&S.overflow)[0]) return;
+            if ((probe & 15) == 15 && lds_relaxed(&S.overflow)) return;
         // a slot's key goes EMPTY -> partner once and never changes again, so a
         // plain LDS read that sees a key is final: hits (>99% of inserts -- a read
         // meets each partner in ~100 shared k-mers) take one atomic, not two, and
         // the CAS only runs on a slot that still reads EMPTY
-        uint32_t old = ((volatile uint32_t *)S.key)[slot];
+        uint32_t old = lds_relaxed(&S.key[slot]);
         if (old == PC_EMPTY) old = atomicCAS(&S.key[slot], PC_EMPTY, partner);
         if (old == PC_EMPTY || old == partner) {
             if (old == PC_EMPTY && atomicAdd(&S.fill, 1u) >= FILL_MAX) {
@@ -464,7 +464,7 @@ __device__ __forceinline__ void pcm_insert(PcmShared &S, unsigned long long key,
     constexpr uint32_t FILL_MAX = PCM_TAB * 3 / 4;
     uint32_t slot = pcm_hash(key);
     for (int probe = 0; probe < PC_PROBE_MAX; ++probe) {  // bounded as in pc_insert
-        unsigned long long old = ((volatile unsigned long long *)S.key)[slot];  // final once set (pc_insert)
+        unsigned long long old = lds_relaxed(&S.key[slot]);  // final once set (pc_insert)
         if (old == PCM_EMPTY) old = atomicCAS(&S.key[slot], PCM_EMPTY, key);
         if (old == PCM_EMPTY || old == key) {
             if (old == PCM_EMPTY && atomicAdd(&S.fill, 1u) >= FILL_MAX) S.overflow = 1;

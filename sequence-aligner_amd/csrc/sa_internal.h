@@ -105,6 +105,14 @@ __device__ __forceinline__ uint2 encode_rec(uint64_t c, uint32_t nE, uint32_t nD
 __device__ __forceinline__ uint4 decoded_rec(uint64_t c, uint32_t nE, uint32_t nD, uint32_t me) {
     return make_uint4((uint32_t)c, nE | (me << 30), (uint32_t)(c >> 32), nD);
 }
+// Relaxed LDS load of a word other lanes may be updating (hash-table keys,
+// flags): a volatile access through a generic pointer compiles to a FLAT load
+// (vmcnt + lgkmcnt waits that also drain every outstanding global load); the
+// relaxed atomic keeps the LDS address space -> one ds_read
+template <typename T>
+__device__ __forceinline__ T lds_relaxed(T *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 __device__ __forceinline__ uint4 decode_rec(uint2 r, const uint4 *xrec) {
     if ((r.y >> 30) == 3u) return xrec[r.y & 0x3FFFFFFFu];
     return decoded_rec(((uint64_t)((r.y >> 28) & 3u) << 32) | r.x, r.y & 0x3FFFu, (r.y >> 14) & 0x3FFFu, r.y >> 30);
