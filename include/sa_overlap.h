@@ -136,6 +136,15 @@ int sa_get_alignments(sa_ctx *ctx, const sa_alignment **out, size_t *n);
 int sa_write_ovl(sa_ctx *ctx, const char *path);
 /* The same bytes into a library-owned buffer. */
 int sa_get_ovl(sa_ctx *ctx, const char **text, size_t *len);
+/* AMOS message file for `bank-transact -c -b X.bnk -m X.afg` (SURVEY.md 8(f)
+ * rank 1): the bank toAmos_new builds from the .seq (Rakefile.rb:174) and the
+ * .ovl that bank-transact -m loads into it (:180-184), in one file.  One {RED}
+ * per read in id order (iid = read id, eid = eids[id - 1], or the id when eids
+ * or the entry is NULL / empty; seq = the read as the context holds it; qlt =
+ * '0' + quality on every base, quality 0..60; clr and qcr = 0,len), then the
+ * {OVL} records of sa_write_ovl, byte for byte.  One-process contexts only
+ * (SA_E_ARG in rank mode); SA_E_STATE before an alignment. */
+int sa_write_afg(sa_ctx *ctx, const char *path, const char *const *eids, int quality);
 
 /* Options. */
 enum sa_option {

@@ -1569,6 +1569,46 @@ int sa_write_ovl(sa_ctx *c, const char *path) {
     return w == text->size() ? SA_OK : fail(c, SA_E_INPUT, "short write");
 }
 
+// AMOS message file: what toAmos_new puts in the bank (Rakefile.rb:174) as
+// {RED} messages, then the .ovl records bank-transact -m loads (Rakefile.rb:180-184)
+int sa_write_afg(sa_ctx *c, const char *path, const char *const *eids, int quality) {
+    if (!c || !path) return SA_E_ARG;
+    if (quality < 0 || quality > 60) return fail(c, SA_E_ARG, "afg quality must be 0..60");
+    if (multi_rank_mode(c)) return fail(c, SA_E_ARG, "sa_write_afg: one-process contexts only");
+    if (!c->aligned) return fail(c, SA_E_STATE, "no alignments");
+    const int rc = multi_sharded(c) ? multi_host_results(c) : host_results(c);
+    if (rc) return rc;
+    FILE *f = fopen(path, "wb");
+    if (!f) return fail(c, SA_E_INPUT, std::string("cannot write ") + path);
+    const uint32_t n = (uint32_t)(c->boff.size() - 1);
+    constexpr size_t LINE = 60;  // sequence / quality line width
+    std::string m;
+    bool ok = true;
+    for (uint32_t id = 1; id <= n && ok; ++id) {
+        const char *seq = c->bases.data() + c->boff[id - 1];
+        const size_t len = (size_t)(c->boff[id] - c->boff[id - 1]);
+        m.clear();
+        m += "{RED\niid:" + std::to_string(id) + "\neid:";
+        if (eids && eids[id - 1] && *eids[id - 1]) m += eids[id - 1];
+        else m += std::to_string(id);
+        m += "\nseq:\n";
+        for (size_t p = 0; p < len; p += LINE) {
+            m.append(seq + p, std::min(LINE, len - p));
+            m += '\n';
+        }
+        m += ".\nqlt:\n";
+        for (size_t p = 0; p < len; p += LINE) {
+            m.append(std::min(LINE, len - p), (char)('0' + quality));
+            m += '\n';
+        }
+        m += ".\nclr:0," + std::to_string(len) + "\nqcr:0," + std::to_string(len) + "\n}\n";
+        ok = fwrite(m.data(), 1, m.size(), f) == m.size();
+    }
+    if (ok) ok = fwrite(c->ovl.data(), 1, c->ovl.size(), f) == c->ovl.size();
+    ok = (fclose(f) == 0) && ok;
+    return ok ? SA_OK : fail(c, SA_E_INPUT, "short write");
+}
+
 int sa_set_option(sa_ctx *c, int option, int64_t value) {
     if (!c) return SA_E_ARG;
     switch (option) {

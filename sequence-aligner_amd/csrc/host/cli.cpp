@@ -8,6 +8,9 @@
 // prints, except --test-alignment / --test-overlaps (alignment strings).
 // Diagnostics go to stderr so stdout stays a clean .ovl stream.
 // Extra flags: --wide-ids / --strict-ids, --device N, --stats,
+// --afg FILE [--afg-quality Q] (also an AMOS message file: the reads as {RED}
+// messages, eid = the FASTA header's first word, then the {OVL} records --
+// toAmos_new + bank-transact -m in one file),
 // --gpus P (one process over devices 0..P-1, one shard each, RCCL exchanges;
 // SURVEY.md 8(b)) and --shards S (S virtual shards on one device: the sharded
 // path on one GPU).  The output is identical for any P and S.
@@ -90,6 +93,33 @@ static std::string java_float(float f) {
         out = digits.substr(0, 1) + "." + (digits.size() > 1 ? digits.substr(1) : "0") + "E" + std::to_string(ex);
     }
     return sign + out;
+}
+
+// FASTA header names in read order, under read_fasta's line rules (fasta.cpp):
+// every '>' line opens a read; its eid is the text up to the first blank
+static std::vector<std::string> fasta_eids(const std::string &path) {
+    std::vector<std::string> out;
+    FILE *f = fopen(path.c_str(), "rb");
+    if (!f) return out;
+    std::string line;
+    int ch;
+    bool more = true;
+    while (more) {
+        line.clear();
+        while ((ch = fgetc(f)) != EOF && ch != '\n' && ch != '\r') line.push_back((char)ch);
+        if (ch == '\r') {
+            const int nx = fgetc(f);
+            if (nx != '\n' && nx != EOF) ungetc(nx, f);
+        }
+        more = ch != EOF;
+        if (!line.empty() && line[0] == '>') {
+            size_t e = 1;
+            while (e < line.size() && !isspace((unsigned char)line[e])) ++e;
+            out.push_back(line.substr(1, e - 1));
+        }
+    }
+    fclose(f);
+    return out;
 }
 
 // --gpus / --shards: a sharded context (sa_ctx_create_multi) or one device
@@ -304,7 +334,8 @@ static int mode_bench_align(const sa_settings &s, int device, const std::string 
 int main(int argc, char **argv) {
     sa_settings s;
     sa_default_settings(&s);
-    std::string input, output, hoxd;
+    std::string input, output, hoxd, afg;
+    int afg_quality = 20;
     int device = 0;
     bool stats = false;
     int aligner = SA_ALIGNER_LINEAR;
@@ -376,7 +407,15 @@ int main(int argc, char **argv) {
             (a == "--gpus" ? g_gpus : g_shards) = iv;
         }
         else if (a == "--stats") stats = true;
-        else {
+        else if (a == "--afg") afg = str();
+        else if (a == "--afg-quality") {
+            need(&iv, nullptr);
+            if (iv < 0 || iv > 60) {
+                fprintf(stderr, "Invalid value for %s : %d (0..60)\n", a.c_str(), iv);
+                return 1;
+            }
+            afg_quality = iv;
+        } else {
             fprintf(stderr, "Invalid Argument : %s\nExiting Program.\n", a.c_str());
             return 1;
         }
@@ -413,6 +452,12 @@ int main(int argc, char **argv) {
     if (rc == SA_OK && (rc = sa_read_fasta(ctx, input.c_str())) == SA_OK && (rc = sa_build_candidates(ctx)) == SA_OK &&
         (rc = sa_align(ctx)) == SA_OK) {
         rc = sa_write_ovl(ctx, output.empty() ? nullptr : output.c_str());
+    }
+    if (rc == SA_OK && !afg.empty()) {
+        const std::vector<std::string> names = fasta_eids(input);
+        std::vector<const char *> eids(sa_num_reads(ctx), nullptr);
+        for (size_t i = 0; i < eids.size() && i < names.size(); ++i) eids[i] = names[i].c_str();
+        rc = sa_write_afg(ctx, afg.c_str(), eids.data(), afg_quality);
     }
     if (rc != SA_OK) {
         fprintf(stderr, "sa-overlap: %s (%d)\n", sa_last_error(ctx), rc);

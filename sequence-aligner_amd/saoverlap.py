@@ -36,7 +36,7 @@ FLAG_DUD, FLAG_VALID, FLAG_OVL_VALID = 1, 2, 4
 # exported symbols declared in include/sa_overlap.h
 EXPORTS = ("sa_default_settings", "sa_ctx_create", "sa_ctx_destroy", "sa_last_error", "sa_load_hoxd",
            "sa_add_reads", "sa_read_fasta", "sa_num_reads", "sa_get_read", "sa_build_candidates", "sa_get_dispatch",
-           "sa_get_pairs", "sa_kmer_histogram", "sa_align", "sa_get_alignments", "sa_write_ovl", "sa_get_ovl", "sa_set_option",
+           "sa_get_pairs", "sa_kmer_histogram", "sa_align", "sa_get_alignments", "sa_write_ovl", "sa_get_ovl", "sa_write_afg", "sa_set_option",
            "sa_get_stats", "sa_get_stage_times", "sa_reset_stage_times", "sa_device_build", "sa_device_align",
            "sa_sync", "sa_dist_init", "sa_dist_local_kmers", "sa_dist_emit", "sa_dist_count", "sa_dist_partials",
            "sa_dist_reduce", "sa_dist_codes", "sa_dist_set_reads", "sa_ctx_create_multi", "sa_rccl_unique_id",
@@ -94,6 +94,7 @@ def lib():
         L.sa_kmer_histogram.argtypes = [vp, P(C.c_uint64), P(P(C.c_uint64)), P(P(C.c_uint64)), P(C.c_size_t)]
         L.sa_write_ovl.argtypes = [vp, C.c_char_p]
         L.sa_get_ovl.argtypes = [vp, P(C.c_char_p), P(C.c_size_t)]
+        L.sa_write_afg.argtypes = [vp, C.c_char_p, P(C.c_char_p), C.c_int]
         L.sa_set_option.argtypes = [vp, C.c_int, C.c_int64]
         L.sa_get_stats.argtypes = [vp, P(Stats)]
         L.sa_get_stage_times.argtypes = [vp, P(C.c_double), P(C.c_uint64), C.c_int]
@@ -289,6 +290,13 @@ class Overlapper:
 
     def write_ovl(self, path=None):
         self._chk(lib().sa_write_ovl(self.h, path.encode() if path else None))
+
+    def write_afg(self, path, eids=None, quality=20):
+        """AMOS {RED} + {OVL} message file (sa_write_afg); eids: one name per read or None."""
+        arr = None
+        if eids is not None:
+            arr = (C.c_char_p * len(eids))(*[e.encode() if e else None for e in eids])
+        self._chk(lib().sa_write_afg(self.h, path.encode(), arr, quality))
 
     def stats(self):
         st = Stats()
