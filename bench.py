@@ -123,8 +123,10 @@ def pmc_summary(tag):
     def tag_of(path):
         base = os.path.basename(path)[:-4]
         return base.split("__", 1)[1] if "__" in base else DEFAULT_WORKLOAD
-    files = sorted((f for f in glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_summary*.csv")) if tag_of(f) == tag),
-                   key=natural)
+    # any depth under profiles/ (profiles/r03/v1/..., profiles/r03/slices_v2/c3/...); newest by
+    # round, then version, in natural order of the path
+    files = sorted((f for f in glob.glob(os.path.join(ROOT, "profiles", "**", "pmc_summary*.csv"), recursive=True)
+                    if tag_of(f) == tag), key=lambda f: natural(os.path.relpath(f, ROOT)))
     if not files:
         return {}, None
     with open(files[-1]) as f:

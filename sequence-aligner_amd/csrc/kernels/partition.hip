@@ -139,14 +139,7 @@ __device__ __forceinline__ void lds_radix_sort(SH &S, uint32_t n, int bits) {
             const bool valid = i < n;
             const uint32_t d = (uint32_t)(k[j] >> shift) & dmask;
             dg[j] = d;
-            uint64_t peer = __ballot(valid);
-#pragma unroll
-            for (int b = 0; b < 8; ++b) {
-                if (b >= nbits) break;  // uniform
-                const bool bit = (d >> b) & 1u;
-                const uint64_t bb = __ballot(bit);
-                peer &= bit ? bb : ~bb;
-            }
+            const uint64_t peer = wave_peers(d, valid, nbits);
             const uint32_t before = valid ? S.cnt[w][d] : 0u;
             rk[j] = before + __popcll(peer & lt_mask);
             __builtin_amdgcn_wave_barrier();
@@ -244,6 +237,7 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
     uint32_t md_c = 0, ed_c = 0, last_bh = 0, last_gh = 0, first_gh = 0xFFFFFFFFu, first_bh = 0xFFFFFFFFu;
     uint32_t n_bh = 0, n_gh = 0;
     uint32_t tagv[IT];
+    uint32_t fbh = 0, fgh = 0;  // bit j: item b0 + j heads a bucket / a loc group (kept for the outputs)
 #pragma unroll
     for (int j = 0; j < IT; ++j) {
         const uint32_t s = b0 + j;
@@ -254,6 +248,8 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
             tagv[j] = t;
             const bool bh = s == 0 || (S.key[s - 1] >> lb) != (k >> lb);
             const bool gh = s == 0 || S.key[s - 1] != k;
+            fbh |= bh ? 1u << j : 0u;
+            fgh |= gh ? 1u << j : 0u;
             md_c += (t & TAG_MD) ? 1u : 0u;
             ed_c += ((t & TAG_ST) ? 1u : 0u) + ((t & TAG_EN) ? 1u : 0u);
             if (bh) { last_bh = s; ++n_bh; if (first_bh == 0xFFFFFFFFu) first_bh = s; }
@@ -328,8 +324,8 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
             const uint32_t s = b0 + j;
             nextg[j] = nx;
             nextb[j] = nb_;
-            if (s < n && (s == 0 || S.key[s - 1] != S.key[s])) nx = s;
-            if (s < n && (s == 0 || (S.key[s - 1] >> lb) != (S.key[s] >> lb))) nb_ = s;
+            if ((fgh >> j) & 1u) nx = s;
+            if ((fbh >> j) & 1u) nb_ = s;
         }
     }
     // ---- outputs --------------------------------------------------------
@@ -338,9 +334,7 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
     for (int j = 0; j < IT; ++j) {
         const uint32_t s = b0 + j;
         if (s >= n) break;
-        const unsigned long long k = S.key[s];
-        const bool isb = s == 0 || (S.key[s - 1] >> lb) != (k >> lb);
-        const bool isg = s == 0 || S.key[s - 1] != k;
+        const bool isb = (fbh >> j) & 1u, isg = (fgh >> j) & 1u;
         if (isb) bh = s;
         if (isg) gh = s;
         const uint32_t t = tagv[j];
@@ -367,6 +361,7 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
         A.rec[g] = encode_rec(c, nE, nD, me);
         if constexpr (STRICT) {
             // bucket extent [bh, be)
+            const unsigned long long k = S.key[s];
             uint32_t be = s + 1;
             while (be < n && (S.key[be] >> lb) == (k >> lb)) ++be;
             uint32_t nst = 0, nmd = 0, nen = 0, st_tot = 0, md_tot = 0, gmin = 0xFFFFFFFFu;

@@ -167,16 +167,7 @@ struct RsShared {
     uint32_t gofs[256];            // global start of each digit run
 };
 
-__device__ __forceinline__ uint64_t wave_peers(uint32_t d, bool valid) {
-    uint64_t peer = __ballot(valid);
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-        const bool bit = (d >> b) & 1u;
-        const uint64_t bb = __ballot(bit);
-        peer &= bit ? bb : ~bb;
-    }
-    return peer;
-}
+// (wave_peers: sa_internal.h)
 
 // VALS = false: key-only sort (records that carry their payload in the key)
 template <bool VALS>

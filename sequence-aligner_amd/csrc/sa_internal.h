@@ -83,6 +83,26 @@ __device__ __forceinline__ uint32_t wave_incl_add(uint32_t v) {
     return v;
 }
 
+// Ballot multisplit: the mask of valid lanes whose digit d agrees with this
+// lane's in bits [0, nbits) (nbits <= 8, wave-uniform).  Per bit: v_bfe_i32 for
+// an all-ones / zero bit mask m, one ballot, and peer &= ~(ballot ^ m) as one
+// v_bitop3_b32 per 32-bit half (truth table 0x90 over (peer, ballot, m)); the
+// ternary `bit ? bb : ~bb` form compiled to 9 VALU per bit (compares, a select,
+// two xors, two ands).
+__device__ __forceinline__ uint64_t wave_peers(uint32_t d, bool valid, int nbits = 8) {
+    const uint64_t v = __ballot(valid);
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        if (b >= nbits) break;  // uniform
+        const uint32_t m = (uint32_t)((int32_t)(d << (31 - b)) >> 31);
+        const uint64_t bb = __ballot(m != 0u);
+        lo = __builtin_amdgcn_bitop3_b32(lo, (uint32_t)bb, m, 0x90);
+        hi = __builtin_amdgcn_bitop3_b32(hi, (uint32_t)(bb >> 32), m, 0x90);
+    }
+    return ((uint64_t)hi << 32) | lo;
+}
+
 // ---- partner lists and per-occurrence records ------------------------------
 // Every bucket owns one slice of the combined partner list `lst` (read index
 // per entry), laid out around a split point c:
@@ -370,10 +390,11 @@ hipError_t launch_dovetail_p1(const DevReads &r, const int32_t *lead, const int3
                               const AlignParams &p, int lw, bool exact, int32_t *p1, uint64_t *rows2_key,
                               uint32_t *order, int32_t *err, unsigned long long *cells, hipStream_t s);
 // phase 1 with two pairs per lane in packed 16-bit halves (band exactly 16
-// cells, int8 costs, gap costs <= 0, every score < 2^16 - 256: the caller checks)
-hipError_t launch_dovetail_p1x2(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
-                                const AlignParams &p, int32_t *p1, uint64_t *rows2_key, uint32_t *order, int32_t *err,
-                                unsigned long long *cells, hipStream_t s);
+// cells, int8 costs, gap costs <= 0, every score < 2^16 - 256: the caller checks),
+// pairs [base, n) (base even)
+hipError_t launch_dovetail_p1x2(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t base,
+                                uint64_t n, const AlignParams &p, int32_t *p1, uint64_t *rows2_key, uint32_t *order,
+                                int32_t *err, unsigned long long *cells, hipStream_t s);
 hipError_t launch_dovetail_p2(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
                               const AlignParams &p, int lw, bool exact, const int32_t *p1, const uint32_t *order,
                               DevAlignment *out, int32_t *err, hipStream_t s);
