@@ -1094,28 +1094,6 @@ int device_build(sa_ctx *c, bool readback) {
 
 int host_results(sa_ctx *c);
 
-// Phase-1 / phase-2 overlap of the packed aligner (device_align): the number of
-// pairs phase 1 leaves for a second launch beside phase 2 -- whatever exceeds
-// whole rounds of one 512-pair workgroup per CU -- or 0 (no split: under one
-// round, an exact number of rounds, or a phase 2 that would need several
-// launches for its codes)
-uint64_t p12_split(sa_ctx *c, uint64_t nd, int32_t maxL) {
-#ifdef SA_NO_P12_SPLIT
-    (void)c; (void)nd; (void)maxL;
-    return 0;
-#else
-    if (!c->n_cu) {
-        int v = 0;
-        c->n_cu = hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && v > 0
-                      ? (uint32_t)v : 256u;
-    }
-    const uint64_t wg = (nd + 511) / 512, full = wg / c->n_cu * c->n_cu;
-    if (full == 0 || full == wg) return 0;
-    if (dovetail_tbx2_words(nd, maxL) > (1ull << 30)) return 0;  // phase 2 chunked (> 4 GiB of codes)
-    return nd - full * 512;
-#endif
-}
-
 int device_align(sa_ctx *c, bool readback) {
     if (!c->built) return fail(c, SA_E_STATE, "sa_align before sa_build_candidates");
     const uint64_t nd = c->n_disp;
@@ -1237,41 +1215,8 @@ int device_align(sa_ctx *c, bool readback) {
             const bool x2 = lw == 16 && exact && P.cost_bits == 8 && P.gap_open <= 0 && P.gap_extend <= 0 &&
                             -(int64_t)P.gap_open < 65536 && -(int64_t)P.gap_extend < 65536 &&
                             cmax * (int64_t)maxL + 255 < 65536;
-            // two pairs per lane in both phases, one phase-2 launch: the phase-1 wave
-            // tail is filled with phase-2 work (below)
-            const bool x2tb = x2 && maxL < 4096 && c->align_kernel != 3;
-            const uint64_t nb_split = x2tb ? p12_split(c, nd, maxL) : 0;
-            if (nb_split) {
-                // Phase 1 runs 128 pairs per wave, all of equal length at uniform read
-                // lengths, so a launch of W waves takes ceil(W / SIMDs) wave times while
-                // its work is W / SIMDs (bench: 5,352 waves on 1,024 SIMDs = 6 for 5.23).
-                // Pairs [0, hA) -- whole rounds of 256 workgroups (one per CU) -- run
-                // first; the remaining [hA, nd) then run phase 1 on the side stream
-                // beside phase 2 of [0, hA), which fills the SIMDs the tail leaves idle.
-                // Each part is sorted by its phase-2 row count on its own stream.
-                const uint64_t hA = nd - nb_split, nB = nb_split;
-                HIPCHK(ensure_side(c));
-                uint8_t *tmp2;
-                ENSURE(c->d_osort2, radix_sort_temp_bytes(nB), &tmp2);
-                uint32_t *tb;
-                ENSURE(c->d_tb, dovetail_tbx2_words(hA, maxL) + dovetail_tbx2_words(nB, maxL), &tb);
-                // (radix_sort swaps the pointers it is given: part B keeps its own)
-                uint64_t *const k0o = k0;
-                uint32_t *const v0o = v0;
-                uint64_t *kB0 = k0 + hA, *kB1 = k1 + hA;
-                uint32_t *vB0 = v0 + hA, *vB1 = v1 + hA;
-                HIPCHK(launch_dovetail_p1x2(AR, dl, dt, 0, hA, P, p1, k0, v0, &cnt->err, cnt->cells, c->stream));
-                HIPCHK(fork_side(c, c->ev_fork));  // part B's phase 1 starts when part A's is done
-                HIPCHK(radix_sort(&k0, &v0, &k1, &v1, hA, 0, 20, tmp, c->stream));
-                HIPCHK(launch_dovetail_p2tbx2(AR, dl, dt, nd, 0, hA, P, p1, v0, out, &cnt->err, tb, c->stream));
-                HIPCHK(launch_dovetail_p1x2(AR, dl, dt, hA, nd, P, p1, k0o, v0o, &cnt->err, cnt->cells, c->side));
-                HIPCHK(radix_sort(&kB0, &vB0, &kB1, &vB1, nB, 0, 20, tmp2, c->side));
-                HIPCHK(launch_dovetail_p2tbx2(AR, dl, dt, nd, hA, nB, P, p1, vB0 - hA, out, &cnt->err,
-                                              tb + dovetail_tbx2_words(hA, maxL), c->side));
-                HIPCHK(join_side(c, c->ev_join));
-            } else {
             if (x2)
-                HIPCHK(launch_dovetail_p1x2(AR, dl, dt, 0, nd, P, p1, k0, v0, &cnt->err, cnt->cells, c->stream));
+                HIPCHK(launch_dovetail_p1x2(AR, dl, dt, nd, P, p1, k0, v0, &cnt->err, cnt->cells, c->stream));
             else
                 HIPCHK(launch_dovetail_p1(AR, dl, dt, nd, P, lw, exact, p1, k0, v0, &cnt->err, cnt->cells,
                                           c->stream));
@@ -1280,6 +1225,7 @@ int device_align(sa_ctx *c, bool readback) {
                 HIPCHK(launch_dovetail_p2(AR, dl, dt, nd, P, lw, exact, p1, v0, out, &cnt->err, c->stream));
             } else {  // 2-bit traceback codes in HBM + per-lane walk, in launches of <= 4 GiB of codes
                 // two pairs per lane as in phase 1 when the argmax row also fits (u << 4 | k in 16 bits)
+                const bool x2tb = x2 && maxL < 4096;
                 const uint64_t per_2 = x2tb ? dovetail_tbx2_words(2, maxL) : dovetail_tb_words(2, maxL, lw);
                 uint64_t chunk = std::max<uint64_t>(512, (2 * ((1ull << 30) / per_2)) & ~511ull);
                 chunk = std::min<uint64_t>(chunk, (nd + 511) & ~511ull);
@@ -1293,7 +1239,6 @@ int device_align(sa_ctx *c, bool readback) {
                         HIPCHK(launch_dovetail_p2tb(AR, dl, dt, nd, t0, chunk, P, lw, exact, p1, v0, out, &cnt->err,
                                                     tb, c->stream));
                 }
-            }
             }
         } else
             HIPCHK(launch_dovetail(AR, (const int32_t *)c->d_lead.p, (const int32_t *)c->d_trail.p, nd, P,

@@ -96,8 +96,6 @@ struct sa_ctx {
     uint32_t *bkt_rank_dev = nullptr;
     DBuf d_pf, d_ps, d_pc, d_pr, d_ovl, d_cnt;
     DBuf d_okeys, d_ovals, d_okeys2, d_ovals2, d_osort;
-    DBuf d_osort2;                   // the aligner's second part (phase 1 / phase 2 overlap)
-    uint32_t n_cu = 0;               // compute units of the device (queried on first use)
     DBuf d_lead, d_trail, d_count, d_aln, d_p1, d_tb, d_ltb, d_lmax;
     DBuf d_rkey, d_rkey2, d_rord, d_rord2, d_rtmp;
     DBuf d_rreg, d_rcnt, d_rex;  // per-read pair regions, counts, their exclusive scan

@@ -452,15 +452,13 @@ __device__ __forceinline__ u16x2 pk_dif(u16x2 a, u16x2 b) { return pk(upk(a) - u
 // a + b per half where neither half reaches 2^16 (no carry crosses)
 __device__ __forceinline__ u16x2 pk_sum(u16x2 a, u16x2 b) { return pk(upk(a) + upk(b)); }
 
-// 4 waves per SIMD (<= 128 VGPRs; 140 unbounded = 3 waves): the only spills are
-// values live across the row loop, stored before it and reloaded after
-__global__ __launch_bounds__(256, 4) void dovetail_p1x2_kernel(DevReads rd, const int32_t *lead, const int32_t *trail,
-                                                            uint64_t base, uint64_t npairs, AlignParams P, int32_t *p1,
+__global__ __launch_bounds__(256) void dovetail_p1x2_kernel(DevReads rd, const int32_t *lead, const int32_t *trail,
+                                                            uint64_t npairs, AlignParams P, int32_t *p1,
                                                             uint64_t *rows2_key, uint32_t *order, int32_t *err,
                                                             unsigned long long *cells_total) {
     constexpr int LW = 16;
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t pairA = base + 2 * t, pairB = base + 2 * t + 1;  // pairs [base, npairs)
+    const uint64_t pairA = 2 * t, pairB = 2 * t + 1;
     const bool haveA = pairA < npairs, haveB = pairB < npairs;
     LanePair qa{0, 0, 0, 0, 0, -100, rd.codes, rd.codes}, qb = qa;
     if (haveA) {
@@ -1060,13 +1058,13 @@ hipError_t launch_dovetail_p2(const DevReads &r, const int32_t *lead, const int3
     return hipGetLastError();
 }
 
-hipError_t launch_dovetail_p1x2(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t base,
-                                uint64_t n, const AlignParams &p, int32_t *p1, uint64_t *rows2_key, uint32_t *order,
-                                int32_t *err, unsigned long long *cells, hipStream_t s) {
-    if (n <= base) return hipSuccess;
-    const uint64_t lanes = (n - base + 1) / 2;
+hipError_t launch_dovetail_p1x2(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
+                                const AlignParams &p, int32_t *p1, uint64_t *rows2_key, uint32_t *order, int32_t *err,
+                                unsigned long long *cells, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const uint64_t lanes = (n + 1) / 2;
     hipLaunchKernelGGL(dovetail_p1x2_kernel, dim3((uint32_t)((lanes + 255) / 256)), dim3(256), 0, s, r, lead, trail,
-                       base, n, p, p1, rows2_key, order, err, cells);
+                       n, p, p1, rows2_key, order, err, cells);
     return hipGetLastError();
 }
 

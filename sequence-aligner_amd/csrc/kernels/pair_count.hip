@@ -31,9 +31,6 @@ constexpr int PC_TAB_BIG = 2048;
 constexpr int PC_TAB_HUGE = 16384;
 constexpr int PC_CHUNK = 512;            // occurrences per pass over a read
 constexpr int PC_BATCH = 8;              // partner loads in flight per thread
-#ifndef PC_MIN_WAVES
-#define PC_MIN_WAVES 1                   // first pass: minimum waves per SIMD (launch bound)
-#endif
 // the per-occurrence records are read once: non-temporal loads keep them from
 // displacing the partner lists in L2
 __device__ __forceinline__ uint4 load_rec(const PairIn &in, uint64_t g) {
@@ -139,7 +136,7 @@ __device__ __forceinline__ void pc_insert(PcShared<TAB> &S, PcSharedStrict<TAB> 
 }
 
 template <bool STRICT, int TAB>
-__global__ __launch_bounds__(PcShape<TAB>::NT, !STRICT && TAB == PC_TAB_SMALL ? PC_MIN_WAVES : 1) void pair_count_kernel(EmitParams e, PairIn in, PairParams p, PairOut o,
+__global__ __launch_bounds__(PcShape<TAB>::NT) void pair_count_kernel(EmitParams e, PairIn in, PairParams p, PairOut o,
                                                                 const uint32_t *read_list) {
     extern __shared__ __align__(16) uint8_t smem[];
     PcShared<TAB> &S = *reinterpret_cast<PcShared<TAB> *>(smem);
@@ -237,30 +234,6 @@ __global__ __launch_bounds__(PcShape<TAB>::NT, !STRICT && TAB == PC_TAB_SMALL ? 
             for (uint32_t e0 = 0; e0 < wn; e0 += NT * BATCH) {
                 uint32_t part[BATCH], wv[BATCH];
                 unsigned long long rk[BATCH];
-                if constexpr (!STRICT) {
-                    // straight-line over the batch (no per-element branches), so the
-                    // element -> occurrence reads, then the range reads, then the
-                    // partner gathers of all BATCH elements each leave together: two
-                    // LDS round trips per batch instead of two per element.  An element
-                    // past the window reads element 0's (valid) entries and is masked.
-                    uint32_t oiv[BATCH];
-#pragma unroll
-                    for (int bb = 0; bb < BATCH; ++bb) {
-                        const uint32_t el = e0 + bb * NT + tid;
-                        oiv[bb] = (uint32_t)S.eo[el < wn ? el : 0u] - 1u;
-                    }
-#pragma unroll
-                    for (int bb = 0; bb < BATCH; ++bb) {
-                        const uint32_t el = e0 + bb * NT + tid, elc = el < wn ? el : 0u;
-                        const uint32_t oi = oiv[bb];
-                        const uint32_t off = w0 + elc - S.pref[oi];
-                        const uint4 rc = S.rec[oi];
-                        const uint32_t got = in.lst[rec_entry(rc, off)];
-                        part[bb] = el < wn ? got : a;  // "same read" = skip
-                        wv[bb] = off < (rc.y & 0x3FFFFFFFu) ? rc.y >> 30 : 1u;
-                        rk[bb] = 0;
-                    }
-                } else
 #pragma unroll
                 for (int bb = 0; bb < BATCH; ++bb) {
                     part[bb] = a;  // "same read" = skip
@@ -300,32 +273,12 @@ __global__ __launch_bounds__(PcShape<TAB>::NT, !STRICT && TAB == PC_TAB_SMALL ? 
                         }
                     }
                 }
-                // every home-slot key of the batch is read before any insert: a key
-                // that equals the partner is final (slots go EMPTY -> key once), so
-                // those hits -- nearly all inserts -- are one fire-and-forget LDS add
-                // each, and the batch waits one LDS round trip instead of BATCH
-                // dependent ones; anything else (EMPTY, another key) takes the probe path
-                // (the home slot is rehashed, not kept: the first pass runs at 8 waves
-                // per SIMD, 64 VGPRs)
-                uint32_t seen[BATCH], ok = 0;
 #pragma unroll
                 for (int bb = 0; bb < BATCH; ++bb) {
                     const uint32_t partner = part[bb];
-                    // same read (KmerTable.scala:61-63); other residue classes of a recount tier
-                    const bool take = partner != a && (split <= 1 || (partner % split) == residue);
-                    seen[bb] = take ? lds_relaxed(&S.key[pc_hash<TAB>(partner)]) : PC_EMPTY;
-                    ok |= take ? 1u << bb : 0u;
-                }
-#pragma unroll
-                for (int bb = 0; bb < BATCH; ++bb) {
-                    if (!((ok >> bb) & 1u)) continue;
-                    if (seen[bb] == part[bb]) {
-                        const uint32_t hs = pc_hash<TAB>(part[bb]);
-                        atomicAdd(&S.cnt[hs], wv[bb]);
-                        if constexpr (STRICT) atomicMin(&X.rank[hs], rk[bb]);
-                        continue;
-                    }
-                    pc_insert<STRICT, TAB>(S, X, part[bb], wv[bb], rk[bb],
+                    if (partner == a) continue;                 // same read (KmerTable.scala:61-63)
+                    if (split > 1 && (partner % split) != residue) continue;
+                    pc_insert<STRICT, TAB>(S, X, partner, wv[bb], rk[bb],
                                            (uint32_t)min(role_pairs - total + w0 + e0 + bb * NT + tid, 0xFFFFFFFEull));
                 }
                 if (S.overflow) break;
@@ -593,35 +546,27 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_multi_kernel(EmitParams
             __syncthreads();
             const uint32_t wn = min((uint32_t)PC_WIN, total - w0);
             for (uint32_t e0 = 0; e0 < wn; e0 += PC_THREADS * PC_BATCH) {
-                // straight-line decode and batched home-slot reads, as in pair_count_kernel
-                uint32_t part[PC_BATCH], wv[PC_BATCH], own[PC_BATCH], oiv[PC_BATCH];
+                uint32_t part[PC_BATCH], wv[PC_BATCH], own[PC_BATCH];
 #pragma unroll
                 for (int bb = 0; bb < PC_BATCH; ++bb) {
+                    part[bb] = 0;
+                    wv[bb] = 0;  // 0: no role pair in this slot
+                    own[bb] = 0;
                     const uint32_t el = e0 + bb * PC_THREADS + tid;
-                    oiv[bb] = (uint32_t)S.eo[el < wn ? el : 0u] - 1u;
-                }
-#pragma unroll
-                for (int bb = 0; bb < PC_BATCH; ++bb) {
-                    const uint32_t el = e0 + bb * PC_THREADS + tid, elc = el < wn ? el : 0u;
-                    const uint32_t oi = oiv[bb];
-                    const uint32_t off = w0 + elc - S.pref[oi];
-                    const uint4 rc = S.rec[oi];
-                    own[bb] = S.aid[oi];
-                    part[bb] = in.lst[rec_entry(rc, off)];
-                    wv[bb] = el >= wn ? 0u : off < (rc.y & 0x3FFFFFFFu) ? rc.y >> 30 : 1u;  // 0: no role pair
-                }
-                unsigned long long seen[PC_BATCH];
-#pragma unroll
-                for (int bb = 0; bb < PC_BATCH; ++bb) {
-                    const unsigned long long key = ((unsigned long long)own[bb] << 32) | part[bb];
-                    seen[bb] = wv[bb] != 0 && part[bb] != own[bb] ? lds_relaxed(&S.key[pcm_hash(key)]) : PCM_EMPTY;
+                    if (el < wn) {
+                        const uint32_t oi = (uint32_t)S.eo[el] - 1u;
+                        const uint32_t off = w0 + el - S.pref[oi];
+                        const uint4 rc = S.rec[oi];
+                        const uint32_t nE = rc.y & 0x3FFFFFFFu;
+                        own[bb] = S.aid[oi];
+                        part[bb] = in.lst[rec_entry(rc, off)];
+                        wv[bb] = off < nE ? rc.y >> 30 : 1u;
+                    }
                 }
 #pragma unroll
                 for (int bb = 0; bb < PC_BATCH; ++bb) {
                     if (wv[bb] == 0 || part[bb] == own[bb]) continue;  // same read (KmerTable.scala:61-63)
-                    const unsigned long long key = ((unsigned long long)own[bb] << 32) | part[bb];
-                    if (seen[bb] == key) atomicAdd(&S.cnt[pcm_hash(key)], wv[bb]);  // a set key is final
-                    else pcm_insert(S, key, wv[bb]);
+                    pcm_insert(S, ((unsigned long long)own[bb] << 32) | part[bb], wv[bb]);
                 }
                 if (S.overflow) break;
             }

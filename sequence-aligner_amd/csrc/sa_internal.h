@@ -390,11 +390,10 @@ hipError_t launch_dovetail_p1(const DevReads &r, const int32_t *lead, const int3
                               const AlignParams &p, int lw, bool exact, int32_t *p1, uint64_t *rows2_key,
                               uint32_t *order, int32_t *err, unsigned long long *cells, hipStream_t s);
 // phase 1 with two pairs per lane in packed 16-bit halves (band exactly 16
-// cells, int8 costs, gap costs <= 0, every score < 2^16 - 256: the caller checks),
-// pairs [base, n) (base even)
-hipError_t launch_dovetail_p1x2(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t base,
-                                uint64_t n, const AlignParams &p, int32_t *p1, uint64_t *rows2_key, uint32_t *order,
-                                int32_t *err, unsigned long long *cells, hipStream_t s);
+// cells, int8 costs, gap costs <= 0, every score < 2^16 - 256: the caller checks)
+hipError_t launch_dovetail_p1x2(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
+                                const AlignParams &p, int32_t *p1, uint64_t *rows2_key, uint32_t *order, int32_t *err,
+                                unsigned long long *cells, hipStream_t s);
 hipError_t launch_dovetail_p2(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
                               const AlignParams &p, int lw, bool exact, const int32_t *p1, const uint32_t *order,
                               DevAlignment *out, int32_t *err, hipStream_t s);
