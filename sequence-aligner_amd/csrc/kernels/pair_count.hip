@@ -417,9 +417,209 @@ static hipError_t pc_launch(const EmitParams &e, const PairIn &in, const PairPar
     return hipSuccess;
 }
 
+// ---------------------------------------------------------------------------
+// First pass, one WAVE per read (wide ids, per-read regions -- the bench path).
+// The one-read workgroup above spends about half its time in per-read framework:
+// ~10 block barriers per read and 8 reads in flight per CU (4 waves each at the
+// 32-wave limit).  Here a 256-thread block carries four reads, one per wave, and
+// every synchronisation is within the wave (LDS operations of a wave complete in
+// order, so a wave barrier -- a compiler fence -- is all the eo / pref / rec
+// hand-offs need): 28 reads in flight per CU (5.6 KB of LDS per read), no block
+// barrier.  Enumeration is the same lane-interleaved walk over 512-element
+// windows of 128-occurrence chunks, the same table (256 slots, 192 at the fill
+// limit), overflow accounting and per-read region as pair_count_kernel<false, 256>.
+// ---------------------------------------------------------------------------
+constexpr int PW_WAVES = 4;
+constexpr int PW_CHUNK = 128;   // occurrences per chunk (2 per lane)
+constexpr int PW_WIN = 512;     // elements per window (one batch of 8 per lane)
+
+struct PwShared {  // one per wave
+    uint32_t key[PC_TAB_SMALL];
+    uint32_t cnt[PC_TAB_SMALL];
+    uint4 rec[PW_CHUNK];
+    uint32_t pref[PW_CHUNK];
+    uint16_t eo[PW_WIN];
+    uint32_t fill, overflow, xfill, pad;
+};
+
+__device__ __forceinline__ void pw_insert(PwShared &S, uint32_t partner, uint32_t w, uint32_t eidx) {
+    constexpr uint32_t FILL_MAX = PC_TAB_SMALL * 3 / 4;
+    uint32_t slot = pc_hash<PC_TAB_SMALL>(partner);
+    for (int probe = 0; probe < PC_TAB_SMALL / 4; ++probe) {  // bounded as in pc_insert
+        uint32_t old = lds_relaxed(&S.key[slot]);  // a set key is final (pc_insert)
+        if (old == PC_EMPTY) old = atomicCAS(&S.key[slot], PC_EMPTY, partner);
+        if (old == PC_EMPTY || old == partner) {
+            if (old == PC_EMPTY && atomicAdd(&S.fill, 1u) >= FILL_MAX) {
+                S.overflow = 1;
+                atomicMin(&S.xfill, eidx);
+            }
+            atomicAdd(&S.cnt[slot], w);
+            return;
+        }
+        slot = (slot + 1) & (PC_TAB_SMALL - 1);
+    }
+    S.overflow = 1;
+}
+
+__global__ __launch_bounds__(PW_WAVES * 64) void pair_count_wave_kernel(EmitParams e, PairIn in, PairParams p,
+                                                                         PairOut o, const uint32_t *read_list,
+                                                                         uint32_t n_blocks) {
+    __shared__ PwShared SH[PW_WAVES];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    PwShared &S = SH[wv];
+    uint32_t bid = blockIdx.x;
+    if (p.xcd_swizzle) bid = (blockIdx.x & 7u) * (n_blocks >> 3) + (blockIdx.x >> 3);  // as pair_count_kernel
+    const uint32_t item = bid * PW_WAVES + wv;
+    if (item >= p.n_items) return;  // whole wave: nothing below synchronises beyond it
+    if (p.abort && *p.abort) return;
+    const uint32_t a = read_list ? read_list[item] : item;
+
+    for (int i = lane; i < PC_TAB_SMALL; i += 64) {
+        S.key[i] = PC_EMPTY;
+        S.cnt[i] = 0;
+    }
+    if (lane == 0) { S.fill = 0; S.overflow = 0; S.xfill = 0xFFFFFFFFu; }
+    const uint64_t g0 = e.npr ? (uint64_t)a * e.npr : e.occ_off[a];
+    const uint32_t nocc = e.npr ? e.npr : (uint32_t)(e.occ_off[a + 1] - g0);
+    unsigned long long role_pairs = 0;
+    unsigned long long x_over = ~0ull;
+    bool over = false;
+    __builtin_amdgcn_wave_barrier();
+
+    for (uint32_t c0 = 0; c0 < nocc && !over; c0 += PW_CHUNK) {
+        const uint32_t cn = min((uint32_t)PW_CHUNK, nocc - c0);
+        uint32_t mytot[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const uint32_t oi = lane * 2 + j;  // lane-contiguous
+            uint32_t tot = 0;
+            if (oi < cn) {
+                const uint4 rc = load_rec(in, g0 + c0 + oi);
+                S.rec[oi] = rc;
+                tot = (rc.y & 0x3FFFFFFFu) + rc.w;
+            }
+            mytot[j] = tot;
+        }
+        const uint32_t sum = mytot[0] + mytot[1];
+        const uint32_t inc = wave_incl_add(sum);
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        const uint32_t myex[2] = {inc - sum, inc - sum + mytot[0]};
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            if (lane * 2 + j < cn) S.pref[lane * 2 + j] = myex[j];
+        const unsigned long long rp0 = role_pairs;  // role pairs before this chunk
+        role_pairs += total;
+        for (uint32_t w0 = 0; w0 < total; w0 += PW_WIN) {
+            __builtin_amdgcn_wave_barrier();  // pref / rec written; the previous window's eo read
+            if (lds_relaxed(&S.overflow)) {   // recounted by the next tier: totals only
+                if (x_over == ~0ull) x_over = rp0 + w0;
+                over = true;
+                break;
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const uint32_t e0 = max(myex[j], w0), e1 = min(myex[j] + mytot[j], w0 + (uint32_t)PW_WIN);
+                const uint16_t v = (uint16_t)(lane * 2 + j + 1);
+                for (uint32_t el = e0; el < e1; ++el) S.eo[el - w0] = v;
+            }
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t wn = min((uint32_t)PW_WIN, total - w0);
+            uint32_t part[PC_BATCH], wt[PC_BATCH];
+#pragma unroll
+            for (int bb = 0; bb < PC_BATCH; ++bb) {
+                part[bb] = a;  // "same read" = skip
+                wt[bb] = 0;
+                const uint32_t el = bb * 64 + lane;
+                if (el < wn) {
+                    const uint32_t oi = (uint32_t)S.eo[el] - 1u;
+                    const uint32_t off = w0 + el - S.pref[oi];
+                    const uint4 rc = S.rec[oi];
+                    part[bb] = in.lst[rec_entry(rc, off)];
+                    wt[bb] = off < (rc.y & 0x3FFFFFFFu) ? rc.y >> 30 : 1u;
+                }
+            }
+#pragma unroll
+            for (int bb = 0; bb < PC_BATCH; ++bb) {
+                if (part[bb] == a) continue;  // same read (KmerTable.scala:61-63)
+                pw_insert(S, part[bb], wt[bb], (uint32_t)min(rp0 + w0 + bb * 64 + lane, 0xFFFFFFFEull));
+            }
+        }
+        // the rest of the read's chunks still count their role pairs after an overflow
+        if (over)
+            for (uint32_t c1 = c0 + PW_CHUNK; c1 < nocc; c1 += PW_CHUNK) {
+                const uint32_t cn1 = min((uint32_t)PW_CHUNK, nocc - c1);
+                uint32_t t = 0;
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const uint32_t oi = lane * 2 + j;
+                    if (oi < cn1) {
+                        const uint4 rc = load_rec(in, g0 + c1 + oi);
+                        t += (rc.y & 0x3FFFFFFFu) + rc.w;
+                    }
+                }
+                role_pairs += (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_add(t), 63);
+            }
+        __builtin_amdgcn_wave_barrier();
+    }
+    const bool overflow = lds_relaxed(&S.overflow) != 0;
+    const uint32_t shard = item % NSHARD;
+    if (lane == 0 && role_pairs) atomicAdd(&o.role_pairs[shard], role_pairs);
+    if (lane == 0 && !overflow) atomicAdd(&o.distinct[shard], (unsigned long long)lds_relaxed(&S.fill));
+    if (overflow) {  // recounted by the next tier (pair_count_kernel, 2,048 / 16,384 slots)
+        if (lane == 0) {
+            o.rcnt[a] = 0;
+            const uint32_t at = atomicAdd(o.overflow_n, 1u);
+            o.overflow_list[at] = a << 6;
+            if (o.overflow_rp) {  // distinct partners extrapolated from the fill point (pair_count_kernel)
+                const uint32_t xf = lds_relaxed(&S.xfill);
+                const unsigned long long x = xf != 0xFFFFFFFFu ? (unsigned long long)xf + 1
+                                             : x_over == ~0ull || x_over == 0 ? role_pairs : x_over;
+                const unsigned long long est = (unsigned long long)(PC_TAB_SMALL * 3 / 4) * role_pairs / (x ? x : 1);
+                o.overflow_rp[at] = est > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)est;
+            }
+        }
+        return;
+    }
+    // ---- per-read region: the kept keys compacted, each ranked by its trail
+    uint32_t kk[4], kc[4], keep = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        kk[j] = S.key[lane * 4 + j];
+        kc[j] = S.cnt[lane * 4 + j];
+        if (kk[j] != PC_EMPTY && (int32_t)kc[j] >= p.min_coll && (int32_t)kc[j] <= p.max_coll) keep |= 1u << j;
+    }
+    const uint32_t mine = __popc(keep);
+    const uint32_t kin = wave_incl_add(mine);
+    const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)kin, 63);
+    uint32_t *ck = reinterpret_cast<uint32_t *>(S.rec);  // enumeration state is dead (m <= 192 words)
+    uint32_t at = kin - mine;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (keep & (1u << j)) ck[at++] = kk[j];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (!(keep & (1u << j))) continue;
+        uint32_t r = 0;
+        for (uint32_t i = 0; i < m; ++i) r += ck[i] < kk[j] ? 1u : 0u;
+        o.rreg[(uint64_t)a * PC_RREG + r] = make_uint2(kk[j], kc[j]);
+    }
+    if (lane == 0) o.rcnt[a] = m;
+}
+
 hipError_t launch_pair_count(const EmitParams &e, const PairIn &in, const PairParams &p, PairOut &o,
                              const uint32_t *read_list, uint32_t n_blocks, hipStream_t s) {
     if (n_blocks == 0) return hipSuccess;
+    // the wide-id first pass with per-read regions: one wave per read
+    if (!p.strict && p.table == PC_TAB_SMALL && p.per_read && !p.coded && p.split <= 1) {
+        const uint32_t nb = (p.n_items + PW_WAVES - 1) / PW_WAVES;
+        const uint32_t grid = p.xcd_swizzle ? (nb + 7) & ~7u : nb;
+        if (!p.max_blocks || grid <= p.max_blocks) {
+            hipLaunchKernelGGL(pair_count_wave_kernel, dim3(grid), dim3(PW_WAVES * 64), 0, s, e, in, p, o, read_list,
+                               grid);
+            return hipGetLastError();
+        }
+    }
     if (p.strict) {
         if (p.table == PC_TAB_SMALL) return pc_launch<true, PC_TAB_SMALL>(e, in, p, o, read_list, n_blocks, s);
         if (p.table == PC_TAB_BIG) return pc_launch<true, PC_TAB_BIG>(e, in, p, o, read_list, n_blocks, s);
