@@ -430,17 +430,25 @@ static hipError_t pc_launch(const EmitParams &e, const PairIn &in, const PairPar
 // limit), overflow accounting and per-read region as pair_count_kernel<false, 256>.
 // ---------------------------------------------------------------------------
 constexpr int PW_WAVES = 4;
-constexpr int PW_CHUNK = 128;   // occurrences per chunk (2 per lane)
-constexpr int PW_WIN = 512;     // elements per window (one batch of 8 per lane)
+#ifndef PW_CHUNK_OCC
+#define PW_CHUNK_OCC 64
+#endif
+#ifndef PW_BATCH_EL
+#define PW_BATCH_EL 8
+#endif
+constexpr int PW_CHUNK = PW_CHUNK_OCC;     // occurrences per chunk
+constexpr int PW_OCC = PW_CHUNK / 64;      // ... per lane
+constexpr int PW_BATCH = PW_BATCH_EL;      // partner gathers in flight per lane
+constexpr int PW_WIN = 64 * PW_BATCH;      // elements per window (one batch per lane)
 
 struct PwShared {  // one per wave
     uint32_t key[PC_TAB_SMALL];
     uint32_t cnt[PC_TAB_SMALL];
-    uint4 rec[PW_CHUNK];
-    uint32_t pref[PW_CHUNK];
+    uint4 rec[PW_CHUNK];   // {list entry of element 0 (u64), edge-role end, edge weight} per occurrence
     uint16_t eo[PW_WIN];
     uint32_t fill, overflow, xfill, pad;
 };
+static_assert(PW_BATCH % 8 == 0, "each lane owns PW_BATCH contiguous u16 entries of eo, in 16-byte words");
 
 __device__ __forceinline__ void pw_insert(PwShared &S, uint32_t partner, uint32_t w, uint32_t eidx) {
     constexpr uint32_t FILL_MAX = PC_TAB_SMALL * 3 / 4;
@@ -488,27 +496,41 @@ __global__ __launch_bounds__(PW_WAVES * 64) void pair_count_wave_kernel(EmitPara
 
     for (uint32_t c0 = 0; c0 < nocc && !over; c0 += PW_CHUNK) {
         const uint32_t cn = min((uint32_t)PW_CHUNK, nocc - c0);
-        uint32_t mytot[2];
+        uint32_t mytot[PW_OCC];
+        uint4 rcj[PW_OCC];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const uint32_t oi = lane * 2 + j;  // lane-contiguous
+        for (int j = 0; j < PW_OCC; ++j) {
+            const uint32_t oi = lane * PW_OCC + j;  // lane-contiguous
             uint32_t tot = 0;
+            rcj[j] = make_uint4(0, 0, 0, 0);
             if (oi < cn) {
-                const uint4 rc = load_rec(in, g0 + c0 + oi);
-                S.rec[oi] = rc;
-                tot = (rc.y & 0x3FFFFFFFu) + rc.w;
+                rcj[j] = load_rec(in, g0 + c0 + oi);
+                tot = (rcj[j].y & 0x3FFFFFFFu) + rcj[j].w;
             }
             mytot[j] = tot;
         }
-        const uint32_t sum = mytot[0] + mytot[1];
+        uint32_t sum = 0;
+#pragma unroll
+        for (int j = 0; j < PW_OCC; ++j) sum += mytot[j];
         const uint32_t inc = wave_incl_add(sum);
         const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-        const uint32_t myex[2] = {inc - sum, inc - sum + mytot[0]};
+        uint32_t myex[PW_OCC];
+        myex[0] = inc - sum;
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-            if (lane * 2 + j < cn) S.pref[lane * 2 + j] = myex[j];
+        for (int j = 1; j < PW_OCC; ++j) myex[j] = myex[j - 1] + mytot[j - 1];
+        // per occurrence, what an element ew of the chunk needs: its list entry is
+        // adj + ew (adj = c - nE - first element), it is an edge-role pair (weight
+        // me) while ew < first element + nE, else a middle one (weight 1)
+#pragma unroll
+        for (int j = 0; j < PW_OCC; ++j)
+            if (lane * PW_OCC + j < cn) {
+                const uint32_t nE = rcj[j].y & 0x3FFFFFFFu;
+                const uint64_t adj = (((uint64_t)rcj[j].z << 32) | rcj[j].x) - nE - myex[j];
+                S.rec[lane * PW_OCC + j] = make_uint4((uint32_t)adj, (uint32_t)(adj >> 32), myex[j] + nE, rcj[j].y >> 30);
+            }
         const unsigned long long rp0 = role_pairs;  // role pairs before this chunk
         role_pairs += total;
+        uint32_t carry = 0;  // occurrence (+1) owning the window's first element
         for (uint32_t w0 = 0; w0 < total; w0 += PW_WIN) {
             __builtin_amdgcn_wave_barrier();  // pref / rec written; the previous window's eo read
             if (lds_relaxed(&S.overflow)) {   // recounted by the next tier: totals only
@@ -516,30 +538,64 @@ __global__ __launch_bounds__(PW_WAVES * 64) void pair_count_wave_kernel(EmitPara
                 over = true;
                 break;
             }
+            // element -> occurrence map of the window without a per-element loop:
+            // zero it, mark the first element of every non-empty occurrence that
+            // starts inside (positions are distinct), then a max-scan -- over the
+            // lane's PW_BATCH contiguous entries in registers, then across lanes
+            // (DPP), seeded with the occurrence running into the window
+            uint4 *eo4 = reinterpret_cast<uint4 *>(S.eo);
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const uint32_t e0 = max(myex[j], w0), e1 = min(myex[j] + mytot[j], w0 + (uint32_t)PW_WIN);
-                const uint16_t v = (uint16_t)(lane * 2 + j + 1);
-                for (uint32_t el = e0; el < e1; ++el) S.eo[el - w0] = v;
+            for (int q = 0; q < PW_BATCH / 8; ++q) eo4[lane * (PW_BATCH / 8) + q] = make_uint4(0, 0, 0, 0);
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int j = 0; j < PW_OCC; ++j)
+                if (mytot[j] && myex[j] >= w0 && myex[j] < w0 + (uint32_t)PW_WIN)
+                    S.eo[myex[j] - w0] = (uint16_t)(lane * PW_OCC + j + 1);
+            __builtin_amdgcn_wave_barrier();
+            {
+                uint32_t v[PW_BATCH];
+#pragma unroll
+                for (int q = 0; q < PW_BATCH / 8; ++q) {
+                    const uint4 x = eo4[lane * (PW_BATCH / 8) + q];
+                    const uint32_t w4[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        v[8 * q + 2 * t] = w4[t] & 0xFFFFu;
+                        v[8 * q + 2 * t + 1] = w4[t] >> 16;
+                    }
+                }
+                uint32_t run = 0;
+#pragma unroll
+                for (int i = 0; i < PW_BATCH; ++i) { run = max(run, v[i]); v[i] = run; }
+                const uint32_t incl = wave_incl_max(run);
+                const uint32_t into = max(carry, wave_shr1(incl));  // owner entering this lane's entries
+#pragma unroll
+                for (int q = 0; q < PW_BATCH / 8; ++q) {
+                    uint32_t w4[4];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        w4[t] = max(v[8 * q + 2 * t], into) | (max(v[8 * q + 2 * t + 1], into) << 16);
+                    eo4[lane * (PW_BATCH / 8) + q] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+                }
+                carry = max(carry, (uint32_t)__builtin_amdgcn_readlane((int)incl, 63));
             }
             __builtin_amdgcn_wave_barrier();
             const uint32_t wn = min((uint32_t)PW_WIN, total - w0);
-            uint32_t part[PC_BATCH], wt[PC_BATCH];
+            uint32_t part[PW_BATCH], wt[PW_BATCH];
 #pragma unroll
-            for (int bb = 0; bb < PC_BATCH; ++bb) {
+            for (int bb = 0; bb < PW_BATCH; ++bb) {
                 part[bb] = a;  // "same read" = skip
                 wt[bb] = 0;
                 const uint32_t el = bb * 64 + lane;
                 if (el < wn) {
-                    const uint32_t oi = (uint32_t)S.eo[el] - 1u;
-                    const uint32_t off = w0 + el - S.pref[oi];
-                    const uint4 rc = S.rec[oi];
-                    part[bb] = in.lst[rec_entry(rc, off)];
-                    wt[bb] = off < (rc.y & 0x3FFFFFFFu) ? rc.y >> 30 : 1u;
+                    const uint32_t ew = w0 + el;
+                    const uint4 r = S.rec[(uint32_t)S.eo[el] - 1u];
+                    part[bb] = in.lst[(((uint64_t)r.y << 32) | r.x) + ew];
+                    wt[bb] = ew < r.z ? r.w : 1u;
                 }
             }
 #pragma unroll
-            for (int bb = 0; bb < PC_BATCH; ++bb) {
+            for (int bb = 0; bb < PW_BATCH; ++bb) {
                 if (part[bb] == a) continue;  // same read (KmerTable.scala:61-63)
                 pw_insert(S, part[bb], wt[bb], (uint32_t)min(rp0 + w0 + bb * 64 + lane, 0xFFFFFFFEull));
             }
@@ -550,8 +606,8 @@ __global__ __launch_bounds__(PW_WAVES * 64) void pair_count_wave_kernel(EmitPara
                 const uint32_t cn1 = min((uint32_t)PW_CHUNK, nocc - c1);
                 uint32_t t = 0;
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const uint32_t oi = lane * 2 + j;
+                for (int j = 0; j < PW_OCC; ++j) {
+                    const uint32_t oi = lane * PW_OCC + j;
                     if (oi < cn1) {
                         const uint4 rc = load_rec(in, g0 + c1 + oi);
                         t += (rc.y & 0x3FFFFFFFu) + rc.w;

@@ -83,6 +83,20 @@ __device__ __forceinline__ uint32_t wave_incl_add(uint32_t v) {
     return v;
 }
 
+// The same scan with max (values >= 0): inclusive, and exclusive (wave_shr:1)
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {  // lane l gets lane l - 1's value, lane 0 gets 0
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+}
+
 // Ballot multisplit: the mask of valid lanes whose digit d agrees with this
 // lane's in bits [0, nbits) (nbits <= 8, wave-uniform).  Per bit: v_bfe_i32 for
 // an all-ones / zero bit mask m, one ballot, and peer &= ~(ballot ^ m) as one
