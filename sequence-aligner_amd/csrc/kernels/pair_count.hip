@@ -436,6 +436,9 @@ constexpr int PW_WAVES = 4;
 #ifndef PW_BATCH_EL
 #define PW_BATCH_EL 8
 #endif
+#ifndef PW_MIN_WAVES
+#define PW_MIN_WAVES 8                     // per SIMD: <= 64 VGPRs, the 32-wave CU limit
+#endif
 constexpr int PW_CHUNK = PW_CHUNK_OCC;     // occurrences per chunk
 constexpr int PW_OCC = PW_CHUNK / 64;      // ... per lane
 constexpr int PW_BATCH = PW_BATCH_EL;      // partner gathers in flight per lane
@@ -450,9 +453,9 @@ struct PwShared {  // one per wave
 };
 static_assert(PW_BATCH % 8 == 0, "each lane owns PW_BATCH contiguous u16 entries of eo, in 16-byte words");
 
-__device__ __forceinline__ void pw_insert(PwShared &S, uint32_t partner, uint32_t w, uint32_t eidx) {
+__device__ __forceinline__ void pw_insert_probe(PwShared &S, uint32_t partner, uint32_t w, uint32_t eidx,
+                                                uint32_t slot) {
     constexpr uint32_t FILL_MAX = PC_TAB_SMALL * 3 / 4;
-    uint32_t slot = pc_hash<PC_TAB_SMALL>(partner);
     for (int probe = 0; probe < PC_TAB_SMALL / 4; ++probe) {  // bounded as in pc_insert
         uint32_t old = lds_relaxed(&S.key[slot]);  // a set key is final (pc_insert)
         if (old == PC_EMPTY) old = atomicCAS(&S.key[slot], PC_EMPTY, partner);
@@ -468,8 +471,19 @@ __device__ __forceinline__ void pw_insert(PwShared &S, uint32_t partner, uint32_
     }
     S.overflow = 1;
 }
+// a read meets each partner in ~100 shared k-mers, so nearly every insert finds
+// its key in the home slot: that case is one read + one add, outside the probe
+// loop (whose exec-mask bookkeeping is ~30 scalar instructions per insert)
+__device__ __forceinline__ void pw_insert(PwShared &S, uint32_t partner, uint32_t w, uint32_t eidx) {
+    const uint32_t h = pc_hash<PC_TAB_SMALL>(partner);
+    if (lds_relaxed(&S.key[h]) == partner) {
+        atomicAdd(&S.cnt[h], w);
+        return;
+    }
+    pw_insert_probe(S, partner, w, eidx, h);
+}
 
-__global__ __launch_bounds__(PW_WAVES * 64) void pair_count_wave_kernel(EmitParams e, PairIn in, PairParams p,
+__global__ __launch_bounds__(PW_WAVES * 64, PW_MIN_WAVES) void pair_count_wave_kernel(EmitParams e, PairIn in, PairParams p,
                                                                          PairOut o, const uint32_t *read_list,
                                                                          uint32_t n_blocks) {
     __shared__ PwShared SH[PW_WAVES];
