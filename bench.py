@@ -333,7 +333,7 @@ def main():
 
     note("hash stage timed: %.3f ms/step" % (t_build / args.steps * 1e3))
     # ---- end-to-end incl. banded HOXD alignment (configs[2]) --------------
-    asteps = args.align_steps if args.align_steps is not None else max(1, args.steps // 2)
+    asteps = max(1, args.align_steps) if args.align_steps is not None else max(1, args.steps // 2)  # (>= 1: the aligner fields need one timed step)
     xbytes = (ov.exchanged_bytes() - xb0) / max(args.steps, 1)
     # first align of a sharded context all-gathers the packed reads: timed apart
     barrier()
