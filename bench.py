@@ -410,10 +410,13 @@ def main():
                   "void sa::part_build_kernel<4096")
     roofline = roof(16.0 * kmers_g, per_launch("buckets"), bk_kernels,
                     "bucket build: part_bounds + part_build<1024|2048|4096>")
-    roofline_pc = roof(8.0 * kmers_g + 16.0 * pairs_g, per_launch("pairs"), ("void sa::pair_count_kernel<false, 256",),
-                       "pair_count_kernel<false, 256>")
-    pc_conf = pmc_sum(rows, ("void sa::pair_count_kernel<false, 256",), "SQ_LDS_BANK_CONFLICT_avg")
-    pc_act = pmc_sum(rows, ("void sa::pair_count_kernel<false, 256",), "SQ_LDS_IDX_ACTIVE_avg")
+    # the first pair-count pass: one wave per read (round 3; wide ids, per-read regions), or
+    # the one-read workgroup kernel in profiles of earlier trees / other modes
+    pc_k = ("sa::pair_count_wave_kernel",) if any(k.startswith("sa::pair_count_wave_kernel") for k in rows) \
+        else ("void sa::pair_count_kernel<false, 256",)
+    roofline_pc = roof(8.0 * kmers_g + 16.0 * pairs_g, per_launch("pairs"), pc_k, pc_k[0].split("sa::")[1])
+    pc_conf = pmc_sum(rows, pc_k, "SQ_LDS_BANK_CONFLICT_avg")
+    pc_act = pmc_sum(rows, pc_k, "SQ_LDS_IDX_ACTIVE_avg")
     roofline_pc["lds_bank_conflict_rate"] = round(pc_conf / pc_act, 4) if pc_conf is not None and pc_act else None
     roofline_step = roof(step_bytes, ms_step, None, "whole hash step (every kernel, wall clock)")
     # the aligner (configs[2]): integer VALU, MFMA unused.  Peak = 256 CUs x 4

@@ -3,7 +3,7 @@
 # placed under profiles/$VER/ so the bench line that follows cites it, then the default bench line
 set -u
 mkdir -p gpurun_out
-VER=${VER:-r03/v2}
+VER=${VER:-r03/v3}
 bash tools_profile.sh || exit $?
 mkdir -p profiles/$VER
 cp gpurun_out/pmc_summary__n100000_L500_k15.csv profiles/$VER/ || exit 1
