@@ -11,6 +11,6 @@ step() {  # step <name> <seconds> <cmd...>
     return 0
 }
 step smoke 240 python __graft_entry__.py smoke
-VARIANTS="build_base build_fp1 build" REPS=3 step ab_multi 300 bash tools/gpu/ab_multi.sh
+VARIANTS="build_prev build" REPS=4 step ab_multi 300 bash tools/gpu/ab_multi.sh
 step gpu_tests 700 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread
 exit 0
