@@ -1,4 +1,11 @@
-"""sharded.py -- the multi-GPU hash stage: one process and one
+"""sharded.py -- TEST HARNESS for the sharded hash stage's per-rank C ABI
+(sa_dist_*): the product path is the library's own orchestration (multi.cpp:
+sa_ctx_create_multi / sa_ctx_create_rank, RCCL inside libsa_overlap), which
+bench.py and the CLI use.  This module drives the same per-rank steps from
+Python so the tests can run them over gloo on CPU (with a numpy model worker)
+and compare the HIP worker against it; nothing in the product imports it.
+
+The multi-GPU hash stage: one process and one
 context per GPU, exchanges over torch.distributed (backend "nccl" is RCCL on
 ROCm and moves device tensors over xGMI; "gloo" stages through host memory,
 used by the CPU tests and single-GPU multi-process checks).
