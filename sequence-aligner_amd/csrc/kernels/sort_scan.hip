@@ -126,22 +126,103 @@ constexpr int RS_THREADS = 256;
 constexpr int RS_ITEMS = 16;
 constexpr int RS_TILE = RS_THREADS * RS_ITEMS;
 
+// Tile histograms, BLOCK-major: hist[tile * 256 + digit] (one coalesced 1 KB
+// row per tile; the digit-major layout made every tile write 256 scattered
+// words and the downsweep read them back scattered).  All 16 keys of a thread
+// are loaded before the first count, and each wave counts into its own 256
+// bins (less same-address contention in the LDS atomics).
 __global__ __launch_bounds__(RS_THREADS) void rs_upsweep_kernel(const uint64_t *keys, uint64_t n, int shift,
                                                                 uint32_t *hist, uint32_t nblocks) {
-    __shared__ uint32_t cnt[256];
-    cnt[threadIdx.x] = 0;
-    __syncthreads();
+    (void)nblocks;
+    __shared__ uint32_t cnt[RS_THREADS / 64][256];
+    const int tid = threadIdx.x, w = tid >> 6;
+#pragma unroll
+    for (int q = 0; q < RS_THREADS / 64; ++q) cnt[q][tid] = 0;
     const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
-#pragma unroll 4
+    unsigned long long k[RS_ITEMS];
+#pragma unroll
     for (int j = 0; j < RS_ITEMS; ++j) {
-        const uint64_t i = base + (uint64_t)j * RS_THREADS + threadIdx.x;
-        if (i < n) {
-            const uint64_t key = __builtin_nontemporal_load(keys + i);  // read once per pass
-            atomicAdd(&cnt[(uint32_t)(key >> shift) & 255u], 1u);
-        }
+        const uint64_t i = base + (uint64_t)j * RS_THREADS + tid;
+        k[j] = i < n ? __builtin_nontemporal_load(keys + i) : 0ull;  // read once per pass
     }
     __syncthreads();
-    hist[(uint64_t)threadIdx.x * nblocks + blockIdx.x] = cnt[threadIdx.x];
+#pragma unroll
+    for (int j = 0; j < RS_ITEMS; ++j) {
+        const uint64_t i = base + (uint64_t)j * RS_THREADS + tid;
+        if (i < n) atomicAdd(&cnt[w][(uint32_t)(k[j] >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    uint32_t s = 0;
+#pragma unroll
+    for (int q = 0; q < RS_THREADS / 64; ++q) s += cnt[q][tid];
+    hist[(uint64_t)blockIdx.x * 256 + tid] = s;
+}
+
+// Global scatter offsets from the block-major tile histograms, in place:
+// hist[b*256 + d] <- sum_{d' < d} total[d'] + sum_{b' < b} hist[b'*256 + d].
+// Three launches over chunks of RS_CHUNK tiles, every access a coalesced row:
+// column sums per chunk, a per-digit scan over the chunk sums (+ digit totals),
+// then each chunk's column scan.
+constexpr int RS_CHUNK = 32;
+
+__global__ __launch_bounds__(256) void rs_colsum_kernel(const uint32_t *hist, uint32_t nb, uint32_t *csum) {
+    const uint32_t d = threadIdx.x, c = blockIdx.x;
+    uint32_t v[RS_CHUNK];
+#pragma unroll
+    for (int r = 0; r < RS_CHUNK; ++r) {
+        const uint32_t b = c * RS_CHUNK + r;
+        v[r] = b < nb ? hist[(uint64_t)b * 256 + d] : 0u;
+    }
+    uint32_t s = 0;
+#pragma unroll
+    for (int r = 0; r < RS_CHUNK; ++r) s += v[r];
+    csum[(uint64_t)c * 256 + d] = s;
+}
+
+// one block per digit: exclusive scan of that digit's chunk sums, total -> tot[d]
+__global__ __launch_bounds__(SC_THREADS) void rs_chunkscan_kernel(uint32_t *csum, uint32_t nc, uint32_t *tot) {
+    __shared__ uint32_t lds4[4];
+    const uint32_t d = blockIdx.x;
+    uint32_t carry = 0;
+    for (uint32_t c0 = 0; c0 < nc; c0 += SC_THREADS) {
+        const uint32_t c = c0 + threadIdx.x;
+        const uint32_t v = c < nc ? csum[(uint64_t)c * 256 + d] : 0u;
+        uint32_t t;
+        const uint32_t ex = block_excl_scan(v, lds4, &t);
+        if (c < nc) csum[(uint64_t)c * 256 + d] = carry + ex;
+        carry += t;
+    }
+    if (threadIdx.x == 0) tot[d] = carry;
+}
+
+__global__ __launch_bounds__(256) void rs_colscan_kernel(uint32_t *hist, uint32_t nb, const uint32_t *csum,
+                                                         const uint32_t *tot) {
+    __shared__ uint32_t lds4[4];
+    const uint32_t d = threadIdx.x, c = blockIdx.x;
+    uint32_t t;
+    uint32_t acc = block_excl_scan(tot[d], lds4, &t) + csum[(uint64_t)c * 256 + d];
+    uint32_t v[RS_CHUNK];
+#pragma unroll
+    for (int r = 0; r < RS_CHUNK; ++r) {
+        const uint32_t b = c * RS_CHUNK + r;
+        v[r] = b < nb ? hist[(uint64_t)b * 256 + d] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < RS_CHUNK; ++r) {
+        const uint32_t b = c * RS_CHUNK + r;
+        if (b < nb) hist[(uint64_t)b * 256 + d] = acc;
+        acc += v[r];
+    }
+}
+
+static hipError_t rs_offsets(uint32_t *hist, uint64_t nb, void *tmp, hipStream_t s) {
+    const uint32_t nc = (uint32_t)((nb + RS_CHUNK - 1) / RS_CHUNK);
+    uint32_t *csum = (uint32_t *)tmp, *tot = csum + (uint64_t)nc * 256;
+    hipLaunchKernelGGL(rs_colsum_kernel, dim3(nc), dim3(256), 0, s, (const uint32_t *)hist, (uint32_t)nb, csum);
+    hipLaunchKernelGGL(rs_chunkscan_kernel, dim3(256), dim3(SC_THREADS), 0, s, csum, nc, tot);
+    hipLaunchKernelGGL(rs_colscan_kernel, dim3(nc), dim3(256), 0, s, hist, (uint32_t)nb, (const uint32_t *)csum,
+                       (const uint32_t *)tot);
+    return hipGetLastError();
 }
 
 // the scatter's input keys are read once: non-temporal loads leave L2 to merge
@@ -218,7 +299,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep_kernel(const uint64_t
         __syncthreads();
         const uint32_t lo = pre + inc - tot;
         S.lofs[tid] = lo;
-        S.gofs[tid] = hist[(uint64_t)tid * nblocks + blockIdx.x];
+        S.gofs[tid] = hist[(uint64_t)blockIdx.x * 256 + tid];
         // per-wave bases inside the tile, in place of the counts
         uint32_t acc = lo;
 #pragma unroll
@@ -305,7 +386,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep_kv64_kernel(const uin
         __syncthreads();
         const uint32_t lo = pre + inc - tot;
         S.lofs[tid] = lo;
-        S.gofs[tid] = hist[(uint64_t)tid * nblocks + blockIdx.x];
+        S.gofs[tid] = hist[(uint64_t)blockIdx.x * 256 + tid];
         uint32_t acc = lo;
 #pragma unroll
         for (int q = 0; q < RS_WAVES; ++q) {
@@ -348,8 +429,9 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep_kv64_kernel(const uin
 
 size_t radix_sort_temp_bytes(uint64_t n) {
     const uint64_t nb = (n + RS_TILE - 1) / RS_TILE;
+    const uint64_t nc = (nb + RS_CHUNK - 1) / RS_CHUNK;
     const uint64_t hist = 256 * (nb ? nb : 1);
-    return hist * sizeof(uint32_t) + scan_temp_bytes(hist) + 256;
+    return (hist + 256 * (nc + 1)) * sizeof(uint32_t) + 256;
 }
 
 hipError_t radix_sort(uint64_t **keys, uint32_t **vals, uint64_t **keys_alt, uint32_t **vals_alt,
@@ -370,7 +452,7 @@ hipError_t radix_sort(uint64_t **keys, uint32_t **vals, uint64_t **keys_alt, uin
     for (int shift = lo; shift < hi; shift += 8) {
         hipLaunchKernelGGL(rs_upsweep_kernel, dim3((uint32_t)nb), dim3(RS_THREADS), 0, s, *keys, n, shift, hist,
                            (uint32_t)nb);
-        hipError_t e = exclusive_scan_u32(hist, hist, 256 * nb, nullptr, stmp, s);
+        hipError_t e = rs_offsets(hist, nb, stmp, s);
         if (e != hipSuccess) return e;
         if (with_vals) {
             hipLaunchKernelGGL((rs_downsweep_kernel<true>), dim3((uint32_t)nb), dim3(RS_THREADS), sizeof(RsShared<true>),
@@ -403,7 +485,7 @@ hipError_t radix_sort_kv64(uint64_t **keys, uint64_t **vals, uint64_t **keys_alt
     for (int shift = lo; shift < hi; shift += 8) {
         hipLaunchKernelGGL(rs_upsweep_kernel, dim3((uint32_t)nb), dim3(RS_THREADS), 0, s, *keys, n, shift, hist,
                            (uint32_t)nb);
-        hipError_t e = exclusive_scan_u32(hist, hist, 256 * nb, nullptr, stmp, s);
+        hipError_t e = rs_offsets(hist, nb, stmp, s);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(rs_downsweep_kv64_kernel, dim3((uint32_t)nb), dim3(RS_THREADS), sizeof(RsSharedKV), s,
                            *keys, *vals, *keys_alt, *vals_alt, n, shift, (const uint32_t *)hist, (uint32_t)nb);
