@@ -96,6 +96,27 @@ def synth_workload(n_reads, read_len, genome_len, gc, seed, shard=0, min_len=Non
 DEFAULT_WORKLOAD = "n100000_L500_k15"
 
 
+def workload_label(reads, read_len, min_len, k, n_gpus, mode):
+    """config.workload: which BASELINE.json config (or which per-GPU slice of one)
+    this shape is, from the shape itself."""
+    shape = "%s synthetic %s bp reads/GPU, k=%d" % (
+        "%gM" % (reads / 1e6) if reads >= 1000000 else "%dk" % (reads // 1000),
+        "%d" % read_len if min_len is None else "%d-%d" % (min_len, read_len), k)
+    uniform500 = min_len is None and read_len == 500
+    mixed = min_len == 100 and read_len == 1000
+    if uniform500 and k == 15 and reads == 100000:
+        what = "configs[1]" if n_gpus == 1 else "configs[1] weak-scaled to %d GPUs" % n_gpus
+        return "%s: %s, bucket build + edge/middle pair filter" % (what, shape)
+    if uniform500 and k == 15 and reads == 1250000:
+        return "configs[3] per-GPU slice (10M reads / 8 GPUs) on %s: %s" % (
+            "one GPU" if mode == "single" else mode, shape)
+    if mixed and k in (12, 15) and reads == 6250000:
+        return "configs[4] per-GPU slice (50M reads / 8 GPUs), k=%d pass: %s" % (k, shape)
+    if mixed and k in (12, 15):
+        return "configs[4]-shaped (mixed 100-1000 bp, k=%d pass), not its size: %s" % (k, shape)
+    return "custom shape (not a BASELINE config): %s" % shape
+
+
 def workload_tag(reads, read_len, min_len, k, gc=0.50, shards=1):
     """Key of a PMC summary: the workload its rocprofv3 passes ran (reads, read
     length(s), k, and GC / virtual shards when not the default)."""
@@ -109,8 +130,8 @@ def workload_tag(reads, read_len, min_len, k, gc=0.50, shards=1):
 
 def pmc_summary(tag):
     """Per-kernel counter averages of the newest committed PMC summary of THIS
-    workload: profiles/<round>/pmc_summary*__<tag>.csv (tools_profile.sh /
-    tools_slice_prof.sh write them from separate rocprofv3 --pmc passes of this
+    workload: profiles/<round>/pmc_summary*__<tag>.csv (tools/prof/profile.sh /
+    tools/prof/slice_prof.sh write them from separate rocprofv3 --pmc passes of this
     bench).  Summaries without a tag are the default bench workload's
     (rounds 1-2).  No summary of the workload -> ({}, None): the traffic and
     VALU fields are then null rather than another workload's counters."""
@@ -410,6 +431,10 @@ def main():
                   "void sa::part_build_kernel<4096")
     roofline = roof(16.0 * kmers_g, per_launch("buckets"), bk_kernels,
                     "bucket build: part_bounds + part_build<1024|2048|4096>")
+    # the bucket build runs in one of two per-process modes at the bench shape
+    # ("Bucket-build bimodality"): say which one this line hit
+    if tag == DEFAULT_WORKLOAD:
+        roofline["bucket_build_mode"] = "slow (> 1.2 ms)" if per_launch("buckets") > 1.2 else "fast (<= 1.2 ms)"
     # the first pair-count pass: one wave per read (round 3; wide ids, per-read regions), or
     # the one-read workgroup kernel in profiles of earlier trees / other modes
     pc_k = ("sa::pair_count_wave_kernel",) if any(k.startswith("sa::pair_count_wave_kernel") for k in rows) \
@@ -590,10 +615,7 @@ def main():
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic (splitmix64 genome, error-free reads)",
-            "config": {"workload": "configs[1]: %dk synthetic %s bp reads/GPU, k=%d, bucket build + "
-                                   "edge/middle pair filter" % (args.reads // 1000, (
-                                       "%d" % args.len if args.min_len is None else
-                                       "%d-%d" % (args.min_len, args.len)), args.k),
+            "config": {"workload": workload_label(args.reads, args.len, args.min_len, args.k, n_gpus, mode),
                        "reads_per_gpu": args.reads, "read_len": args.len, "min_len": args.min_len, "k": args.k,
                        "genome_bp_per_gpu": G, "ids": "wide", "pmc_key": tag,
                        "parallelism": {"rank": "rccl-a2a, one process per GPU", "process":

@@ -140,8 +140,10 @@ int sa_get_ovl(sa_ctx *ctx, const char **text, size_t *len);
  * rank 1): the bank toAmos_new builds from the .seq (Rakefile.rb:174) and the
  * .ovl that bank-transact -m loads into it (:180-184), in one file.  One {RED}
  * per read in id order (iid = read id, eid = eids[id - 1], or the id when eids
- * or the entry is NULL / empty; seq = the read as the context holds it; qlt =
- * '0' + quality on every base, quality 0..60; clr and qcr = 0,len), then the
+ * or the entry is NULL / empty; eids, when given, holds one entry per read and
+ * an entry with whitespace, ':' or braces fails with SA_E_ARG; seq = the read as
+ * the context holds it; qlt = '0' + quality on every base, quality 0..60; clr =
+ * 0,len and no other range, as the reference bank's RED records hold), then the
  * {OVL} records of sa_write_ovl, byte for byte.  One-process contexts only
  * (SA_E_ARG in rank mode); SA_E_STATE before an alignment. */
 int sa_write_afg(sa_ctx *ctx, const char *path, const char *const *eids, int quality);
@@ -161,7 +163,10 @@ enum sa_option {
                                   (measurement: clean per-shard stage times on one device) */
     SA_OPT_LAUNCH_SLICE = 7    /* pair counter: at most this many workgroups per launch (0 =
                                   default: lists are sliced only where a dispatch's 32-bit
-                                  work-item count would wrap; a test hook for that path) */
+                                  work-item count would wrap; a test hook for that path).
+                                  Applies to the launches that walk a read / item list
+                                  (every build passes one); a list-less launch larger
+                                  than the slice fails with SA_E_HIP */
 };
 
 /* Project4's fdAlign switch (Project4.scala:187-192, :585-604).

@@ -923,6 +923,9 @@ static int cmp_u64(const void *a, const void *b) {
     const uint64_t x = *(const uint64_t *)a, y = *(const uint64_t *)b;
     return (x > y) - (x < y);
 }
+static int lead_owner(uint64_t lead, uint32_t n, int nt) { /* ids 1..n in nt ranges */
+    return (int)(((lead - 1) * (uint64_t)nt) / ((uint64_t)n + 1));
+}
 static uint32_t bin_mix(uint32_t h) { /* spreads hashes over the 2^16 bins */
     h ^= h >> 16; h *= 0x7feb352du; h ^= h >> 15; h *= 0x846ca68bu; h ^= h >> 16;
     return h;
@@ -1046,7 +1049,8 @@ int orc_run_wide_mt(orc_ctx *c, const orc_settings *s, int threads, uint64_t *ro
     free(koff); free(hist); free(bstart); free(recs);
     if (rc) goto out;
     {
-        /* merge: thread t owns the leads with fst % nt == t (counts summed) */
+        /* merge: thread t owns the leads of one contiguous id range (counts summed),
+         * so the threads' sorted arrays concatenate to the (fst, snd) order */
         wmap *fin = (wmap *)calloc((size_t)nt, sizeof(wmap));
         uint64_t *cnt_t = (uint64_t *)calloc((size_t)nt + 1, sizeof(uint64_t));
         int64_t **arr = (int64_t **)calloc((size_t)nt, sizeof(int64_t *));
@@ -1059,7 +1063,7 @@ int orc_run_wide_mt(orc_ctx *c, const orc_settings *s, int threads, uint64_t *ro
                 const wmap *w = &loc_maps[q];
                 for (size_t i = 0; i < w->cap && !lrc; i++) {
                     const uint64_t key = w->keys[i];
-                    if (key == UINT64_MAX || (int)((key >> 32) % (uint64_t)nt) != t) continue;
+                    if (key == UINT64_MAX || lead_owner(key >> 32, n, nt) != t) continue;
                     if ((lrc = wmap_add(f, key))) break;
                     /* wmap_add counted 1: add the rest of this map's count */
                     size_t j = mix64(key) & (f->cap - 1);
@@ -1072,6 +1076,8 @@ int orc_run_wide_mt(orc_ctx *c, const orc_settings *s, int threads, uint64_t *ro
             if (a)
                 for (size_t i = 0; i < f->cap; i++)
                     if (f->keys[i] != UINT64_MAX) { a[2 * z] = (int64_t)f->keys[i]; a[2 * z + 1] = f->cnt[i]; z++; }
+            free(f->keys); free(f->cnt); /* (host memory at configs[4]-shaped sizes) */
+            f->keys = NULL; f->cnt = NULL;
             if (a) qsort(a, z, 2 * sizeof(int64_t), cmp_wide_pair);
             arr[t] = a;
             cnt_t[t] = z;
@@ -1081,7 +1087,7 @@ int orc_run_wide_mt(orc_ctx *c, const orc_settings *s, int threads, uint64_t *ro
             }
         }
         if (!rc) {
-            /* leads are spread over the threads by residue: one global merge by key */
+            /* lead ranges ascend with t: the concatenation is sorted by key */
             size_t np = 0;
             for (int t = 0; t < nt; t++) np += cnt_t[t];
             int64_t *all = (int64_t *)malloc((np + 1) * 2 * sizeof(int64_t));
@@ -1089,8 +1095,9 @@ int orc_run_wide_mt(orc_ctx *c, const orc_settings *s, int threads, uint64_t *ro
             for (int t = 0; t < nt; t++) {
                 memcpy(all + 2 * z, arr[t], cnt_t[t] * 2 * sizeof(int64_t));
                 z += cnt_t[t];
+                free(arr[t]);
+                arr[t] = NULL;
             }
-            qsort(all, np, 2 * sizeof(int64_t), cmp_wide_pair);
             c->np = np;
             c->p_fst = (int32_t *)malloc((np + 1) * sizeof(int32_t));
             c->p_snd = (int32_t *)malloc((np + 1) * sizeof(int32_t));

@@ -13,6 +13,7 @@
 #include "../../../include/sa_overlap.h"
 
 #include <hip/hip_runtime.h>
+#include <ctype.h>
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -940,7 +941,7 @@ int device_build(sa_ctx *c, bool readback) {
         // regions empty): those pairs sorted lead-descending / trail-ascending,
         // each such read's segment start into rsh[read] (+1) and its length
         // into rcnt[read]; the copy then takes those reads from the segments
-        const int32_t *sl = nullptr, *stl = nullptr, *scn = nullptr;
+        const int32_t *stl = nullptr, *scn = nullptr;
         uint32_t *rsh = nullptr;
         if (np) {
             int32_t *shl, *sht, *shc;
@@ -961,12 +962,11 @@ int device_build(sa_ctx *c, bool readback) {
                                        (const uint32_t *)c->d_pc.p, shl, sht, shc, c->stream));
             HIPCHK(hipMemsetAsync(rsh, 0, (size_t)nr * 4, c->stream));
             HIPCHK(launch_mark_segments(shl, np, rsh, rcnt, c->stream));
-            sl = shl; stl = sht; scn = shc;
+            stl = sht; scn = shc;
             stmp2 = otmp;
         } else {
             ENSURE(c->d_osort, scan_temp_bytes(nr), &stmp2);
         }
-        (void)sl;
         HIPCHK(exclusive_scan_u32(rcnt, rex, nr, &cnt->rtotal, stmp2, c->stream));
         HIPCHK(launch_copy_read_regions((const uint2 *)c->d_rreg.p, rcnt, rex, &cnt->rtotal, nr, rsh, stl, scn,
                                         dlead, dtrail, dcount, c->stream));
@@ -1096,6 +1096,10 @@ int host_results(sa_ctx *c);
 
 int device_align(sa_ctx *c, bool readback) {
     if (!c->built) return fail(c, SA_E_STATE, "sa_align before sa_build_candidates");
+    // this run's records or none: a failure below must not leave the previous
+    // run's alignments / .ovl readable through the getters
+    c->aligned = false;
+    c->host_valid = false;
     const uint64_t nd = c->n_disp;
     // reads the aligner sees: this device's, or (distributed) the all-gathered set
     DevReads AR = dev_reads(c);
@@ -1581,6 +1585,11 @@ int sa_write_afg(sa_ctx *c, const char *path, const char *const *eids, int quali
     FILE *f = fopen(path, "wb");
     if (!f) return fail(c, SA_E_INPUT, std::string("cannot write ") + path);
     const uint32_t n = (uint32_t)(c->boff.size() - 1);
+    // an eid is one message-field token: no whitespace, no ':' / '{' / '}'
+    for (uint32_t id = 1; eids && id <= n; ++id)
+        for (const char *e = eids[id - 1]; e && *e; ++e)
+            if (isspace((unsigned char)*e) || *e == ':' || *e == '{' || *e == '}')
+                return fail(c, SA_E_ARG, "afg eid of read " + std::to_string(id) + " is not one token");
     constexpr size_t LINE = 60;  // sequence / quality line width
     std::string m;
     bool ok = true;
@@ -1601,7 +1610,9 @@ int sa_write_afg(sa_ctx *c, const char *path, const char *const *eids, int quali
             m.append(std::min(LINE, len - p), (char)('0' + quality));
             m += '\n';
         }
-        m += ".\nclr:0," + std::to_string(len) + "\nqcr:0," + std::to_string(len) + "\n}\n";
+        // clr only: the reference bank's RED records hold the clear range (0, len)
+        // and leave every other range unset (RED.0.0.fix, tests/golden/c_ruddii_bank_red.npz)
+        m += ".\nclr:0," + std::to_string(len) + "\n}\n";
         ok = fwrite(m.data(), 1, m.size(), f) == m.size();
     }
     if (ok) ok = fwrite(c->ovl.data(), 1, c->ovl.size(), f) == c->ovl.size();

@@ -8,8 +8,10 @@
 // prints, except --test-alignment / --test-overlaps (alignment strings).
 // Diagnostics go to stderr so stdout stays a clean .ovl stream.
 // Extra flags: --wide-ids / --strict-ids, --device N, --stats,
-// --afg FILE [--afg-quality Q] (also an AMOS message file: the reads as {RED}
-// messages, eid = the FASTA header's first word, then the {OVL} records --
+// --afg FILE [--afg-quality Q] [--afg-header-eids] (also an AMOS message file:
+// the reads as {RED} messages, eid = the read ordinal as in the reference's
+// c_ruddii bank map, or with --afg-header-eids the FASTA header's first word;
+// then the {OVL} records --
 // toAmos_new + bank-transact -m in one file),
 // --gpus P (one process over devices 0..P-1, one shard each, RCCL exchanges;
 // SURVEY.md 8(b)) and --shards S (S virtual shards on one device: the sharded
@@ -336,6 +338,7 @@ int main(int argc, char **argv) {
     sa_default_settings(&s);
     std::string input, output, hoxd, afg;
     int afg_quality = 20;
+    bool afg_header_eids = false;
     int device = 0;
     bool stats = false;
     int aligner = SA_ALIGNER_LINEAR;
@@ -408,6 +411,7 @@ int main(int argc, char **argv) {
         }
         else if (a == "--stats") stats = true;
         else if (a == "--afg") afg = str();
+        else if (a == "--afg-header-eids") afg_header_eids = true;
         else if (a == "--afg-quality") {
             need(&iv, nullptr);
             if (iv < 0 || iv > 60) {
@@ -454,10 +458,13 @@ int main(int argc, char **argv) {
         rc = sa_write_ovl(ctx, output.empty() ? nullptr : output.c_str());
     }
     if (rc == SA_OK && !afg.empty()) {
-        const std::vector<std::string> names = fasta_eids(input);
+        // default eid = ordinal (the only bank the reference holds maps iid = bid =
+        // eid = ordinal, amos/c_ruddii.bnk/RED.0.map); header names are opt-in and
+        // not pinned against toAmos_new
+        const std::vector<std::string> names = afg_header_eids ? fasta_eids(input) : std::vector<std::string>();
         std::vector<const char *> eids(sa_num_reads(ctx), nullptr);
         for (size_t i = 0; i < eids.size() && i < names.size(); ++i) eids[i] = names[i].c_str();
-        rc = sa_write_afg(ctx, afg.c_str(), eids.data(), afg_quality);
+        rc = sa_write_afg(ctx, afg.c_str(), afg_header_eids ? eids.data() : nullptr, afg_quality);
     }
     if (rc != SA_OK) {
         fprintf(stderr, "sa-overlap: %s (%d)\n", sa_last_error(ctx), rc);

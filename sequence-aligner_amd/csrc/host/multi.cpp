@@ -479,6 +479,8 @@ int multi_align(sa_ctx *c, bool readback, int (*single_align)(sa_ctx *, bool)) {
     sa_multi *m = c->multi;
     if (!m->sharded) return single_align(c, readback);
     if (!c->built) return set_err(c, SA_E_STATE, "sa_align before sa_build_candidates");
+    c->aligned = false;  // as device_align: no previous run's records after a failure
+    c->host_valid = false;
     const int P = m->P;
     int rc;
     if (!m->reads_gathered) {

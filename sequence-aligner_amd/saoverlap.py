@@ -292,9 +292,15 @@ class Overlapper:
         self._chk(lib().sa_write_ovl(self.h, path.encode() if path else None))
 
     def write_afg(self, path, eids=None, quality=20):
-        """AMOS {RED} + {OVL} message file (sa_write_afg); eids: one name per read or None."""
+        """AMOS {RED} + {OVL} message file (sa_write_afg); eids: one name per read
+        (no whitespace, ':' or braces) or None for the read ordinals."""
         arr = None
         if eids is not None:
+            if len(eids) != self.n_reads:
+                raise ValueError("write_afg: %d eids for %d reads" % (len(eids), self.n_reads))
+            bad = [e for e in eids if e and any(ch.isspace() or ch in ":{}" for ch in e)]
+            if bad:
+                raise ValueError("write_afg: eid %r is not one token" % bad[0])
             arr = (C.c_char_p * len(eids))(*[e.encode() if e else None for e in eids])
         self._chk(lib().sa_write_afg(self.h, path.encode(), arr, quality))
 

@@ -249,6 +249,36 @@ def test_non_acgt_errors_like_matcherror(oracle_mod):
     assert e.value.name == "SA_E_NON_ACGT"
 
 
+@pytest.mark.parametrize("wide", [False, True])
+def test_failed_realign_leaves_no_stale_records(oracle_mod, wide):
+    """A second align that fails must not leave the first run's records behind
+    (ADVICE r3): 1,600 bp reads have 33-cell bands, so the first align runs the
+    lane-group kernel; forcing the lane-per-pair kernel (SA_OPT_ALIGN_KERNEL=2,
+    an option that does not reset the context) then fails the next align, and
+    the getters and the .ovl writer report SA_E_STATE instead of the previous
+    run's records.  Aligning again under the automatic choice gives them back."""
+    rng = np.random.default_rng(77)
+    g = "".join("ACGT"[x] for x in rng.integers(0, 4, 4000))
+    reads = [g[s:s + 1600] for s in range(0, 2401, 40)]
+    st = dict(kmer_size=15, min_collisions=3, max_ignore=2000)  # edge x middle offsets are ~1,000 bp
+    r = oracle_mod.Run(reads=reads, settings=oracle_settings(oracle_mod, **st), wide=wide)
+    ov = gpu_run(reads=reads, wide=wide, **st)
+    assert ov.ovl() == r.ovl and r.ovl.count(b"{OVL") > 100
+    ov._chk(sao.lib().sa_set_option(ov.h, sao.SA_OPT_ALIGN_KERNEL, sao.ALIGN_LANE))
+    for align in (ov.align, ov.device_align):
+        with pytest.raises(sao.SAError) as e:
+            align()
+        assert e.value.name == "SA_E_ARG"
+        for getter in (ov.alignments, ov.ovl, ov.write_ovl):
+            with pytest.raises(sao.SAError) as e:
+                getter()
+            assert e.value.name == "SA_E_STATE"
+    ov._chk(sao.lib().sa_set_option(ov.h, sao.SA_OPT_ALIGN_KERNEL, sao.ALIGN_AUTO))
+    ov.device_align()
+    assert ov.ovl() == r.ovl
+    ov.close()
+
+
 def test_strict_rejects_aliasing_sizes():
     ov = sao.Overlapper(id_mode=sao.SA_IDS_STRICT)
     ov.add_reads(["ACGTACGTACGTACGT"] * 65536)

@@ -35,6 +35,13 @@ def compare(ov, r, pairs=True):
     lead, trail, count = ov.dispatch()
     np.testing.assert_array_equal(lead, r.lead)
     np.testing.assert_array_equal(trail, r.trail)
+    # every dispatched pair's count = the oracle's PairData count of that key
+    # (wide ids: the oracle's pairs are sorted by (fst, snd))
+    okey = (r.pair_fst.astype(np.uint64) << np.uint64(32)) | r.pair_snd.astype(np.uint64)
+    dkey = (lead.astype(np.uint64) << np.uint64(32)) | trail.astype(np.uint64)
+    pos = np.minimum(np.searchsorted(okey, dkey), max(len(okey) - 1, 0))
+    assert (okey[pos] == dkey).all()
+    np.testing.assert_array_equal(count, r.pair_cnt[pos])
     if pairs:
         pf, ps, pc = ov.pairs()
         np.testing.assert_array_equal(pf, r.pair_fst)
@@ -59,7 +66,8 @@ def test_bench_workload_matches_oracle(oracle_mod):
     st = ov.stats()
     assert st["kmers"] == 48600000 and st["dispatched"] > 600000
     r = oracle_mod.Run(packed=(b.tobytes(), o), settings=oracle_mod.default_settings(kmer_size=15), wide=True)
-    compare(ov, r, pairs=False)
+    compare(ov, r, pairs=False)  # dispatch, its counts, every tuple, the .ovl
+    assert st["pairs"] == len(r.pair_fst)
     _, _, count = ov.dispatch()
     assert ((count >= 7) & (count <= 222)).all()
     assert st["ovl_records"] == ov.ovl().count(b"{OVL") > 100000

@@ -1,4 +1,4 @@
-"""Average rocprofv3 --pmc counters per kernel over the passes tools_profile.sh
+"""Average rocprofv3 --pmc counters per kernel over the passes tools/prof/profile.sh
 wrote (gpurun_out/pmc_*/pmc_counter_collection.csv) -> one CSV (stdout or path)."""
 import collections
 import csv

@@ -1,5 +1,5 @@
 """Hash stage only (no alignment), for timing ablation libraries that break the
-dispatch: python tools/gpu/build_only.py [reads] [len] [k] -> stage ms per step."""
+dispatch: python tools/prof/build_only.py [reads] [len] [k] -> stage ms per step."""
 import json, os, sys, time
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "sequence-aligner_amd"))

@@ -1,5 +1,6 @@
 #!/bin/bash
-# One GPU session: tests, bench, profile.  Stops at the first crash/timeout.
+# One GPU session: smoke + GPU tests, bench, profile (tools/prof/session.sh [all|tests|bench|prof],
+# from the repository root).  Stops at the first crash / timeout.
 set -u
 mkdir -p gpurun_out
 step() {  # step <name> <seconds> <cmd...>
@@ -13,11 +14,11 @@ step() {  # step <name> <seconds> <cmd...>
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = tests ]; then
     step smoke 240 python __graft_entry__.py smoke
-    step gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+    step gpu_tests 1050 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
     step bench 600 python bench.py --steps 10 --warmup 2
 fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
-    bash tools_profile.sh
+    bash tools/prof/profile.sh
 fi

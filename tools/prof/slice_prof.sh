@@ -2,7 +2,7 @@
 # Profile a large single-GPU slice: rocprofv3 kernel stats, then one PMC pass per
 # counter group (FETCH_SIZE / WRITE_SIZE / SQ), all on the SAME workload, so the
 # summary (tools/pmc_summary.py) is keyed to it.  Usage:
-#   tools_slice_prof.sh <name> <bench args...>
+#   tools/prof/slice_prof.sh <name> <bench args...>
 # Outputs under gpurun_out/sp_<name>/; stops at the first failure.
 set -u
 R=$GRAFT_REPO_ROOT
