@@ -339,6 +339,40 @@ int ensure_prepared(sa_ctx *c) {
     return SA_OK;
 }
 
+// PartArgs' two shortcuts around table lookups (checked against the tables,
+// off when they do not hold): loc rank = position for uniform lengths, and the
+// tags as three loc-rank intervals
+static void set_part_shortcuts(const sa_ctx *c, PartArgs &PA, uint32_t npr) {
+    PA.lr_ident = 0;
+    if (npr >= 2 && (size_t)npr - 1 < c->lbase.size()) {
+        const uint32_t b = c->lbase[npr - 1];
+        bool id = (size_t)b + npr <= c->lrank.size();
+        for (uint32_t i = 0; id && i < npr; ++i) id = c->lrank[b + i] == i;
+        PA.lr_ident = id ? 1 : 0;
+    }
+    const std::vector<uint8_t> &t = c->tagtab;
+    const uint32_t T = (uint32_t)t.size();
+    auto run = [&](uint8_t bit, uint32_t &lo, uint32_t &cnt) {
+        lo = 0;
+        while (lo < T && !(t[lo] & bit)) ++lo;
+        uint32_t hi = lo;
+        while (hi < T && (t[hi] & bit)) ++hi;
+        cnt = hi - lo;
+        if (lo == T) lo = 0;
+    };
+    uint32_t st0, stn;
+    run(TAG_ST, st0, stn);
+    run(TAG_MD, PA.tg_md0, PA.tg_mdn);
+    run(TAG_EN, PA.tg_en0, PA.tg_enn);
+    PA.tg_st = stn ? st0 + stn : 0;
+    PA.tg_on = stn == 0 || st0 == 0;
+    for (uint32_t q = 0; PA.tg_on && q < T; ++q) {
+        const uint32_t v = (q < PA.tg_st ? (uint32_t)TAG_ST : 0u) | (q - PA.tg_md0 < PA.tg_mdn ? (uint32_t)TAG_MD : 0u) |
+                           (q - PA.tg_en0 < PA.tg_enn ? (uint32_t)TAG_EN : 0u);
+        PA.tg_on = v == t[q];
+    }
+}
+
 // Bucket build over one device's k-mer records (keys = mix << lb | locrank,
 // vals = occurrence index): partition radix sort on the top PB bits of the
 // mix, then one LDS workgroup per partition (part_build), the global scan path
@@ -359,9 +393,13 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
     // ~700 records per partition (LDS capacity 1,024); up to 2^24 partitions
     // (1.25M reads of 500 bp = 607M k-mers per GPU -> 2^20), but stay at 16 bits
     // (two radix passes) while the average still fits the 1,024-record kernel
+    // (A/B knobs, experiments only: SA_PART_TARGET records per partition,
+    // SA_MAIN_CAP 1024 / 2048 for the tier that takes one block per partition)
+    static const uint64_t part_target = getenv("SA_PART_TARGET") ? strtoull(getenv("SA_PART_TARGET"), nullptr, 10) : 700;
+    static const uint32_t main_cap = getenv("SA_MAIN_CAP") && atoi(getenv("SA_MAIN_CAP")) >= 2048 ? 2048u : 1024u;
     int PB = 1;
-    while (PB < 24 && ((uint64_t)700 << PB) < n) ++PB;
-    if (PB > 16 && (n >> 16) <= 900) PB = 16;
+    while (PB < 24 && (part_target << PB) < n) ++PB;
+    if (main_cap == 1024 && PB > 16 && (n >> 16) <= 900) PB = 16;
     const uint32_t nparts = 1u << PB;
     const int kbits = 32 + c->lb;  // LDS sort key: mix << lb | loc rank
     uint2 *srl = nullptr;
@@ -407,6 +445,7 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
         PA.lbase = (const uint32_t *)c->d_lbase.p;
         PA.lrank = (const uint32_t *)c->d_lrank.p;
         PA.k = c->set.kmer_size;
+        set_part_shortcuts(c, PA, npr);
         PA.pos_bits = rl || pv ? 0 : c->pos_bits;  // (occurrence indices + the {read, loc rank} table)
         PA.meta = (const uint2 *)c->d_meta.p;
         ENSURE(c->d_md, 3 * n + 3, &PA.lst);
@@ -417,6 +456,7 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
         PA.mid_list = biglist + nparts + 1; PA.mid_n = &cnt->mid_n;
         PA.mid2_list = biglist + 2 * ((size_t)nparts + 1); PA.mid2_n = &cnt->mid2_n;
         PA.counts = cnt->bkt_counts;
+        PA.main_cap = main_cap;
         if (strict) {
             ENSURE(c->d_mdidx, 3 * n + 3, &PA.lidx);
             ENSURE(c->d_srec, n + 1, &PA.srec);
@@ -436,9 +476,14 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
             HIPCHK(launch_part_starts(PA, n, 64 - skip_bits - PB, c->stream));
             HIPCHK(ensure_side(c));
             HIPCHK(fork_side(c, c->ev_fork2));
-            HIPCHK(launch_part_build(PA, strict, 2048, c->side));
-            HIPCHK(launch_part_build(PA, strict, 4096, c->side));
-            HIPCHK(launch_part_build(PA, strict, 1024, c->stream));
+            if (PA.main_cap >= 2048) {
+                HIPCHK(launch_part_build(PA, strict, 4096, c->side));
+                HIPCHK(launch_part_build(PA, strict, 2048, c->stream));
+            } else {
+                HIPCHK(launch_part_build(PA, strict, 2048, c->side));
+                HIPCHK(launch_part_build(PA, strict, 4096, c->side));
+                HIPCHK(launch_part_build(PA, strict, 1024, c->stream));
+            }
             HIPCHK(join_side(c, c->ev_join2));
         }
         if (phase == 1) return SA_OK;
@@ -704,6 +749,7 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
         };
         std::vector<uint32_t> failed;
         int rc_t;
+        uint64_t wide_limit = 64ull * 12288u;  // distinct partners per read the tiers can count
         if ((rc_t = run_tier(2048, 1, q_big, failed))) return rc_t;
         if (strict) {
             if ((rc_t = run_tier(2048, 64, refine(failed, 1, 64), failed))) return rc_t;
@@ -717,27 +763,38 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
             // classes chosen from it ran 1M k=12 reads 172 -> 219 ms):
             // configs[4]'s k = 12 slice has ~24k partners per read -> 2-4
             // classes, not 8; a class that still overflows is refined again
+            // The packed form (one word per slot: 32,768 slots, 24,576 partners, in
+            // the same 128 KB) whenever its 8-bit counts and 24-bit partner ids
+            // hold: every count that matters is <= max_coll <= 255, and only the
+            // dispatched pairs are emitted.  (SA_PACKED_TIER=0: the two-word
+            // table, for A/B runs.)
+            static const bool packed_ok = !getenv("SA_PACKED_TIER") || atoi(getenv("SA_PACKED_TIER")) != 0;
+            const bool packed = packed_ok && !P.emit_all && P.max_coll <= 255 && n_items < 0xFFFFFFu;
+            const int htab = packed ? 32768 : 16384;
+            const uint32_t hcap = (uint32_t)htab * 3u / 4u;
+            wide_limit = 64ull * hcap;
             std::vector<uint32_t> lv[7];  // split 1, 2, 4, ..., 64
             lv[0] = q_huge;
             lv[0].insert(lv[0].end(), failed.begin(), failed.end());  // the 2,048-slot tier's overflow
             failed.clear();
             for (int e = 0; e <= 6; ++e) {
                 std::vector<uint32_t> fest;
-                if ((rc_t = run_tier(16384, 1 << e, lv[e], failed, &fest))) return rc_t;
+                if ((rc_t = run_tier(htab, 1 << e, lv[e], failed, &fest))) return rc_t;
                 if (failed.empty() || e == 6) continue;
                 for (size_t i = 0; i < failed.size(); ++i) {
-                    // classes so that each holds <= 12,288 of this class's
+                    // classes so that each holds <= hcap of this class's
                     // estimated partners (at least 2x finer, at most 64 in all)
                     int ne = e + 1;
-                    while (ne < 6 && (uint64_t)fest[i] > (uint64_t)12288u << (ne - e)) ++ne;
+                    while (ne < 6 && (uint64_t)fest[i] > (uint64_t)hcap << (ne - e)) ++ne;
                     for (uint32_t j = 0; j < (1u << (ne - e)); ++j) lv[ne].push_back(failed[i] + (1u << e) * j);
                 }
                 failed.clear();
             }
         }
         if (!failed.empty() && cur_max() <= cap_s)
-            return fail(c, SA_E_OVERFLOW, strict ? "a read has more than 98,304 distinct partners"
-                                                 : "a read has more than 786,432 distinct partners");
+            return fail(c, SA_E_OVERFLOW, strict ? std::string("a read has more than 98,304 distinct partners")
+                                                 : "a read has more than " + std::to_string(wide_limit) +
+                                                       " distinct partners");
         if (cur_max() <= cap_s) {
             if (P.per_read) {  // regions kept; the recounted reads' pairs are in the shared regions
                 *per_read = true;

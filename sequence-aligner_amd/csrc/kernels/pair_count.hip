@@ -18,6 +18,8 @@
 // Bound: gather latency / LDS atomics; HBM bytes are small.
 #include "../sa_internal.h"
 
+#include <type_traits>
+
 namespace sa {
 
 constexpr int PC_THREADS = 256;
@@ -29,14 +31,24 @@ constexpr int PC_THREADS = 256;
 constexpr int PC_TAB_SMALL = 256;
 constexpr int PC_TAB_BIG = 2048;
 constexpr int PC_TAB_HUGE = 16384;
+// the packed form of the big tier (wide ids, partners < 2^24 - 1, max_coll <=
+// 255): one word per slot, partner | count << 24, and a bitmap of the slots
+// whose 8-bit count wrapped (count > 255: never inside [min, max]); 32,768
+// slots (24,576 partners at 3/4 load) in the 16,384-slot tier's 128 KB, so
+// configs[4]'s k = 12 reads (~24k partners at the 6.25M slice) need one pass
+// where the two-word table needed two or three (one per partner-residue class)
+constexpr int PC_TAB_HUGE2 = 32768;
 constexpr int PC_CHUNK = 512;            // occurrences per pass over a read
 constexpr int PC_BATCH = 8;              // partner loads in flight per thread
 // the per-occurrence records are read once: non-temporal loads keep them from
 // displacing the partner lists in L2
-__device__ __forceinline__ uint4 load_rec(const PairIn &in, uint64_t g) {
+__device__ __forceinline__ uint2 load_rec_raw(const PairIn &in, uint64_t g) {
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
     const u32x2 w = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(in.rec + g));
-    return decode_rec(make_uint2(w.x, w.y), in.xrec);
+    return make_uint2(w.x, w.y);
+}
+__device__ __forceinline__ uint4 load_rec(const PairIn &in, uint64_t g) {
+    return decode_rec(load_rec_raw(in, g), in.xrec);
 }
 constexpr uint32_t PC_EMPTY = 0xFFFFFFFFu;
 constexpr int PC_PROBE_MAX = 256;
@@ -57,6 +69,7 @@ constexpr int PC_WIN = 2048;
 // partner loads in flight per thread); the smaller tables keep 256 threads.
 template <int TAB> struct PcShape {
     static constexpr int NT = TAB >= PC_TAB_HUGE ? 1024 : PC_THREADS;
+    static constexpr bool PACKED = TAB >= PC_TAB_HUGE2;
     static constexpr int CHUNK = TAB >= PC_TAB_HUGE ? 1024 : PC_CHUNK;
     static constexpr int WIN = TAB >= PC_TAB_HUGE ? 4096 : PC_WIN;
     static constexpr int BATCH = TAB >= PC_TAB_HUGE ? 4 : PC_BATCH;
@@ -65,10 +78,14 @@ template <int TAB> struct PcShape {
 template <int TAB>
 struct PcShared {
     static constexpr int NT = PcShape<TAB>::NT, CHUNK = PcShape<TAB>::CHUNK;
-    uint32_t key[TAB];
-    uint32_t cnt[TAB];
+    static constexpr bool PACKED = PcShape<TAB>::PACKED;
+    uint32_t key[TAB];         // packed: partner | count << 24
+    uint32_t cnt[PACKED ? 1 : TAB];
+    uint32_t sat[PACKED ? TAB / 32 : 1];  // packed: the slot's count wrapped past 255
     uint32_t pref[CHUNK + 1];
-    uint4 rec[CHUNK];          // per-occurrence partner ranges (partition.hip)
+    // per-occurrence partner ranges (partition.hip): decoded, or (packed, to fit
+    // the LDS) the raw 8-byte records, decoded where an element is read
+    typename std::conditional<PACKED, uint2, uint4>::type rec[CHUNK];
     uint16_t eo[PcShape<TAB>::WIN];  // element -> occurrence (+1) of the current window
     uint32_t lds4[NT / 64];
     uint32_t emit4[2][NT / 64];  // emission: per-wave kept counts (double-buffered)
@@ -100,10 +117,40 @@ __device__ __forceinline__ uint32_t pc_block_excl_scan(uint32_t v, uint32_t *lds
     return off + inc - v;
 }
 
+__device__ __forceinline__ uint4 pc_rec(const uint4 &r, const PairIn &) { return r; }
+__device__ __forceinline__ uint4 pc_rec(const uint2 &r, const PairIn &in) { return decode_rec(r, in.xrec); }
+
 template <bool STRICT, int TAB>
 __device__ __forceinline__ void pc_insert(PcShared<TAB> &S, PcSharedStrict<TAB> &X, uint32_t partner, uint32_t w,
                                           unsigned long long rank, uint32_t eidx) {
     constexpr uint32_t FILL_MAX = TAB * 3 / 4;
+    if constexpr (PcShape<TAB>::PACKED) {
+        // one word per slot: a CAS inserts (partner, w), a hit adds w << 24 and
+        // marks the slot saturated when the 8-bit count wraps
+        uint32_t slot = pc_hash<TAB>(partner);
+        for (int probe = 0; probe < PC_PROBE_MAX; ++probe) {
+            if ((probe & 15) == 15 && lds_relaxed(&S.overflow)) return;
+            uint32_t old = lds_relaxed(&S.key[slot]);
+            if (old == PC_EMPTY) {
+                old = atomicCAS(&S.key[slot], PC_EMPTY, partner | (w << 24));
+                if (old == PC_EMPTY) {
+                    if (atomicAdd(&S.fill, 1u) >= FILL_MAX) {
+                        S.overflow = 1;
+                        atomicMin(&S.xfill, eidx);
+                    }
+                    return;
+                }
+            }
+            if ((old & 0xFFFFFFu) == partner) {
+                const uint32_t prev = atomicAdd(&S.key[slot], w << 24);
+                if ((prev >> 24) + w > 255u) atomicOr(&S.sat[slot >> 5], 1u << (slot & 31));
+                return;
+            }
+            slot = (slot + 1) & (TAB - 1);
+        }
+        S.overflow = 1;
+        return;
+    }
     uint32_t slot = pc_hash<TAB>(partner);
     // probe runs are bounded: at <= 3/4 load they average < 9 slots, and a run
     // of TAB / 4 (<= PC_PROBE_MAX) only happens in a table that is (nearly) full -- it is
@@ -167,9 +214,11 @@ __global__ __launch_bounds__(PcShape<TAB>::NT) void pair_count_kernel(EmitParams
 
     for (int i = tid; i < TAB; i += NT) {
         S.key[i] = PC_EMPTY;
-        S.cnt[i] = 0;
+        if constexpr (!PcShape<TAB>::PACKED) S.cnt[i] = 0;
         if constexpr (STRICT) X.rank[i] = ~0ull;
     }
+    if constexpr (PcShape<TAB>::PACKED)
+        for (int i = tid; i < TAB / 32; i += NT) S.sat[i] = 0;
     if (tid == 0) { S.fill = 0; S.overflow = 0; S.xfill = 0xFFFFFFFFu; }
 
     // (uniform lengths: no dependent offset load before the record loads)
@@ -189,8 +238,15 @@ __global__ __launch_bounds__(PcShape<TAB>::NT) void pair_count_kernel(EmitParams
             const uint32_t oi = tid * PER + j;  // thread-contiguous
             uint32_t tot = 0;
             if (oi < cn) {
-                const uint4 rc = load_rec(in, g0 + c0 + oi);
-                S.rec[oi] = rc;
+                uint4 rc;
+                if constexpr (PcShape<TAB>::PACKED) {
+                    const uint2 raw = load_rec_raw(in, g0 + c0 + oi);
+                    S.rec[oi] = raw;
+                    rc = decode_rec(raw, in.xrec);
+                } else {
+                    rc = load_rec(in, g0 + c0 + oi);
+                    S.rec[oi] = rc;
+                }
                 tot = (rc.y & 0x3FFFFFFFu) + rc.w;
                 if constexpr (STRICT) X.srec[oi] = in.srec[g0 + c0 + oi];
             }
@@ -243,7 +299,7 @@ __global__ __launch_bounds__(PcShape<TAB>::NT) void pair_count_kernel(EmitParams
                     if (el < wn) {
                         const uint32_t oi = (uint32_t)S.eo[el] - 1u;
                         const uint32_t off = w0 + el - S.pref[oi];
-                        const uint4 rc = S.rec[oi];
+                        const uint4 rc = pc_rec(S.rec[oi], in);
                         const uint32_t nE = rc.y & 0x3FFFFFFFu;
                         const uint64_t q = rec_entry(rc, off);
                         part[bb] = in.lst[q];
@@ -341,9 +397,16 @@ __global__ __launch_bounds__(PcShape<TAB>::NT) void pair_count_kernel(EmitParams
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
             const uint32_t sl = tid * PER + c0 + j;
-            const uint32_t c = S.cnt[sl];
-            if (S.key[sl] != PC_EMPTY && (p.emit_all || ((int32_t)c >= p.min_coll && (int32_t)c <= p.max_coll)))
-                keep |= 1u << j;
+            if constexpr (PcShape<TAB>::PACKED) {  // (no emit_all: the host keeps max_coll <= 255)
+                const uint32_t kw = S.key[sl], c = kw >> 24;
+                if (kw != PC_EMPTY && !((S.sat[sl >> 5] >> (sl & 31)) & 1u) && (int32_t)c >= p.min_coll &&
+                    (int32_t)c <= p.max_coll)
+                    keep |= 1u << j;
+            } else {
+                const uint32_t c = S.cnt[sl];
+                if (S.key[sl] != PC_EMPTY && (p.emit_all || ((int32_t)c >= p.min_coll && (int32_t)c <= p.max_coll)))
+                    keep |= 1u << j;
+            }
         }
         const int buf = (c0 / CH) & 1;  // slow readers of the previous chunk's counts are not overwritten
         const uint32_t mine = __popc(keep);
@@ -370,8 +433,13 @@ __global__ __launch_bounds__(PcShape<TAB>::NT) void pair_count_kernel(EmitParams
             const unsigned long long at = region + lat;
             if (lat < o.cap_s) {
                 o.fst[at] = a;
-                o.snd[at] = S.key[sl];
-                o.cnt[at] = S.cnt[sl];
+                if constexpr (PcShape<TAB>::PACKED) {
+                    o.snd[at] = S.key[sl] & 0xFFFFFFu;
+                    o.cnt[at] = S.key[sl] >> 24;
+                } else {
+                    o.snd[at] = S.key[sl];
+                    o.cnt[at] = S.cnt[sl];
+                }
                 if constexpr (STRICT) o.rank[at] = X.rank[sl];
             }
         }
@@ -698,6 +766,11 @@ hipError_t launch_pair_count(const EmitParams &e, const PairIn &in, const PairPa
     if (p.table == PC_TAB_SMALL) return pc_launch<false, PC_TAB_SMALL>(e, in, p, o, read_list, n_blocks, s);
     if (p.table == PC_TAB_BIG) return pc_launch<false, PC_TAB_BIG>(e, in, p, o, read_list, n_blocks, s);
     if (p.table == PC_TAB_HUGE) return pc_launch<false, PC_TAB_HUGE>(e, in, p, o, read_list, n_blocks, s);
+    if (p.table == PC_TAB_HUGE2) {
+        // (the host routes here only with partners < 2^24 - 1, max_coll <= 255, no emit_all)
+        if (p.emit_all || p.max_coll > 255) return hipErrorInvalidValue;
+        return pc_launch<false, PC_TAB_HUGE2>(e, in, p, o, read_list, n_blocks, s);
+    }
     return hipErrorInvalidValue;
 }
 

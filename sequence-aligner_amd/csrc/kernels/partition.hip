@@ -71,8 +71,12 @@ __device__ __forceinline__ unsigned long long record_key(uint64_t rec, const Par
     } else {
         const uint32_t r = read_of_g(g, A.occ_off, A.n_reads, A.npr, A.npr_magic);
         const uint32_t pos = A.npr ? g - r * A.npr : g - (uint32_t)A.occ_off[r];
-        const int32_t d = A.npr ? (int32_t)A.npr - 1 : A.len[r] - A.k;
-        lr = A.lrank[A.lbase[d] + pos];
+        if (A.lr_ident) {
+            lr = pos;
+        } else {
+            const int32_t d = A.npr ? (int32_t)A.npr - 1 : A.len[r] - A.k;
+            lr = A.lrank[A.lbase[d] + pos];
+        }
     }
     return ((rec >> 32) << A.lb) | lr;
 }
@@ -244,7 +248,7 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
         tagv[j] = 0;
         if (s < n) {
             const unsigned long long k = S.key[s];
-            const uint32_t t = A.tagtab[k & lbm];
+            const uint32_t t = part_tag(A, (uint32_t)(k & lbm));
             tagv[j] = t;
             const bool bh = s == 0 || (S.key[s - 1] >> lb) != (k >> lb);
             const bool gh = s == 0 || S.key[s - 1] != k;
@@ -401,12 +405,12 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
 // block is spent reading the bounds of a partition already built while holding
 // 44 / 84 KB of LDS, and a partition of ~1,100 records is sorted over 2,048
 // slots, not 4,096 (the tail of the stage is one such block's latency).
-template <int CAP, bool STRICT>
+template <int CAP, bool STRICT, bool MAIN>
 __global__ __launch_bounds__(PB_THREADS) void part_build_kernel(PartArgs A) {
     extern __shared__ __align__(16) uint8_t smem_raw[];
     PartShared<CAP> &S = *reinterpret_cast<PartShared<CAP> *>(smem_raw);
     uint32_t *Sr = A.rl || A.pv ? reinterpret_cast<uint32_t *>(smem_raw + sizeof(PartShared<CAP>)) : nullptr;
-    if constexpr (CAP < 2048) {
+    if constexpr (MAIN) {  // the main pass: one block per partition
         part_build_one<CAP, STRICT>(A, blockIdx.x, S, Sr);
     } else {
         const uint32_t *list = CAP >= 4096 ? A.mid2_list : A.mid_list;
@@ -511,7 +515,7 @@ __global__ void records_from_tables_kernel(const uint64_t *sk, const uint32_t *s
 // the 2,048 / 4,096-record tiers need not wait for the 1,024-record pass: they
 // run beside it on a second stream.
 __global__ void part_bounds_kernel(const uint64_t *sk, uint64_t n, int shift, uint32_t mask, uint32_t np,
-                                   uint32_t *start, uint32_t *mid_list, uint32_t *mid_n) {
+                                   uint32_t *start, uint32_t *mid_list, uint32_t *mid_n, uint32_t main_cap) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p > np) return;
     const bool two = p < np;
@@ -527,12 +531,16 @@ __global__ void part_bounds_kernel(const uint64_t *sk, uint64_t n, int shift, ui
         }
     }
     start[p] = (uint32_t)lo;
-    if (two && lo1 - lo > 1024u) mid_list[atomicAdd(mid_n, 1u)] = p;
+    if (two && lo1 - lo > main_cap) mid_list[atomicAdd(mid_n, 1u)] = p;
 }
 
 hipError_t launch_part_starts(const PartArgs &a, uint64_t n, int shift, hipStream_t s) {
+    // partitions above the main pass's capacity are listed for the next tier
+    // (main 1,024: the 2,048 tier's list; main 2,048: the 4,096 tier's)
+    const bool m2 = a.main_cap >= 2048;
     hipLaunchKernelGGL(part_bounds_kernel, dim3((a.np + 1 + 255) / 256), dim3(256), 0, s, a.sk, n, shift, a.np - 1,
-                       a.np, const_cast<uint32_t *>(a.start), a.mid_list, a.mid_n);
+                       a.np, const_cast<uint32_t *>(a.start), m2 ? a.mid2_list : a.mid_list, m2 ? a.mid2_n : a.mid_n,
+                       m2 ? 2048u : 1024u);
     return hipGetLastError();
 }
 
@@ -540,20 +548,26 @@ hipError_t launch_part_starts(const PartArgs &a, uint64_t n, int shift, hipStrea
 // over the lists the bounds kernel / the 2,048 tier made
 hipError_t launch_part_build(const PartArgs &a, bool strict, int cap, hipStream_t s) {
     if (!a.np) return hipSuccess;
-#define PB_LAUNCH(CAPV, GRID, ST)                                                                          \
+#define PB_LAUNCH(CAPV, GRID, ST, MAINV)                                                                   \
     do {                                                                                                 \
         const size_t lds = part_lds<CAPV>() + (a.rl || a.pv ? 4 * (size_t)(CAPV) : 0);                   \
-        (void)hipFuncSetAttribute((const void *)part_build_kernel<CAPV, ST>,                             \
+        (void)hipFuncSetAttribute((const void *)part_build_kernel<CAPV, ST, MAINV>,                      \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                 \
-        hipLaunchKernelGGL((part_build_kernel<CAPV, ST>), dim3(GRID), dim3(PB_THREADS), lds, s, a);     \
+        hipLaunchKernelGGL((part_build_kernel<CAPV, ST, MAINV>), dim3(GRID), dim3(PB_THREADS), lds, s, a); \
     } while (0)
     const uint32_t mid_grid = a.np < 1024u ? a.np : 1024u;
+    const bool m2 = a.main_cap >= 2048;
     if (cap == 1024) {
-        if (strict) PB_LAUNCH(1024, a.np, true); else PB_LAUNCH(1024, a.np, false);
+        if (m2) return hipSuccess;  // (no 1,024 pass: the 2,048-record pass is the main one)
+        if (strict) PB_LAUNCH(1024, a.np, true, true); else PB_LAUNCH(1024, a.np, false, true);
     } else if (cap == 2048) {
-        if (strict) PB_LAUNCH(2048, mid_grid, true); else PB_LAUNCH(2048, mid_grid, false);
+        if (m2) {
+            if (strict) PB_LAUNCH(2048, a.np, true, true); else PB_LAUNCH(2048, a.np, false, true);
+        } else {
+            if (strict) PB_LAUNCH(2048, mid_grid, true, false); else PB_LAUNCH(2048, mid_grid, false, false);
+        }
     } else {
-        if (strict) PB_LAUNCH(4096, mid_grid, true); else PB_LAUNCH(4096, mid_grid, false);
+        if (strict) PB_LAUNCH(4096, mid_grid, true, false); else PB_LAUNCH(4096, mid_grid, false, false);
     }
 #undef PB_LAUNCH
     return hipGetLastError();

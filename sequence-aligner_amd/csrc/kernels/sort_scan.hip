@@ -123,7 +123,10 @@ hipError_t exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, uin
 // radix sort
 // ---------------------------------------------------------------------------
 constexpr int RS_THREADS = 256;
-constexpr int RS_ITEMS = 16;
+#ifndef SA_RS_ITEMS
+#define SA_RS_ITEMS 16  // keys per thread of a radix tile (A/B builds: make OUT=build_x EXTRA=-DSA_RS_ITEMS=8)
+#endif
+constexpr int RS_ITEMS = SA_RS_ITEMS;
 constexpr int RS_TILE = RS_THREADS * RS_ITEMS;
 
 // Tile histograms, BLOCK-major: hist[tile * 256 + digit] (one coalesced 1 KB

@@ -339,6 +339,15 @@ struct PartArgs {
     const int32_t *len;
     const uint32_t *lbase, *lrank;
     int32_t k;
+    // uniform lengths whose loc ranks are the positions themselves (no NaN loc):
+    // lrank[lbase[npr - 1] + pos] == pos, so the rank needs no dependent gather
+    int32_t lr_ident;
+    // the tags as loc-rank intervals (tagtab is three runs in rank order: st a
+    // prefix, md an interval, en an interval ending below the NaN rank):
+    // tag = [lr < tg_st] st | [lr - tg_md0 < tg_mdn] md | [lr - tg_en0 < tg_enn] en;
+    // tg_on = 0: look tagtab up instead
+    int32_t tg_on;
+    uint32_t tg_st, tg_md0, tg_mdn, tg_en0, tg_enn;
     // mixed read lengths, wide ids: records carry read << pos_bits | pos and
     // meta[read] = {first occurrence index, lrank offset of its length}
     int32_t pos_bits;
@@ -351,12 +360,19 @@ struct PartArgs {
     uint32_t *mid_list, *mid_n;    // partitions above 1,024 records (2,048-record LDS pass)
     uint32_t *mid2_list, *mid2_n;  // partitions above 2,048 records (4,096-record LDS pass)
     unsigned long long *counts;  // [2][NSHARD]: buckets, groups
+    uint32_t main_cap;           // 1,024 or 2,048: the tier that takes one block per partition
     // strict
     uint32_t *lidx;              // parallel to lst
     uint4 *srec;                 // [n_occ] by g
     uint32_t *bkt_nst, *bkt_nmd, *bkt_first;  // at bucket head sorted positions
     uint8_t *is_head;            // [n] head flags
 };
+// the tag of loc rank lr (tagtab[lr], by intervals when tg_on)
+__device__ __forceinline__ uint32_t part_tag(const PartArgs &A, uint32_t lr) {
+    if (!A.tg_on) return A.tagtab[lr];
+    return (lr < A.tg_st ? (uint32_t)TAG_ST : 0u) | (lr - A.tg_md0 < A.tg_mdn ? (uint32_t)TAG_MD : 0u) |
+           (lr - A.tg_en0 < A.tg_enn ? (uint32_t)TAG_EN : 0u);
+}
 hipError_t launch_part_starts(const PartArgs &a, uint64_t n, int shift, hipStream_t s);
 hipError_t launch_part_build(const PartArgs &a, bool strict, int cap, hipStream_t s);
 // 8-byte records of one big partition -> (mix << lb | locrank, g) for the global scan path

@@ -118,16 +118,19 @@ def test_readme_record_pinned():
     assert out.index(README_RECORD) == golden.index(README_RECORD)
 
 
-@pytest.mark.parametrize("n_edge", [5000, 12800, 110000])
-def test_many_partner_reads_recount_tiers(oracle_mod, n_edge):
+@pytest.mark.parametrize("n_edge,max_coll", [(5000, 222), (12800, 222), (110000, 222), (12800, 300),
+                                            (110000, 300)])
+def test_many_partner_reads_recount_tiers(oracle_mod, n_edge, max_coll):
     """Reads with thousands to >98k distinct partners (configs[4]'s k = 12
     stress in miniature): 8 reads carry a 17 bp motif in their middle region,
     n_edge reads carry it at their start, so each middle read leads a pair with
     every edge read (the 15-mers inside the motif, plus those straddling its
-    edges that share their few random bases).  5,000 partners take the
-    16,384-slot tier, 12,800 its 8-way residue split, 110,000 the 64-way split
-    (which refines only the classes that overflowed).  Dispatch and counts vs
-    the oracle, wide ids."""
+    edges that share their few random bases).  max_collisions 222: the packed
+    32,768-slot tier (5,000 and 12,800 partners in one pass, 110,000 in residue
+    classes); max_collisions 300 (counts past 8 bits matter): the two-word
+    16,384-slot tier, 12,800 partners in its 8-way residue split, 110,000 in the
+    64-way split (which refines only the classes that overflowed).  Dispatch
+    and counts vs the oracle, wide ids."""
     rng = np.random.default_rng(n_edge)
     motif = "".join("ACGT"[x] for x in rng.integers(0, 4, 17))
     n_mid = 8
@@ -136,7 +139,7 @@ def test_many_partner_reads_recount_tiers(oracle_mod, n_edge):
         s_ = "".join("ACGT"[x] for x in rng.integers(0, 4, 120))
         p_ = 55 if i < n_mid else 5   # loc 0.52 (md) vs 0.05 (st), L - k = 105
         reads.append(s_[:p_] + motif + s_[p_ + 17:])
-    st = dict(kmer_size=15, min_collisions=3)
+    st = dict(kmer_size=15, min_collisions=3, max_collisions=max_coll)
     ov = sao.Overlapper(id_mode=sao.SA_IDS_WIDE, **st)
     ov.add_reads(reads)
     ov.build()
@@ -159,6 +162,40 @@ def test_many_partner_reads_recount_tiers(oracle_mod, n_edge):
     np.testing.assert_array_equal(t2, trail)
     np.testing.assert_array_equal(c2, count)
     sl.close()
+
+
+def test_packed_tier_count_saturation(oracle_mod):
+    """The packed tier's 8-bit counts: a pair that collides hundreds of times (a
+    40 bp poly-A run in the middle of one read and at the start of another) must
+    stay above max_collisions although its count field wraps (e.g. 729 = 2 x 256
+    + 217, inside [3, 222]); the lead has 3,000 other partners,
+    so it is counted in the packed 32,768-slot tier.  Dispatch and counts vs
+    the oracle."""
+    rng = np.random.default_rng(676)
+    motif = "".join("ACGT"[x] for x in rng.integers(0, 4, 17))
+    reads = []
+    for i in range(8 + 3000):
+        s_ = "".join("ACGT"[x] for x in rng.integers(0, 4, 120))
+        p_ = 55 if i < 8 else 5
+        reads.append(s_[:p_] + motif + s_[p_ + 17:])
+    # a 300 bp middle read: the motif at loc 0.53, the run at locs 0.32-0.40 (md)
+    s_ = "".join("ACGT"[x] for x in rng.integers(0, 4, 300))
+    reads[0] = s_[:90] + "A" * 40 + s_[130:150] + motif + s_[167:]
+    reads.append("A" * 40 + reads[8][40:])  # a new edge read: the run at its start
+    st = dict(kmer_size=15, min_collisions=3, max_collisions=222)
+    r = oracle_mod.Run(reads=reads, settings=oracle_mod.default_settings(**st), wide=True, skip_align=True)
+    okey = (r.pair_fst.astype(np.int64) << 32) | r.pair_snd
+    big = r.pair_cnt[np.searchsorted(okey, (1 << 32) | len(reads))]
+    assert big > 255  # the wrapping pair exists in the reference's counts
+    ov = sao.Overlapper(id_mode=sao.SA_IDS_WIDE, **st)
+    ov.add_reads(reads)
+    ov.build()
+    lead, trail, count = ov.dispatch()
+    np.testing.assert_array_equal(lead, r.lead)
+    np.testing.assert_array_equal(trail, r.trail)
+    assert ov.stats()["flags"] & sao.SA_STATS_RECOUNTED
+    assert not ((lead == 1) & (trail == len(reads))).any()
+    ov.close()
 
 
 @pytest.mark.parametrize("shards", [4, 8])
