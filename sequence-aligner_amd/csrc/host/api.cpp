@@ -572,7 +572,8 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
 int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bool emit_all,
                const uint32_t *read_order, uint32_t n_items, Counters *cnt, uint64_t &np, uint64_t &cap_s_out,
                const uint32_t *item_start = nullptr, uint32_t n_multi = 0, const uint32_t *abort_flag = nullptr,
-               bool *aborted = nullptr, bool *per_read = nullptr, uint64_t *distinct_ub = nullptr) {
+               bool *aborted = nullptr, bool *per_read = nullptr, uint64_t *distinct_ub = nullptr,
+               bool all_partials = false) {
     // per_read (in: allowed; out: used): the first pass writes each read's
     // dispatched pairs, trail-ascending, into a fixed region of PC_RREG slots
     // (wide ids, dispatched pairs only, one device); a read whose table
@@ -586,6 +587,10 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
     PairParams P;
     P.min_coll = c->set.min_collisions;
     P.max_coll = c->set.max_collisions;
+    if (all_partials) {  // sharded path, per-read regions: every distinct partial (count >= 1)
+        P.min_coll = 1;
+        P.max_coll = INT32_MAX;
+    }
     P.emit_all = emit_all ? 1 : 0;
     P.strict = strict ? 1 : 0;
     P.split = 1;
@@ -815,6 +820,53 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
 }
 
 
+// The per-read regions (pair_stage's per_read mode) as one (lead, trail, count)
+// list, lead descending, trail ascending, ids 1-based: the regions in order of
+// an exclusive scan of their counts, with the reads the tiers recounted (np
+// pairs in the shared regions, their regions empty) taken from those pairs
+// sorted lead-descending / trail-ascending -- each such read's segment start in
+// rsh[read] (+1), its length in rcnt[read].  The total lands in cnt->rtotal.
+int assemble_read_regions(sa_ctx *c, uint32_t nr, uint64_t np, uint64_t np_ub, uint64_t cap_s, Counters *cnt,
+                          int32_t **dlead, int32_t **dtrail, int32_t **dcount) {
+    uint32_t *rex; uint8_t *stmp2;
+    uint64_t *ok, *ok2; uint32_t *ov, *ov2; uint8_t *otmp;
+    ENSURE(c->d_lead, np_ub, dlead);
+    ENSURE(c->d_trail, np_ub, dtrail);
+    ENSURE(c->d_count, np_ub, dcount);
+    ENSURE(c->d_rex, (uint64_t)nr + 1, &rex);
+    uint32_t *rcnt = (uint32_t *)c->d_rcnt.p;
+    const int32_t *stl = nullptr, *scn = nullptr;
+    uint32_t *rsh = nullptr;
+    if (np) {
+        int32_t *shl, *sht, *shc;
+        ENSURE(c->d_okeys, np, &ok);
+        ENSURE(c->d_okeys2, np, &ok2);
+        ENSURE(c->d_ovals, np, &ov);
+        ENSURE(c->d_ovals2, np, &ov2);
+        ENSURE(c->d_osort, std::max(radix_sort_temp_bytes(np), scan_temp_bytes(nr)), &otmp);
+        ENSURE(c->d_shl, np, &shl);
+        ENSURE(c->d_sht, np, &sht);
+        ENSURE(c->d_shc, np, &shc);
+        ENSURE(c->d_rsh, nr, &rsh);
+        const int idb = bits_for(nr ? nr - 1 : 0);
+        HIPCHK(launch_make_order_keys((const uint32_t *)c->d_pf.p, (const uint32_t *)c->d_ps.p, nullptr,
+                                      cnt->cursor, cap_s, 0, idb, ok, ov, cnt->shard_off, c->stream));
+        HIPCHK(radix_sort(&ok, &ov, &ok2, &ov2, np, 0, 2 * idb, otmp, c->stream));
+        HIPCHK(launch_gather_pairs(ov, np, (const uint32_t *)c->d_pf.p, (const uint32_t *)c->d_ps.p,
+                                   (const uint32_t *)c->d_pc.p, shl, sht, shc, c->stream));
+        HIPCHK(hipMemsetAsync(rsh, 0, (size_t)nr * 4, c->stream));
+        HIPCHK(launch_mark_segments(shl, np, rsh, rcnt, c->stream));
+        stl = sht; scn = shc;
+        stmp2 = otmp;
+    } else {
+        ENSURE(c->d_osort, scan_temp_bytes(nr), &stmp2);
+    }
+    HIPCHK(exclusive_scan_u32(rcnt, rex, nr, &cnt->rtotal, stmp2, c->stream));
+    HIPCHK(launch_copy_read_regions((const uint2 *)c->d_rreg.p, rcnt, rex, &cnt->rtotal, nr, rsh, stl, scn,
+                                    *dlead, *dtrail, *dcount, c->stream));
+    return SA_OK;
+}
+
 // ---------------------------------------------------------------------------
 // candidate build (device), optional host readback
 // ---------------------------------------------------------------------------
@@ -987,46 +1039,8 @@ int device_build(sa_ctx *c, bool readback) {
     int32_t *dlead, *dtrail, *dcount;
     uint64_t *ok, *ok2; uint32_t *ov, *ov2; uint8_t *otmp;
     if (per_read) {
-        uint32_t *rex; uint8_t *stmp2;
-        ENSURE(c->d_lead, np_ub, &dlead);
-        ENSURE(c->d_trail, np_ub, &dtrail);
-        ENSURE(c->d_count, np_ub, &dcount);
-        ENSURE(c->d_rex, (uint64_t)nr + 1, &rex);
-        uint32_t *rcnt = (uint32_t *)c->d_rcnt.p;
         StageScope st(c, SA_STAGE_ORDER);
-        // reads the tiers recounted (np pairs in the shared regions, their
-        // regions empty): those pairs sorted lead-descending / trail-ascending,
-        // each such read's segment start into rsh[read] (+1) and its length
-        // into rcnt[read]; the copy then takes those reads from the segments
-        const int32_t *stl = nullptr, *scn = nullptr;
-        uint32_t *rsh = nullptr;
-        if (np) {
-            int32_t *shl, *sht, *shc;
-            ENSURE(c->d_okeys, np, &ok);
-            ENSURE(c->d_okeys2, np, &ok2);
-            ENSURE(c->d_ovals, np, &ov);
-            ENSURE(c->d_ovals2, np, &ov2);
-            ENSURE(c->d_osort, std::max(radix_sort_temp_bytes(np), scan_temp_bytes(nr)), &otmp);
-            ENSURE(c->d_shl, np, &shl);
-            ENSURE(c->d_sht, np, &sht);
-            ENSURE(c->d_shc, np, &shc);
-            ENSURE(c->d_rsh, nr, &rsh);
-            const int idb = bits_for(nr ? nr - 1 : 0);
-            HIPCHK(launch_make_order_keys((const uint32_t *)c->d_pf.p, (const uint32_t *)c->d_ps.p, nullptr,
-                                          cnt->cursor, cap_s, 0, idb, ok, ov, cnt->shard_off, c->stream));
-            HIPCHK(radix_sort(&ok, &ov, &ok2, &ov2, np, 0, 2 * idb, otmp, c->stream));
-            HIPCHK(launch_gather_pairs(ov, np, (const uint32_t *)c->d_pf.p, (const uint32_t *)c->d_ps.p,
-                                       (const uint32_t *)c->d_pc.p, shl, sht, shc, c->stream));
-            HIPCHK(hipMemsetAsync(rsh, 0, (size_t)nr * 4, c->stream));
-            HIPCHK(launch_mark_segments(shl, np, rsh, rcnt, c->stream));
-            stl = sht; scn = shc;
-            stmp2 = otmp;
-        } else {
-            ENSURE(c->d_osort, scan_temp_bytes(nr), &stmp2);
-        }
-        HIPCHK(exclusive_scan_u32(rcnt, rex, nr, &cnt->rtotal, stmp2, c->stream));
-        HIPCHK(launch_copy_read_regions((const uint2 *)c->d_rreg.p, rcnt, rex, &cnt->rtotal, nr, rsh, stl, scn,
-                                        dlead, dtrail, dcount, c->stream));
+        if ((rc = assemble_read_regions(c, nr, np, np_ub, cap_s, cnt, &dlead, &dtrail, &dcount))) return rc;
     }
     if (!per_read) {
         ENSURE(c->d_okeys, np, &ok);
@@ -1421,7 +1435,7 @@ void sa_ctx_destroy(sa_ctx *c) {
                     &c->d_ovl, &c->d_cnt, &c->d_okeys, &c->d_ovals, &c->d_okeys2, &c->d_ovals2, &c->d_osort,
                     &c->d_lead, &c->d_trail, &c->d_count, &c->d_aln, &c->d_p1, &c->d_tb, &c->d_rkey, &c->d_rkey2, &c->d_rord, &c->d_rord2, &c->d_rtmp, &c->d_gocc, &c->d_seg, &c->d_rl, &c->d_srl, &c->d_srl2, &c->d_loff, &c->d_starts, &c->d_bounds, &c->d_gcodes, &c->d_gwoff, &c->d_glen, &c->d_gbad, &c->d_psum, &c->d_pkeep, &c->d_ppos, &c->d_scan, &c->d_pstart, &c->d_biglist, &c->d_rec,
                     &c->d_srec, &c->d_bnmd, &c->d_ishead, &c->d_bnst2, &c->d_tmd, &c->d_ted, &c->d_tmdi,
-                    &c->d_tedi, &c->d_xrec, &c->d_tier, &c->d_ovlrp, &c->d_meta, &c->d_items, &c->d_lr, &c->d_bigtot, &c->d_hk0, &c->d_hk1, &c->d_hflag,
+                    &c->d_tedi, &c->d_xrec, &c->d_tier, &c->d_ovlrp, &c->d_meta, &c->d_items, &c->d_pq, &c->d_lr, &c->d_bigtot, &c->d_hk0, &c->d_hk1, &c->d_hflag,
                     &c->d_hidx, &c->d_hpos, &c->d_htmp, &c->d_hist, &c->d_hovf, &c->d_hsmall,
                     &c->d_ltb, &c->d_lmax, &c->d_rreg, &c->d_rcnt, &c->d_rex,
                     &c->d_shl, &c->d_sht, &c->d_shc, &c->d_rsh};
@@ -1924,13 +1938,51 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint6
     EmitParams E = emit_params(c);
     E.occ_off = loff;  // occurrences of read a on this rank: [loff[a], loff[a+1])
     E.npr = 0;
-    // every global read has ~1/P of its occurrences here: blocks take ranges of
-    // reads with ~PCM_TARGET local occurrences (pair_count.hip, multi-read blocks)
+    uint64_t np = 0, cap_s = 0;
+    // Every global read has ~1/P of its occurrences here.  Per-read regions
+    // (one wave per read, as the single-device first pass, over the read's
+    // local occurrences [loff[a], loff[a + 1])) with every distinct partial kept
+    // (count >= 1: the filter needs the global sums): the list comes out lead-
+    // descending, so each owner's partials are one contiguous range -- no owner
+    // sort, no per-block output claims.  Regions beyond 32 GB (or
+    // SA_SHARD_MULTI=1, A/B runs): multi-read blocks over ~PCM_TARGET local
+    // occurrences, partials sorted by owner.
+    static const bool multi_forced = getenv("SA_SHARD_MULTI") && atoi(getenv("SA_SHARD_MULTI")) != 0;
+    bool per_read = !multi_forced && (uint64_t)N * PC_RREG * sizeof(uint2) <= (32ull << 30);
+    uint64_t np_ub = 0;
+    if (per_read) {
+        rc = pair_stage(c, E, PI, false, false, nullptr, N, cnt, np, cap_s, nullptr, 0, nullptr, nullptr, &per_read,
+                        &np_ub, true);
+        if (rc) return rc;
+    }
+    c->part_per_read = per_read;
+    if (per_read) {
+        int32_t *dl, *dt, *dc;
+        uint64_t *q;
+        ENSURE(c->d_bounds, (size_t)c->nranks + 1, &q);
+        {
+            StageScope st(c, SA_STAGE_ORDER);
+            if ((rc = assemble_read_regions(c, N, np, np_ub, cap_s, cnt, &dl, &dt, &dc))) return rc;
+            HIPCHK(launch_desc_owner_bounds(dl, &cnt->rtotal, (const uint32_t *)c->d_starts.p, (uint32_t)c->nranks, q,
+                                            c->stream));
+        }
+        Counters hc;
+        c->part_q.assign((size_t)c->nranks + 1, 0);
+        HIPCHK(hipMemcpyAsync(&hc, cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(c->part_q.data(), q, c->part_q.size() * 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        resolve_timing(c);
+        for (int o = 0; o < c->nranks; ++o) counts[o] = c->part_q[o] - c->part_q[o + 1];
+        c->part_np = hc.rtotal;
+        c->part_perm = nullptr;
+        c->stats.buckets = shard_sum(hc.bkt_counts) + big_buckets;
+        c->stats.role_pairs = shard_sum(hc.role_pairs);
+        return SA_OK;
+    }
     const uint32_t n_multi = (uint32_t)((n + PCM_TARGET - 1) / PCM_TARGET) + 1;
     uint32_t *items;
     ENSURE(c->d_items, (size_t)n_multi + 1, &items);
     HIPCHK(launch_pc_items(loff, N, PCM_TARGET, n_multi, items, c->stream));
-    uint64_t np = 0, cap_s = 0;
     rc = pair_stage(c, E, PI, false, true, nullptr, N, cnt, np, cap_s, items, n_multi);
     if (rc) return rc;
     // partials grouped by the rank owning their lead (one stable pass on the
@@ -1971,6 +2023,26 @@ int sa_dist_partials(sa_ctx *c, void *fst, void *snd, void *cnt_out) {
     if (!c->dist) return fail(c, SA_E_STATE, "sa_dist_init first");
     if (c->part_np && (!fst || !snd || !cnt_out)) return SA_E_ARG;
     (void)hipSetDevice(c->device);
+    if (c->part_per_read) {
+        // owners ascending: owner o's partials [part_q[o + 1], part_q[o]) of the
+        // lead-descending list go to out[oo[o] ..]
+        const uint32_t P = (uint32_t)c->nranks;
+        std::vector<uint64_t> oq(2 * ((size_t)P + 1));
+        uint64_t acc = 0;
+        for (uint32_t o = 0; o <= P; ++o) {
+            oq[o] = c->part_q[o];
+            oq[P + 1 + o] = acc;
+            if (o < P) acc += c->part_q[o] - c->part_q[o + 1];
+        }
+        uint64_t *doq;
+        ENSURE(c->d_pq, oq.size(), &doq);
+        HIPCHK(hipMemcpyAsync(doq, oq.data(), oq.size() * 8, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(launch_copy_partials((const int32_t *)c->d_lead.p, (const int32_t *)c->d_trail.p,
+                                    (const int32_t *)c->d_count.p, c->part_np, doq, P, (uint32_t *)fst, (uint32_t *)snd,
+                                    (uint32_t *)cnt_out, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        return SA_OK;
+    }
     HIPCHK(launch_gather_partials(c->part_perm, c->part_np, (const uint32_t *)c->d_pf.p, (const uint32_t *)c->d_ps.p,
                                   (const uint32_t *)c->d_pc.p, (uint32_t *)fst, (uint32_t *)snd, (uint32_t *)cnt_out,
                                   c->stream));

@@ -84,11 +84,18 @@ __device__ __forceinline__ unsigned long long record_key(uint64_t rec, const Par
 // ---------------------------------------------------------------------------
 // the LDS partition builder
 // ---------------------------------------------------------------------------
-constexpr int PB_THREADS = 256;
-
+// A tier of CAP records runs CAP / 4 threads (4 items each): the 1,024-record
+// tier 4 waves, the 2,048-record tier 8, the 4,096-record tier 16.  A block's
+// latency is set by its chain of LDS passes and barriers, nearly the same for
+// any CAP at 4 items per thread, so bigger partitions spread that chain over
+// more records.
+template <int CAP> struct PbShape {
+    static constexpr int NT = CAP / 4, WAVES = NT / 64, IT = 4;
+};
 
 template <int CAP>
 struct PartShared {
+    static constexpr int WAVES = PbShape<CAP>::WAVES;
     unsigned long long key[CAP];
     uint32_t g[CAP];                 // occurrence code of load slot i
     uint16_t oi[CAP];                // load slot of sorted item s (moves with the key)
@@ -97,14 +104,14 @@ struct PartShared {
     // (<= 2 * CAP), so the 1,024-record block fits 18.5 KB -> 8 blocks per CU
     union {
         struct {
-            uint32_t cnt[4][256];    // LDS radix sort: per-wave digit counts
-            uint16_t ofs[4][256];    // each wave's scatter base per digit
+            uint32_t cnt[WAVES][256];  // LDS radix sort: per-wave digit counts
+            uint16_t ofs[WAVES][256];  // each wave's scatter base per digit
         };
         struct {
-            uint16_t mdx[CAP + 2];   // exclusive md count (partition-local)
-            uint16_t edx[CAP + 2];   // exclusive edge-role count
-            uint4 agg[4];            // per-wave inclusive aggregates of the combined block scan
-            uint2 aggu[4];
+            uint16_t mdx[CAP + 2];     // exclusive md count (partition-local)
+            uint16_t edx[CAP + 2];     // exclusive edge-role count
+            uint4 agg[WAVES];          // per-wave inclusive aggregates of the combined block scan
+            uint2 aggu[WAVES];
         };
     };
 };
@@ -119,7 +126,8 @@ static_assert(sizeof(PartShared<1024>) <= 20480, "1,024-record block must fit 8 
 // barriers (counts complete; scatter complete).
 template <int CAP, class SH>
 __device__ __forceinline__ void lds_radix_sort(SH &S, uint32_t n, int bits) {
-    constexpr int SUB = CAP / 4, SL = SUB / 64;
+    constexpr int WAVES = PbShape<CAP>::WAVES;
+    constexpr int SUB = CAP / WAVES, SL = SUB / 64;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     for (int shift = 0; shift < bits; shift += 8) {
@@ -154,7 +162,7 @@ __device__ __forceinline__ void lds_radix_sort(SH &S, uint32_t n, int bits) {
         {
             uint32_t tot[4] = {0, 0, 0, 0}, mine[4] = {0, 0, 0, 0};
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < WAVES; ++q) {
                 const uint4 c = reinterpret_cast<const uint4 *>(S.cnt[q])[lane];
                 tot[0] += c.x; tot[1] += c.y; tot[2] += c.z; tot[3] += c.w;
                 if (q < w) { mine[0] += c.x; mine[1] += c.y; mine[2] += c.z; mine[3] += c.w; }
@@ -188,7 +196,7 @@ __device__ __forceinline__ void lds_radix_sort(SH &S, uint32_t n, int bits) {
 template <int CAP, bool STRICT>
 __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t p, PartShared<CAP> &S,
                                                uint32_t *Sr) {
-    constexpr int IT = CAP / PB_THREADS;
+    constexpr int IT = PbShape<CAP>::IT, NT = PbShape<CAP>::NT;
     const int tid = threadIdx.x;
     const uint32_t ps = A.start[p], pe = A.start[p + 1];
     const uint32_t n = pe - ps;
@@ -207,7 +215,7 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
         uint64_t recs[IT];
 #pragma unroll
         for (int j = 0; j < IT; ++j) {
-            const uint32_t i = tid + j * PB_THREADS;
+            const uint32_t i = tid + j * NT;
             recs[j] = load_sk(A.sk + ps + (i < n ? i : n - 1));
         }
         // (keys of the clamped slots too: their loc-rank gathers issue together)
@@ -215,7 +223,7 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
         uint32_t gg[IT], rr[IT];
 #pragma unroll
         for (int j = 0; j < IT; ++j) {
-            const uint32_t i = tid + j * PB_THREADS, ic = i < n ? i : n - 1;
+            const uint32_t i = tid + j * NT, ic = i < n ? i : n - 1;
             rr[j] = 0;
             const uint2 *rlp = A.srl ? A.srl + ps + ic : (A.rl ? A.rl + (uint32_t)recs[j] : nullptr);
             const uint32_t *pvp = A.spv ? A.spv + ps + ic : (A.pv ? A.pv + (uint32_t)recs[j] : nullptr);
@@ -223,7 +231,7 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
         }
 #pragma unroll
         for (int j = 0; j < IT; ++j) {
-            const uint32_t i = tid + j * PB_THREADS;
+            const uint32_t i = tid + j * NT;
             if (i < n) {
                 S.key[i] = kk[j];
                 S.g[i] = gg[j];
@@ -294,7 +302,7 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
     __syncthreads();
     uint32_t blk_heads = 0;
 #pragma unroll
-    for (int q = 0; q < PB_THREADS / 64; ++q) {
+    for (int q = 0; q < PbShape<CAP>::WAVES; ++q) {
         const uint4 a = S.agg[q];
         const uint2 u = S.aggu[q];
         blk_heads += a.y;
@@ -406,7 +414,7 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
 // 44 / 84 KB of LDS, and a partition of ~1,100 records is sorted over 2,048
 // slots, not 4,096 (the tail of the stage is one such block's latency).
 template <int CAP, bool STRICT, bool MAIN>
-__global__ __launch_bounds__(PB_THREADS) void part_build_kernel(PartArgs A) {
+__global__ __launch_bounds__(PbShape<CAP>::NT) void part_build_kernel(PartArgs A) {
     extern __shared__ __align__(16) uint8_t smem_raw[];
     PartShared<CAP> &S = *reinterpret_cast<PartShared<CAP> *>(smem_raw);
     uint32_t *Sr = A.rl || A.pv ? reinterpret_cast<uint32_t *>(smem_raw + sizeof(PartShared<CAP>)) : nullptr;
@@ -553,7 +561,7 @@ hipError_t launch_part_build(const PartArgs &a, bool strict, int cap, hipStream_
         const size_t lds = part_lds<CAPV>() + (a.rl || a.pv ? 4 * (size_t)(CAPV) : 0);                   \
         (void)hipFuncSetAttribute((const void *)part_build_kernel<CAPV, ST, MAINV>,                      \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                 \
-        hipLaunchKernelGGL((part_build_kernel<CAPV, ST, MAINV>), dim3(GRID), dim3(PB_THREADS), lds, s, a); \
+        hipLaunchKernelGGL((part_build_kernel<CAPV, ST, MAINV>), dim3(GRID), dim3(PbShape<CAPV>::NT), lds, s, a); \
     } while (0)
     const uint32_t mid_grid = a.np < 1024u ? a.np : 1024u;
     const bool m2 = a.main_cap >= 2048;

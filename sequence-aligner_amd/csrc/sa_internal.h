@@ -472,6 +472,11 @@ hipError_t launch_local_offsets(const uint2 *rl, const uint32_t *pv, int lb, uin
                                 uint64_t *loff, hipStream_t s);
 hipError_t launch_owner_bounds(const uint64_t *keys, uint64_t n, int shift, uint32_t P, uint64_t *bounds,
                                hipStream_t s);
+hipError_t launch_desc_owner_bounds(const int32_t *lead, const uint32_t *n_dev, const uint32_t *starts, uint32_t P,
+                                    uint64_t *q, hipStream_t s);
+hipError_t launch_copy_partials(const int32_t *lead, const int32_t *trail, const int32_t *count, uint64_t n,
+                                const uint64_t *oq, uint32_t P, uint32_t *of, uint32_t *os, uint32_t *oc,
+                                hipStream_t s);
 hipError_t launch_gather_partials(const uint32_t *perm, uint64_t n, const uint32_t *fst, const uint32_t *snd,
                                   const uint32_t *cnt, uint32_t *of, uint32_t *os, uint32_t *oc, hipStream_t s);
 hipError_t launch_reduce_keys(const uint32_t *fst, const uint32_t *snd, uint64_t n, int idb, uint64_t *keys,
