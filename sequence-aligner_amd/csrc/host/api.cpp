@@ -393,10 +393,11 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
     // ~700 records per partition (LDS capacity 1,024); up to 2^24 partitions
     // (1.25M reads of 500 bp = 607M k-mers per GPU -> 2^20), but stay at 16 bits
     // (two radix passes) while the average still fits the 1,024-record kernel
-    // (A/B knobs, experiments only: SA_PART_TARGET records per partition,
-    // SA_MAIN_CAP 1024 / 2048 for the tier that takes one block per partition)
-    static const uint64_t part_target = getenv("SA_PART_TARGET") ? strtoull(getenv("SA_PART_TARGET"), nullptr, 10) : 700;
-    static const uint32_t main_cap = getenv("SA_MAIN_CAP") && atoi(getenv("SA_MAIN_CAP")) >= 2048 ? 2048u : 1024u;
+    // (round 4, same-box A/B at the bench shape: ~1,100-1,400-record partitions
+    // with the 2,048-record tier as the main pass -- 8 waves per block -- built
+    // buckets in 1.53-1.55 ms against 1.15 for ~700-record ones on the 1,024 tier)
+    const uint64_t part_target = 700;
+    const uint32_t main_cap = 1024;
     int PB = 1;
     while (PB < 24 && (part_target << PB) < n) ++PB;
     if (main_cap == 1024 && PB > 16 && (n >> 16) <= 900) PB = 16;

@@ -123,20 +123,27 @@ hipError_t exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, uin
 // radix sort
 // ---------------------------------------------------------------------------
 constexpr int RS_THREADS = 256;
-#ifndef SA_RS_ITEMS
-#define SA_RS_ITEMS 16  // keys per thread of a radix tile (A/B builds: make OUT=build_x EXTRA=-DSA_RS_ITEMS=8)
-#endif
-constexpr int RS_ITEMS = SA_RS_ITEMS;
-constexpr int RS_TILE = RS_THREADS * RS_ITEMS;
+// keys per thread of a radix tile: 32 (8,192-key tiles) for key-only sorts --
+// the k-mer partition sort: digit runs of ~32 keys leave as longer coalesced
+// stores (same-box A/B at the bench shape, sort 0.58 -> 0.55 ms; 2,048-key
+// tiles 0.69 ms), 16 where values ride along (their LDS staging at 8,192 keys
+// would leave one workgroup per CU)
+constexpr int RS_ITEMS_KEYS = 32;
+constexpr int RS_ITEMS_VALS = 16;
+template <int ITEMS> struct RsTile {
+    static constexpr int TILE = RS_THREADS * ITEMS;
+};
 
 // Tile histograms, BLOCK-major: hist[tile * 256 + digit] (one coalesced 1 KB
 // row per tile; the digit-major layout made every tile write 256 scattered
 // words and the downsweep read them back scattered).  All 16 keys of a thread
 // are loaded before the first count, and each wave counts into its own 256
 // bins (less same-address contention in the LDS atomics).
+template <int RS_ITEMS>
 __global__ __launch_bounds__(RS_THREADS) void rs_upsweep_kernel(const uint64_t *keys, uint64_t n, int shift,
                                                                 uint32_t *hist, uint32_t nblocks) {
     (void)nblocks;
+    constexpr int RS_TILE = RsTile<RS_ITEMS>::TILE;
     __shared__ uint32_t cnt[RS_THREADS / 64][256];
     const int tid = threadIdx.x, w = tid >> 6;
 #pragma unroll
@@ -239,10 +246,8 @@ __device__ __forceinline__ unsigned long long rs_load_key(const uint64_t *p) { r
 // tile is then staged in LDS in digit order and written out in digit-contiguous
 // runs (coalesced), at hist[digit][block] + run offset.
 constexpr int RS_WAVES = RS_THREADS / 64;
-constexpr int RS_SUB = RS_TILE / RS_WAVES;   // 1024 elements per wave
-constexpr int RS_SLICES = RS_SUB / 64;       // 16
 
-template <bool VALS>
+template <bool VALS, int RS_TILE>
 struct RsShared {
     unsigned long long key[RS_TILE];
     uint32_t val[VALS ? RS_TILE : 1];
@@ -254,13 +259,14 @@ struct RsShared {
 // (wave_peers: sa_internal.h)
 
 // VALS = false: key-only sort (records that carry their payload in the key)
-template <bool VALS>
+template <bool VALS, int RS_ITEMS>
 __global__ __launch_bounds__(RS_THREADS) void rs_downsweep_kernel(const uint64_t *kin, const uint32_t *vin,
                                                                   uint64_t *kout, uint32_t *vout, uint64_t n,
                                                                   int shift, const uint32_t *hist,
                                                                   uint32_t nblocks) {
+    constexpr int RS_TILE = RsTile<RS_ITEMS>::TILE, RS_SUB = RS_TILE / RS_WAVES, RS_SLICES = RS_SUB / 64;
     extern __shared__ __align__(16) uint8_t rs_smem[];
-    RsShared<VALS> &S = *reinterpret_cast<RsShared<VALS> *>(rs_smem);
+    RsShared<VALS, RS_TILE> &S = *reinterpret_cast<RsShared<VALS, RS_TILE> *>(rs_smem);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
@@ -337,9 +343,10 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep_kernel(const uint64_t
 // 16-byte records (u64 key, u64 value): the tile is staged through LDS twice --
 // keys (with their digits), then the values in the same slots -- so the LDS
 // footprint stays that of a key-only tile (3 workgroups per CU, not 2)
+constexpr int RS_TILE_KV = RsTile<RS_ITEMS_VALS>::TILE;
 struct RsSharedKV {
-    unsigned long long buf[RS_TILE];  // staged keys, then staged values
-    uint8_t dig[RS_TILE];
+    unsigned long long buf[RS_TILE_KV];  // staged keys, then staged values
+    uint8_t dig[RS_TILE_KV];
     uint32_t cnt[RS_WAVES][256];
     uint32_t lofs[256];
     uint32_t gofs[256];
@@ -349,6 +356,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep_kv64_kernel(const uin
                                                                        uint64_t *kout, uint64_t *vout, uint64_t n,
                                                                        int shift, const uint32_t *hist,
                                                                        uint32_t nblocks) {
+    constexpr int RS_TILE = RS_TILE_KV, RS_SUB = RS_TILE / RS_WAVES, RS_SLICES = RS_SUB / 64;
     extern __shared__ __align__(16) uint8_t rs_smem[];
     RsSharedKV &S = *reinterpret_cast<RsSharedKV *>(rs_smem);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -430,7 +438,8 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep_kv64_kernel(const uin
     }
 }
 
-size_t radix_sort_temp_bytes(uint64_t n) {
+size_t radix_sort_temp_bytes(uint64_t n) {  // (the smaller tile: the most tiles)
+    constexpr int RS_TILE = RsTile<RS_ITEMS_VALS>::TILE;
     const uint64_t nb = (n + RS_TILE - 1) / RS_TILE;
     const uint64_t nc = (nb + RS_CHUNK - 1) / RS_CHUNK;
     const uint64_t hist = 256 * (nb ? nb : 1);
@@ -440,30 +449,37 @@ size_t radix_sort_temp_bytes(uint64_t n) {
 hipError_t radix_sort(uint64_t **keys, uint32_t **vals, uint64_t **keys_alt, uint32_t **vals_alt,
                       uint64_t n, int lo, int hi, void *tmp, hipStream_t s) {
     if (n <= 1 || hi <= lo) return hipSuccess;
-    const uint64_t nb = (n + RS_TILE - 1) / RS_TILE;
+    constexpr int TK = RsTile<RS_ITEMS_KEYS>::TILE, TV = RsTile<RS_ITEMS_VALS>::TILE;
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void *)rs_downsweep_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)sizeof(RsShared<true>));
-        (void)hipFuncSetAttribute((const void *)rs_downsweep_kernel<false>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(RsShared<false>));
+        (void)hipFuncSetAttribute((const void *)rs_downsweep_kernel<true, RS_ITEMS_VALS>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(RsShared<true, TV>));
+        (void)hipFuncSetAttribute((const void *)rs_downsweep_kernel<false, RS_ITEMS_KEYS>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(RsShared<false, TK>));
         attr_set = true;
     }
     const bool with_vals = vals != nullptr && *vals != nullptr;
+    const uint64_t tile = with_vals ? TV : TK;
+    const uint64_t nb = (n + tile - 1) / tile;
     uint32_t *hist = (uint32_t *)tmp;
     void *stmp = (void *)(hist + 256 * nb);
     for (int shift = lo; shift < hi; shift += 8) {
-        hipLaunchKernelGGL(rs_upsweep_kernel, dim3((uint32_t)nb), dim3(RS_THREADS), 0, s, *keys, n, shift, hist,
-                           (uint32_t)nb);
+        if (with_vals)
+            hipLaunchKernelGGL((rs_upsweep_kernel<RS_ITEMS_VALS>), dim3((uint32_t)nb), dim3(RS_THREADS), 0, s, *keys, n,
+                               shift, hist, (uint32_t)nb);
+        else
+            hipLaunchKernelGGL((rs_upsweep_kernel<RS_ITEMS_KEYS>), dim3((uint32_t)nb), dim3(RS_THREADS), 0, s, *keys, n,
+                               shift, hist, (uint32_t)nb);
         hipError_t e = rs_offsets(hist, nb, stmp, s);
         if (e != hipSuccess) return e;
         if (with_vals) {
-            hipLaunchKernelGGL((rs_downsweep_kernel<true>), dim3((uint32_t)nb), dim3(RS_THREADS), sizeof(RsShared<true>),
-                               s, *keys, *vals, *keys_alt, *vals_alt, n, shift, (const uint32_t *)hist, (uint32_t)nb);
+            hipLaunchKernelGGL((rs_downsweep_kernel<true, RS_ITEMS_VALS>), dim3((uint32_t)nb), dim3(RS_THREADS),
+                               sizeof(RsShared<true, TV>), s, *keys, *vals, *keys_alt, *vals_alt, n, shift,
+                               (const uint32_t *)hist, (uint32_t)nb);
             uint32_t *tv = *vals; *vals = *vals_alt; *vals_alt = tv;
         } else {
-            hipLaunchKernelGGL((rs_downsweep_kernel<false>), dim3((uint32_t)nb), dim3(RS_THREADS),
-                               sizeof(RsShared<false>), s, *keys, nullptr, *keys_alt, nullptr, n, shift,
+            hipLaunchKernelGGL((rs_downsweep_kernel<false, RS_ITEMS_KEYS>), dim3((uint32_t)nb), dim3(RS_THREADS),
+                               sizeof(RsShared<false, TK>), s, *keys, nullptr, *keys_alt, nullptr, n, shift,
                                (const uint32_t *)hist, (uint32_t)nb);
         }
         uint64_t *tk = *keys; *keys = *keys_alt; *keys_alt = tk;
@@ -476,7 +492,7 @@ hipError_t radix_sort(uint64_t **keys, uint32_t **vals, uint64_t **keys_alt, uin
 hipError_t radix_sort_kv64(uint64_t **keys, uint64_t **vals, uint64_t **keys_alt, uint64_t **vals_alt, uint64_t n,
                            int lo, int hi, void *tmp, hipStream_t s) {
     if (n <= 1 || hi <= lo) return hipSuccess;
-    const uint64_t nb = (n + RS_TILE - 1) / RS_TILE;
+    const uint64_t nb = (n + RS_TILE_KV - 1) / RS_TILE_KV;
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void *)rs_downsweep_kv64_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -486,8 +502,8 @@ hipError_t radix_sort_kv64(uint64_t **keys, uint64_t **vals, uint64_t **keys_alt
     uint32_t *hist = (uint32_t *)tmp;
     void *stmp = (void *)(hist + 256 * nb);
     for (int shift = lo; shift < hi; shift += 8) {
-        hipLaunchKernelGGL(rs_upsweep_kernel, dim3((uint32_t)nb), dim3(RS_THREADS), 0, s, *keys, n, shift, hist,
-                           (uint32_t)nb);
+        hipLaunchKernelGGL((rs_upsweep_kernel<RS_ITEMS_VALS>), dim3((uint32_t)nb), dim3(RS_THREADS), 0, s, *keys, n,
+                           shift, hist, (uint32_t)nb);
         hipError_t e = rs_offsets(hist, nb, stmp, s);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(rs_downsweep_kv64_kernel, dim3((uint32_t)nb), dim3(RS_THREADS), sizeof(RsSharedKV), s,

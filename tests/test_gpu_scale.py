@@ -36,12 +36,14 @@ def compare(ov, r, pairs=True):
     np.testing.assert_array_equal(lead, r.lead)
     np.testing.assert_array_equal(trail, r.trail)
     # every dispatched pair's count = the oracle's PairData count of that key
-    # (wide ids: the oracle's pairs are sorted by (fst, snd))
+    # (wide ids list PairData sorted by (fst, snd); strict ids in Trove order)
     okey = (r.pair_fst.astype(np.uint64) << np.uint64(32)) | r.pair_snd.astype(np.uint64)
+    o = np.argsort(okey, kind="stable")
+    okey, ocnt = okey[o], r.pair_cnt[o]
     dkey = (lead.astype(np.uint64) << np.uint64(32)) | trail.astype(np.uint64)
     pos = np.minimum(np.searchsorted(okey, dkey), max(len(okey) - 1, 0))
     assert (okey[pos] == dkey).all()
-    np.testing.assert_array_equal(count, r.pair_cnt[pos])
+    np.testing.assert_array_equal(count, ocnt[pos])
     if pairs:
         pf, ps, pc = ov.pairs()
         np.testing.assert_array_equal(pf, r.pair_fst)
