@@ -739,6 +739,9 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
             HIPCHK(hipStreamSynchronize(c->stream));
             failed.resize(nf);
             if (nf) HIPCHK(hipMemcpy(failed.data(), fl, (size_t)nf * 4, hipMemcpyDeviceToHost));
+            static const bool dbg_tiers = getenv("SA_DEBUG_TIERS") != nullptr;  // (diagnostics: stderr)
+            if (dbg_tiers)
+                fprintf(stderr, "[sa tiers] table %d split %d items %zu failed %u\n", table, split, items.size(), nf);
             if (fest) {
                 fest->resize(nf);
                 if (nf) HIPCHK(hipMemcpy(fest->data(), fe, (size_t)nf * 4, hipMemcpyDeviceToHost));
@@ -1948,8 +1951,12 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint6
     // sort, no per-block output claims.  Regions beyond 32 GB (or
     // SA_SHARD_MULTI=1, A/B runs): multi-read blocks over ~PCM_TARGET local
     // occurrences, partials sorted by owner.
-    static const bool multi_forced = getenv("SA_SHARD_MULTI") && atoi(getenv("SA_SHARD_MULTI")) != 0;
-    bool per_read = !multi_forced && (uint64_t)N * PC_RREG * sizeof(uint2) <= (32ull << 30);
+    // (round 4, 8 serial virtual shards of the bench shape: per-read regions
+    // 2.55 ms of pair counting per step against 1.55 for multi-read blocks -- a
+    // read has ~60 local occurrences, too few to pay for a wave's table setup
+    // and region ranking; SA_SHARD_PER_READ=1 runs them for A/B)
+    static const bool per_read_on = getenv("SA_SHARD_PER_READ") && atoi(getenv("SA_SHARD_PER_READ")) != 0;
+    bool per_read = per_read_on && (uint64_t)N * PC_RREG * sizeof(uint2) <= (32ull << 30);
     uint64_t np_ub = 0;
     if (per_read) {
         rc = pair_stage(c, E, PI, false, false, nullptr, N, cnt, np, cap_s, nullptr, 0, nullptr, nullptr, &per_read,

@@ -120,66 +120,116 @@ __device__ __forceinline__ uint32_t pc_block_excl_scan(uint32_t v, uint32_t *lds
 __device__ __forceinline__ uint4 pc_rec(const uint4 &r, const PairIn &) { return r; }
 __device__ __forceinline__ uint4 pc_rec(const uint2 &r, const PairIn &in) { return decode_rec(r, in.xrec); }
 
+// Returns whether the insert created the key.  The table's fill is counted by
+// the caller, one LDS atomic per wave and batch (pc_fill).
+//
+// The recount tiers (TAB >= 2,048) probe in 16-byte buckets of four slots: one
+// LDS round trip reads a bucket, the insert takes its first empty slot.  A
+// lane's probes are a chain of dependent LDS reads, and a wave waits for its
+// longest chain: near 3/4 load, slot-by-slot linear probing made that tail
+// tens of round trips per insert (configs[4]'s k = 12 reads, whose inserts
+// mostly create keys, spent ~200 us per read in the 32,768-slot tier).  Keys
+// only ever go EMPTY -> key, and always into the first empty slot of the probe
+// order, so the filled slots are a prefix of it: a scan stops at the first
+// match or empty slot, and a CAS that loses to another key re-reads the bucket.
+template <int TAB>
+__device__ __forceinline__ bool pc_key_is(uint32_t word, uint32_t partner) {
+    if constexpr (PcShape<TAB>::PACKED) return (word & 0xFFFFFFu) == partner;  // (EMPTY's low bits are not an id)
+    else return word == partner;
+}
+
 template <bool STRICT, int TAB>
-__device__ __forceinline__ void pc_insert(PcShared<TAB> &S, PcSharedStrict<TAB> &X, uint32_t partner, uint32_t w,
-                                          unsigned long long rank, uint32_t eidx) {
-    constexpr uint32_t FILL_MAX = TAB * 3 / 4;
-    if constexpr (PcShape<TAB>::PACKED) {
-        // one word per slot: a CAS inserts (partner, w), a hit adds w << 24 and
-        // marks the slot saturated when the 8-bit count wraps
-        uint32_t slot = pc_hash<TAB>(partner);
-        for (int probe = 0; probe < PC_PROBE_MAX; ++probe) {
-            if ((probe & 15) == 15 && lds_relaxed(&S.overflow)) return;
-            uint32_t old = lds_relaxed(&S.key[slot]);
-            if (old == PC_EMPTY) {
-                old = atomicCAS(&S.key[slot], PC_EMPTY, partner | (w << 24));
-                if (old == PC_EMPTY) {
-                    if (atomicAdd(&S.fill, 1u) >= FILL_MAX) {
-                        S.overflow = 1;
-                        atomicMin(&S.xfill, eidx);
-                    }
-                    return;
-                }
+__device__ __forceinline__ void pc_hit(PcShared<TAB> &S, PcSharedStrict<TAB> &X, uint32_t slot, uint32_t w,
+                                       unsigned long long rank) {
+    if constexpr (PcShape<TAB>::PACKED) {  // count << 24, wrap -> the slot's saturation bit
+        const uint32_t prev = atomicAdd(&S.key[slot], w << 24);
+        if ((prev >> 24) + w > 255u) atomicOr(&S.sat[slot >> 5], 1u << (slot & 31));
+    } else {
+        atomicAdd(&S.cnt[slot], w);
+        if constexpr (STRICT) atomicMin(&X.rank[slot], rank);
+    }
+}
+
+template <bool STRICT, int TAB>
+__device__ __forceinline__ bool pc_insert(PcShared<TAB> &S, PcSharedStrict<TAB> &X, uint32_t partner, uint32_t w,
+                                          unsigned long long rank) {
+    if constexpr (TAB >= PC_TAB_BIG) {
+        const uint32_t fresh = PcShape<TAB>::PACKED ? partner | (w << 24) : partner;
+        uint32_t b = pc_hash<TAB>(partner) & ~3u;
+        // bounded: a retry means another key took a slot of this bucket (<= 4 per
+        // bucket), and a run of PC_PROBE_MAX / 4 buckets only happens in a table
+        // that is (nearly) full -- then recounted by a finer class
+        for (int it = 0; it < PC_PROBE_MAX; ++it) {
+            if ((it & 7) == 7 && lds_relaxed(&S.overflow)) return false;
+            uint32_t k[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) k[i] = lds_relaxed(&S.key[b + i]);
+            int at = 4;
+            bool hit = false;
+#pragma unroll
+            for (int i = 3; i >= 0; --i) {  // the first match or empty slot
+                if (pc_key_is<TAB>(k[i], partner)) { at = i; hit = true; }
+                else if (k[i] == PC_EMPTY) { at = i; hit = false; }
             }
-            if ((old & 0xFFFFFFu) == partner) {
-                const uint32_t prev = atomicAdd(&S.key[slot], w << 24);
-                if ((prev >> 24) + w > 255u) atomicOr(&S.sat[slot >> 5], 1u << (slot & 31));
-                return;
+            if (at == 4) {  // bucket full of other keys: the next one
+                b = (b + 4) & (TAB - 1);
+                continue;
+            }
+            if (hit) {
+                pc_hit<STRICT, TAB>(S, X, b + at, w, rank);
+                return false;
+            }
+            const uint32_t old = atomicCAS(&S.key[b + at], PC_EMPTY, fresh);
+            if (old == PC_EMPTY) {
+                if constexpr (!PcShape<TAB>::PACKED) pc_hit<STRICT, TAB>(S, X, b + at, w, rank);
+                return true;
+            }
+            if (pc_key_is<TAB>(old, partner)) {
+                pc_hit<STRICT, TAB>(S, X, b + at, w, rank);
+                return false;
+            }
+            // another key took the slot: read the bucket again
+        }
+        S.overflow = 1;
+        return false;
+    } else {
+        uint32_t slot = pc_hash<TAB>(partner);
+        // probe runs are bounded: at <= 3/4 load they average < 9 slots, and a
+        // run of TAB / 4 only happens in a table that is (nearly) full -- it is
+        // then recounted by a bigger tier, so every insert stays O(TAB / 4)
+        constexpr int PMAX = TAB / 4 < PC_PROBE_MAX ? TAB / 4 : PC_PROBE_MAX;
+        for (int probe = 0; probe < PMAX; ++probe) {
+            // a slot's key goes EMPTY -> partner once and never changes again, so a
+            // plain LDS read that sees a key is final: hits (>99% of inserts at 20x --
+            // a read meets each partner in ~100 shared k-mers) take one atomic, not
+            // two, and the CAS only runs on a slot that still reads EMPTY
+            uint32_t old = lds_relaxed(&S.key[slot]);
+            if (old == PC_EMPTY) old = atomicCAS(&S.key[slot], PC_EMPTY, partner);
+            if (old == PC_EMPTY || old == partner) {
+                pc_hit<STRICT, TAB>(S, X, slot, w, rank);
+                return old == PC_EMPTY;
             }
             slot = (slot + 1) & (TAB - 1);
         }
         S.overflow = 1;
-        return;
+        return false;
     }
-    uint32_t slot = pc_hash<TAB>(partner);
-    // probe runs are bounded: at <= 3/4 load they average < 9 slots, and a run
-    // of TAB / 4 (<= PC_PROBE_MAX) only happens in a table that is (nearly) full -- it is
-    // then recounted by a bigger tier, so every insert stays O(PC_PROBE_MAX).
-    // The recount tiers (big tables, reads with thousands of partners) also
-    // stop as soon as another lane has marked the table full; the first pass
-    // does not poll (it keeps its SGPRs for the hot loop)
-    constexpr int PMAX = TAB / 4 < PC_PROBE_MAX ? TAB / 4 : PC_PROBE_MAX;
-    for (int probe = 0; probe < PMAX; ++probe) {
-        if constexpr (TAB >= PC_TAB_BIG)
-            if ((probe & 15) == 15 && lds_relaxed(&S.overflow)) return;
-        // a slot's key goes EMPTY -> partner once and never changes again, so a
-        // plain LDS read that sees a key is final: hits (>99% of inserts -- a read
-        // meets each partner in ~100 shared k-mers) take one atomic, not two, and
-        // the CAS only runs on a slot that still reads EMPTY
-        uint32_t old = lds_relaxed(&S.key[slot]);
-        if (old == PC_EMPTY) old = atomicCAS(&S.key[slot], PC_EMPTY, partner);
-        if (old == PC_EMPTY || old == partner) {
-            if (old == PC_EMPTY && atomicAdd(&S.fill, 1u) >= FILL_MAX) {
-                S.overflow = 1;
-                atomicMin(&S.xfill, eidx);
-            }
-            atomicAdd(&S.cnt[slot], w);
-            if constexpr (STRICT) atomicMin(&X.rank[slot], rank);
-            return;
+}
+
+// the wave's new keys of one batch into the fill count: past 3/4 of the table
+// the block is recounted by the next tier (xfill: the batch's first element,
+// the role-pair index where the table was found full)
+template <int TAB>
+__device__ __forceinline__ void pc_fill(PcShared<TAB> &S, uint32_t newk, uint32_t eidx) {
+    constexpr uint32_t FILL_MAX = TAB * 3 / 4;
+    const uint32_t wtot = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_add(newk), 63);
+    if ((threadIdx.x & 63) == 0 && wtot) {
+        const uint32_t old = atomicAdd(&S.fill, wtot);
+        if (old + wtot > FILL_MAX) {
+            S.overflow = 1;
+            atomicMin(&S.xfill, eidx);
         }
-        slot = (slot + 1) & (TAB - 1);
     }
-    S.overflow = 1;
 }
 
 template <bool STRICT, int TAB>
@@ -329,14 +379,18 @@ __global__ __launch_bounds__(PcShape<TAB>::NT) void pair_count_kernel(EmitParams
                         }
                     }
                 }
+                // (round 4: issuing a batch's first bucket reads and CASes together
+                // measured slower on configs[4]'s k = 12 slice, 7.1 -> 8.6 s of pair
+                // counting: the per-insert loop stays)
+                uint32_t newk = 0;
 #pragma unroll
                 for (int bb = 0; bb < BATCH; ++bb) {
                     const uint32_t partner = part[bb];
                     if (partner == a) continue;                 // same read (KmerTable.scala:61-63)
                     if (split > 1 && (partner % split) != residue) continue;
-                    pc_insert<STRICT, TAB>(S, X, partner, wv[bb], rk[bb],
-                                           (uint32_t)min(role_pairs - total + w0 + e0 + bb * NT + tid, 0xFFFFFFFEull));
+                    newk += pc_insert<STRICT, TAB>(S, X, partner, wv[bb], rk[bb]) ? 1u : 0u;
                 }
+                pc_fill<TAB>(S, newk, (uint32_t)min(role_pairs - total + w0 + e0, 0xFFFFFFFEull));
                 if (S.overflow) break;
             }
         }
