@@ -699,7 +699,7 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
                 // on configs[4]'s k = 12 shape (~3,900 partners per read) 86 % of
                 // the reads the 2,048-slot tier took filled it and were re-run
                 // anyway (57 ms of 221 ms of pair counting, 1M reads)
-                (strict || rps[i] <= 1536u * 3u / 2u ? q_big : q_huge).push_back(codes[i]);
+                (strict || rps[i] <= pc_fill_max(2048) * 3u / 2u ? q_big : q_huge).push_back(codes[i]);
         }
         // one tier over host-side items; returns its failures (codes)
         auto run_tier = [&](int table, int split, const std::vector<uint32_t> &items, std::vector<uint32_t> &failed,
@@ -758,7 +758,7 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
         };
         std::vector<uint32_t> failed;
         int rc_t;
-        uint64_t wide_limit = 64ull * 12288u;  // distinct partners per read the tiers can count
+        uint64_t wide_limit = 64ull * pc_fill_max(16384);  // distinct partners per read the tiers can count
         if ((rc_t = run_tier(2048, 1, q_big, failed))) return rc_t;
         if (strict) {
             if ((rc_t = run_tier(2048, 64, refine(failed, 1, 64), failed))) return rc_t;
@@ -780,7 +780,7 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
             static const bool packed_ok = !getenv("SA_PACKED_TIER") || atoi(getenv("SA_PACKED_TIER")) != 0;
             const bool packed = packed_ok && !P.emit_all && P.max_coll <= 255 && n_items < 0xFFFFFFu;
             const int htab = packed ? 32768 : 16384;
-            const uint32_t hcap = (uint32_t)htab * 3u / 4u;
+            const uint32_t hcap = pc_fill_max((uint32_t)htab);
             wide_limit = 64ull * hcap;
             std::vector<uint32_t> lv[7];  // split 1, 2, 4, ..., 64
             lv[0] = q_huge;
@@ -801,9 +801,9 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
             }
         }
         if (!failed.empty() && cur_max() <= cap_s)
-            return fail(c, SA_E_OVERFLOW, strict ? std::string("a read has more than 98,304 distinct partners")
-                                                 : "a read has more than " + std::to_string(wide_limit) +
-                                                       " distinct partners");
+            return fail(c, SA_E_OVERFLOW, "a read has more than " +
+                                              std::to_string(strict ? 64ull * pc_fill_max(2048) : wide_limit) +
+                                              " distinct partners");
         if (cur_max() <= cap_s) {
             if (P.per_read) {  // regions kept; the recounted reads' pairs are in the shared regions
                 *per_read = true;

@@ -161,9 +161,11 @@ __device__ __forceinline__ bool pc_insert(PcShared<TAB> &S, PcSharedStrict<TAB> 
         // that is (nearly) full -- then recounted by a finer class
         for (int it = 0; it < PC_PROBE_MAX; ++it) {
             if ((it & 7) == 7 && lds_relaxed(&S.overflow)) return false;
-            uint32_t k[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) k[i] = lds_relaxed(&S.key[b + i]);
+            // the bucket as two relaxed 8-byte loads (ds_read_b64: half the LDS
+            // instructions of four word loads; each word is read atomically)
+            const uint64_t k01 = lds_relaxed(reinterpret_cast<uint64_t *>(&S.key[b]));
+            const uint64_t k23 = lds_relaxed(reinterpret_cast<uint64_t *>(&S.key[b + 2]));
+            const uint32_t k[4] = {(uint32_t)k01, (uint32_t)(k01 >> 32), (uint32_t)k23, (uint32_t)(k23 >> 32)};
             int at = 4;
             bool hit = false;
 #pragma unroll
@@ -221,7 +223,7 @@ __device__ __forceinline__ bool pc_insert(PcShared<TAB> &S, PcSharedStrict<TAB> 
 // the role-pair index where the table was found full)
 template <int TAB>
 __device__ __forceinline__ void pc_fill(PcShared<TAB> &S, uint32_t newk, uint32_t eidx) {
-    constexpr uint32_t FILL_MAX = TAB * 3 / 4;
+    constexpr uint32_t FILL_MAX = pc_fill_max(TAB);
     const uint32_t wtot = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_add(newk), 63);
     if ((threadIdx.x & 63) == 0 && wtot) {
         const uint32_t old = atomicAdd(&S.fill, wtot);
@@ -413,7 +415,7 @@ __global__ __launch_bounds__(PcShape<TAB>::NT) void pair_count_kernel(EmitParams
             if (o.overflow_rp) {
                 const unsigned long long x = S.xfill != 0xFFFFFFFFu ? (unsigned long long)S.xfill + 1
                                              : x_over == ~0ull || x_over == 0 ? role_pairs : x_over;
-                const unsigned long long est = (unsigned long long)(TAB * 3 / 4) * role_pairs / (x ? x : 1);
+                const unsigned long long est = (unsigned long long)pc_fill_max(TAB) * role_pairs / (x ? x : 1);
                 o.overflow_rp[at] = est > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)est;
             }
         }

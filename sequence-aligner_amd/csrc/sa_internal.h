@@ -237,6 +237,14 @@ struct PairOut {
     uint32_t *rcnt;
 };
 constexpr uint32_t PC_RREG = 192;  // = the first pass's fill limit (256 slots at 3/4)
+// fill limit of the recount tiers' tables (2,048 slots and up, bucketed
+// probing), in eighths of the slots; the host sizes tiers and classes with it
+#ifndef SA_TIER_FILL_EIGHTHS
+#define SA_TIER_FILL_EIGHTHS 6
+#endif
+__host__ __device__ constexpr uint32_t pc_fill_max(uint32_t tab) {
+    return tab >= 2048 ? tab / 8 * SA_TIER_FILL_EIGHTHS : tab * 3 / 4;
+}
 
 // Four alignment costs indexed by a 2-bit base code given as x8 = 8 * code.
 // Cost8: one word of int8 bytes (HOXD70 and every matrix whose entries fit a
