@@ -139,33 +139,44 @@ template <int ITEMS> struct RsTile {
 // words and the downsweep read them back scattered).  All 16 keys of a thread
 // are loaded before the first count, and each wave counts into its own 256
 // bins (less same-address contention in the LDS atomics).
+// (an 8,192-key tile is counted by 512 threads, 16 keys each: the same work per
+// thread as the 4,096-key tiles' upsweep; 256 threads x 32 keys ran 68 us per
+// pass at the bench shape against ~35)
 template <int RS_ITEMS>
-__global__ __launch_bounds__(RS_THREADS) void rs_upsweep_kernel(const uint64_t *keys, uint64_t n, int shift,
-                                                                uint32_t *hist, uint32_t nblocks) {
+struct RsUp {
+    static constexpr int THREADS = RS_ITEMS > 16 ? RS_THREADS * (RS_ITEMS / 16) : RS_THREADS;
+    static constexpr int ITEMS = RS_ITEMS > 16 ? 16 : RS_ITEMS;
+};
+template <int RS_ITEMS>
+__global__ __launch_bounds__(RsUp<RS_ITEMS>::THREADS) void rs_upsweep_kernel(const uint64_t *keys, uint64_t n,
+                                                                            int shift, uint32_t *hist,
+                                                                            uint32_t nblocks) {
     (void)nblocks;
-    constexpr int RS_TILE = RsTile<RS_ITEMS>::TILE;
-    __shared__ uint32_t cnt[RS_THREADS / 64][256];
+    constexpr int RS_TILE = RsTile<RS_ITEMS>::TILE, NT = RsUp<RS_ITEMS>::THREADS, IT = RsUp<RS_ITEMS>::ITEMS;
+    constexpr int NW = NT / 64;
+    __shared__ uint32_t cnt[NW][256];
     const int tid = threadIdx.x, w = tid >> 6;
-#pragma unroll
-    for (int q = 0; q < RS_THREADS / 64; ++q) cnt[q][tid] = 0;
+    for (int i = tid; i < NW * 256; i += NT) (&cnt[0][0])[i] = 0;
     const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
-    unsigned long long k[RS_ITEMS];
+    unsigned long long k[IT];
 #pragma unroll
-    for (int j = 0; j < RS_ITEMS; ++j) {
-        const uint64_t i = base + (uint64_t)j * RS_THREADS + tid;
+    for (int j = 0; j < IT; ++j) {
+        const uint64_t i = base + (uint64_t)j * NT + tid;
         k[j] = i < n ? __builtin_nontemporal_load(keys + i) : 0ull;  // read once per pass
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < RS_ITEMS; ++j) {
-        const uint64_t i = base + (uint64_t)j * RS_THREADS + tid;
+    for (int j = 0; j < IT; ++j) {
+        const uint64_t i = base + (uint64_t)j * NT + tid;
         if (i < n) atomicAdd(&cnt[w][(uint32_t)(k[j] >> shift) & 255u], 1u);
     }
     __syncthreads();
-    uint32_t s = 0;
+    if (tid < 256) {
+        uint32_t s = 0;
 #pragma unroll
-    for (int q = 0; q < RS_THREADS / 64; ++q) s += cnt[q][tid];
-    hist[(uint64_t)blockIdx.x * 256 + tid] = s;
+        for (int q = 0; q < NW; ++q) s += cnt[q][tid];
+        hist[(uint64_t)blockIdx.x * 256 + tid] = s;
+    }
 }
 
 // Global scatter offsets from the block-major tile histograms, in place:
@@ -247,26 +258,38 @@ __device__ __forceinline__ unsigned long long rs_load_key(const uint64_t *p) { r
 // runs (coalesced), at hist[digit][block] + run offset.
 constexpr int RS_WAVES = RS_THREADS / 64;
 
-template <bool VALS, int RS_TILE>
+// An 8,192-key tile runs 512 threads (8 waves of 1,024 keys, 16 per lane: the
+// per-wave work and registers of the 4,096-key tiles, twice the waves to hide
+// the loads); a 4,096-key tile 256 threads.
+template <int RS_ITEMS>
+struct RsDown {
+    static constexpr int TILE = RsTile<RS_ITEMS>::TILE;
+    static constexpr int WAVES = TILE / 1024, THREADS = WAVES * 64, SUB = 1024, SLICES = SUB / 64;
+};
+
+template <bool VALS, int RS_TILE, int WAVES>
 struct RsShared {
     unsigned long long key[RS_TILE];
     uint32_t val[VALS ? RS_TILE : 1];
-    uint32_t cnt[RS_WAVES][256];   // per-wave digit counts
+    uint32_t cnt[WAVES][256];      // per-wave digit counts
     uint32_t lofs[256];            // tile-local start of each digit run
     uint32_t gofs[256];            // global start of each digit run
+    uint32_t wsum[4];              // the digit scan's wave sums
 };
 
 // (wave_peers: sa_internal.h)
 
 // VALS = false: key-only sort (records that carry their payload in the key)
 template <bool VALS, int RS_ITEMS>
-__global__ __launch_bounds__(RS_THREADS) void rs_downsweep_kernel(const uint64_t *kin, const uint32_t *vin,
-                                                                  uint64_t *kout, uint32_t *vout, uint64_t n,
-                                                                  int shift, const uint32_t *hist,
-                                                                  uint32_t nblocks) {
-    constexpr int RS_TILE = RsTile<RS_ITEMS>::TILE, RS_SUB = RS_TILE / RS_WAVES, RS_SLICES = RS_SUB / 64;
+__global__ __launch_bounds__(RsDown<RS_ITEMS>::THREADS) void rs_downsweep_kernel(const uint64_t *kin,
+                                                                                 const uint32_t *vin, uint64_t *kout,
+                                                                                 uint32_t *vout, uint64_t n, int shift,
+                                                                                 const uint32_t *hist,
+                                                                                 uint32_t nblocks) {
+    using D = RsDown<RS_ITEMS>;
+    constexpr int RS_TILE = D::TILE, RS_SUB = D::SUB, RS_SLICES = D::SLICES, WAVES = D::WAVES, NT = D::THREADS;
     extern __shared__ __align__(16) uint8_t rs_smem[];
-    RsShared<VALS, RS_TILE> &S = *reinterpret_cast<RsShared<VALS, RS_TILE> *>(rs_smem);
+    RsShared<VALS, RS_TILE, WAVES> &S = *reinterpret_cast<RsShared<VALS, RS_TILE, WAVES> *>(rs_smem);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const uint64_t base = (uint64_t)blockIdx.x * RS_TILE;
@@ -294,25 +317,26 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep_kernel(const uint64_t
         __builtin_amdgcn_wave_barrier();
     }
     __syncthreads();
-    // digit tid: tile total, tile-local run start (exclusive scan over digits), global start
-    {
-        uint32_t tot = 0;
+    // digit tid (threads 0-255): tile total, tile-local run start (exclusive scan
+    // over digits), global start
+    uint32_t tot = 0, inc = 0;
+    if (tid < 256) {
 #pragma unroll
-        for (int q = 0; q < RS_WAVES; ++q) tot += S.cnt[q][tid];
-        // block exclusive scan of tot over the 256 digits
-        const uint32_t inc = wave_incl_add(tot);
-        if (lane == 63) S.lofs[w] = inc;  // temporarily: wave sums
-        __syncthreads();
+        for (int q = 0; q < WAVES; ++q) tot += S.cnt[q][tid];
+        inc = wave_incl_add(tot);  // block exclusive scan of tot over the 256 digits
+        if (lane == 63) S.wsum[w] = inc;
+    }
+    __syncthreads();
+    if (tid < 256) {
         uint32_t pre = 0;
-        for (int q = 0; q < w; ++q) pre += S.lofs[q];
-        __syncthreads();
+        for (int q = 0; q < w; ++q) pre += S.wsum[q];
         const uint32_t lo = pre + inc - tot;
         S.lofs[tid] = lo;
         S.gofs[tid] = hist[(uint64_t)blockIdx.x * 256 + tid];
         // per-wave bases inside the tile, in place of the counts
         uint32_t acc = lo;
 #pragma unroll
-        for (int q = 0; q < RS_WAVES; ++q) {
+        for (int q = 0; q < WAVES; ++q) {
             const uint32_t c = S.cnt[q][tid];
             S.cnt[q][tid] = acc;
             acc += c;
@@ -331,7 +355,7 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep_kernel(const uint64_t
     }
     __syncthreads();
     const uint32_t nt = (uint32_t)min((uint64_t)RS_TILE, n - base);
-    for (uint32_t i = tid; i < nt; i += RS_THREADS) {
+    for (uint32_t i = tid; i < nt; i += NT) {
         const unsigned long long kk = S.key[i];
         const uint32_t d = (uint32_t)(kk >> shift) & 255u;
         const uint32_t pos = S.gofs[d] + (i - S.lofs[d]);
@@ -450,12 +474,14 @@ hipError_t radix_sort(uint64_t **keys, uint32_t **vals, uint64_t **keys_alt, uin
                       uint64_t n, int lo, int hi, void *tmp, hipStream_t s) {
     if (n <= 1 || hi <= lo) return hipSuccess;
     constexpr int TK = RsTile<RS_ITEMS_KEYS>::TILE, TV = RsTile<RS_ITEMS_VALS>::TILE;
+    using SK = RsShared<false, TK, RsDown<RS_ITEMS_KEYS>::WAVES>;
+    using SV = RsShared<true, TV, RsDown<RS_ITEMS_VALS>::WAVES>;
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void *)rs_downsweep_kernel<true, RS_ITEMS_VALS>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(RsShared<true, TV>));
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(SV));
         (void)hipFuncSetAttribute((const void *)rs_downsweep_kernel<false, RS_ITEMS_KEYS>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(RsShared<false, TK>));
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(SK));
         attr_set = true;
     }
     const bool with_vals = vals != nullptr && *vals != nullptr;
@@ -465,21 +491,21 @@ hipError_t radix_sort(uint64_t **keys, uint32_t **vals, uint64_t **keys_alt, uin
     void *stmp = (void *)(hist + 256 * nb);
     for (int shift = lo; shift < hi; shift += 8) {
         if (with_vals)
-            hipLaunchKernelGGL((rs_upsweep_kernel<RS_ITEMS_VALS>), dim3((uint32_t)nb), dim3(RS_THREADS), 0, s, *keys, n,
-                               shift, hist, (uint32_t)nb);
+            hipLaunchKernelGGL((rs_upsweep_kernel<RS_ITEMS_VALS>), dim3((uint32_t)nb),
+                               dim3(RsUp<RS_ITEMS_VALS>::THREADS), 0, s, *keys, n, shift, hist, (uint32_t)nb);
         else
-            hipLaunchKernelGGL((rs_upsweep_kernel<RS_ITEMS_KEYS>), dim3((uint32_t)nb), dim3(RS_THREADS), 0, s, *keys, n,
-                               shift, hist, (uint32_t)nb);
+            hipLaunchKernelGGL((rs_upsweep_kernel<RS_ITEMS_KEYS>), dim3((uint32_t)nb),
+                               dim3(RsUp<RS_ITEMS_KEYS>::THREADS), 0, s, *keys, n, shift, hist, (uint32_t)nb);
         hipError_t e = rs_offsets(hist, nb, stmp, s);
         if (e != hipSuccess) return e;
         if (with_vals) {
-            hipLaunchKernelGGL((rs_downsweep_kernel<true, RS_ITEMS_VALS>), dim3((uint32_t)nb), dim3(RS_THREADS),
-                               sizeof(RsShared<true, TV>), s, *keys, *vals, *keys_alt, *vals_alt, n, shift,
+            hipLaunchKernelGGL((rs_downsweep_kernel<true, RS_ITEMS_VALS>), dim3((uint32_t)nb),
+                               dim3(RsDown<RS_ITEMS_VALS>::THREADS), sizeof(SV), s, *keys, *vals, *keys_alt, *vals_alt, n, shift,
                                (const uint32_t *)hist, (uint32_t)nb);
             uint32_t *tv = *vals; *vals = *vals_alt; *vals_alt = tv;
         } else {
-            hipLaunchKernelGGL((rs_downsweep_kernel<false, RS_ITEMS_KEYS>), dim3((uint32_t)nb), dim3(RS_THREADS),
-                               sizeof(RsShared<false, TK>), s, *keys, nullptr, *keys_alt, nullptr, n, shift,
+            hipLaunchKernelGGL((rs_downsweep_kernel<false, RS_ITEMS_KEYS>), dim3((uint32_t)nb),
+                               dim3(RsDown<RS_ITEMS_KEYS>::THREADS), sizeof(SK), s, *keys, nullptr, *keys_alt, nullptr, n, shift,
                                (const uint32_t *)hist, (uint32_t)nb);
         }
         uint64_t *tk = *keys; *keys = *keys_alt; *keys_alt = tk;
@@ -502,8 +528,8 @@ hipError_t radix_sort_kv64(uint64_t **keys, uint64_t **vals, uint64_t **keys_alt
     uint32_t *hist = (uint32_t *)tmp;
     void *stmp = (void *)(hist + 256 * nb);
     for (int shift = lo; shift < hi; shift += 8) {
-        hipLaunchKernelGGL((rs_upsweep_kernel<RS_ITEMS_VALS>), dim3((uint32_t)nb), dim3(RS_THREADS), 0, s, *keys, n,
-                           shift, hist, (uint32_t)nb);
+        hipLaunchKernelGGL((rs_upsweep_kernel<RS_ITEMS_VALS>), dim3((uint32_t)nb), dim3(RsUp<RS_ITEMS_VALS>::THREADS), 0,
+                           s, *keys, n, shift, hist, (uint32_t)nb);
         hipError_t e = rs_offsets(hist, nb, stmp, s);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(rs_downsweep_kv64_kernel, dim3((uint32_t)nb), dim3(RS_THREADS), sizeof(RsSharedKV), s,
