@@ -470,44 +470,68 @@ size_t radix_sort_temp_bytes(uint64_t n) {  // (the smaller tile: the most tiles
     return (hist + 256 * (nc + 1)) * sizeof(uint32_t) + 256;
 }
 
+// one key-only pass at RS_ITEMS keys per lane-slot of a tile
+template <int RS_ITEMS>
+static hipError_t rs_pass_keys(const uint64_t *kin, uint64_t *kout, uint64_t n, int shift, uint32_t *hist,
+                               void *stmp, hipStream_t s) {
+    using SK = RsShared<false, RsTile<RS_ITEMS>::TILE, RsDown<RS_ITEMS>::WAVES>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void *)rs_downsweep_kernel<false, RS_ITEMS>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(SK));
+        attr_set = true;
+    }
+    const uint64_t nb = (n + RsTile<RS_ITEMS>::TILE - 1) / RsTile<RS_ITEMS>::TILE;
+    hipLaunchKernelGGL((rs_upsweep_kernel<RS_ITEMS>), dim3((uint32_t)nb), dim3(RsUp<RS_ITEMS>::THREADS), 0, s, kin, n,
+                       shift, hist, (uint32_t)nb);
+    hipError_t e = rs_offsets(hist, nb, stmp, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((rs_downsweep_kernel<false, RS_ITEMS>), dim3((uint32_t)nb), dim3(RsDown<RS_ITEMS>::THREADS),
+                       sizeof(SK), s, kin, nullptr, kout, nullptr, n, shift, (const uint32_t *)hist, (uint32_t)nb);
+    return hipGetLastError();
+}
+
+// key-only passes past 2^27 keys (1 GB per pass: configs[3]'s per-GPU slice)
+// take 16,384-key tiles on 16 waves -- runs of ~64 keys per digit, for an
+// output far beyond the MALL: slice sort 12.0 -> 10.5 ms; at the bench shape
+// (48.6M keys) they measured slower than 8,192 (0.53 vs 0.50 ms)
+constexpr uint64_t RS_BIG_TILE_KEYS = 1ull << 27;
+
 hipError_t radix_sort(uint64_t **keys, uint32_t **vals, uint64_t **keys_alt, uint32_t **vals_alt,
                       uint64_t n, int lo, int hi, void *tmp, hipStream_t s) {
     if (n <= 1 || hi <= lo) return hipSuccess;
-    constexpr int TK = RsTile<RS_ITEMS_KEYS>::TILE, TV = RsTile<RS_ITEMS_VALS>::TILE;
-    using SK = RsShared<false, TK, RsDown<RS_ITEMS_KEYS>::WAVES>;
+    constexpr int TV = RsTile<RS_ITEMS_VALS>::TILE;
     using SV = RsShared<true, TV, RsDown<RS_ITEMS_VALS>::WAVES>;
+    const bool with_vals = vals != nullptr && *vals != nullptr;
+    uint32_t *hist = (uint32_t *)tmp;
+    if (!with_vals) {
+        void *stmp = (void *)(hist + 256 * ((n + RsTile<RS_ITEMS_KEYS>::TILE - 1) / RsTile<RS_ITEMS_KEYS>::TILE));
+        for (int shift = lo; shift < hi; shift += 8) {
+            const hipError_t e = n >= RS_BIG_TILE_KEYS
+                                     ? rs_pass_keys<2 * RS_ITEMS_KEYS>(*keys, *keys_alt, n, shift, hist, stmp, s)
+                                     : rs_pass_keys<RS_ITEMS_KEYS>(*keys, *keys_alt, n, shift, hist, stmp, s);
+            if (e != hipSuccess) return e;
+            uint64_t *tk = *keys; *keys = *keys_alt; *keys_alt = tk;
+        }
+        return hipGetLastError();
+    }
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void *)rs_downsweep_kernel<true, RS_ITEMS_VALS>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(SV));
-        (void)hipFuncSetAttribute((const void *)rs_downsweep_kernel<false, RS_ITEMS_KEYS>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(SK));
         attr_set = true;
     }
-    const bool with_vals = vals != nullptr && *vals != nullptr;
-    const uint64_t tile = with_vals ? TV : TK;
-    const uint64_t nb = (n + tile - 1) / tile;
-    uint32_t *hist = (uint32_t *)tmp;
+    const uint64_t nb = (n + TV - 1) / TV;
     void *stmp = (void *)(hist + 256 * nb);
     for (int shift = lo; shift < hi; shift += 8) {
-        if (with_vals)
-            hipLaunchKernelGGL((rs_upsweep_kernel<RS_ITEMS_VALS>), dim3((uint32_t)nb),
-                               dim3(RsUp<RS_ITEMS_VALS>::THREADS), 0, s, *keys, n, shift, hist, (uint32_t)nb);
-        else
-            hipLaunchKernelGGL((rs_upsweep_kernel<RS_ITEMS_KEYS>), dim3((uint32_t)nb),
-                               dim3(RsUp<RS_ITEMS_KEYS>::THREADS), 0, s, *keys, n, shift, hist, (uint32_t)nb);
+        hipLaunchKernelGGL((rs_upsweep_kernel<RS_ITEMS_VALS>), dim3((uint32_t)nb), dim3(RsUp<RS_ITEMS_VALS>::THREADS), 0,
+                           s, *keys, n, shift, hist, (uint32_t)nb);
         hipError_t e = rs_offsets(hist, nb, stmp, s);
         if (e != hipSuccess) return e;
-        if (with_vals) {
-            hipLaunchKernelGGL((rs_downsweep_kernel<true, RS_ITEMS_VALS>), dim3((uint32_t)nb),
-                               dim3(RsDown<RS_ITEMS_VALS>::THREADS), sizeof(SV), s, *keys, *vals, *keys_alt, *vals_alt, n, shift,
-                               (const uint32_t *)hist, (uint32_t)nb);
-            uint32_t *tv = *vals; *vals = *vals_alt; *vals_alt = tv;
-        } else {
-            hipLaunchKernelGGL((rs_downsweep_kernel<false, RS_ITEMS_KEYS>), dim3((uint32_t)nb),
-                               dim3(RsDown<RS_ITEMS_KEYS>::THREADS), sizeof(SK), s, *keys, nullptr, *keys_alt, nullptr, n, shift,
-                               (const uint32_t *)hist, (uint32_t)nb);
-        }
+        hipLaunchKernelGGL((rs_downsweep_kernel<true, RS_ITEMS_VALS>), dim3((uint32_t)nb),
+                           dim3(RsDown<RS_ITEMS_VALS>::THREADS), sizeof(SV), s, *keys, *vals, *keys_alt, *vals_alt, n,
+                           shift, (const uint32_t *)hist, (uint32_t)nb);
+        uint32_t *tv = *vals; *vals = *vals_alt; *vals_alt = tv;
         uint64_t *tk = *keys; *keys = *keys_alt; *keys_alt = tk;
     }
     return hipGetLastError();
