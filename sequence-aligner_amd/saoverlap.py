@@ -199,6 +199,10 @@ class Overlapper:
         self._chk(lib().sa_kmer_histogram(self.h, C.byref(u), C.byref(sp), C.byref(cp), C.byref(n)))
         return u.value, {int(sp[i]): int(cp[i]) for i in range(n.value)}
 
+    def set_timing(self, on):
+        """SA_OPT_TIMING: HIP events around every stage (sa_get_stage_times)."""
+        self._chk(lib().sa_set_option(self.h, SA_OPT_TIMING, 1 if on else 0))
+
     def set_aligner(self, aligner):
         """SA_OPT_ALIGNER: SA_ALIGNER_LINEAR (--linear-align) or SA_ALIGNER_QUADRATIC."""
         self._chk(lib().sa_set_option(self.h, SA_OPT_ALIGNER, aligner))
