@@ -950,12 +950,16 @@ int device_build(sa_ctx *c, bool readback) {
         else HIPCHK(launch_kmer_emit(R, E, keys, vals, c->stream));
     }
     // reads in locality order (overlapping reads adjacent) for pair_count: by
-    // the top 16 bits of their minimum k-mer mix (reads sharing it stay
-    // adjacent; two radix passes of a 100k-key sort are launch-bound), on the
-    // side stream beside the partition sort and the bucket build
+    // their minimum k-mer mix (reads sharing it stay adjacent), on the side
+    // stream beside the partition sort and the bucket build.  The minimum of
+    // a read's ~500 mixes sits far below 2^32 (mean 2^32 / 487 ~ 2^23), so
+    // the sort must reach below the top 16 bits to separate distinct minima
+#ifndef SA_LOCALITY_LO
+#define SA_LOCALITY_LO 8  // (A/B: 16 -> 8, pairs 0.595-0.608 -> 0.578-0.588 ms)
+#endif
     HIPCHK(ensure_side(c));
     HIPCHK(fork_side(c, c->ev_fork));
-    HIPCHK(radix_sort(&rk0, &ro0, &rk1, &ro1, nr, 16, 32, rtmp, c->side));
+    HIPCHK(radix_sort(&rk0, &ro0, &rk1, &ro1, nr, SA_LOCALITY_LO, 32, rtmp, c->side));
     HIPCHK(hipEventRecord(c->ev_join, c->side));
     const uint32_t *read_order = ro0;
     PartArgs PA{};
