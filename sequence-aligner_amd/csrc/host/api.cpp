@@ -645,7 +645,8 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
                 PairParams PM = P;
                 PM.n_items = n_multi;
                 PM.table = 1024;
-                HIPCHK(launch_pair_count_multi(E, PI, PM, O, item_start, n_multi, c->stream));
+                if (c->multi_wave_items) HIPCHK(launch_pair_count_multi_wave(E, PI, PM, O, item_start, n_multi, c->stream));
+                else HIPCHK(launch_pair_count_multi(E, PI, PM, O, item_start, n_multi, c->stream));
             } else {
                 HIPCHK(launch_pair_count(E, PI, P, O, read_order, read_order ? ((n_items + 7) & ~7u) : n_items,
                                          c->stream));
@@ -1991,10 +1992,15 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint6
         c->stats.role_pairs = shard_sum(hc.role_pairs);
         return SA_OK;
     }
-    const uint32_t n_multi = (uint32_t)((n + PCM_TARGET - 1) / PCM_TARGET) + 1;
+    // one wave per ~PMW_TARGET local occurrences (SA_SHARD_BLOCKS=1: the
+    // 256-thread multi-read blocks over ~PCM_TARGET, for A/B runs)
+    static const bool blocks_forced = getenv("SA_SHARD_BLOCKS") && atoi(getenv("SA_SHARD_BLOCKS")) != 0;
+    c->multi_wave_items = !blocks_forced;
+    const uint32_t target = c->multi_wave_items ? PMW_TARGET : PCM_TARGET;
+    const uint32_t n_multi = (uint32_t)((n + target - 1) / target) + 1;
     uint32_t *items;
     ENSURE(c->d_items, (size_t)n_multi + 1, &items);
-    HIPCHK(launch_pc_items(loff, N, PCM_TARGET, n_multi, items, c->stream));
+    HIPCHK(launch_pc_items(loff, N, target, n_multi, items, c->stream));
     rc = pair_stage(c, E, PI, false, true, nullptr, N, cnt, np, cap_s, items, n_multi);
     if (rc) return rc;
     // partials grouped by the rank owning their lead (one stable pass on the

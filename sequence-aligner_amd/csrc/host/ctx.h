@@ -120,6 +120,7 @@ struct sa_ctx {
     // per-read mode (part_perm unused): the partials are d_lead / d_trail /
     // d_count, lead descending; owner o's are [part_q[o + 1], part_q[o])
     bool part_per_read = false;
+    bool multi_wave_items = true;    // sharded pair count: wave per item (else 256-thread blocks)
     std::vector<uint64_t> part_q;
     DBuf d_gocc, d_seg, d_rl, d_srl, d_srl2, d_loff, d_starts, d_bounds, d_gcodes, d_gwoff, d_glen, d_gbad, d_psum, d_pkeep, d_ppos;
     DBuf d_scan, d_bigtot, d_items, d_pq;

@@ -1013,6 +1013,242 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_multi_kernel(EmitParams
     }
 }
 
+// ---------------------------------------------------------------------------
+// Multi-read items, one WAVE each (sharded hash stage, round 4).  The block
+// form above runs ~16 block barriers per 512-occurrence item; here a 256-thread
+// block carries four items of ~PMW_TARGET local occurrences (a few reads), one
+// per wave, with the single-device wave kernel's hand-offs (wave barriers,
+// marker + max-scan element map, per-occurrence list bases) and a wave-private
+// 256-slot table keyed by (read, partner).  Every distinct partial is kept
+// (count >= 1: the filter needs the global sums).  Output claims are made once
+// per BLOCK: the four waves' kept counts are scanned at one block barrier and
+// one device atomic claims the block's range (a claim per item made the wave
+// form slower than the blocks in round 3).  An item whose table fills appends
+// its reads to the overflow list for the recount tiers.
+// ---------------------------------------------------------------------------
+constexpr int PMW_WAVES = 4;
+constexpr int PMW_TAB = 256;
+constexpr int PMW_CHUNK = 128;              // occurrences per chunk (2 per lane)
+constexpr int PMW_OCC = PMW_CHUNK / 64;
+constexpr int PMW_BATCH = 8;                // partner gathers in flight per lane
+constexpr int PMW_WIN = 64 * PMW_BATCH;     // elements per window
+constexpr uint32_t PMW_FILL_MAX = PMW_TAB * 3 / 4;
+
+struct PmwShared {  // one per wave
+    unsigned long long key[PMW_TAB];
+    uint32_t cnt[PMW_TAB];
+    uint4 rec[PMW_CHUNK];     // {list entry of element 0 (u64), edge-role end, edge weight}
+    uint32_t aid[PMW_CHUNK];  // read of each occurrence of the chunk
+    uint16_t eo[PMW_WIN];
+    uint32_t fill, overflow, kept, pad;
+};
+
+__device__ __forceinline__ void pmw_insert(PmwShared &S, unsigned long long key, uint32_t w) {
+    uint32_t slot = pcm_hash(key) >> 2;  // (pcm_hash: 10 bits)
+    for (int probe = 0; probe < PMW_TAB / 4; ++probe) {
+        unsigned long long old = lds_relaxed(&S.key[slot]);  // final once set
+        if (old == PCM_EMPTY) old = atomicCAS(&S.key[slot], PCM_EMPTY, key);
+        if (old == PCM_EMPTY || old == key) {
+            if (old == PCM_EMPTY && atomicAdd(&S.fill, 1u) >= PMW_FILL_MAX) S.overflow = 1;
+            atomicAdd(&S.cnt[slot], w);
+            return;
+        }
+        slot = (slot + 1) & (PMW_TAB - 1);
+    }
+    S.overflow = 1;
+}
+
+__global__ __launch_bounds__(PMW_WAVES * 64) void pair_count_multi_wave_kernel(EmitParams e, PairIn in, PairParams p,
+                                                                                PairOut o,
+                                                                                const uint32_t *item_start) {
+    __shared__ PmwShared SH[PMW_WAVES];
+    __shared__ uint32_t wkept[PMW_WAVES], blk_base;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    PmwShared &S = SH[wv];
+    const uint32_t item = blockIdx.x * PMW_WAVES + wv;
+    // (no early return: every wave reaches the block's output claim)
+    const bool live = item < p.n_items;
+    const uint32_t ra = live ? item_start[item] : 0u, rb = live ? item_start[item + 1] : 0u;
+    for (int i = lane; i < PMW_TAB; i += 64) {
+        S.key[i] = PCM_EMPTY;
+        S.cnt[i] = 0;
+    }
+    if (lane == 0) { S.fill = 0; S.overflow = 0; }
+    const uint64_t g0 = ra < rb ? e.occ_off[ra] : 0ull;
+    const uint32_t nocc = ra < rb ? (uint32_t)(e.occ_off[rb] - g0) : 0u;
+    unsigned long long role_pairs = 0;
+    bool over = false;
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t c0 = 0; c0 < nocc; c0 += PMW_CHUNK) {
+        const uint32_t cn = min((uint32_t)PMW_CHUNK, nocc - c0);
+        uint32_t mytot[PMW_OCC];
+        uint4 rcj[PMW_OCC];
+        uint32_t own[PMW_OCC];
+#pragma unroll
+        for (int j = 0; j < PMW_OCC; ++j) {
+            const uint32_t oi = lane * PMW_OCC + j;  // lane-contiguous
+            rcj[j] = make_uint4(0, 0, 0, 0);
+            mytot[j] = 0;
+            own[j] = ra;
+            if (oi < cn) {
+                const uint64_t g = g0 + c0 + oi;
+                rcj[j] = load_rec(in, g);
+                mytot[j] = (rcj[j].y & 0x3FFFFFFFu) + rcj[j].w;
+                // owning read: largest r with occ_off[r] <= g (a few cached loads;
+                // the item's boundaries broadcast from registers measured slower)
+                uint32_t lo = ra, hi = rb;
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (e.occ_off[mid] <= g) lo = mid; else hi = mid;
+                }
+                own[j] = lo;
+            }
+        }
+        uint32_t sum = 0;
+#pragma unroll
+        for (int j = 0; j < PMW_OCC; ++j) sum += mytot[j];
+        const uint32_t inc = wave_incl_add(sum);
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        uint32_t myex[PMW_OCC];
+        myex[0] = inc - sum;
+#pragma unroll
+        for (int j = 1; j < PMW_OCC; ++j) myex[j] = myex[j - 1] + mytot[j - 1];
+        if (!over) {
+#pragma unroll
+            for (int j = 0; j < PMW_OCC; ++j)
+                if (lane * PMW_OCC + j < cn) {
+                    const uint32_t nE = rcj[j].y & 0x3FFFFFFFu;
+                    const uint64_t adj = (((uint64_t)rcj[j].z << 32) | rcj[j].x) - nE - myex[j];
+                    S.rec[lane * PMW_OCC + j] = make_uint4((uint32_t)adj, (uint32_t)(adj >> 32), myex[j] + nE,
+                                                           rcj[j].y >> 30);
+                    S.aid[lane * PMW_OCC + j] = own[j];
+                }
+        }
+        role_pairs += total;
+        uint32_t carry = 0;
+        for (uint32_t w0 = 0; w0 < total && !over; w0 += PMW_WIN) {
+            __builtin_amdgcn_wave_barrier();
+            if (lds_relaxed(&S.overflow)) {
+                over = true;
+                break;
+            }
+            uint4 *eo4 = reinterpret_cast<uint4 *>(S.eo);
+#pragma unroll
+            for (int q = 0; q < PMW_BATCH / 8; ++q) eo4[lane * (PMW_BATCH / 8) + q] = make_uint4(0, 0, 0, 0);
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int j = 0; j < PMW_OCC; ++j)
+                if (mytot[j] && myex[j] >= w0 && myex[j] < w0 + (uint32_t)PMW_WIN)
+                    S.eo[myex[j] - w0] = (uint16_t)(lane * PMW_OCC + j + 1);
+            __builtin_amdgcn_wave_barrier();
+            {
+                uint32_t v[PMW_BATCH];
+#pragma unroll
+                for (int q = 0; q < PMW_BATCH / 8; ++q) {
+                    const uint4 x = eo4[lane * (PMW_BATCH / 8) + q];
+                    const uint32_t w4[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        v[8 * q + 2 * t] = w4[t] & 0xFFFFu;
+                        v[8 * q + 2 * t + 1] = w4[t] >> 16;
+                    }
+                }
+                uint32_t run = 0;
+#pragma unroll
+                for (int i = 0; i < PMW_BATCH; ++i) { run = max(run, v[i]); v[i] = run; }
+                const uint32_t incl = wave_incl_max(run);
+                const uint32_t into = max(carry, wave_shr1(incl));
+#pragma unroll
+                for (int q = 0; q < PMW_BATCH / 8; ++q) {
+                    uint32_t w4[4];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        w4[t] = max(v[8 * q + 2 * t], into) | (max(v[8 * q + 2 * t + 1], into) << 16);
+                    eo4[lane * (PMW_BATCH / 8) + q] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+                }
+                carry = max(carry, (uint32_t)__builtin_amdgcn_readlane((int)incl, 63));
+            }
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t wn = min((uint32_t)PMW_WIN, total - w0);
+            uint32_t part[PMW_BATCH], wt[PMW_BATCH], ow[PMW_BATCH];
+#pragma unroll
+            for (int bb = 0; bb < PMW_BATCH; ++bb) {
+                wt[bb] = 0;
+                part[bb] = 0;
+                ow[bb] = 0;
+                const uint32_t el = bb * 64 + lane;
+                if (el < wn) {
+                    const uint32_t ew = w0 + el;
+                    const uint32_t oc = (uint32_t)S.eo[el] - 1u;
+                    const uint4 r = S.rec[oc];
+                    ow[bb] = S.aid[oc];
+                    part[bb] = in.lst[(((uint64_t)r.y << 32) | r.x) + ew];
+                    wt[bb] = ew < r.z ? r.w : 1u;
+                }
+            }
+#pragma unroll
+            for (int bb = 0; bb < PMW_BATCH; ++bb) {
+                if (wt[bb] == 0 || part[bb] == ow[bb]) continue;  // same read (KmerTable.scala:61-63)
+                pmw_insert(S, ((unsigned long long)ow[bb] << 32) | part[bb], wt[bb]);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    over = over || lds_relaxed(&S.overflow) != 0;
+    const uint32_t shard = blockIdx.x % NSHARD;
+    if (live && lane == 0 && role_pairs) atomicAdd(&o.role_pairs[shard], role_pairs);
+    if (live && over && lane == 0) {  // recount these reads one per block (pair_count_kernel tiers)
+        const uint32_t at = atomicAdd(o.overflow_n, rb - ra);
+        for (uint32_t r = ra; r < rb; ++r) o.overflow_list[at + (r - ra)] = r << 6;
+    }
+    // kept keys of this wave (none when it overflowed), then one claim per block
+    uint32_t keep = 0;
+#pragma unroll
+    for (int j = 0; j < PMW_TAB / 64; ++j) {
+        const uint32_t sl = lane * (PMW_TAB / 64) + j;
+        if (live && !over && S.key[sl] != PCM_EMPTY) keep |= 1u << j;
+    }
+    const uint32_t mine = __popc(keep);
+    const uint32_t winc = wave_incl_add(mine);
+    if (lane == 63) wkept[wv] = winc;
+    if (live && !over && lane == 0) atomicAdd(&o.distinct[shard], (unsigned long long)lds_relaxed(&S.fill));
+    __syncthreads();
+    uint32_t btot = 0, wex = 0;
+#pragma unroll
+    for (int q = 0; q < PMW_WAVES; ++q) {
+        const uint32_t x = wkept[q];
+        if (q < wv) wex += x;
+        btot += x;
+    }
+    if (threadIdx.x == 0) blk_base = btot ? (uint32_t)atomicAdd(&o.cursor[shard], (unsigned long long)btot) : 0u;
+    __syncthreads();
+    if (!mine) return;
+    const unsigned long long region = (unsigned long long)shard * o.cap_s;
+    unsigned long long lat = (unsigned long long)blk_base + wex + (winc - mine);
+#pragma unroll
+    for (int j = 0; j < PMW_TAB / 64; ++j) {
+        if (!(keep & (1u << j))) continue;
+        const uint32_t sl = lane * (PMW_TAB / 64) + j;
+        if (lat < o.cap_s) {
+            const unsigned long long at = region + lat;
+            o.fst[at] = (uint32_t)(S.key[sl] >> 32);
+            o.snd[at] = (uint32_t)S.key[sl];
+            o.cnt[at] = S.cnt[sl];
+        }
+        ++lat;
+    }
+}
+
+hipError_t launch_pair_count_multi_wave(const EmitParams &e, const PairIn &in, const PairParams &p, PairOut &o,
+                                        const uint32_t *item_start, uint32_t n_items, hipStream_t s) {
+    if (n_items == 0) return hipSuccess;
+    PairParams q = p;
+    q.n_items = n_items;
+    hipLaunchKernelGGL(pair_count_multi_wave_kernel, dim3((n_items + PMW_WAVES - 1) / PMW_WAVES), dim3(PMW_WAVES * 64),
+                       0, s, e, in, q, o, item_start);
+    return hipGetLastError();
+}
+
 hipError_t launch_pair_count_multi(const EmitParams &e, const PairIn &in, const PairParams &p, PairOut &o,
                                    const uint32_t *item_start, uint32_t n_items, hipStream_t s) {
     if (n_items == 0) return hipSuccess;

@@ -129,7 +129,8 @@ constexpr int RS_THREADS = 256;
 // tiles 0.69 ms), 16 where values ride along (their LDS staging at 8,192 keys
 // would leave one workgroup per CU)
 constexpr int RS_ITEMS_KEYS = 32;
-constexpr int RS_ITEMS_VALS = 16;
+constexpr int RS_ITEMS_VALS = 32;  // (8 serial shards of the bench shape: 12-byte records' sort 1.32 -> 1.20 ms per shard)
+constexpr int RS_ITEMS_KV = 16;    // 16-byte records: 4,096-key tiles of 4 waves
 template <int ITEMS> struct RsTile {
     static constexpr int TILE = RS_THREADS * ITEMS;
 };
@@ -367,7 +368,7 @@ __global__ __launch_bounds__(RsDown<RS_ITEMS>::THREADS) void rs_downsweep_kernel
 // 16-byte records (u64 key, u64 value): the tile is staged through LDS twice --
 // keys (with their digits), then the values in the same slots -- so the LDS
 // footprint stays that of a key-only tile (3 workgroups per CU, not 2)
-constexpr int RS_TILE_KV = RsTile<RS_ITEMS_VALS>::TILE;
+constexpr int RS_TILE_KV = RsTile<RS_ITEMS_KV>::TILE;
 struct RsSharedKV {
     unsigned long long buf[RS_TILE_KV];  // staged keys, then staged values
     uint8_t dig[RS_TILE_KV];
@@ -462,8 +463,8 @@ __global__ __launch_bounds__(RS_THREADS) void rs_downsweep_kv64_kernel(const uin
     }
 }
 
-size_t radix_sort_temp_bytes(uint64_t n) {  // (the smaller tile: the most tiles)
-    constexpr int RS_TILE = RsTile<RS_ITEMS_VALS>::TILE;
+size_t radix_sort_temp_bytes(uint64_t n) {  // (the smallest tile: the most tiles)
+    constexpr int RS_TILE = RsTile<RS_ITEMS_KV>::TILE;
     const uint64_t nb = (n + RS_TILE - 1) / RS_TILE;
     const uint64_t nc = (nb + RS_CHUNK - 1) / RS_CHUNK;
     const uint64_t hist = 256 * (nb ? nb : 1);
@@ -552,7 +553,7 @@ hipError_t radix_sort_kv64(uint64_t **keys, uint64_t **vals, uint64_t **keys_alt
     uint32_t *hist = (uint32_t *)tmp;
     void *stmp = (void *)(hist + 256 * nb);
     for (int shift = lo; shift < hi; shift += 8) {
-        hipLaunchKernelGGL((rs_upsweep_kernel<RS_ITEMS_VALS>), dim3((uint32_t)nb), dim3(RsUp<RS_ITEMS_VALS>::THREADS), 0,
+        hipLaunchKernelGGL((rs_upsweep_kernel<RS_ITEMS_KV>), dim3((uint32_t)nb), dim3(RsUp<RS_ITEMS_KV>::THREADS), 0,
                            s, *keys, n, shift, hist, (uint32_t)nb);
         hipError_t e = rs_offsets(hist, nb, stmp, s);
         if (e != hipSuccess) return e;

@@ -318,6 +318,13 @@ hipError_t launch_pair_count(const EmitParams &e, const PairIn &in, const PairPa
 // sharded path: one block per range of reads with ~PCM_TARGET local occurrences
 // (launch_pc_items builds item_start[n_items + 1] from the occurrence offsets)
 constexpr uint32_t PCM_TARGET = 512;
+// ... or one WAVE per range of ~PMW_TARGET local occurrences (round 4)
+#ifndef SA_PMW_TARGET
+#define SA_PMW_TARGET 128
+#endif
+constexpr uint32_t PMW_TARGET = SA_PMW_TARGET;
+hipError_t launch_pair_count_multi_wave(const EmitParams &e, const PairIn &in, const PairParams &p, PairOut &o,
+                                        const uint32_t *item_start, uint32_t n_items, hipStream_t s);
 hipError_t launch_pair_count_multi(const EmitParams &e, const PairIn &in, const PairParams &p, PairOut &o,
                                    const uint32_t *item_start, uint32_t n_items, hipStream_t s);
 hipError_t launch_pc_items(const uint64_t *occ_off, uint32_t n_reads, uint32_t target, uint32_t n_items,
