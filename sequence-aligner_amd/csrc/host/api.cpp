@@ -477,9 +477,20 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
             HIPCHK(launch_part_starts(PA, n, 64 - skip_bits - PB, c->stream));
             HIPCHK(ensure_side(c));
             HIPCHK(fork_side(c, c->ev_fork2));
+            // (A/B knob, experiments only: SA_TIER_ORDER=1 runs the 2,048 / 4,096
+            // tiers after the main pass on the main stream, 2 before it)
+            static const int tier_order = getenv("SA_TIER_ORDER") ? atoi(getenv("SA_TIER_ORDER")) : 0;
             if (PA.main_cap >= 2048) {
                 HIPCHK(launch_part_build(PA, strict, 4096, c->side));
                 HIPCHK(launch_part_build(PA, strict, 2048, c->stream));
+            } else if (tier_order == 1) {
+                HIPCHK(launch_part_build(PA, strict, 1024, c->stream));
+                HIPCHK(launch_part_build(PA, strict, 2048, c->stream));
+                HIPCHK(launch_part_build(PA, strict, 4096, c->stream));
+            } else if (tier_order == 2) {
+                HIPCHK(launch_part_build(PA, strict, 2048, c->stream));
+                HIPCHK(launch_part_build(PA, strict, 4096, c->stream));
+                HIPCHK(launch_part_build(PA, strict, 1024, c->stream));
             } else {
                 HIPCHK(launch_part_build(PA, strict, 2048, c->side));
                 HIPCHK(launch_part_build(PA, strict, 4096, c->side));

@@ -89,6 +89,9 @@ __device__ __forceinline__ unsigned long long record_key(uint64_t rec, const Par
 // latency is set by its chain of LDS passes and barriers, nearly the same for
 // any CAP at 4 items per thread, so bigger partitions spread that chain over
 // more records.
+#ifndef SA_PB_PAIR
+#define SA_PB_PAIR 0  // 1: the main pass builds two partitions per block (A/B builds)
+#endif
 template <int CAP> struct PbShape {
     static constexpr int NT = CAP / 4, WAVES = NT / 64, IT = 4;
 };
@@ -193,13 +196,33 @@ __device__ __forceinline__ void lds_radix_sort(SH &S, uint32_t n, int bits) {
 // the 1,024-record kernel lists them for the 2,048-record pass (mid_list), that
 // pass lists its overflow for the 4,096-record pass (mid2_list), and that one
 // lists the partitions above 4,096 for the global path (big_list).
+// a partition's bounds and its records, loaded into registers (all of a
+// thread's loads issued before any is used)
+template <int CAP>
+struct PartLoad {
+    uint32_t ps, n;
+    uint64_t recs[PbShape<CAP>::IT];
+};
+template <int CAP>
+__device__ __forceinline__ void part_load(const PartArgs &A, const uint32_t p, PartLoad<CAP> &L) {
+    constexpr int IT = PbShape<CAP>::IT, NT = PbShape<CAP>::NT;
+    L.ps = A.start[p];
+    L.n = A.start[p + 1] - L.ps;
+    if (L.n == 0 || L.n > (uint32_t)CAP) return;
+#pragma unroll
+    for (int j = 0; j < IT; ++j) {
+        const uint32_t i = threadIdx.x + j * NT;
+        L.recs[j] = load_sk(A.sk + L.ps + (i < L.n ? i : L.n - 1));
+    }
+}
+
 template <int CAP, bool STRICT>
 __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t p, PartShared<CAP> &S,
-                                               uint32_t *Sr) {
+                                               uint32_t *Sr, const PartLoad<CAP> &L) {
     constexpr int IT = PbShape<CAP>::IT, NT = PbShape<CAP>::NT;
     const int tid = threadIdx.x;
-    const uint32_t ps = A.start[p], pe = A.start[p + 1];
-    const uint32_t n = pe - ps;
+    const uint32_t ps = L.ps;
+    const uint32_t n = L.n;
     if (n == 0) return;
     if (n > (uint32_t)CAP) {  // (the bounds kernel listed the partitions above 1,024)
         if (tid == 0) {
@@ -212,12 +235,7 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
     //      (all of a thread's record loads are issued before any is used, so a
     //      block waits one HBM latency here, not one per record)
     {
-        uint64_t recs[IT];
-#pragma unroll
-        for (int j = 0; j < IT; ++j) {
-            const uint32_t i = tid + j * NT;
-            recs[j] = load_sk(A.sk + ps + (i < n ? i : n - 1));
-        }
+        const uint64_t *recs = L.recs;
         // (keys of the clamped slots too: their loc-rank gathers issue together)
         unsigned long long kk[IT];
         uint32_t gg[IT], rr[IT];
@@ -418,14 +436,29 @@ __global__ __launch_bounds__(PbShape<CAP>::NT) void part_build_kernel(PartArgs A
     extern __shared__ __align__(16) uint8_t smem_raw[];
     PartShared<CAP> &S = *reinterpret_cast<PartShared<CAP> *>(smem_raw);
     uint32_t *Sr = A.rl || A.pv ? reinterpret_cast<uint32_t *>(smem_raw + sizeof(PartShared<CAP>)) : nullptr;
-    if constexpr (MAIN) {  // the main pass: one block per partition
-        part_build_one<CAP, STRICT>(A, blockIdx.x, S, Sr);
+    if constexpr (MAIN) {
+#if SA_PB_PAIR
+        // two partitions per block: the second one's records load while the
+        // first is built
+        PartLoad<CAP> L0, L1;
+        part_load<CAP>(A, 2 * blockIdx.x, L0);
+        part_load<CAP>(A, 2 * blockIdx.x + 1, L1);
+        part_build_one<CAP, STRICT>(A, 2 * blockIdx.x, S, Sr, L0);
+        __syncthreads();  // LDS of the first partition fully consumed
+        part_build_one<CAP, STRICT>(A, 2 * blockIdx.x + 1, S, Sr, L1);
+#else
+        PartLoad<CAP> L;  // the main pass: one block per partition
+        part_load<CAP>(A, blockIdx.x, L);
+        part_build_one<CAP, STRICT>(A, blockIdx.x, S, Sr, L);
+#endif
     } else {
         const uint32_t *list = CAP >= 4096 ? A.mid2_list : A.mid_list;
         const uint32_t m = *(CAP >= 4096 ? A.mid2_n : A.mid_n);
         for (uint32_t i = blockIdx.x; i < m; i += gridDim.x) {
             __syncthreads();  // LDS of the previous partition fully consumed
-            part_build_one<CAP, STRICT>(A, list[i], S, Sr);
+            PartLoad<CAP> L;
+            part_load<CAP>(A, list[i], L);
+            part_build_one<CAP, STRICT>(A, list[i], S, Sr, L);
         }
     }
 }
@@ -565,12 +598,13 @@ hipError_t launch_part_build(const PartArgs &a, bool strict, int cap, hipStream_
     } while (0)
     const uint32_t mid_grid = a.np < 1024u ? a.np : 1024u;
     const bool m2 = a.main_cap >= 2048;
+    const uint32_t main_grid = SA_PB_PAIR ? (a.np + 1) / 2 : a.np;  // (np: a power of two)
     if (cap == 1024) {
         if (m2) return hipSuccess;  // (no 1,024 pass: the 2,048-record pass is the main one)
-        if (strict) PB_LAUNCH(1024, a.np, true, true); else PB_LAUNCH(1024, a.np, false, true);
+        if (strict) PB_LAUNCH(1024, main_grid, true, true); else PB_LAUNCH(1024, main_grid, false, true);
     } else if (cap == 2048) {
         if (m2) {
-            if (strict) PB_LAUNCH(2048, a.np, true, true); else PB_LAUNCH(2048, a.np, false, true);
+            if (strict) PB_LAUNCH(2048, main_grid, true, true); else PB_LAUNCH(2048, main_grid, false, true);
         } else {
             if (strict) PB_LAUNCH(2048, mid_grid, true, false); else PB_LAUNCH(2048, mid_grid, false, false);
         }
