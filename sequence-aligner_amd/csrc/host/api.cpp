@@ -397,10 +397,9 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
     // with the 2,048-record tier as the main pass -- 8 waves per block -- built
     // buckets in 1.53-1.55 ms against 1.15 for ~700-record ones on the 1,024 tier)
     const uint64_t part_target = 700;
-    const uint32_t main_cap = 1024;
     int PB = 1;
     while (PB < 24 && (part_target << PB) < n) ++PB;
-    if (main_cap == 1024 && PB > 16 && (n >> 16) <= 900) PB = 16;
+    if (PB > 16 && (n >> 16) <= 900) PB = 16;
     const uint32_t nparts = 1u << PB;
     const int kbits = 32 + c->lb;  // LDS sort key: mix << lb | loc rank
     uint2 *srl = nullptr;
@@ -457,7 +456,6 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
         PA.mid_list = biglist + nparts + 1; PA.mid_n = &cnt->mid_n;
         PA.mid2_list = biglist + 2 * ((size_t)nparts + 1); PA.mid2_n = &cnt->mid2_n;
         PA.counts = cnt->bkt_counts;
-        PA.main_cap = main_cap;
         if (strict) {
             ENSURE(c->d_mdidx, 3 * n + 3, &PA.lidx);
             ENSURE(c->d_srec, n + 1, &PA.srec);
@@ -477,25 +475,11 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
             HIPCHK(launch_part_starts(PA, n, 64 - skip_bits - PB, c->stream));
             HIPCHK(ensure_side(c));
             HIPCHK(fork_side(c, c->ev_fork2));
-            // (A/B knob, experiments only: SA_TIER_ORDER=1 runs the 2,048 / 4,096
-            // tiers after the main pass on the main stream, 2 before it)
-            static const int tier_order = getenv("SA_TIER_ORDER") ? atoi(getenv("SA_TIER_ORDER")) : 0;
-            if (PA.main_cap >= 2048) {
-                HIPCHK(launch_part_build(PA, strict, 4096, c->side));
-                HIPCHK(launch_part_build(PA, strict, 2048, c->stream));
-            } else if (tier_order == 1) {
-                HIPCHK(launch_part_build(PA, strict, 1024, c->stream));
-                HIPCHK(launch_part_build(PA, strict, 2048, c->stream));
-                HIPCHK(launch_part_build(PA, strict, 4096, c->stream));
-            } else if (tier_order == 2) {
-                HIPCHK(launch_part_build(PA, strict, 2048, c->stream));
-                HIPCHK(launch_part_build(PA, strict, 4096, c->stream));
-                HIPCHK(launch_part_build(PA, strict, 1024, c->stream));
-            } else {
-                HIPCHK(launch_part_build(PA, strict, 2048, c->side));
-                HIPCHK(launch_part_build(PA, strict, 4096, c->side));
-                HIPCHK(launch_part_build(PA, strict, 1024, c->stream));
-            }
+            // (the same tiers in line on one stream, before or after the main
+            // pass, measured the same: profiles/r04/ab/ab_tier_order_pair_build.txt)
+            HIPCHK(launch_part_build(PA, strict, 2048, c->side));
+            HIPCHK(launch_part_build(PA, strict, 4096, c->side));
+            HIPCHK(launch_part_build(PA, strict, 1024, c->stream));
             HIPCHK(join_side(c, c->ev_join2));
         }
         if (phase == 1) return SA_OK;
@@ -1945,7 +1929,7 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint6
                                        (const uint64_t *)c->d_gocc.p, c->gnpr,
                                        (const int32_t *)c->d_glen.p, (const uint32_t *)c->d_lbase.p,
                                        (const uint32_t *)c->d_lrank.p, c->set.kmer_size, packed ? nullptr : rl, pv,
-                                       c->lb, c->stream));
+                                       c->lb, loff, c->stream));
         HIPCHK(launch_local_offsets(packed ? nullptr : rl, pv, c->lb, n, N, loff, c->stream));
     }
     PartArgs PA{};

@@ -35,7 +35,7 @@ __global__ void prepare_received_kernel(uint64_t *recs, uint64_t n, const uint64
                                         const uint32_t *__restrict__ starts, const uint64_t *occ_off, uint32_t npr,
                                         const int32_t *len, const uint32_t *__restrict__ lbase,
                                         const uint32_t *lrank, int32_t k, uint2 *rl, uint32_t *pv, int lb,
-                                        unsigned long long npr_magic) {
+                                        unsigned long long npr_magic, uint64_t *loff) {
     const uint64_t i = (uint64_t)blockIdx.x * DT + threadIdx.x;
     if (i >= n) return;
     // the source whose segment holds i: searched once per wave on its first
@@ -68,10 +68,31 @@ __global__ void prepare_received_kernel(uint64_t *recs, uint64_t n, const uint64
         r = lo;
         pos = (uint32_t)(g - occ_off[r]);
     }
+    // local_offsets fused in: loff[a] = first i with read(i) >= a.  Record i
+    // opens the reads (read(i - 1), read(i)], read(i - 1) from the lane before;
+    // the first lane of each wave and the end are left to local_offsets_fix
+    const uint32_t prev = __shfl_up((int)r, 1, 64);
     const uint32_t lr = lrank[(npr ? lbase[npr - 1] : lbase[len[r] - k]) + pos];
     if (pv) pv[i] = (r << lb) | lr;
     else rl[i] = make_uint2(r, lr);
     recs[i] = (rec & 0xFFFFFFFF00000000ull) | (uint32_t)i;
+    if (loff && (threadIdx.x & 63) != 0)
+        for (uint32_t a = prev + 1; a <= r; ++a) loff[a] = i;
+}
+
+// the read boundaries prepare_received leaves: at each wave's first record
+// (and record 0) and past the last record (reads after it: loff = n)
+__global__ void local_offsets_fix_kernel(const uint2 *rl, const uint32_t *pv, int lb, uint64_t n, uint32_t n_reads,
+                                         uint64_t *loff) {
+    const uint64_t w = (uint64_t)blockIdx.x * DT + threadIdx.x;
+    const uint64_t i = w * 64;
+    if (i > n) return;
+    auto read_of = [&](uint64_t j) { return pv ? pv[j] >> lb : rl[j].x; };
+    const uint32_t prev = i == 0 ? 0u : read_of(i - 1) + 1u;  // first read not yet started
+    const uint32_t cur = i == n ? n_reads + 1u : read_of(i) + 1u;
+    for (uint32_t a = prev; a < cur; ++a) loff[a] = i;
+    if (i < n && i + 64 > n)  // n not a multiple of 64: the reads after the last record
+        for (uint32_t a = read_of(n - 1) + 1u; a <= n_reads; ++a) loff[a] = n;
 }
 
 // loff[a] = first i with rl[i].x >= a, for a in [0, n_reads] (reads ascending):
@@ -429,16 +450,21 @@ hipError_t launch_iota(uint32_t *v, uint64_t n, hipStream_t s) {
 hipError_t launch_prepare_received(uint64_t *recs, uint64_t n, const uint64_t *seg, uint32_t P,
                                    const uint32_t *starts, const uint64_t *occ_off, uint32_t npr, const int32_t *len,
                                    const uint32_t *lbase, const uint32_t *lrank, int32_t k, uint2 *rl,
-                                   uint32_t *pv, int lb, hipStream_t s) {
+                                   uint32_t *pv, int lb, uint64_t *loff, hipStream_t s) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(prepare_received_kernel, grid_for(n), dim3(DT), 0, s, recs, n, seg, P, starts, occ_off, npr,
-                       len, lbase, lrank, k, rl, pv, lb, npr >= 2 ? ~0ull / npr + 1 : 0ull);
+                       len, lbase, lrank, k, rl, pv, lb, npr >= 2 ? ~0ull / npr + 1 : 0ull, loff);
     return hipGetLastError();
 }
 
 hipError_t launch_local_offsets(const uint2 *rl, const uint32_t *pv, int lb, uint64_t n, uint32_t n_reads,
                                 uint64_t *loff, hipStream_t s) {
-    hipLaunchKernelGGL(local_offsets_kernel, grid_for(n + 1), dim3(DT), 0, s, rl, pv, lb, n, n_reads, loff);
+    if (!n) {
+        hipLaunchKernelGGL(local_offsets_kernel, grid_for(n + 1), dim3(DT), 0, s, rl, pv, lb, n, n_reads, loff);
+        return hipGetLastError();
+    }
+    // (prepare_received wrote the boundaries inside each wave)
+    hipLaunchKernelGGL(local_offsets_fix_kernel, grid_for(n / 64 + 1), dim3(DT), 0, s, rl, pv, lb, n, n_reads, loff);
     return hipGetLastError();
 }
 

@@ -554,9 +554,6 @@ static hipError_t pc_launch(const EmitParams &e, const PairIn &in, const PairPar
 // limit), overflow accounting and per-read region as pair_count_kernel<false, 256>.
 // ---------------------------------------------------------------------------
 constexpr int PW_WAVES = 4;
-#ifndef SA_PW_PREFETCH
-#define SA_PW_PREFETCH 1
-#endif
 #ifndef PW_CHUNK_OCC
 #define PW_CHUNK_OCC 64
 #endif
@@ -635,10 +632,9 @@ __global__ __launch_bounds__(PW_WAVES * 64, PW_MIN_WAVES) void pair_count_wave_k
     bool over = false;
     __builtin_amdgcn_wave_barrier();
 
-    // records are prefetched one chunk ahead: chunk c + 1's loads are issued
-    // after chunk c's first partner gathers, so they are in flight while the
-    // gathers are awaited and inserted (the chunk loop was one record-load
-    // latency plus one gather latency per chunk)
+    // a chunk's records are loaded at the end of the one before (issuing them
+    // behind the chunk's first partner gathers instead measured slower: 0.594
+    // vs 0.578 ms per bench step, the live registers cost the gathers' batch)
     uint2 nxt[PW_OCC];
 #pragma unroll
     for (int j = 0; j < PW_OCC; ++j) {
@@ -660,16 +656,6 @@ __global__ __launch_bounds__(PW_WAVES * 64, PW_MIN_WAVES) void pair_count_wave_k
             }
             mytot[j] = tot;
         }
-        bool pf = false;  // next chunk's records issued
-        const uint32_t c1 = c0 + PW_CHUNK;
-        auto prefetch = [&]() {
-#pragma unroll
-            for (int j = 0; j < PW_OCC; ++j) {
-                const uint32_t oi = lane * PW_OCC + j;
-                if (c1 + oi < nocc) nxt[j] = load_rec_raw(in, g0 + c1 + oi);
-            }
-            pf = true;
-        };
         uint32_t sum = 0;
 #pragma unroll
         for (int j = 0; j < PW_OCC; ++j) sum += mytot[j];
@@ -755,14 +741,18 @@ __global__ __launch_bounds__(PW_WAVES * 64, PW_MIN_WAVES) void pair_count_wave_k
                     wt[bb] = ew < r.z ? r.w : 1u;
                 }
             }
-            if (SA_PW_PREFETCH && !pf) prefetch();
 #pragma unroll
             for (int bb = 0; bb < PW_BATCH; ++bb) {
                 if (part[bb] == a) continue;  // same read (KmerTable.scala:61-63)
                 pw_insert(S, part[bb], wt[bb], (uint32_t)min(rp0 + w0 + bb * 64 + lane, 0xFFFFFFFEull));
             }
         }
-        if (!pf && !over) prefetch();  // (SA_PW_PREFETCH 0: here, after the chunk)
+        if (!over)
+#pragma unroll
+            for (int j = 0; j < PW_OCC; ++j) {
+                const uint32_t oi = lane * PW_OCC + j;
+                if (c0 + PW_CHUNK + oi < nocc) nxt[j] = load_rec_raw(in, g0 + c0 + PW_CHUNK + oi);
+            }
         // the rest of the read's chunks still count their role pairs after an overflow
         if (over)
             for (uint32_t c1 = c0 + PW_CHUNK; c1 < nocc; c1 += PW_CHUNK) {

@@ -89,9 +89,6 @@ __device__ __forceinline__ unsigned long long record_key(uint64_t rec, const Par
 // latency is set by its chain of LDS passes and barriers, nearly the same for
 // any CAP at 4 items per thread, so bigger partitions spread that chain over
 // more records.
-#ifndef SA_PB_PAIR
-#define SA_PB_PAIR 0  // 1: the main pass builds two partitions per block (A/B builds)
-#endif
 template <int CAP> struct PbShape {
     static constexpr int NT = CAP / 4, WAVES = NT / 64, IT = 4;
 };
@@ -437,20 +434,12 @@ __global__ __launch_bounds__(PbShape<CAP>::NT) void part_build_kernel(PartArgs A
     PartShared<CAP> &S = *reinterpret_cast<PartShared<CAP> *>(smem_raw);
     uint32_t *Sr = A.rl || A.pv ? reinterpret_cast<uint32_t *>(smem_raw + sizeof(PartShared<CAP>)) : nullptr;
     if constexpr (MAIN) {
-#if SA_PB_PAIR
-        // two partitions per block: the second one's records load while the
-        // first is built
-        PartLoad<CAP> L0, L1;
-        part_load<CAP>(A, 2 * blockIdx.x, L0);
-        part_load<CAP>(A, 2 * blockIdx.x + 1, L1);
-        part_build_one<CAP, STRICT>(A, 2 * blockIdx.x, S, Sr, L0);
-        __syncthreads();  // LDS of the first partition fully consumed
-        part_build_one<CAP, STRICT>(A, 2 * blockIdx.x + 1, S, Sr, L1);
-#else
-        PartLoad<CAP> L;  // the main pass: one block per partition
+        // the main pass: one block per partition (two per block, the second's
+        // records loading while the first is built, measured no faster: 1.32 ms
+        // either way, profiles/r04/ab/ab_tier_order_pair_build.txt)
+        PartLoad<CAP> L;
         part_load<CAP>(A, blockIdx.x, L);
         part_build_one<CAP, STRICT>(A, blockIdx.x, S, Sr, L);
-#endif
     } else {
         const uint32_t *list = CAP >= 4096 ? A.mid2_list : A.mid_list;
         const uint32_t m = *(CAP >= 4096 ? A.mid2_n : A.mid_n);
@@ -556,7 +545,7 @@ __global__ void records_from_tables_kernel(const uint64_t *sk, const uint32_t *s
 // the 2,048 / 4,096-record tiers need not wait for the 1,024-record pass: they
 // run beside it on a second stream.
 __global__ void part_bounds_kernel(const uint64_t *sk, uint64_t n, int shift, uint32_t mask, uint32_t np,
-                                   uint32_t *start, uint32_t *mid_list, uint32_t *mid_n, uint32_t main_cap) {
+                                   uint32_t *start, uint32_t *mid_list, uint32_t *mid_n) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p > np) return;
     const bool two = p < np;
@@ -572,16 +561,13 @@ __global__ void part_bounds_kernel(const uint64_t *sk, uint64_t n, int shift, ui
         }
     }
     start[p] = (uint32_t)lo;
-    if (two && lo1 - lo > main_cap) mid_list[atomicAdd(mid_n, 1u)] = p;
+    if (two && lo1 - lo > 1024) mid_list[atomicAdd(mid_n, 1u)] = p;
 }
 
 hipError_t launch_part_starts(const PartArgs &a, uint64_t n, int shift, hipStream_t s) {
-    // partitions above the main pass's capacity are listed for the next tier
-    // (main 1,024: the 2,048 tier's list; main 2,048: the 4,096 tier's)
-    const bool m2 = a.main_cap >= 2048;
+    // partitions above the main pass's 1,024 records are listed for the 2,048 tier
     hipLaunchKernelGGL(part_bounds_kernel, dim3((a.np + 1 + 255) / 256), dim3(256), 0, s, a.sk, n, shift, a.np - 1,
-                       a.np, const_cast<uint32_t *>(a.start), m2 ? a.mid2_list : a.mid_list, m2 ? a.mid2_n : a.mid_n,
-                       m2 ? 2048u : 1024u);
+                       a.np, const_cast<uint32_t *>(a.start), a.mid_list, a.mid_n);
     return hipGetLastError();
 }
 
@@ -597,17 +583,10 @@ hipError_t launch_part_build(const PartArgs &a, bool strict, int cap, hipStream_
         hipLaunchKernelGGL((part_build_kernel<CAPV, ST, MAINV>), dim3(GRID), dim3(PbShape<CAPV>::NT), lds, s, a); \
     } while (0)
     const uint32_t mid_grid = a.np < 1024u ? a.np : 1024u;
-    const bool m2 = a.main_cap >= 2048;
-    const uint32_t main_grid = SA_PB_PAIR ? (a.np + 1) / 2 : a.np;  // (np: a power of two)
     if (cap == 1024) {
-        if (m2) return hipSuccess;  // (no 1,024 pass: the 2,048-record pass is the main one)
-        if (strict) PB_LAUNCH(1024, main_grid, true, true); else PB_LAUNCH(1024, main_grid, false, true);
+        if (strict) PB_LAUNCH(1024, a.np, true, true); else PB_LAUNCH(1024, a.np, false, true);
     } else if (cap == 2048) {
-        if (m2) {
-            if (strict) PB_LAUNCH(2048, main_grid, true, true); else PB_LAUNCH(2048, main_grid, false, true);
-        } else {
-            if (strict) PB_LAUNCH(2048, mid_grid, true, false); else PB_LAUNCH(2048, mid_grid, false, false);
-        }
+        if (strict) PB_LAUNCH(2048, mid_grid, true, false); else PB_LAUNCH(2048, mid_grid, false, false);
     } else {
         if (strict) PB_LAUNCH(4096, mid_grid, true, false); else PB_LAUNCH(4096, mid_grid, false, false);
     }

@@ -375,7 +375,6 @@ struct PartArgs {
     uint32_t *mid_list, *mid_n;    // partitions above 1,024 records (2,048-record LDS pass)
     uint32_t *mid2_list, *mid2_n;  // partitions above 2,048 records (4,096-record LDS pass)
     unsigned long long *counts;  // [2][NSHARD]: buckets, groups
-    uint32_t main_cap;           // 1,024 or 2,048: the tier that takes one block per partition
     // strict
     uint32_t *lidx;              // parallel to lst
     uint4 *srec;                 // [n_occ] by g
@@ -478,11 +477,13 @@ hipError_t launch_kmer_hist(const uint64_t *sorted, uint64_t n, uint32_t *flag, 
 
 // distributed (multi-GPU) glue, dist.hip
 hipError_t launch_iota(uint32_t *v, uint64_t n, hipStream_t s);
-// rl[i] = {read, loc rank}; or, with pv, pv[i] = read << lb | loc rank
+// rl[i] = {read, loc rank}; or, with pv, pv[i] = read << lb | loc rank.  With
+// loff, also the read offsets loff[a] whose boundary falls inside a wave;
+// launch_local_offsets (same rl / pv, loff) then fills in the rest
 hipError_t launch_prepare_received(uint64_t *recs, uint64_t n, const uint64_t *seg, uint32_t P,
                                    const uint32_t *starts, const uint64_t *occ_off, uint32_t npr, const int32_t *len,
                                    const uint32_t *lbase, const uint32_t *lrank, int32_t k, uint2 *rl,
-                                   uint32_t *pv, int lb, hipStream_t s);
+                                   uint32_t *pv, int lb, uint64_t *loff, hipStream_t s);
 hipError_t launch_local_offsets(const uint2 *rl, const uint32_t *pv, int lb, uint64_t n, uint32_t n_reads,
                                 uint64_t *loff, hipStream_t s);
 hipError_t launch_owner_bounds(const uint64_t *keys, uint64_t n, int shift, uint32_t P, uint64_t *bounds,
