@@ -26,5 +26,6 @@ pass lds SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE
 # the lane-group aligner (LDS traceback, DPP) is not the default at the bench
 # shape; one LDS pass over it gives that DP kernel's bank-conflict rate
 BENCH="$BENCH --align-kernel 1" pass lds_group SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE
+pass clk GRBM_GUI_ACTIVE GRBM_COUNT
 pass sq SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY
 python3 $R/tools/pmc_summary.py $R/gpurun_out $R/gpurun_out/pmc_summary__n100000_L500_k15.csv
