@@ -339,6 +339,26 @@ int ensure_prepared(sa_ctx *c) {
     return SA_OK;
 }
 
+// Uniform lengths (one packed-word count per read, records carrying their
+// occurrence index): the first radix pass over the records generates them from
+// the packed reads (radix_sort_gen), so they are never written and re-read
+// unsorted, and pack_emit only packs and writes the locality keys.
+// SA_KEYGEN=0 keeps the stored records (A/B)
+static bool make_keygen(const sa_ctx *c, const EmitParams &E, uint64_t n, KeyGen &kg) {
+    static const bool env_on = !getenv("SA_KEYGEN") || atoi(getenv("SA_KEYGEN")) != 0;
+    const size_t nr = c->woff.empty() ? 0 : c->woff.size() - 1;
+    if (!env_on || !E.npr || E.pos_bits || E.occ_rl || nr == 0 || n >= (1ull << 32)) return false;
+    const uint64_t nw = c->woff[1] - c->woff[0];
+    for (size_t r = 1; r < nr; ++r)
+        if (c->woff[r + 1] - c->woff[r] != nw) return false;
+    kg.codes = (const uint32_t *)c->d_codes.p;
+    kg.nw = (uint32_t)nw;
+    kg.npr = E.npr;
+    kg.npr_magic = E.npr >= 2 ? ~0ull / E.npr + 1 : 0ull;
+    kg.shift = 32 - 2 * c->m;
+    return true;
+}
+
 // PartArgs' two shortcuts around table lookups (checked against the tables,
 // off when they do not hold): loc rank = position for uniform lengths, and the
 // tags as three loc-rank intervals
@@ -381,7 +401,8 @@ static void set_part_shortcuts(const sa_ctx *c, PartArgs &PA, uint32_t npr) {
 int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, uint32_t *vals2, uint64_t n,
                  const uint64_t *occ_off, uint32_t n_reads, uint32_t npr, const uint2 *rl,
                  const int32_t *len, bool strict, void *stmp, Counters *cnt, PartArgs &PA,
-                 unsigned long long &big_buckets, int skip_bits = 0, int phase = 0, const uint32_t *pv = nullptr) {
+                 unsigned long long &big_buckets, int skip_bits = 0, int phase = 0, const uint32_t *pv = nullptr,
+                 const KeyGen *kgen = nullptr) {
     // phase 0: everything; 1: sort + LDS tiers, no readback (the caller's
     // first pair-count pass aborts on big_n); 2: only the global path of the
     // partitions phase 1 listed (keys / PA as phase 1 left them)
@@ -432,7 +453,12 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
                 srl = (uint2 *)v0;
             } else {
                 uint32_t *nv = nullptr, *nv2 = nullptr;  // key-only: the payload rides in the record
-                HIPCHK(radix_sort(&keys, &nv, &keys2, &nv2, n, 64 - skip_bits - PB, 64 - skip_bits, stmp, c->stream));
+                if (kgen)  // records generated by the first pass, never stored unsorted
+                    HIPCHK(radix_sort_gen(*kgen, &keys, &keys2, n, 64 - skip_bits - PB, 64 - skip_bits, stmp,
+                                          c->stream));
+                else
+                    HIPCHK(radix_sort(&keys, &nv, &keys2, &nv2, n, 64 - skip_bits - PB, 64 - skip_bits, stmp,
+                                      c->stream));
             }
         }
         PA = PartArgs{};
@@ -940,9 +966,11 @@ int device_build(sa_ctx *c, bool readback) {
         ENSURE(c->d_rl, n + 1, &orl);
         E.occ_rl = orl;
     }
+    KeyGen kg{};
+    const bool use_kgen = fused && make_keygen(c, E, n, kg);
     {
         StageScope st(c, SA_STAGE_EMIT);
-        if (fused) HIPCHK(launch_pack_emit(R, E, keys, c->stream));
+        if (fused) HIPCHK(launch_pack_emit(R, E, use_kgen ? nullptr : keys, c->stream));
         else HIPCHK(launch_kmer_emit(R, E, keys, vals, c->stream));
     }
     // reads in locality order (overlapping reads adjacent) for pair_count: by
@@ -964,7 +992,8 @@ int device_build(sa_ctx *c, bool readback) {
     // first pass aborts if a partition needs the global path, see below)
     const int bphase = strict ? 0 : 1;
     rc = bucket_stage(c, keys, keys2, vals, vals2, n, (const uint64_t *)c->d_occ_off.p, nr, c->uniform_npr,
-                      orl, (const int32_t *)c->d_len.p, strict, stmp, cnt, PA, big_buckets, 0, bphase);
+                      orl, (const int32_t *)c->d_len.p, strict, stmp, cnt, PA, big_buckets, 0, bphase, nullptr,
+                      use_kgen ? &kg : nullptr);
     if (rc) return rc;
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
     if (strict) {
@@ -1852,20 +1881,30 @@ int sa_dist_emit(sa_ctx *c, void *send_recs, uint64_t *counts) {
         StageScope st(c, SA_STAGE_PACK);
         HIPCHK(launch_pack_reads(R, c->stream));
     }
+    KeyGen kg{};
+    const bool use_kgen = fused && make_keygen(c, E, n, kg);
     {
         StageScope st(c, SA_STAGE_EMIT);
-        if (fused) HIPCHK(launch_pack_emit(R, E, keys, c->stream));
+        if (fused) HIPCHK(launch_pack_emit(R, E, use_kgen ? nullptr : keys, c->stream));
         else HIPCHK(launch_kmer_emit(R, E, keys, nullptr, c->stream));
     }
     // owner = top log2(P) bits of the mixed hash: one stable radix pass groups
     // the 8-byte records by owner and keeps them in occurrence order within each
-    keys2 = (uint64_t *)send_recs;
     {
         StageScope st(c, SA_STAGE_SORT);
-        uint32_t *nv = nullptr, *nv2 = nullptr;
-        if (c->log_ranks > 0) HIPCHK(radix_sort(&keys, &nv, &keys2, &nv2, n, 64 - c->log_ranks, 64, stmp, c->stream));
-        if (keys != (uint64_t *)send_recs && n)
-            HIPCHK(hipMemcpyAsync(send_recs, keys, n * 8, hipMemcpyDeviceToDevice, c->stream));
+        if (use_kgen) {  // generated straight into the send buffer
+            uint64_t *out = (uint64_t *)send_recs;
+            HIPCHK(radix_sort_gen(kg, &out, &keys, n, 64 - c->log_ranks, 64, stmp, c->stream));
+            if (out != (uint64_t *)send_recs && n)
+                HIPCHK(hipMemcpyAsync(send_recs, out, n * 8, hipMemcpyDeviceToDevice, c->stream));
+        } else {
+            keys2 = (uint64_t *)send_recs;
+            uint32_t *nv = nullptr, *nv2 = nullptr;
+            if (c->log_ranks > 0)
+                HIPCHK(radix_sort(&keys, &nv, &keys2, &nv2, n, 64 - c->log_ranks, 64, stmp, c->stream));
+            if (keys != (uint64_t *)send_recs && n)
+                HIPCHK(hipMemcpyAsync(send_recs, keys, n * 8, hipMemcpyDeviceToDevice, c->stream));
+        }
     }
     uint64_t *bounds;
     ENSURE(c->d_bounds, (size_t)c->nranks + 1, &bounds);

@@ -109,7 +109,9 @@ __global__ __launch_bounds__(256) void kmer_emit_kernel(DevReads r, EmitParams e
     }
 }
 
-// Packing and emission in one pass for reads of <= 1,024 bases (<= 64 words):
+// Packing and emission in one pass for reads of <= 1,024 bases (<= 64 words)
+// (keys == nullptr: packing, bad positions and locality keys only -- the
+// partition sort then generates the records itself, radix_sort_gen):
 // lane q packs word q as pack_reads_kernel does, keeps it in a register, and
 // the k-mer windows are assembled from the wave's words with two lane shuffles
 // -- no second launch, no reload of the packed words.  Records, locality keys
@@ -178,7 +180,7 @@ __global__ __launch_bounds__(256) void pack_emit_kernel(DevReads r, EmitParams e
             const uint32_t h = mix32(x);
             kmin = min(kmin, h);
             const uint32_t occ = e.pos_bits ? (rd << e.pos_bits) | (uint32_t)i : (uint32_t)(g0 + i);
-            keys[g0 + i] = ((uint64_t)h << 32) | (uint64_t)occ;
+            if (keys) keys[g0 + i] = ((uint64_t)h << 32) | (uint64_t)occ;
             if (e.occ_rl) e.occ_rl[g0 + i] = make_uint2(rd, lr[i]);
         }
         if (e.rkey) {

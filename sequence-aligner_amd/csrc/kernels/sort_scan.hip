@@ -148,10 +148,10 @@ struct RsUp {
     static constexpr int THREADS = RS_ITEMS > 16 ? RS_THREADS * (RS_ITEMS / 16) : RS_THREADS;
     static constexpr int ITEMS = RS_ITEMS > 16 ? 16 : RS_ITEMS;
 };
-template <int RS_ITEMS>
+template <int RS_ITEMS, bool GEN = false>
 __global__ __launch_bounds__(RsUp<RS_ITEMS>::THREADS) void rs_upsweep_kernel(const uint64_t *keys, uint64_t n,
                                                                             int shift, uint32_t *hist,
-                                                                            uint32_t nblocks) {
+                                                                            uint32_t nblocks, KeyGen kg) {
     (void)nblocks;
     constexpr int RS_TILE = RsTile<RS_ITEMS>::TILE, NT = RsUp<RS_ITEMS>::THREADS, IT = RsUp<RS_ITEMS>::ITEMS;
     constexpr int NW = NT / 64;
@@ -163,7 +163,8 @@ __global__ __launch_bounds__(RsUp<RS_ITEMS>::THREADS) void rs_upsweep_kernel(con
 #pragma unroll
     for (int j = 0; j < IT; ++j) {
         const uint64_t i = base + (uint64_t)j * NT + tid;
-        k[j] = i < n ? __builtin_nontemporal_load(keys + i) : 0ull;  // read once per pass
+        if constexpr (GEN) k[j] = i < n ? gen_key(kg, i) : 0ull;
+        else k[j] = i < n ? __builtin_nontemporal_load(keys + i) : 0ull;  // read once per pass
     }
     __syncthreads();
 #pragma unroll
@@ -281,12 +282,12 @@ struct RsShared {
 // (wave_peers: sa_internal.h)
 
 // VALS = false: key-only sort (records that carry their payload in the key)
-template <bool VALS, int RS_ITEMS>
+template <bool VALS, int RS_ITEMS, bool GEN = false>
 __global__ __launch_bounds__(RsDown<RS_ITEMS>::THREADS) void rs_downsweep_kernel(const uint64_t *kin,
                                                                                  const uint32_t *vin, uint64_t *kout,
                                                                                  uint32_t *vout, uint64_t n, int shift,
                                                                                  const uint32_t *hist,
-                                                                                 uint32_t nblocks) {
+                                                                                 uint32_t nblocks, KeyGen kg) {
     using D = RsDown<RS_ITEMS>;
     constexpr int RS_TILE = D::TILE, RS_SUB = D::SUB, RS_SLICES = D::SLICES, WAVES = D::WAVES, NT = D::THREADS;
     extern __shared__ __align__(16) uint8_t rs_smem[];
@@ -302,7 +303,8 @@ __global__ __launch_bounds__(RsDown<RS_ITEMS>::THREADS) void rs_downsweep_kernel
 #pragma unroll
     for (int j = 0; j < RS_SLICES; ++j) {
         const uint64_t i = sub + (uint64_t)j * 64 + lane;
-        k[j] = i < n ? rs_load_key(kin + i) : ~0ull;
+        if constexpr (GEN) k[j] = i < n ? gen_key(kg, i) : ~0ull;
+        else k[j] = i < n ? rs_load_key(kin + i) : ~0ull;
         v[j] = (VALS && i < n) ? vin[i] : 0u;
     }
 #pragma unroll
@@ -472,23 +474,24 @@ size_t radix_sort_temp_bytes(uint64_t n) {  // (the smallest tile: the most tile
 }
 
 // one key-only pass at RS_ITEMS keys per lane-slot of a tile
-template <int RS_ITEMS>
+template <int RS_ITEMS, bool GEN = false>
 static hipError_t rs_pass_keys(const uint64_t *kin, uint64_t *kout, uint64_t n, int shift, uint32_t *hist,
-                               void *stmp, hipStream_t s) {
+                               void *stmp, hipStream_t s, const KeyGen &kg = KeyGen{}) {
     using SK = RsShared<false, RsTile<RS_ITEMS>::TILE, RsDown<RS_ITEMS>::WAVES>;
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void *)rs_downsweep_kernel<false, RS_ITEMS>,
+        (void)hipFuncSetAttribute((const void *)rs_downsweep_kernel<false, RS_ITEMS, GEN>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(SK));
         attr_set = true;
     }
     const uint64_t nb = (n + RsTile<RS_ITEMS>::TILE - 1) / RsTile<RS_ITEMS>::TILE;
-    hipLaunchKernelGGL((rs_upsweep_kernel<RS_ITEMS>), dim3((uint32_t)nb), dim3(RsUp<RS_ITEMS>::THREADS), 0, s, kin, n,
-                       shift, hist, (uint32_t)nb);
+    hipLaunchKernelGGL((rs_upsweep_kernel<RS_ITEMS, GEN>), dim3((uint32_t)nb), dim3(RsUp<RS_ITEMS>::THREADS), 0, s,
+                       kin, n, shift, hist, (uint32_t)nb, kg);
     hipError_t e = rs_offsets(hist, nb, stmp, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((rs_downsweep_kernel<false, RS_ITEMS>), dim3((uint32_t)nb), dim3(RsDown<RS_ITEMS>::THREADS),
-                       sizeof(SK), s, kin, nullptr, kout, nullptr, n, shift, (const uint32_t *)hist, (uint32_t)nb);
+    hipLaunchKernelGGL((rs_downsweep_kernel<false, RS_ITEMS, GEN>), dim3((uint32_t)nb),
+                       dim3(RsDown<RS_ITEMS>::THREADS), sizeof(SK), s, kin, nullptr, kout, nullptr, n, shift,
+                       (const uint32_t *)hist, (uint32_t)nb, kg);
     return hipGetLastError();
 }
 
@@ -526,13 +529,40 @@ hipError_t radix_sort(uint64_t **keys, uint32_t **vals, uint64_t **keys_alt, uin
     void *stmp = (void *)(hist + 256 * nb);
     for (int shift = lo; shift < hi; shift += 8) {
         hipLaunchKernelGGL((rs_upsweep_kernel<RS_ITEMS_VALS>), dim3((uint32_t)nb), dim3(RsUp<RS_ITEMS_VALS>::THREADS), 0,
-                           s, *keys, n, shift, hist, (uint32_t)nb);
+                           s, *keys, n, shift, hist, (uint32_t)nb, KeyGen{});
         hipError_t e = rs_offsets(hist, nb, stmp, s);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL((rs_downsweep_kernel<true, RS_ITEMS_VALS>), dim3((uint32_t)nb),
                            dim3(RsDown<RS_ITEMS_VALS>::THREADS), sizeof(SV), s, *keys, *vals, *keys_alt, *vals_alt, n,
-                           shift, (const uint32_t *)hist, (uint32_t)nb);
+                           shift, (const uint32_t *)hist, (uint32_t)nb, KeyGen{});
         uint32_t *tv = *vals; *vals = *vals_alt; *vals_alt = tv;
+        uint64_t *tk = *keys; *keys = *keys_alt; *keys_alt = tk;
+    }
+    return hipGetLastError();
+}
+
+__global__ void gen_keys_kernel(KeyGen g, uint64_t n, uint64_t *keys) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) keys[i] = gen_key(g, i);
+}
+
+hipError_t radix_sort_gen(const KeyGen &g, uint64_t **keys, uint64_t **keys_alt, uint64_t n, int lo, int hi,
+                          void *tmp, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    if (n <= 1 || hi <= lo) {  // nothing to sort: the records as emitted
+        hipLaunchKernelGGL(gen_keys_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, g, n, *keys);
+        return hipGetLastError();
+    }
+    uint32_t *hist = (uint32_t *)tmp;
+    void *stmp = (void *)(hist + 256 * ((n + RsTile<RS_ITEMS_KEYS>::TILE - 1) / RsTile<RS_ITEMS_KEYS>::TILE));
+    // first pass: generated keys -> *keys; the rest as radix_sort
+    hipError_t e = n >= RS_BIG_TILE_KEYS ? rs_pass_keys<2 * RS_ITEMS_KEYS, true>(nullptr, *keys, n, lo, hist, stmp, s, g)
+                                         : rs_pass_keys<RS_ITEMS_KEYS, true>(nullptr, *keys, n, lo, hist, stmp, s, g);
+    if (e != hipSuccess) return e;
+    for (int shift = lo + 8; shift < hi; shift += 8) {
+        e = n >= RS_BIG_TILE_KEYS ? rs_pass_keys<2 * RS_ITEMS_KEYS>(*keys, *keys_alt, n, shift, hist, stmp, s)
+                                  : rs_pass_keys<RS_ITEMS_KEYS>(*keys, *keys_alt, n, shift, hist, stmp, s);
+        if (e != hipSuccess) return e;
         uint64_t *tk = *keys; *keys = *keys_alt; *keys_alt = tk;
     }
     return hipGetLastError();
@@ -554,7 +584,7 @@ hipError_t radix_sort_kv64(uint64_t **keys, uint64_t **vals, uint64_t **keys_alt
     void *stmp = (void *)(hist + 256 * nb);
     for (int shift = lo; shift < hi; shift += 8) {
         hipLaunchKernelGGL((rs_upsweep_kernel<RS_ITEMS_KV>), dim3((uint32_t)nb), dim3(RsUp<RS_ITEMS_KV>::THREADS), 0,
-                           s, *keys, n, shift, hist, (uint32_t)nb);
+                           s, *keys, n, shift, hist, (uint32_t)nb, KeyGen{});
         hipError_t e = rs_offsets(hist, nb, stmp, s);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(rs_downsweep_kv64_kernel, dim3((uint32_t)nb), dim3(RS_THREADS), sizeof(RsSharedKV), s,

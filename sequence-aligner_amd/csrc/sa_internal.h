@@ -69,6 +69,23 @@ __device__ __forceinline__ uint32_t kmer_mix(const uint32_t *w, int32_t p, int s
     return mix32(x);
 }
 
+// The k-mer records of uniform-length reads (read r's packed words at
+// codes + r * nw, npr k-mers each), generated where a sort pass would load them:
+// record i = mix32(seqHash) << 32 | i, exactly what pack_emit_kernel stores at
+// keys[i] (radix_sort_gen)
+struct KeyGen {
+    const uint32_t *codes;
+    uint32_t nw;               // packed words per read
+    uint32_t npr;              // k-mers per read (>= 1)
+    uint64_t npr_magic;        // floor((2^64 - 1) / npr) + 1 (npr >= 2)
+    int shift;                 // 32 - 2 min(16, k)
+};
+__device__ __forceinline__ uint64_t gen_key(const KeyGen &g, uint64_t i) {
+    const uint32_t r = g.npr == 1 ? (uint32_t)i : (uint32_t)__umul64hi((unsigned long long)i, g.npr_magic);
+    const int32_t pos = (int32_t)((uint32_t)i - r * g.npr);
+    return ((uint64_t)kmer_mix(g.codes + (uint64_t)r * g.nw, pos, g.shift) << 32) | (uint32_t)i;
+}
+
 // Inclusive add-scan over the 64 lanes of a wave in DPP moves (row_shr 1, 2, 4,
 // 8 within each row of 16, then row_bcast 15 / 31 across rows): VALU only, where
 // a __shfl_up ladder is six dependent ds_bpermute round trips through the LDS
@@ -295,6 +312,11 @@ size_t radix_sort_temp_bytes(uint64_t n);
 hipError_t radix_sort(uint64_t **keys, uint32_t **vals, uint64_t **keys_alt, uint32_t **vals_alt,
                       uint64_t n, int lo, int hi, void *tmp, hipStream_t s);
 // the same with 64-bit values (16-byte records)
+// radix_sort (key-only) of the n records KeyGen g describes: the first pass
+// generates its keys instead of loading them (the records are never written
+// unsorted); result in *keys
+hipError_t radix_sort_gen(const KeyGen &g, uint64_t **keys, uint64_t **keys_alt, uint64_t n, int lo, int hi,
+                          void *tmp, hipStream_t s);
 hipError_t radix_sort_kv64(uint64_t **keys, uint64_t **vals, uint64_t **keys_alt, uint64_t **vals_alt, uint64_t n,
                            int lo, int hi, void *tmp, hipStream_t s);
 
