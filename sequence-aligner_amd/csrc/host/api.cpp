@@ -482,6 +482,33 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
         PA.mid_list = biglist + nparts + 1; PA.mid_n = &cnt->mid_n;
         PA.mid2_list = biglist + 2 * ((size_t)nparts + 1); PA.mid2_n = &cnt->mid2_n;
         PA.counts = cnt->bkt_counts;
+#ifdef SA_PB_PROBE_DUP
+        {   // bandwidth probe builds: a second record array the bucket build also scatters to
+            static uint2 *dup = nullptr;
+            static uint64_t dup_n = 0;
+            if (dup_n < n + 1) {
+                if (dup) (void)hipFree(dup);
+                HIPCHK(hipMalloc(&dup, (n + 1) * sizeof(uint2)));
+                dup_n = n + 1;
+            }
+            PA.rec_dup = dup;
+        }
+#endif
+#ifdef SA_PB_STAMPS
+        {   // timing probe builds: SA_PB_STAMPS_OUT=<path> gets the last build's stamps
+            static uint64_t *stamps = nullptr;
+            static uint32_t stamps_np = 0;
+            if (stamps_np < nparts) {
+                if (stamps) (void)hipFree(stamps);
+                HIPCHK(hipMalloc(&stamps, 8 * sizeof(uint64_t) * nparts));
+                stamps_np = nparts;
+            }
+            HIPCHK(hipMemsetAsync(stamps, 0, 8 * sizeof(uint64_t) * nparts, c->stream));
+            PA.stamps = stamps;
+            c->stamps_dev = stamps;
+            c->stamps_np = nparts;
+        }
+#endif
         if (strict) {
             ENSURE(c->d_mdidx, 3 * n + 3, &PA.lidx);
             ENSURE(c->d_srec, n + 1, &PA.srec);
@@ -508,6 +535,17 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
             HIPCHK(launch_part_build(PA, strict, 1024, c->stream));
             HIPCHK(join_side(c, c->ev_join2));
         }
+#ifdef SA_PB_STAMPS
+        if (const char *path = getenv("SA_PB_STAMPS_OUT")) {
+            std::vector<uint64_t> h(8 * (size_t)c->stamps_np);
+            HIPCHK(hipMemcpyAsync(h.data(), c->stamps_dev, h.size() * 8, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            if (FILE *f = fopen(path, "wb")) {
+                fwrite(h.data(), 8, h.size(), f);
+                fclose(f);
+            }
+        }
+#endif
         if (phase == 1) return SA_OK;
     }
     uint32_t big_n = 0;

@@ -135,6 +135,10 @@ struct sa_ctx {
     int aligner = SA_ALIGNER_LINEAR;  // SA_OPT_ALIGNER (--linear-align / --quadratic-align)
     uint64_t local_batch_bytes = 16ull << 30;  // traceback-code budget of one quadratic launch
     bool built = false, aligned = false;
+#ifdef SA_PB_STAMPS
+    uint64_t *stamps_dev = nullptr;  // (timing probe builds, partition.hip PB_STAMP)
+    uint32_t stamps_np = 0;
+#endif
     bool host_valid = false;  // alns / ovl hold the last alignment's results (sa_align or first use)
     // results (host)
     std::vector<int32_t> lead, trail, count;

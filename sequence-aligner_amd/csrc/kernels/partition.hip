@@ -213,6 +213,17 @@ __device__ __forceinline__ void part_load(const PartArgs &A, const uint32_t p, P
     }
 }
 
+// timing probe builds (make OUT=build_stamps EXTRA=-DSA_PB_STAMPS=1): thread 0
+// of each main-pass block records wall_clock64() at its phase boundaries
+#ifdef SA_PB_STAMPS
+#define PB_STAMP(A, p, i)                                                              \
+    do {                                                                               \
+        if (CAP == 1024 && threadIdx.x == 0 && (A).stamps) (A).stamps[8 * (uint64_t)(p) + (i)] = wall_clock64(); \
+    } while (0)
+#else
+#define PB_STAMP(A, p, i) do { } while (0)
+#endif
+
 template <int CAP, bool STRICT>
 __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t p, PartShared<CAP> &S,
                                                uint32_t *Sr, const PartLoad<CAP> &L) {
@@ -256,7 +267,9 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
         }
     }
     __syncthreads();
+    PB_STAMP(A, p, 1);
     lds_radix_sort<CAP>(S, n, A.sort_bits);
+    PB_STAMP(A, p, 2);
     // ---- per-thread contiguous items: flags and local aggregates -----------
     const int lb = A.lb;
     const unsigned long long lbm = (1ull << lb) - 1;
@@ -341,6 +354,7 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
         if (b0 + IT == (uint32_t)CAP && n == (uint32_t)CAP) { S.mdx[CAP] = m; S.edx[CAP] = e; }
     }
     __syncthreads();
+    PB_STAMP(A, p, 3);
     // next group head and next bucket head per item (suffix within the thread,
     // then gh_next / bh_next)
     uint32_t nextg[IT], nextb[IT];
@@ -356,6 +370,21 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
         }
     }
     // ---- outputs --------------------------------------------------------
+    // The partition's list slice [3 ps, 3 ps + ltot) is assembled in LDS (the
+    // key array is free once the heads are found; 2 CAP words hold any default
+    // tag layout, <= 2 entries per record) and leaves as coalesced non-temporal
+    // stores: the ~230 MB of lists then stay out of the 256 MB MALL, which is
+    // left to merge the records' scattered 8-byte stores (389 MB at the bench).
+    // Same box (profiles/r04/ab/ab_lst_staged_nt.txt): bucket build 1.32 ->
+    // 1.20 ms; staged with plain stores 1.32 (SA_LST_STAGE A/B: 0 direct
+    // scattered stores, 1 staged, 2 staged + non-temporal)
+#ifndef SA_LST_STAGE
+#define SA_LST_STAGE 2
+#endif
+    uint32_t *stg = reinterpret_cast<uint32_t *>(S.key);
+    const uint32_t ltot = S.mdx[n] + S.edx[n];
+    const bool staged = SA_LST_STAGE && !STRICT && ltot <= 2u * (uint32_t)CAP;
+    const uint64_t lbase = 3ull * ps;
     uint32_t bh = bh_in, gh = gh_in;
 #pragma unroll
     for (int j = 0; j < IT; ++j) {
@@ -379,13 +408,22 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
         // split point of the bucket [bh, nextb): its md entries end at c
         const uint64_t c = 3ull * ps + S.mdx[nextb[j]] + S.edx[bh];
         const uint64_t mpos = c - 1u - (S.mdx[s] - S.mdx[bh]), epos = c + (S.edx[s] - S.edx[bh]);
-        if (md) A.lst[mpos] = r;
-        if (st) A.lst[epos] = r;
-        if (en) A.lst[epos + st] = r;
+        if (staged) {
+            if (md) stg[mpos - lbase] = r;
+            if (st) stg[epos - lbase] = r;
+            if (en) stg[epos + st - lbase] = r;
+        } else {
+            if (md) A.lst[mpos] = r;
+            if (st) A.lst[epos] = r;
+            if (en) A.lst[epos + st] = r;
+        }
         const uint32_t me = st + en;
         const uint32_t nE = me ? (S.mdx[gh] - S.mdx[bh]) : 0u;        // <= CAP: no escape here
         const uint32_t nD = md ? (S.edx[nextg[j]] - S.edx[bh]) : 0u;  // <= 2 CAP
         A.rec[g] = encode_rec(c, nE, nD, me);
+#ifdef SA_PB_PROBE_DUP
+        if (A.rec_dup) A.rec_dup[g] = encode_rec(c, nE, nD, me);  // (probe: twice the scattered stores)
+#endif
         if constexpr (STRICT) {
             // bucket extent [bh, be)
             const unsigned long long k = S.key[s];
@@ -416,6 +454,17 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
             }
         }
     }
+    if (staged) {
+        __syncthreads();
+        for (uint32_t i = tid; i < ltot; i += NT) {
+            if (SA_LST_STAGE == 2) __builtin_nontemporal_store(stg[i], A.lst + lbase + i);
+            else A.lst[lbase + i] = stg[i];
+        }
+    }
+    PB_STAMP(A, p, 4);
+#ifdef SA_PB_STAMPS
+    if (CAP == 1024 && tid == 0 && A.stamps) A.stamps[8 * (uint64_t)p + 5] = (uint64_t)__smid() | ((uint64_t)n << 32);
+#endif
     // bucket / group counts for statistics (block totals of the combined scan), sharded
     if (tid == 0) {
         atomicAdd(&A.counts[p % NSHARD], (unsigned long long)(blk_heads & 0xFFFFu));
@@ -438,6 +487,7 @@ __global__ __launch_bounds__(PbShape<CAP>::NT) void part_build_kernel(PartArgs A
         // records loading while the first is built, measured no faster: 1.32 ms
         // either way, profiles/r04/ab/ab_tier_order_pair_build.txt)
         PartLoad<CAP> L;
+        PB_STAMP(A, blockIdx.x, 0);
         part_load<CAP>(A, blockIdx.x, L);
         part_build_one<CAP, STRICT>(A, blockIdx.x, S, Sr, L);
     } else {

@@ -360,6 +360,12 @@ struct PartArgs {
     uint32_t np;
     int lb;
     int sort_bits;               // key bits below the partition id (sorted in LDS)
+#ifdef SA_PB_STAMPS
+    uint64_t *stamps;            // (timing probe builds: 8 words per partition of the main pass)
+#endif
+#ifdef SA_PB_PROBE_DUP
+    uint2 *rec_dup;              // (bandwidth probe builds: every record stored a second time here)
+#endif
     const uint8_t *tagtab;
     const uint64_t *occ_off;
     uint32_t n_reads, npr;
