@@ -450,7 +450,9 @@ def main():
     # the bucket build runs in one of two per-process modes at the bench shape
     # ("Bucket-build bimodality"): say which one this line hit
     if tag == DEFAULT_WORKLOAD:
-        roofline["bucket_build_mode"] = "slow (> 1.2 ms)" if per_launch("buckets") > 1.2 else "fast (<= 1.2 ms)"
+        # (round 4: the slow mode moved from 1.31-1.33 to 1.19-1.21 ms with the
+        # lists written non-temporally; the fast mode was 1.05-1.15 before that)
+        roofline["bucket_build_mode"] = "slow (> 1.1 ms)" if per_launch("buckets") > 1.1 else "fast (<= 1.1 ms)"
     # the first pair-count pass: one wave per read (round 3; wide ids, per-read regions), or
     # the one-read workgroup kernel in profiles of earlier trees / other modes
     pc_k = ("sa::pair_count_wave_kernel",) if any(k.startswith("sa::pair_count_wave_kernel") for k in rows) \
