@@ -347,7 +347,10 @@ int ensure_prepared(sa_ctx *c) {
 static bool make_keygen(const sa_ctx *c, const EmitParams &E, uint64_t n, KeyGen &kg) {
     static const bool env_on = !getenv("SA_KEYGEN") || atoi(getenv("SA_KEYGEN")) != 0;
     const size_t nr = c->woff.empty() ? 0 : c->woff.size() - 1;
-    if (!env_on || !E.npr || E.pos_bits || E.occ_rl || nr == 0 || n >= (1ull << 32)) return false;
+    // (up to 2^27 records: at configs[3]'s slice, 607.5M records, generating the
+    // first pass's keys twice -- upsweep and downsweep -- cost more than storing
+    // them: hash step 48.4 -> 49.1 ms, profiles/r04/ab/ab_c3_keygen_vs_old.txt)
+    if (!env_on || !E.npr || E.pos_bits || E.occ_rl || nr == 0 || n >= (1ull << 27)) return false;
     const uint64_t nw = c->woff[1] - c->woff[0];
     for (size_t r = 1; r < nr; ++r)
         if (c->woff[r + 1] - c->woff[r] != nw) return false;
