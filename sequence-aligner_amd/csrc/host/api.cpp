@@ -430,7 +430,7 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
     const uint32_t *spv = nullptr;
     uint32_t *pstart, *biglist;
     ENSURE(c->d_pstart, nparts + 1, &pstart);
-    ENSURE(c->d_biglist, 3 * ((size_t)nparts + 1), &biglist);  // big list, mid list, mid2 list
+    ENSURE(c->d_biglist, 4 * ((size_t)nparts + 1), &biglist);  // big list, mid list, mid2 list, fb list
     const uint8_t *tagtab = (const uint8_t *)c->d_tagtab.p;
     if (phase != 2) {
         {
@@ -484,6 +484,9 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
         PA.big_list = biglist; PA.big_n = &cnt->big_n;
         PA.mid_list = biglist + nparts + 1; PA.mid_n = &cnt->mid_n;
         PA.mid2_list = biglist + 2 * ((size_t)nparts + 1); PA.mid2_n = &cnt->mid2_n;
+        PA.fb_list = biglist + 3 * ((size_t)nparts + 1); PA.fb_n = &cnt->fb_n;
+        static const bool split_env = !getenv("SA_SPLIT_TIER") || atoi(getenv("SA_SPLIT_TIER")) != 0;  // (A/B)
+        PA.split = split_env && !strict && !srl && !spv ? 1 : 0;
         PA.counts = cnt->bkt_counts;
 #ifdef SA_PB_PROBE_DUP
         {   // bandwidth probe builds: a second record array the bucket build also scatters to
@@ -522,7 +525,7 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
             ENSURE(c->d_brank, n + 1, &c->bkt_rank_dev);
             HIPCHK(hipMemsetAsync(PA.is_head, 0, n + 1, c->stream));
         }
-        HIPCHK(hipMemsetAsync(&cnt->mid_n, 0, 2 * sizeof(uint32_t), c->stream));  // mid_n, mid2_n
+        HIPCHK(hipMemsetAsync(&cnt->mid_n, 0, 3 * sizeof(uint32_t), c->stream));  // mid_n, mid2_n, fb_n
         {
             // the bounds kernel lists the partitions above 1,024 records; their
             // 2,048 / 4,096-record tiers (~1 % of partitions, a few blocks' latency)
@@ -533,6 +536,7 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
             HIPCHK(fork_side(c, c->ev_fork2));
             // (the same tiers in line on one stream, before or after the main
             // pass, measured the same: profiles/r04/ab/ab_tier_order_pair_build.txt)
+            if (PA.split) HIPCHK(launch_part_build(PA, strict, 1, c->side));  // (then 2,048: fb_list only)
             HIPCHK(launch_part_build(PA, strict, 2048, c->side));
             HIPCHK(launch_part_build(PA, strict, 4096, c->side));
             HIPCHK(launch_part_build(PA, strict, 1024, c->stream));

@@ -35,6 +35,7 @@ struct Counters {
     uint32_t big_n;
     uint32_t mid_n;
     uint32_t mid2_n;
+    uint32_t fb_n;   // (split tier) partitions whose halves do not fit 1,024 records
     uint32_t xrec_n;     // escape records written (big partitions)
     uint32_t rtotal;     // per-read pair mode: dispatched pairs (scan total)
     uint32_t shard_off[NSHARD + 2];

@@ -89,6 +89,7 @@ __device__ __forceinline__ unsigned long long record_key(uint64_t rec, const Par
 // latency is set by its chain of LDS passes and barriers, nearly the same for
 // any CAP at 4 items per thread, so bigger partitions spread that chain over
 // more records.
+constexpr uint32_t SPLIT_MAX = 2048;  // partitions the split tier takes (grid 2 SPLIT_MAX)
 template <int CAP> struct PbShape {
     static constexpr int NT = CAP / 4, WAVES = NT / 64, IT = 4;
 };
@@ -494,14 +495,96 @@ __global__ __launch_bounds__(PbShape<CAP>::NT) void part_build_kernel(PartArgs A
         part_load<CAP>(A, blockIdx.x, L);
         part_build_one<CAP, STRICT>(A, blockIdx.x, S, Sr, L);
     } else {
-        const uint32_t *list = CAP >= 4096 ? A.mid2_list : A.mid_list;
-        const uint32_t m = *(CAP >= 4096 ? A.mid2_n : A.mid_n);
-        for (uint32_t i = blockIdx.x; i < m; i += gridDim.x) {
+        // (split tier: the partitions it handed on, then the mid-list entries past its grid)
+        const bool fb = CAP < 4096 && A.split;
+        const uint32_t *list = CAP >= 4096 ? A.mid2_list : (fb ? A.fb_list : A.mid_list);
+        const uint32_t m0 = *(CAP >= 4096 ? A.mid2_n : (fb ? A.fb_n : A.mid_n));
+        const uint32_t mid = fb ? *A.mid_n : 0u, extra = mid > SPLIT_MAX ? mid - SPLIT_MAX : 0u;
+        for (uint32_t i = blockIdx.x; i < m0 + extra; i += gridDim.x) {
             __syncthreads();  // LDS of the previous partition fully consumed
+            const uint32_t p = i < m0 ? list[i] : A.mid_list[SPLIT_MAX + (i - m0)];
             PartLoad<CAP> L;
-            part_load<CAP>(A, list[i], L);
-            part_build_one<CAP, STRICT>(A, list[i], S, Sr, L);
+            part_load<CAP>(A, p, L);
+            part_build_one<CAP, STRICT>(A, p, S, Sr, L);
         }
+    }
+}
+
+// The split tier (PartArgs::split): a partition of 1,025-2,048 records is built
+// as two halves -- the next hash bit below the partition id, so every bucket
+// stays whole in one half -- by two 1,024-record blocks, each loading the whole
+// partition and keeping its half in load order (one block scan).  Half h's list
+// slice starts at 3 (ps + h n0).  These blocks have the main pass's shape and
+// interleave with it; the 2,048-record blocks they replace (8 waves, 37 KB of
+// LDS, ~650 partitions at the bench shape) were starved beside the main pass and
+// then crowded its last ~200 us (profiles/r04/pb_stamps.txt).  Partitions whose
+// halves do not fit 1,024 records go to the 2,048-record pass (fb_list), those
+// above 2,048 to the 4,096-record pass.
+#ifndef SA_SPLIT_MIN_WAVES
+#define SA_SPLIT_MIN_WAVES 6  // per SIMD: <= 80 VGPRs, near the main pass's 7
+#endif
+__global__ __launch_bounds__(PbShape<1024>::NT, SA_SPLIT_MIN_WAVES) void part_split_kernel(PartArgs A) {
+    constexpr int CAP = 1024, NT = PbShape<CAP>::NT, IT = PbShape<CAP>::IT, R = 2 * CAP / NT;
+    extern __shared__ __align__(16) uint8_t smem_raw[];
+    PartShared<CAP> &S = *reinterpret_cast<PartShared<CAP> *>(smem_raw);
+    uint32_t *Sr = A.rl || A.pv ? reinterpret_cast<uint32_t *>(smem_raw + sizeof(PartShared<CAP>)) : nullptr;
+    __shared__ uint32_t wtot[NT / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t m = min(*A.mid_n, SPLIT_MAX);  // (the 2,048-record pass takes the rest)
+    const int hbit = 31 + A.sort_bits - A.lb;  // the record bit under the partition id
+    const uint32_t item = blockIdx.x;  // one half per block (no loop: a loop around the
+    if (item < 2 * m) {                // build keeps the arguments live, ~120 VGPRs)
+        const uint32_t p = A.mid_list[item >> 1], h = item & 1u;
+        const uint32_t ps = A.start[p], n = A.start[p + 1] - ps;
+        if (n > 2u * CAP) {  // the 4,096-record pass (or the global path)
+            if (h == 0 && tid == 0) A.mid2_list[atomicAdd(A.mid2_n, 1u)] = p;
+            return;
+        }
+        // records tid * R .. tid * R + R - 1: counted, then read again (L2) to stage
+        uint32_t c0 = 0, ch = 0;
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const uint32_t i = tid * R + j;
+            const uint64_t r = i < n ? A.sk[ps + i] : 0ull;
+            const uint32_t b = (uint32_t)(r >> hbit) & 1u;
+            c0 += (i < n && b == 0) ? 1u : 0u;
+            ch += (i < n && b == h) ? 1u : 0u;
+        }
+        const uint32_t v = c0 | (ch << 16);  // (counts <= 2,048)
+        const uint32_t inc = wave_incl_add(v);
+        if (lane == 63) wtot[wv] = inc;
+        __syncthreads();
+        uint32_t pre = 0, tot = 0;
+#pragma unroll
+        for (int q = 0; q < NT / 64; ++q) {
+            const uint32_t x = wtot[q];
+            if (q < wv) pre += x;
+            tot += x;
+        }
+        const uint32_t n0 = tot & 0xFFFFu, nh = h ? n - n0 : n0;
+        if (n0 > (uint32_t)CAP || n - n0 > (uint32_t)CAP) {  // a half too large: the 2,048-record pass
+            if (h == 0 && tid == 0) A.fb_list[atomicAdd(A.fb_n, 1u)] = p;
+            return;
+        }
+        // the half in load order, staged in the key array, then in part_load's layout
+        uint32_t pos = (pre + inc - v) >> 16;
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const uint32_t i = tid * R + j;
+            const uint64_t r = i < n ? A.sk[ps + i] : 0ull;
+            if (i < n && ((uint32_t)(r >> hbit) & 1u) == h) S.key[pos++] = r;
+        }
+        __syncthreads();
+        PartLoad<CAP> L;
+        L.ps = ps + (h ? n0 : 0u);
+        L.n = nh;
+#pragma unroll
+        for (int j = 0; j < IT; ++j) {
+            const uint32_t i = tid + j * NT;
+            L.recs[j] = S.key[i < nh ? i : (nh ? nh - 1 : 0u)];
+        }
+        __syncthreads();  // staging read before part_build_one reuses the key array
+        part_build_one<CAP, false>(A, p, S, Sr, L);
     }
 }
 
@@ -636,7 +719,13 @@ hipError_t launch_part_build(const PartArgs &a, bool strict, int cap, hipStream_
         hipLaunchKernelGGL((part_build_kernel<CAPV, ST, MAINV>), dim3(GRID), dim3(PbShape<CAPV>::NT), lds, s, a); \
     } while (0)
     const uint32_t mid_grid = a.np < 1024u ? a.np : 1024u;
-    if (cap == 1024) {
+    if (cap == 1) {  // the split tier (non-strict, records without sorted values)
+        const size_t lds = part_lds<1024>() + (a.rl || a.pv ? 4 * (size_t)1024 : 0);
+        (void)hipFuncSetAttribute((const void *)part_split_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        hipLaunchKernelGGL(part_split_kernel, dim3(2 * (a.np < SPLIT_MAX ? a.np : SPLIT_MAX)), dim3(PbShape<1024>::NT),
+                           lds, s, a);
+    } else if (cap == 1024) {
         if (strict) PB_LAUNCH(1024, a.np, true, true); else PB_LAUNCH(1024, a.np, false, true);
     } else if (cap == 2048) {
         if (strict) PB_LAUNCH(2048, mid_grid, true, false); else PB_LAUNCH(2048, mid_grid, false, false);

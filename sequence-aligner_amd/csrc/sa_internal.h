@@ -402,6 +402,11 @@ struct PartArgs {
     uint32_t *big_list, *big_n;  // partitions above 4,096 records (global path)
     uint32_t *mid_list, *mid_n;    // partitions above 1,024 records (2,048-record LDS pass)
     uint32_t *mid2_list, *mid2_n;  // partitions above 2,048 records (4,096-record LDS pass)
+    // split tier (split = 1): the partitions of 1,025-2,048 records are built as two
+    // halves by the next hash bit by 1,024-record blocks; the ones whose halves do
+    // not fit go to the 2,048-record pass through fb_list
+    uint32_t *fb_list, *fb_n;
+    int32_t split;
     unsigned long long *counts;  // [2][NSHARD]: buckets, groups
     // strict
     uint32_t *lidx;              // parallel to lst
