@@ -441,12 +441,14 @@ def main():
         return ms_ / max(n_, 1)
 
     # dominant kernel by time: the bucket build (part_bounds + part_build at the
-    # 1,024 / 2,048 / 4,096-record tiers, one HIP-event scope on the library's
-    # stream); 16 B per k-mer in the model
+    # 1,024 / 2,048 / 4,096-record tiers + the split tier, one HIP-event scope on
+    # the library's stream); 16 B per k-mer in the model
     bk_kernels = ("sa::part_bounds_kernel", "void sa::part_build_kernel<1024", "void sa::part_build_kernel<2048",
                   "void sa::part_build_kernel<4096")
+    if any(k.startswith("sa::part_split_kernel") for k in rows):  # (summaries of trees with the split tier)
+        bk_kernels += ("sa::part_split_kernel",)
     roofline = roof(16.0 * kmers_g, per_launch("buckets"), bk_kernels,
-                    "bucket build: part_bounds + part_build<1024|2048|4096>")
+                    "bucket build: part_bounds + part_build<1024|2048|4096> + part_split")
     # the bucket build runs in one of two per-process modes at the bench shape
     # ("Bucket-build bimodality"): say which one this line hit
     if tag == DEFAULT_WORKLOAD:
