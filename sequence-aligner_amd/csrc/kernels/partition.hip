@@ -382,12 +382,9 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
 #ifndef SA_LST_STAGE
 #define SA_LST_STAGE 2
 #endif
-#ifndef SA_LST_STAGE_TIERS
-#define SA_LST_STAGE_TIERS 1  // (A/B builds: 0 = the 2,048 / 4,096 tiers store directly)
-#endif
     uint32_t *stg = reinterpret_cast<uint32_t *>(S.key);
     const uint32_t ltot = S.mdx[n] + S.edx[n];
-    const bool staged = SA_LST_STAGE && !STRICT && (SA_LST_STAGE_TIERS || CAP == 1024) && ltot <= 2u * (uint32_t)CAP;
+    const bool staged = SA_LST_STAGE && !STRICT && ltot <= 2u * (uint32_t)CAP;
     const uint64_t lbase = 3ull * ps;
     uint32_t bh = bh_in, gh = gh_in;
 #pragma unroll
