@@ -525,7 +525,8 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
             ENSURE(c->d_brank, n + 1, &c->bkt_rank_dev);
             HIPCHK(hipMemsetAsync(PA.is_head, 0, n + 1, c->stream));
         }
-        HIPCHK(hipMemsetAsync(&cnt->mid_n, 0, 3 * sizeof(uint32_t), c->stream));  // mid_n, mid2_n, fb_n
+        if (!c->counters_fresh)  // (a fresh Counters block is all zero already)
+            HIPCHK(hipMemsetAsync(&cnt->mid_n, 0, 3 * sizeof(uint32_t), c->stream));  // mid_n, mid2_n, fb_n
         {
             // the bounds kernel lists the partitions above 1,024 records; their
             // 2,048 / 4,096-record tiers (~1 % of partitions, a few blocks' latency)
@@ -703,8 +704,11 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
         O.rcnt = rcnt;
         // (cursor, role pairs, dummy, distinct: a pass re-run after an abort or
         // in the shared-region mode counts from zero)
-        HIPCHK(hipMemsetAsync(cnt->cursor, 0, 4 * NSHARD * sizeof(unsigned long long), c->stream));
-        HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(uint32_t), c->stream));
+        if (!c->counters_fresh) {  // (the first pass after the build's Counters clear skips these)
+            HIPCHK(hipMemsetAsync(cnt->cursor, 0, 4 * NSHARD * sizeof(unsigned long long), c->stream));
+            HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(uint32_t), c->stream));
+        }
+        c->counters_fresh = false;
         {
             StageScope st(c, SA_STAGE_PAIRS);
             if (item_start) {  // multi-read blocks (sharded path)
@@ -955,6 +959,7 @@ int device_build(sa_ctx *c, bool readback) {
     Counters *cnt;
     ENSURE(c->d_cnt, 1, &cnt);
     HIPCHK(hipMemsetAsync(cnt, 0, sizeof(Counters), c->stream));
+    c->counters_fresh = true;
 
     uint64_t *keys, *keys2; uint32_t *vals, *vals2; void *stmp;
     ENSURE(c->d_keys, n, &keys);
@@ -1989,6 +1994,7 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint6
     Counters *cnt;
     ENSURE(c->d_cnt, 1, &cnt);
     HIPCHK(hipMemsetAsync(cnt, 0, sizeof(Counters), c->stream));
+    c->counters_fresh = true;
     // received records are in global occurrence order (sources in rank order,
     // each in occurrence order): local index i <-> i-th owned occurrence
     uint2 *rl; uint32_t *vals, *vals2; uint64_t *loff, *keys2, *dseg; uint8_t *stmp;
