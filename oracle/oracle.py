@@ -74,6 +74,10 @@ def lib():
         L.orc_align_batch.argtypes = [C.c_char_p, P(C.c_uint64), C.c_uint32, P(C.c_int32), P(C.c_int32), C.c_size_t,
                                       P(Settings), C.c_int, P(Align)]
         L.orc_max_threads.restype = C.c_int
+        L.orc_lead_rows.argtypes = [C.c_char_p, P(C.c_uint64), C.c_uint32, P(Settings), P(C.c_int32), C.c_size_t,
+                                    C.c_int, P(C.c_uint64), P(P(C.c_int32)), P(P(C.c_int32))]
+        L.orc_free.argtypes = [C.c_void_p]
+        L.orc_free.restype = None
         _lib = L
     return _lib
 
@@ -203,6 +207,28 @@ def align_batch(bases, offsets, lead, trail, settings=None, threads=1):
         raise OracleError(rc)
     raw = np.ctypeslib.as_array(C.cast(out, P(C.c_int32)), shape=(max(len(ld), 1) * len(ALIGN_FIELDS),))
     return raw.reshape(-1, len(ALIGN_FIELDS))[:len(ld)].copy()
+
+
+def lead_rows(bases, offsets, leads, settings=None, threads=0):
+    """PairData rows of the sampled leads (orc_lead_rows): returns (row_off,
+    snd, cnt) with lead leads[i]'s partners (ascending) and counts in
+    [row_off[i], row_off[i + 1]).  leads: 1-based, strictly ascending."""
+    s = settings or default_settings()
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ld = np.ascontiguousarray(leads, dtype=np.int32)
+    ro = np.zeros(len(ld) + 1, dtype=np.uint64)
+    sp, cp = C.POINTER(C.c_int32)(), C.POINTER(C.c_int32)()
+    P = C.POINTER
+    rc = lib().orc_lead_rows(bases, off.ctypes.data_as(P(C.c_uint64)), len(off) - 1, C.byref(s),
+                             ld.ctypes.data_as(P(C.c_int32)), len(ld), threads, ro.ctypes.data_as(P(C.c_uint64)),
+                             C.byref(sp), C.byref(cp))
+    if rc:
+        raise OracleError(rc)
+    n = int(ro[-1])
+    snd, cnt = _arr(sp, n, np.int32), _arr(cp, n, np.int32)
+    lib().orc_free(C.cast(sp, C.c_void_p))
+    lib().orc_free(C.cast(cp, C.c_void_p))
+    return ro.astype(np.int64), snd, cnt
 
 
 def max_threads():

@@ -1137,6 +1137,203 @@ out:
     return rc;
 }
 
+/* ------------------------------------------------------------------------ */
+/* sampled-lead PairData rows: the checker for read sets whose whole PairData  */
+/* does not fit host memory (configs[4]'s 6.25M-read slice at k = 12 has      */
+/* 1.5e11 distinct pairs).  For every sampled lead r, every PairData entry     */
+/* (r, snd, count) of calcPairData (KmerTable.scala:85-149) whose fst is r,   */
+/* with addKmerPair's orientation (:57-80: fst = the occurrence with the       */
+/* larger loc, tie -> the middle one; same-read pairs skipped; every st x md   */
+/* and en x md occurrence pair counts once).  Only the buckets of r's k-mers   */
+/* can hold such a pair, so:                                                   */
+/*   pass 1  the seqHashes of the sampled leads' k-mers (a bitmap over the     */
+/*           2 * min(k, 16)-bit hash space, ObjectStore.scala:48-67)            */
+/*   pass 2  every read streamed; occurrences in those buckets kept as          */
+/*           (read, pos), grouped by hash (counting sort)                       */
+/*   rows    per lead (OpenMP over leads), per occurrence o of r in bucket B:  */
+/*           o edge (st / en, once per role) x every middle e of B with         */
+/*           loc(o) > loc(e)  -> (r, read(e)); o middle x every edge role of    */
+/*           e in B with loc(e) <= loc(o) -> (r, read(e)).  A role pair whose   */
+/*           fst is r is exactly one of these (orc_run's loop, :1024-1037).     */
+/* Memory is the sampled buckets, not the pairs of the whole read set.         */
+/* ------------------------------------------------------------------------ */
+static int cmp_i32(const void *a, const void *b) {
+    const int32_t x = *(const int32_t *)a, y = *(const int32_t *)b;
+    return (x > y) - (x < y);
+}
+static inline uint32_t hash_code(char ch) { /* Kmer.seqHash codes: A0 C1 T2 G3, others 0 */
+    if (ch >= 'a' && ch <= 'z') ch = (char)(ch - 32);
+    return ch == 'C' ? 1u : ch == 'T' ? 2u : ch == 'G' ? 3u : 0u;
+}
+
+/* seqHash of every k-mer of one read, rolling (== seq_hash(sq + i, k)) */
+static void read_hashes(const char *sq, int64_t L, int k, uint32_t *out) {
+    const int w = k < 16 ? k : 16;
+    const uint32_t mask = w == 16 ? 0xffffffffu : ((1u << (2 * w)) - 1u);
+    uint32_t h = 0;
+    for (int i = 0; i < w - 1 && i < L; i++) h = (h << 2) | hash_code(sq[i]);
+    for (int64_t i = 0; i + k <= L; i++) {
+        h = ((h << 2) | hash_code(sq[i + w - 1])) & mask;
+        out[i] = h;
+    }
+}
+
+int orc_lead_rows(const char *bases, const uint64_t *offsets, uint32_t n, const orc_settings *s,
+                  const int32_t *leads, size_t n_leads, int threads, uint64_t *row_off, int32_t **snd_out,
+                  int32_t **cnt_out) {
+    *snd_out = NULL;
+    *cnt_out = NULL;
+    const int nt = threads > 0 ? threads : orc_max_threads();
+    const int k = s->kmer_size;
+    const int w = k < 16 ? k : 16;
+    const float head = s->kmer_edge, tail = 1.0f - s->kmer_edge;
+    const float midLead = 0.5f - (s->kmer_center * 0.5f), midTail = 0.5f + (s->kmer_center * 0.5f);
+    for (size_t i = 0; i < n_leads; i++)
+        if (leads[i] < 1 || (uint32_t)leads[i] > n || (i && leads[i] <= leads[i - 1])) return ORC_E_INPUT;
+    const uint64_t nbits = 1ull << (2 * w), nwords = nbits / 64;
+    uint64_t *bits = (uint64_t *)calloc(nwords, sizeof(uint64_t));
+    uint32_t *rank = (uint32_t *)malloc((nwords + 1) * sizeof(uint32_t));
+    int64_t maxL = 0;
+    for (uint32_t r = 0; r < n; r++)
+        if ((int64_t)(offsets[r + 1] - offsets[r]) > maxL) maxL = (int64_t)(offsets[r + 1] - offsets[r]);
+    if (!bits || !rank) { free(bits); free(rank); return ORC_E_NOMEM; }
+    /* pass 1: the sampled leads' hashes */
+    {
+        uint32_t *hs = (uint32_t *)malloc(((size_t)maxL + 1) * sizeof(uint32_t));
+        for (size_t i = 0; i < n_leads && hs; i++) {
+            const uint32_t r = (uint32_t)leads[i] - 1u;
+            const int64_t L = (int64_t)(offsets[r + 1] - offsets[r]);
+            read_hashes(bases + offsets[r], L, k, hs);
+            for (int64_t p = 0; p + k <= L; p++) bits[hs[p] >> 6] |= 1ull << (hs[p] & 63);
+        }
+        if (!hs) { free(bits); free(rank); return ORC_E_NOMEM; }
+        free(hs);
+    }
+    uint64_t m = 0;
+    for (uint64_t q = 0; q < nwords; q++) { rank[q] = (uint32_t)m; m += (uint64_t)__builtin_popcountll(bits[q]); }
+    rank[nwords] = (uint32_t)m;
+    /* pass 2: occurrences in those buckets, counted then placed by hash rank */
+    uint64_t *bstart = (uint64_t *)calloc(m + 2, sizeof(uint64_t));
+    if (!bstart) { free(bits); free(rank); return ORC_E_NOMEM; }
+#define HIT_RANK(h) (rank[(h) >> 6] + (uint32_t)__builtin_popcountll(bits[(h) >> 6] & ((1ull << ((h) & 63)) - 1ull)))
+#define IS_HIT(h) ((bits[(h) >> 6] >> ((h) & 63)) & 1ull)
+    int rc = ORC_OK;
+    for (int phase = 0; phase < 2; phase++) {
+        uint64_t *cur = bstart + 1;
+        uint32_t *occ = NULL;
+        if (phase == 1) {
+            for (uint64_t q = 0; q < m; q++) bstart[q + 1] += bstart[q];
+            occ = (uint32_t *)malloc((bstart[m] + 1) * 2 * sizeof(uint32_t));
+            if (!occ) { rc = ORC_E_NOMEM; break; }
+            cur = (uint64_t *)malloc((m + 1) * sizeof(uint64_t));
+            if (!cur) { free(occ); rc = ORC_E_NOMEM; break; }
+            memcpy(cur, bstart, (m + 1) * sizeof(uint64_t));
+        }
+#pragma omp parallel num_threads(nt)
+        {
+            uint32_t *hs = (uint32_t *)malloc(((size_t)maxL + 1) * sizeof(uint32_t));
+#pragma omp for schedule(dynamic, 1024)
+            for (uint32_t r = 0; r < n; r++) {
+                const int64_t L = (int64_t)(offsets[r + 1] - offsets[r]);
+                if (!hs || L < k) continue;
+                read_hashes(bases + offsets[r], L, k, hs);
+                for (int64_t p = 0; p + k <= L; p++) {
+                    const uint32_t h = hs[p];
+                    if (!IS_HIT(h)) continue;
+                    const uint32_t b = HIT_RANK(h);
+                    uint64_t slot;
+#pragma omp atomic capture
+                    slot = cur[b]++;
+                    if (phase == 1) { occ[2 * slot] = r; occ[2 * slot + 1] = (uint32_t)p; }
+                }
+            }
+            if (!hs) {
+#pragma omp critical
+                rc = ORC_E_NOMEM;
+            }
+            free(hs);
+        }
+        if (phase == 0) continue;
+        free(cur);
+        if (rc) { free(occ); break; }
+        /* rows, one lead at a time per thread */
+        int32_t **rs = (int32_t **)calloc(n_leads + 1, sizeof(int32_t *));
+        int32_t **rcn = (int32_t **)calloc(n_leads + 1, sizeof(int32_t *));
+        uint64_t *rn = (uint64_t *)calloc(n_leads + 1, sizeof(uint64_t));
+        if (!rs || !rcn || !rn) { free(rs); free(rcn); free(rn); free(occ); rc = ORC_E_NOMEM; break; }
+#pragma omp parallel num_threads(nt)
+        {
+            int32_t *acc = (int32_t *)calloc((size_t)n + 1, sizeof(int32_t));
+            uint32_t *hs = (uint32_t *)malloc(((size_t)maxL + 1) * sizeof(uint32_t));
+            ivec touched = {0};
+            int lrc = (!acc || !hs) ? ORC_E_NOMEM : ORC_OK;
+#pragma omp for schedule(dynamic, 1)
+            for (size_t li = 0; li < n_leads; li++) {
+                if (lrc) continue;
+                const uint32_t r = (uint32_t)leads[li] - 1u;
+                const int64_t L = (int64_t)(offsets[r + 1] - offsets[r]);
+                const float dr = (float)(L - k);
+                read_hashes(bases + offsets[r], L, k, hs);
+                touched.n = 0;
+                for (int64_t p = 0; p + k <= L; p++) {
+                    const float lo = (float)p / dr;
+                    const int o_st = lo <= head, o_md = midLead <= lo && lo <= midTail, o_en = tail <= lo;
+                    const int o_ed = o_st + o_en;
+                    if (!o_ed && !o_md) continue;
+                    const uint32_t b = HIT_RANK(hs[p]);
+                    for (uint64_t x = bstart[b]; x < bstart[b + 1]; x++) {
+                        const uint32_t q = occ[2 * x];
+                        if (q == r) continue;
+                        const float le = (float)occ[2 * x + 1] / (float)((int64_t)(offsets[q + 1] - offsets[q]) - k);
+                        const int e_md = midLead <= le && le <= midTail;
+                        const int e_ed = (le <= head) + (tail <= le);
+                        int add = 0;
+                        if (o_ed && e_md && lo > le) add += o_ed;    /* o edge, e middle, fst = o */
+                        if (o_md && e_ed && !(le > lo)) add += e_ed; /* e edge, o middle, fst = o */
+                        if (!add) continue;
+                        if (acc[q] == 0 && iv_push(&touched, (int32_t)q)) { lrc = ORC_E_NOMEM; break; }
+                        acc[q] += add;
+                    }
+                }
+                int32_t *sv = (int32_t *)malloc((touched.n + 1) * sizeof(int32_t));
+                int32_t *cv = (int32_t *)malloc((touched.n + 1) * sizeof(int32_t));
+                if (!sv || !cv) { free(sv); free(cv); lrc = ORC_E_NOMEM; continue; }
+                /* partners ascending: sort the touched read indices */
+                for (size_t z = 0; z < touched.n; z++) sv[z] = touched.v[z];
+                qsort(sv, touched.n, sizeof(int32_t), cmp_i32);
+                for (size_t z = 0; z < touched.n; z++) { cv[z] = acc[sv[z]]; acc[sv[z]] = 0; sv[z] += 1; }
+                rs[li] = sv; rcn[li] = cv; rn[li] = touched.n;
+            }
+            free(acc); free(hs); free(touched.v);
+            if (lrc) {
+#pragma omp critical
+                rc = lrc;
+            }
+        }
+        free(occ);
+        if (!rc) {
+            row_off[0] = 0;
+            for (size_t li = 0; li < n_leads; li++) row_off[li + 1] = row_off[li] + rn[li];
+            *snd_out = (int32_t *)malloc((row_off[n_leads] + 1) * sizeof(int32_t));
+            *cnt_out = (int32_t *)malloc((row_off[n_leads] + 1) * sizeof(int32_t));
+            if (!*snd_out || !*cnt_out) rc = ORC_E_NOMEM;
+            for (size_t li = 0; li < n_leads && !rc; li++) {
+                memcpy(*snd_out + row_off[li], rs[li], rn[li] * sizeof(int32_t));
+                memcpy(*cnt_out + row_off[li], rcn[li], rn[li] * sizeof(int32_t));
+            }
+        }
+        for (size_t li = 0; li < n_leads; li++) { free(rs[li]); free(rcn[li]); }
+        free(rs); free(rcn); free(rn);
+    }
+#undef HIT_RANK
+#undef IS_HIT
+    free(bits); free(rank); free(bstart);
+    if (rc) { free(*snd_out); free(*cnt_out); *snd_out = *cnt_out = NULL; }
+    return rc;
+}
+
+void orc_free(void *p) { free(p); }
+
 size_t orc_num_kmers(const orc_ctx *c) { return c->nk; }
 void orc_kmers(const orc_ctx *c, const int32_t **hash, const int32_t **read_id, const float **loc) {
     *hash = c->k_hash; *read_id = c->k_id; *loc = c->k_loc;

@@ -86,6 +86,17 @@ int orc_run(orc_ctx *c, const orc_settings *s, int flags);
  * all-core CPU baseline of the hash stage (bench.py). */
 int orc_run_wide_mt(orc_ctx *c, const orc_settings *s, int threads, uint64_t *role_pairs);
 
+/* Sampled-lead PairData rows (checker for read sets whose whole PairData does
+ * not fit host memory): for each lead of `leads` (1-based, strictly ascending)
+ * every PairData entry whose fst is that lead -- snd ascending, count >= 1 --
+ * in (*snd_out, *cnt_out)[row_off[i] .. row_off[i + 1]).  Same semantics as
+ * orc_run's wide branch (KmerTable.scala:57-149); memory is bounded by the
+ * sampled leads' buckets.  Free the outputs with orc_free. */
+int orc_lead_rows(const char *bases, const uint64_t *offsets, uint32_t n_reads, const orc_settings *s,
+                  const int32_t *leads, size_t n_leads, int threads, uint64_t *row_off, int32_t **snd_out,
+                  int32_t **cnt_out);
+void orc_free(void *p);
+
 /* Results of orc_run (arrays owned by ctx, valid until destroy/next run). */
 size_t orc_num_kmers(const orc_ctx *c);
 void orc_kmers(const orc_ctx *c, const int32_t **hash, const int32_t **read_id,

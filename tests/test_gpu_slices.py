@@ -38,7 +38,7 @@ ALIGN_CMP = ("start_i", "start_j", "end_i", "end_j", "correct", "error", "ahg", 
 SAMPLE = 20000
 
 
-def slice_vs_oracle(oracle_mod, n, read_len, min_len, k):
+def slice_vs_oracle(oracle_mod, n, read_len, min_len, k, shards=0):
     mean_len = read_len if min_len is None else (read_len + min_len) / 2.0
     G = int(n * mean_len / 20.0)  # bench.py's 20x coverage
     t0 = time.time()
@@ -54,6 +54,21 @@ def slice_vs_oracle(oracle_mod, n, read_len, min_len, k):
     al = ov.alignments()
     ov.close()
     t_gpu = time.time() - t0
+    if shards:
+        # the sharded path (multi.cpp + dist.hip) on the same reads: the
+        # single-device result, which is checked against the oracle below
+        sv = sao.Overlapper(shards=shards, kmer_size=k, id_mode=sao.SA_IDS_WIDE)
+        sv.add_packed(bases, o)
+        sv.device_build()
+        sv.device_align()
+        ss = sv.stats()
+        for key in ("kmers", "role_pairs", "pairs", "dispatched", "aligned", "ovl_records", "dp_cells"):
+            assert ss[key] == st[key], key
+        for x, y in zip(sv.dispatch(), (lead, trail, count)):
+            np.testing.assert_array_equal(x, y)
+        np.testing.assert_array_equal(sv.alignments(), al)
+        assert sv.exchanged_bytes() > 0
+        sv.close()
     t0 = time.time()
     r = oracle_mod.Run(packed=(bases, o), settings=oracle_mod.default_settings(kmer_size=k), wide=True,
                        skip_align=True, threads=0)
@@ -95,8 +110,10 @@ def test_configs3_per_gpu_slice_matches_oracle(oracle_mod):
 
 
 def test_configs4_shape_k15_matches_oracle(oracle_mod):
-    """configs[4]'s read shape at k = 15: 1M mixed 100-1,000 bp reads."""
-    st = slice_vs_oracle(oracle_mod, 1000000, 1000, 100, 15)
+    """configs[4]'s read shape at k = 15: 1M mixed 100-1,000 bp reads, on one
+    device and on 2 virtual shards x 500k reads (the sharded path with mixed
+    lengths at size: every alignment equal to the single device's)."""
+    st = slice_vs_oracle(oracle_mod, 1000000, 1000, 100, 15, shards=2)
     assert st["dispatched"] > 1000000
 
 

@@ -64,6 +64,46 @@ def test_all_core_hash_stage_equals_single_thread(oracle_mod, threads):
         assert r2.role_pairs > len(r1.pair_fst)
 
 
+@pytest.mark.parametrize("case", ["uniform15", "mixed12", "k18", "edges", "degenerate"])
+def test_lead_rows_equal_full_pairdata(oracle_mod, case):
+    """The sampled-lead checker (orc_lead_rows: only the sampled leads' buckets
+    are kept) gives, for every lead asked for, exactly its rows of the
+    single-threaded restatement's PairData -- partners and counts -- including
+    custom edges where one occurrence carries two roles, k > 16 (16-char
+    seqHash), L == k (NaN loc), reads shorter than k and lowercase / non-ACGT
+    characters."""
+    kw = dict(min_collisions=3)
+    if case == "uniform15":
+        reads, k = H.synth_reads(700, 150, 9000, gc=0.5, seed=21), 15
+    elif case == "mixed12":
+        reads, k = H.synth_reads(900, 200, 12000, gc=0.45, seed=22, mixed=(40, 200)), 12
+    elif case == "k18":
+        reads, k = H.synth_reads(600, 160, 7000, gc=0.5, seed=23, mixed=(100, 160)), 18
+    elif case == "edges":  # st and en overlap (edge 0.55), wide middle
+        reads, k = H.synth_reads(600, 120, 6000, gc=0.5, seed=24), 11
+        kw.update(kmer_edge=0.55, kmer_center=0.9)
+    else:
+        rng = np.random.default_rng(25)
+        reads = H.mutate(H.synth_reads(500, 90, 3000, gc=0.3, seed=25, mixed=(8, 90)), rng, 2)
+        reads = [r.lower() if i % 7 == 0 else (r[:5] + "N" + r[6:] if i % 11 == 0 else r) for i, r in enumerate(reads)]
+        k = 10
+        reads += ["ACGTACGTAC"] * 5 + ["ACG"]  # L == k (NaN loc), L < k
+    s = oracle_mod.default_settings(kmer_size=k, **kw)
+    full = oracle_mod.Run(reads=reads, settings=s, wide=True, skip_align=True)
+    bases = "".join(reads).encode()
+    off = np.zeros(len(reads) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(r) for r in reads])
+    for leads in (np.arange(1, len(reads) + 1), np.unique(np.random.default_rng(3).integers(1, len(reads) + 1, 50))):
+        ro, snd, cnt = oracle_mod.lead_rows(bases, off, leads, settings=s, threads=3)
+        sel = np.isin(full.pair_fst, leads)
+        want_lead = full.pair_fst[sel]
+        got_lead = np.repeat(leads.astype(np.int32), np.diff(ro))
+        np.testing.assert_array_equal(got_lead, want_lead)
+        np.testing.assert_array_equal(snd, full.pair_snd[sel])
+        np.testing.assert_array_equal(cnt, full.pair_cnt[sel])
+    assert len(full.pair_fst) > 100
+
+
 def test_hoxd1_equals_default_matrix(oracle_mod):
     """amos/HOXD1.txt (readHOXD format) == defaultHOXD (BioLibs.scala:122-140)."""
     rows = [l.split(",") for l in open(os.path.join(GOLD, "HOXD1.txt")).read().strip().split("\n")[1:]]
