@@ -140,7 +140,8 @@ int sa_get_ovl(sa_ctx *ctx, const char **text, size_t *len);
  * rank 1): the bank toAmos_new builds from the .seq (Rakefile.rb:174) and the
  * .ovl that bank-transact -m loads into it (:180-184), in one file.  One {RED}
  * per read in id order (iid = read id, eid = eids[id - 1], or the id when eids
- * or the entry is NULL / empty; eids, when given, holds one entry per read and
+ * or the entry is NULL / empty -- the eid rule is parity unpinned: the reference
+ * bank's RED.0.map cannot tell ordinal eids from header words; eids, when given, holds one entry per read and
  * an entry with whitespace, ':' or braces fails with SA_E_ARG; seq = the read as
  * the context holds it; qlt = '0' + quality on every base, quality 0..60; clr =
  * 0,len and no other range, as the reference bank's RED records hold), then the
@@ -161,12 +162,18 @@ enum sa_option {
     SA_OPT_LOCAL_BATCH_MB = 5, /* quadratic aligner: MiB of traceback codes per launch (16384) */
     SA_OPT_SERIAL_SHARDS = 6,  /* sharded context: run the shards' compute one after another
                                   (measurement: clean per-shard stage times on one device) */
-    SA_OPT_LAUNCH_SLICE = 7    /* pair counter: at most this many workgroups per launch (0 =
+    SA_OPT_LAUNCH_SLICE = 7,   /* pair counter: at most this many workgroups per launch (0 =
                                   default: lists are sliced only where a dispatch's 32-bit
                                   work-item count would wrap; a test hook for that path).
                                   Applies to the launches that walk a read / item list
                                   (every build passes one); a list-less launch larger
                                   than the slice fails with SA_E_HIP */
+    SA_OPT_FIRST_PASS = 8      /* pair counter's first pass (wide ids): 0 auto (default: a
+                                  sample of every 64th read runs it first when there are
+                                  >= 2^18 reads; if >= 95 % of the sample overflows its
+                                  256-slot tables, every read goes straight to the big
+                                  recount tier), 1 always run it, 2 always skip it (a
+                                  test hook for the dense path) */
 };
 
 /* Project4's fdAlign switch (Project4.scala:187-192, :585-604).

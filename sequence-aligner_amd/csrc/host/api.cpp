@@ -671,6 +671,7 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
     if (aborted) *aborted = false;
     P.per_read = per_read && *per_read ? 1 : 0;
     P.max_blocks = c->launch_slice;
+    P.early = 0;
     if (per_read) *per_read = false;
     uint2 *rreg = nullptr;
     uint32_t *rcnt = nullptr;
@@ -684,6 +685,52 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
     auto cur_max = [&]() { unsigned long long m = 0; for (auto v : cur) m = std::max(m, v); return m; };
     uint32_t ovn = 0;
     uint64_t cap_s = (c->pair_cap + NSHARD - 1) / NSHARD;
+    // Dense read sets (configs[4]'s k = 12 slice: 12-mers collide at random, and
+    // every read meets ~24k partners): every 256-slot table of the first pass
+    // overflows, and the pass costs its whole launch (0.49 s of ~7 s there) for
+    // nothing.  Every 64th read runs it first, counting only (dummy counters,
+    // no output room); when >= 95 % of that sample overflows, every read goes
+    // straight to the big tier in the shared-region mode, whose split-1 pass then
+    // sums the role pairs (SA_SKIP_PROBE=0: no probe, A/B runs).
+    bool skip_first = false;
+    static const bool probe_on = !getenv("SA_SKIP_PROBE") || atoi(getenv("SA_SKIP_PROBE")) != 0;
+    const bool dense_ok = !strict && !item_start && !P.emit_all;
+    if (dense_ok && c->first_pass == 2) {
+        skip_first = true;
+        P.per_read = 0;
+    } else if (probe_on && dense_ok && c->first_pass == 0 && n_items >= (1u << 18)) {
+        constexpr uint32_t stride = 64;
+        const uint32_t ns = n_items / stride;
+        std::vector<uint32_t> sample(ns);
+        for (uint32_t i = 0; i < ns; ++i) sample[i] = i * stride + stride / 2;
+        uint32_t *sl;
+        ENSURE(c->d_tier, ns, &sl);
+        PairOut OS{};
+        OS.cursor = cnt->role_pairs_dummy;  // (claims only: cap_s = 0, nothing is written)
+        OS.cap_s = 0;
+        OS.role_pairs = cnt->role_pairs_dummy;
+        OS.distinct = cnt->role_pairs_dummy;
+        OS.overflow_n = &cnt->overflow_n;
+        ENSURE(c->d_ovl, (uint64_t)n_items + 3, &OS.overflow_list);
+        ENSURE(c->d_ovlrp, (uint64_t)n_items + 3, &OS.overflow_rp);
+        PairParams PS = P;
+        PS.n_items = ns;
+        PS.xcd_swizzle = 0;
+        PS.per_read = 0;  // (the one-read workgroup: its emission claims land in the dummy)
+        uint32_t nov = 0;
+        HIPCHK(hipMemcpyAsync(sl, sample.data(), (size_t)ns * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(uint32_t), c->stream));
+        {
+            StageScope st(c, SA_STAGE_PAIRS);
+            HIPCHK(launch_pair_count(E, PI, PS, OS, sl, ns, c->stream));
+        }
+        HIPCHK(hipMemcpyAsync(&nov, &cnt->overflow_n, 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(uint32_t), c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        // (a pending big-partition build makes the sample exit at once: nov = 0)
+        skip_first = (uint64_t)nov * 20 >= (uint64_t)ns * 19 && ns > 0;
+        if (skip_first) P.per_read = 0;
+    }
     for (int attempt = 0; attempt < 4; ++attempt) {
         PairOut O;
         const uint64_t tot_cap = cap_s * NSHARD;
@@ -709,7 +756,7 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
             HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(uint32_t), c->stream));
         }
         c->counters_fresh = false;
-        {
+        if (!skip_first) {
             StageScope st(c, SA_STAGE_PAIRS);
             if (item_start) {  // multi-read blocks (sharded path)
                 PairParams PM = P;
@@ -729,8 +776,8 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
         HIPCHK(hipMemcpyAsync(hp, cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         memcpy(cur, hp->cursor, sizeof(cur));
-        ovn = hp->overflow_n;
-        const uint32_t abv = P.abort ? hp->big_n : 0u;
+        ovn = skip_first ? n_items : hp->overflow_n;
+        const uint32_t abv = P.abort && !skip_first ? hp->big_n : 0u;
         unsigned long long dist_h[NSHARD];
         memcpy(dist_h, hp->distinct, sizeof(dist_h));
         if (abv) {
@@ -758,7 +805,27 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
         if (ovn > 0 && n_items >= (1u << 26))
             return fail(c, SA_E_OVERFLOW, "recount tiers address reads with 26 bits");
         std::vector<uint32_t> q_big, q_huge;
-        if (ovn > 0) {
+        if (skip_first) {  // every read, straight to the big tier, in the locality order
+            q_huge.resize(n_items);
+            if (read_order) {
+                // blocks are dealt round-robin over the 8 XCDs: item i runs on XCD
+                // i % 8, so XCD x is given a contiguous run of the locality order
+                // (as the first pass's swizzle does) and shares its partner lists in L2
+                std::vector<uint32_t> ro(n_items);
+                HIPCHK(hipMemcpyAsync(ro.data(), read_order, (size_t)n_items * 4, hipMemcpyDeviceToHost, c->stream));
+                HIPCHK(hipStreamSynchronize(c->stream));
+                const uint32_t per = n_items / 8, rem = n_items % 8;  // XCD x: per + (x < rem) reads
+                uint32_t i = 0;
+                for (uint32_t j = 0; j <= per; ++j)
+                    for (uint32_t x = 0; x < 8; ++x) {
+                        if (j == per && x >= rem) break;
+                        const uint32_t base = x * per + std::min(x, rem);
+                        q_huge[i++] = ro[base + j] << 6;
+                    }
+            } else {
+                for (uint32_t i = 0; i < n_items; ++i) q_huge[i] = i << 6;
+            }
+        } else if (ovn > 0) {
             std::vector<uint32_t> codes(ovn), rps(ovn, 0);
             HIPCHK(hipMemcpy(codes.data(), O.overflow_list, (size_t)ovn * 4, hipMemcpyDeviceToHost));
             if (O.overflow_rp) HIPCHK(hipMemcpy(rps.data(), O.overflow_rp, (size_t)ovn * 4, hipMemcpyDeviceToHost));
@@ -790,8 +857,17 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
             PT.coded = 1;
             PT.n_items = (uint32_t)items.size();
             PT.xcd_swizzle = 0;
+            // big tiers: stop a read whose projected partners pass the fill limit
+            // (SA_EARLY_STOP=n: n/8 of it, default 8; 0 turns it off, A/B runs)
+            // after at least 1/SA_EARLY_FRAC of its role pairs (default 8).
+            // configs[4]'s k = 12 slice, pairs stage: no early stop 7.00 s; 9/8
+            // after 1/4 5.79; 8/8 after 1/8 5.48 s (profiles/r05/c4ab)
+            static const int early_env = getenv("SA_EARLY_STOP") ? atoi(getenv("SA_EARLY_STOP")) : 8;
+            static const int early_frac = getenv("SA_EARLY_FRAC") ? std::max(1, atoi(getenv("SA_EARLY_FRAC"))) : 8;
+            PT.early = table >= 16384 && fest && early_env > 0 ? (early_env & 255) | (early_frac << 8) : 0;
             PairOut OT = O;
-            OT.role_pairs = cnt->role_pairs_dummy;
+            // (skip mode: the split-1 big-tier pass is every read's first pass)
+            OT.role_pairs = skip_first && split == 1 && table >= 16384 ? cnt->role_pairs : cnt->role_pairs_dummy;
             OT.overflow_list = fl;
             OT.overflow_rp = nullptr;
             uint32_t *fe = nullptr;
@@ -1796,6 +1872,10 @@ int sa_set_option(sa_ctx *c, int option, int64_t value) {
     case SA_OPT_LAUNCH_SLICE:
         if (value < 0 || value > 0x7FFFFFFF) return fail(c, SA_E_ARG, "SA_OPT_LAUNCH_SLICE must be 0..2^31-1");
         c->launch_slice = (uint32_t)value;
+        break;
+    case SA_OPT_FIRST_PASS:
+        if (value < 0 || value > 2) return fail(c, SA_E_ARG, "SA_OPT_FIRST_PASS must be 0..2");
+        c->first_pass = (int)value;
         break;
     case SA_OPT_SERIAL_SHARDS:
         if (!c->multi) return fail(c, SA_E_ARG, "SA_OPT_SERIAL_SHARDS needs a sharded context");

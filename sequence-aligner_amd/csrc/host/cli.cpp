@@ -10,7 +10,8 @@
 // Extra flags: --wide-ids / --strict-ids, --device N, --stats,
 // --afg FILE [--afg-quality Q] [--afg-header-eids] (also an AMOS message file:
 // the reads as {RED} messages, eid = the read ordinal as in the reference's
-// c_ruddii bank map, or with --afg-header-eids the FASTA header's first word;
+// c_ruddii bank map, or with --afg-header-eids the FASTA header's first word --
+// which of the two toAmos_new writes is parity unpinned, INTEGRATION.md;
 // then the {OVL} records --
 // toAmos_new + bank-transact -m in one file),
 // --gpus P (one process over devices 0..P-1, one shard each, RCCL exchanges;
@@ -459,8 +460,9 @@ int main(int argc, char **argv) {
     }
     if (rc == SA_OK && !afg.empty()) {
         // default eid = ordinal (the only bank the reference holds maps iid = bid =
-        // eid = ordinal, amos/c_ruddii.bnk/RED.0.map); header names are opt-in and
-        // not pinned against toAmos_new
+        // eid = ordinal, amos/c_ruddii.bnk/RED.0.map -- which cannot tell ordinals
+        // from header words, its .seq being a missing blob: the eid rule is parity
+        // unpinned either way); header names are opt-in
         const std::vector<std::string> names = afg_header_eids ? fasta_eids(input) : std::vector<std::string>();
         std::vector<const char *> eids(sa_num_reads(ctx), nullptr);
         for (size_t i = 0; i < eids.size() && i < names.size(); ++i) eids[i] = names[i].c_str();

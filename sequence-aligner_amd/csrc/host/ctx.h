@@ -132,6 +132,7 @@ struct sa_ctx {
     // options / state
     bool keep_pairs = false, timing = false;
     int align_kernel = 0;  // SA_OPT_ALIGN_KERNEL
+    int first_pass = 0;         // SA_OPT_FIRST_PASS: 0 probe, 1 always, 2 skip (wide ids)
     uint32_t launch_slice = 0;  // SA_OPT_LAUNCH_SLICE (0: only when a grid would pass 2^31 work-items)
     int aligner = SA_ALIGNER_LINEAR;  // SA_OPT_ALIGNER (--linear-align / --quadratic-align)
     uint64_t local_batch_bytes = 16ull << 30;  // traceback-code budget of one quadratic launch

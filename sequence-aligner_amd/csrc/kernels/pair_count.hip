@@ -65,14 +65,22 @@ constexpr int PC_WIN = 2048;
 
 // Per-table block shape.  The 16,384-slot tier holds 128 KB of table, so only
 // one block fits a CU: it runs 1,024 threads (16 waves to hide the partner
-// gathers, not 4), 1,024-occurrence chunks and 4,096-element windows (4
-// partner loads in flight per thread); the smaller tables keep 256 threads.
+// gathers, not 4), 1,024-occurrence chunks and 6,144-element windows (6
+// partner loads in flight per thread: the packed tier's LDS holds 12 KB of
+// window map beside its 128 KB table; 8 would pass the 160 KB); the smaller
+// tables keep 256 threads.
+#ifndef PC_HUGE_CHUNK
+#define PC_HUGE_CHUNK 1024
+#endif
+#ifndef PC_HUGE_BATCH
+#define PC_HUGE_BATCH 6  // (configs[4]'s k = 12 slice, pairs stage: 4 -> 5.79 s, 5 -> 5.57, 6 -> 5.51)
+#endif
 template <int TAB> struct PcShape {
     static constexpr int NT = TAB >= PC_TAB_HUGE ? 1024 : PC_THREADS;
     static constexpr bool PACKED = TAB >= PC_TAB_HUGE2;
-    static constexpr int CHUNK = TAB >= PC_TAB_HUGE ? 1024 : PC_CHUNK;
-    static constexpr int WIN = TAB >= PC_TAB_HUGE ? 4096 : PC_WIN;
-    static constexpr int BATCH = TAB >= PC_TAB_HUGE ? 4 : PC_BATCH;
+    static constexpr int CHUNK = TAB >= PC_TAB_HUGE ? PC_HUGE_CHUNK : PC_CHUNK;
+    static constexpr int WIN = TAB >= PC_TAB_HUGE ? 1024 * PC_HUGE_BATCH : PC_WIN;
+    static constexpr int BATCH = TAB >= PC_TAB_HUGE ? PC_HUGE_BATCH : PC_BATCH;
 };
 
 template <int TAB>
@@ -278,6 +286,7 @@ __global__ __launch_bounds__(PcShape<TAB>::NT) void pair_count_kernel(EmitParams
     const uint32_t nocc = e.npr ? e.npr : (uint32_t)(e.occ_off[a + 1] - g0);
     unsigned long long role_pairs = 0;
     unsigned long long x_over = ~0ull;  // role pairs enumerated when the table filled
+    unsigned long long early_est = 0;   // early stop: the projected distinct partners
     // (the table initialisation is ordered before any insert by the chunk scan's barriers)
 
     for (uint32_t c0 = 0; c0 < nocc; c0 += CHUNK) {
@@ -330,6 +339,23 @@ __global__ __launch_bounds__(PcShape<TAB>::NT) void pair_count_kernel(EmitParams
             if (S.overflow) {
                 if (x_over == ~0ull) x_over = role_pairs - total + w0;
                 break;
+            }
+            // Big tiers: a read that will not fit is found early.  Partners are met
+            // no later than they recur, so fill(x) / x over the first x of the read's
+            // role pairs is at least distinct / total -- the projection over-reads,
+            // and a read only stops when it is past the fill limit by the margin.
+            // (One-chunk reads: total is the read's; S.fill is final for the windows
+            // before this barrier and the same for every thread.)
+            if constexpr (TAB >= PC_TAB_HUGE) {
+                if (p.early && nocc <= (uint32_t)CHUNK && w0 >= total / (uint32_t)(p.early >> 8) && w0 > 0) {
+                    const unsigned long long proj = (unsigned long long)S.fill * total / w0;
+                    if (proj * 8 > (unsigned long long)pc_fill_max(TAB) * (unsigned)(p.early & 255)) {
+                        early_est = proj;
+                        x_over = w0;
+                        if (tid == 0) S.overflow = 1;  // (read again only after the chunk's barrier)
+                        break;
+                    }
+                }
             }
 #pragma unroll
             for (int j = 0; j < PER; ++j) {  // this thread's occurrences' elements inside the window
@@ -415,7 +441,8 @@ __global__ __launch_bounds__(PcShape<TAB>::NT) void pair_count_kernel(EmitParams
             if (o.overflow_rp) {
                 const unsigned long long x = S.xfill != 0xFFFFFFFFu ? (unsigned long long)S.xfill + 1
                                              : x_over == ~0ull || x_over == 0 ? role_pairs : x_over;
-                const unsigned long long est = (unsigned long long)pc_fill_max(TAB) * role_pairs / (x ? x : 1);
+                const unsigned long long est =
+                    early_est ? early_est : (unsigned long long)pc_fill_max(TAB) * role_pairs / (x ? x : 1);
                 o.overflow_rp[at] = est > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)est;
             }
         }

@@ -228,6 +228,11 @@ struct PairParams {
     const uint32_t *abort;
     int32_t per_read;      // 1: emit into PairOut::rreg / rcnt (first pass, wide ids, dispatched pairs only)
     uint32_t max_blocks;   // > 0: at most this many blocks per launch (item lists are sliced; tests)
+    // > 0 (the 16,384 / 32,768-slot tiers): a one-chunk read whose distinct
+    // partners, projected from the table's fill after at least 1 / (early >> 8)
+    // of its role pairs, exceed (early & 255) / 8 x the fill limit stops there
+    // and is handed to finer classes at once, the projection as its estimate
+    int32_t early;
 };
 
 // Device-wide counters are sharded NSHARD ways (shard = blockIdx % NSHARD) and

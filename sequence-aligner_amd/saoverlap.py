@@ -23,7 +23,7 @@ LIB_PATH = os.environ.get("SA_OVERLAP_LIB") or os.path.join(HERE, "build", "libs
 
 SA_IDS_AUTO, SA_IDS_STRICT, SA_IDS_WIDE = 0, 1, 2
 SA_OPT_KEEP_PAIRS, SA_OPT_TIMING, SA_OPT_ALIGN_KERNEL, SA_OPT_ALIGNER, SA_OPT_LOCAL_BATCH_MB = 1, 2, 3, 4, 5
-SA_OPT_SERIAL_SHARDS, SA_OPT_LAUNCH_SLICE = 6, 7
+SA_OPT_SERIAL_SHARDS, SA_OPT_LAUNCH_SLICE, SA_OPT_FIRST_PASS = 6, 7, 8
 SA_ALIGNER_LINEAR, SA_ALIGNER_QUADRATIC = 0, 1   # --linear-align / --quadratic-align
 SA_STATS_PER_READ_REGIONS, SA_STATS_RECOUNTED = 1, 2    # sa_stats.flags bits of the last build
 ALIGN_AUTO, ALIGN_GROUP, ALIGN_LANE, ALIGN_LANE_SUMMARY = 0, 1, 2, 3
@@ -162,7 +162,7 @@ class Overlapper:
 
     def __init__(self, device=0, timing=False, keep_pairs=False, align_kernel=ALIGN_AUTO,
                  aligner=SA_ALIGNER_LINEAR, local_batch_mb=None, gpus=1, shards=1, rank=None, nranks=None,
-                 rccl_id=None, serial_shards=False, launch_slice=0, **kw):
+                 rccl_id=None, serial_shards=False, launch_slice=0, first_pass=0, **kw):
         self.s = settings(**kw)
         h = C.c_void_p()
         if rank is not None:
@@ -189,6 +189,8 @@ class Overlapper:
             self._chk(lib().sa_set_option(h, SA_OPT_SERIAL_SHARDS, 1))
         if launch_slice:
             self._chk(lib().sa_set_option(h, SA_OPT_LAUNCH_SLICE, launch_slice))
+        if first_pass:
+            self._chk(lib().sa_set_option(h, SA_OPT_FIRST_PASS, first_pass))
 
     def kmer_histogram(self):
         """(uniques, {bucket size: number of hashes}) -- KmerTable.uniqueKmers /

@@ -9,7 +9,10 @@ Pins: the {OVL} half must equal the .ovl byte for byte (itself checked against t
 oracle elsewhere).  The {RED} half is checked against the reference's own bank,
 `amos/c_ruddii.bnk` (the 32,000 c_ruddii reads toAmos_new loaded), read as data into
 tests/golden/c_ruddii_bank_red.npz by make_c_ruddii_bank_red.py: RED.0.map gives
-every read's iid / bid / eid (the ordinal, so ordinal eids are the CLI default),
+every read's iid / bid / eid (all the ordinal; the eid RULE stays parity unpinned:
+c_ruddii.seq's headers are a missing blob and may be the ordinals themselves, and
+toAmos_new's source is absent, so the CLI's ordinal default and --afg-header-eids
+are equally consistent with this map),
 RED.0.0.fix every read's length and clear range (0, 100) with every other range
 of the record unset (so the writer emits clr and no qcr).  toAmos_new's default
 quality is not pinned (its var blob, RED.0.0.var, is absent from the fixture):

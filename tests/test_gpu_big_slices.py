@@ -218,3 +218,49 @@ def test_configs4_full_slice_sampled_leads(oracle_mod, c4_slice_reads, k):
     record("c4_slice_k%d_sampled" % k, {"reads": C4_N, "k": k, "stats": st, "sampled_leads": int(len(leads)),
                                        "pairdata_rows": int(len(snd)), "dispatched_rows": int(len(sel)),
                                        "device_s": t_gpu, "oracle_s": t_orc})
+
+
+# ---------------------------------------------------------------------------
+# the dense path: first pass skipped, early-stopped big-tier reads
+# ---------------------------------------------------------------------------
+def test_dense_first_pass_modes_match_sampled_oracle(oracle_mod):
+    """300k mixed 100-1,000 bp reads at k = 10 (a 1M hash space: buckets of
+    ~150 occurrences, ~20-50k distinct partners per read -- past the 32,768-
+    slot tier's 24,576, so reads stop early and go to partner classes).  The
+    first pass run (SA_OPT_FIRST_PASS = 1), skipped (2) and left to the probe
+    (0) give the same dispatch and stats, and the sampled leads' rows equal the
+    oracle's PairData rows."""
+    n, k = 300000, 10
+    b, o = bench.synth_workload(n, 1000, int(n * 550 / 20.0), 0.5, seed=3, min_len=100)
+    bases = b.tobytes()
+    del b
+    outs = []
+    for mode in (1, 2, 0):
+        ov = sao.Overlapper(kmer_size=k, id_mode=sao.SA_IDS_WIDE, first_pass=mode)
+        ov.add_packed(bases, o)
+        ov.device_build()
+        st = ov.stats()
+        outs.append((st, ov.dispatch()))
+        ov.close()
+    for st, d in outs[1:]:
+        for key in ("kmers", "buckets", "role_pairs", "pairs", "dispatched"):
+            assert st[key] == outs[0][0][key], key
+        for x, y in zip(d, outs[0][1]):
+            np.testing.assert_array_equal(x, y)
+    st, (lead, trail, count) = outs[0]
+    assert st["flags"] & sao.SA_STATS_RECOUNTED and st["pairs"] > 2000 * n
+    leads = sampled_leads(n, np.diff(o.astype(np.int64)), count=1500, seed=7)
+    s = oracle_mod.default_settings(kmer_size=k)
+    ro, snd, cnt = oracle_mod.lead_rows(bases, o, leads, settings=s, threads=0)
+    keep = (cnt >= s.min_collisions) & (cnt <= s.max_collisions)
+    neg = -lead.astype(np.int64)
+    lo = np.searchsorted(neg, -leads.astype(np.int64), "left")
+    hi = np.searchsorted(neg, -leads.astype(np.int64), "right")
+    sel = np.concatenate([np.arange(a, b) for a, b in zip(lo, hi)])
+    np.testing.assert_array_equal(lead[sel], np.repeat(leads, np.diff(ro))[keep])
+    np.testing.assert_array_equal(trail[sel], snd[keep])
+    np.testing.assert_array_equal(count[sel], cnt[keep])
+    # the sampled leads' distinct partners bound the device's distinct total from below
+    print("dense k=10: %d pairs, %d dispatched; sampled leads %d rows (max %d partners)"
+          % (st["pairs"], st["dispatched"], len(snd), int(np.diff(ro).max())))
+    assert int(np.diff(ro).max()) > 24576  # some sampled lead is past one big table
