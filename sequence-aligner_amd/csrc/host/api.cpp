@@ -405,7 +405,7 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
                  const uint64_t *occ_off, uint32_t n_reads, uint32_t npr, const uint2 *rl,
                  const int32_t *len, bool strict, void *stmp, Counters *cnt, PartArgs &PA,
                  unsigned long long &big_buckets, int skip_bits = 0, int phase = 0, const uint32_t *pv = nullptr,
-                 const KeyGen *kgen = nullptr) {
+                 const KeyGen *kgen = nullptr, const RecvGen *recv = nullptr) {
     // phase 0: everything; 1: sort + LDS tiers, no readback (the caller's
     // first pair-count pass aborts on big_n); 2: only the global path of the
     // partitions phase 1 listed (keys / PA as phase 1 left them)
@@ -440,8 +440,14 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
                 // rides along as the sort's value: 12-byte records through the
                 // passes instead of 16 (vals / vals2 are free until the global path)
                 uint32_t *v0 = vals, *v1 = vals2;
-                if (n) HIPCHK(hipMemcpyAsync(v0, pv, n * 4, hipMemcpyDeviceToDevice, c->stream));
-                HIPCHK(radix_sort(&keys, &v0, &keys2, &v1, n, 64 - skip_bits - PB, 64 - skip_bits, stmp, c->stream));
+                if (recv) {  // received records: relabelled and decoded by the first pass
+                    HIPCHK(radix_sort_recv(*recv, &keys, &v0, &keys2, &v1, n, 64 - skip_bits - PB, 64 - skip_bits,
+                                           stmp, c->stream));
+                } else {
+                    if (n && v0 != pv) HIPCHK(hipMemcpyAsync(v0, pv, n * 4, hipMemcpyDeviceToDevice, c->stream));
+                    HIPCHK(radix_sort(&keys, &v0, &keys2, &v1, n, 64 - skip_bits - PB, 64 - skip_bits, stmp,
+                                      c->stream));
+                }
                 spv = v0;
             } else if (rl) {
                 // an occurrence table rides along as the sort's 8-byte value, so the
@@ -636,12 +642,14 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
 
 // Pair counting (pair_count.hip) with output-capacity growth and the
 // partner-residue split pass for reads whose LDS table overflows.  Leaves np
-// entries in the NSHARD output regions of cap_s_out entries each.
+// entries in the NSHARD output regions of cap_s_out entries each -- or, with
+// owners > 1 (sharded path), in owners x NSHARD regions grouped by the rank
+// owning the lead (owner_starts, device), their fill in c->d_ocur / c->ocur.
 int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bool emit_all,
                const uint32_t *read_order, uint32_t n_items, Counters *cnt, uint64_t &np, uint64_t &cap_s_out,
                const uint32_t *item_start = nullptr, uint32_t n_multi = 0, const uint32_t *abort_flag = nullptr,
                bool *aborted = nullptr, bool *per_read = nullptr, uint64_t *distinct_ub = nullptr,
-               bool all_partials = false) {
+               uint32_t owners = 1, const uint32_t *owner_starts = nullptr, const uint32_t *item_owner = nullptr) {
     // per_read (in: allowed; out: used): the first pass writes each read's
     // dispatched pairs, trail-ascending, into a fixed region of PC_RREG slots
     // (wide ids, dispatched pairs only, one device); a read whose table
@@ -655,10 +663,6 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
     PairParams P;
     P.min_coll = c->set.min_collisions;
     P.max_coll = c->set.max_collisions;
-    if (all_partials) {  // sharded path, per-read regions: every distinct partial (count >= 1)
-        P.min_coll = 1;
-        P.max_coll = INT32_MAX;
-    }
     P.emit_all = emit_all ? 1 : 0;
     P.strict = strict ? 1 : 0;
     P.split = 1;
@@ -680,11 +684,19 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
         ENSURE(c->d_rcnt, (uint64_t)n_items + 1, &rcnt);
     }
     if (c->pair_cap == 0) c->pair_cap = std::max<uint64_t>(1 << 16, (uint64_t)n_items * (P.emit_all ? 64 : 24));
-    // output regions: NSHARD x cap_s entries (a block appends to region blockIdx % NSHARD)
-    unsigned long long cur[NSHARD];
+    // output regions: NSHARD (x owners) of cap_s entries (a block appends to
+    // region blockIdx % NSHARD, of its lead's owner)
+    const uint32_t R = NSHARD * std::max(owners, 1u);
+    unsigned long long *dcur = cnt->cursor;
+    if (owners > 1) ENSURE(c->d_ocur, R, &dcur);
+    std::vector<unsigned long long> cur(R, 0);
     auto cur_max = [&]() { unsigned long long m = 0; for (auto v : cur) m = std::max(m, v); return m; };
+    auto read_cur = [&]() -> int {  // (stream work up to here complete)
+        if (owners > 1) HIPCHK(hipMemcpy(cur.data(), dcur, (size_t)R * 8, hipMemcpyDeviceToHost));
+        return SA_OK;
+    };
     uint32_t ovn = 0;
-    uint64_t cap_s = (c->pair_cap + NSHARD - 1) / NSHARD;
+    uint64_t cap_s = (c->pair_cap + R - 1) / R;
     // Dense read sets (configs[4]'s k = 12 slice: 12-mers collide at random, and
     // every read meets ~24k partners): every 256-slot table of the first pass
     // overflows, and the pass costs its whole launch (0.49 s of ~7 s there) for
@@ -732,8 +744,8 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
         if (skip_first) P.per_read = 0;
     }
     for (int attempt = 0; attempt < 4; ++attempt) {
-        PairOut O;
-        const uint64_t tot_cap = cap_s * NSHARD;
+        PairOut O{};
+        const uint64_t tot_cap = cap_s * R;
         ENSURE(c->d_pf, tot_cap, &O.fst);
         ENSURE(c->d_ps, tot_cap, &O.snd);
         ENSURE(c->d_pc, tot_cap, &O.cnt);
@@ -742,7 +754,10 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
         ENSURE(c->d_ovl, (uint64_t)n_items + 3, &O.overflow_list);  // reads whose table overflowed
         ENSURE(c->d_ovlrp, (uint64_t)n_items + 3, &O.overflow_rp);  // and their role pairs
         if (item_start) O.overflow_rp = nullptr;  // multi-read blocks: the host routes by table
-        O.cursor = cnt->cursor;
+        O.cursor = dcur;
+        O.owners = owners;
+        O.owner_starts = owner_starts;
+        O.item_owner = item_owner;
         O.cap_s = cap_s;
         O.role_pairs = cnt->role_pairs;
         O.overflow_n = &cnt->overflow_n;
@@ -756,14 +771,14 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
             HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(uint32_t), c->stream));
         }
         c->counters_fresh = false;
+        if (owners > 1) HIPCHK(hipMemsetAsync(dcur, 0, (size_t)R * 8, c->stream));
         if (!skip_first) {
             StageScope st(c, SA_STAGE_PAIRS);
             if (item_start) {  // multi-read blocks (sharded path)
                 PairParams PM = P;
                 PM.n_items = n_multi;
                 PM.table = 1024;
-                if (c->multi_wave_items) HIPCHK(launch_pair_count_multi_wave(E, PI, PM, O, item_start, n_multi, c->stream));
-                else HIPCHK(launch_pair_count_multi(E, PI, PM, O, item_start, n_multi, c->stream));
+                HIPCHK(launch_pair_count_multi_wave(E, PI, PM, O, item_start, n_multi, c->stream));
             } else {
                 HIPCHK(launch_pair_count(E, PI, P, O, read_order, read_order ? ((n_items + 7) & ~7u) : n_items,
                                          c->stream));
@@ -775,7 +790,8 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
         if (int rc_p = pinned_counters(c, &hp)) return rc_p;
         HIPCHK(hipMemcpyAsync(hp, cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
-        memcpy(cur, hp->cursor, sizeof(cur));
+        if (owners > 1) { if (int rc_c = read_cur()) return rc_c; }
+        else memcpy(cur.data(), hp->cursor, NSHARD * 8);
         ovn = skip_first ? n_items : hp->overflow_n;
         const uint32_t abv = P.abort && !skip_first ? hp->big_n : 0u;
         unsigned long long dist_h[NSHARD];
@@ -881,7 +897,7 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
                 HIPCHK(launch_pair_count(E, PI, PT, OT, tl, PT.n_items, c->stream));
             }
             uint32_t nf = 0;
-            HIPCHK(hipMemcpyAsync(cur, cnt->cursor, sizeof(cur), hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipMemcpyAsync(cur.data(), dcur, (size_t)R * 8, hipMemcpyDeviceToHost, c->stream));
             HIPCHK(hipMemcpyAsync(&nf, &cnt->overflow_n, 4, hipMemcpyDeviceToHost, c->stream));
             HIPCHK(hipStreamSynchronize(c->stream));
             failed.resize(nf);
@@ -961,11 +977,12 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
             break;
         }
         cap_s = cur_max() + cur_max() / 4 + 1024;  // grow and recount
-        c->pair_cap = cap_s * NSHARD;
+        c->pair_cap = cap_s * R;
         if (attempt == 3) return fail(c, SA_E_OVERFLOW, "pair output did not fit");
     }
     np = 0;
     for (auto v : cur) np += v;
+    if (owners > 1) c->ocur = cur;
     cap_s_out = cap_s;
     return SA_OK;
 }
@@ -1594,7 +1611,7 @@ void sa_ctx_destroy(sa_ctx *c) {
                     &c->d_ovl, &c->d_cnt, &c->d_okeys, &c->d_ovals, &c->d_okeys2, &c->d_ovals2, &c->d_osort,
                     &c->d_lead, &c->d_trail, &c->d_count, &c->d_aln, &c->d_p1, &c->d_tb, &c->d_rkey, &c->d_rkey2, &c->d_rord, &c->d_rord2, &c->d_rtmp, &c->d_gocc, &c->d_seg, &c->d_rl, &c->d_srl, &c->d_srl2, &c->d_loff, &c->d_starts, &c->d_bounds, &c->d_gcodes, &c->d_gwoff, &c->d_glen, &c->d_gbad, &c->d_psum, &c->d_pkeep, &c->d_ppos, &c->d_scan, &c->d_pstart, &c->d_biglist, &c->d_rec,
                     &c->d_srec, &c->d_bnmd, &c->d_ishead, &c->d_bnst2, &c->d_tmd, &c->d_ted, &c->d_tmdi,
-                    &c->d_tedi, &c->d_xrec, &c->d_tier, &c->d_ovlrp, &c->d_meta, &c->d_items, &c->d_pq, &c->d_lr, &c->d_bigtot, &c->d_hk0, &c->d_hk1, &c->d_hflag,
+                    &c->d_tedi, &c->d_xrec, &c->d_tier, &c->d_ovlrp, &c->d_meta, &c->d_items, &c->d_pq, &c->d_ocur, &c->d_lr, &c->d_bigtot, &c->d_hk0, &c->d_hk1, &c->d_hflag,
                     &c->d_hidx, &c->d_hpos, &c->d_htmp, &c->d_hist, &c->d_hovf, &c->d_hsmall,
                     &c->d_ltb, &c->d_lmax, &c->d_rreg, &c->d_rcnt, &c->d_rex,
                     &c->d_shl, &c->d_sht, &c->d_shc, &c->d_rsh};
@@ -2080,21 +2097,38 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint6
     uint2 *rl; uint32_t *vals, *vals2; uint64_t *loff, *keys2, *dseg; uint8_t *stmp;
     ENSURE(c->d_seg, seg.size(), &dseg);
     HIPCHK(hipMemcpyAsync(dseg, seg.data(), seg.size() * 8, hipMemcpyHostToDevice, c->stream));
-    ENSURE(c->d_rl, n, &rl);
     // reads and loc ranks fit 4 bytes (e.g. 800k global reads of 500 bp: 20 + 9
-    // bits): the occurrence table is packed, 12-byte records in the partition sort
+    // bits): the occurrence table is packed, 12-byte records in the partition
+    // sort, written straight into the sort's value buffer (else {read, loc rank}
+    // pairs, 16-byte records)
     const bool packed = bits_for(N ? N - 1 : 0) + c->lb <= 32;
-    uint32_t *pv = packed ? (uint32_t *)rl : nullptr;
+    rl = nullptr;
+    if (!packed) ENSURE(c->d_rl, n, &rl);
     ENSURE(c->d_loff, (size_t)N + 1, &loff);
     ENSURE(c->d_vals, n, &vals);
+    uint32_t *pv = packed ? vals : nullptr;
     ENSURE(c->d_vals2, n, &vals2);
     ENSURE(c->d_keys2, n, &keys2);
     ENSURE(c->d_sorttmp, std::max(radix_sort_temp_bytes(n), buckets_temp_bytes(n)), &stmp);
     uint64_t *keys = (uint64_t *)recv_recs;
-    {
+    // the read id and loc rank of every received occurrence, its record's low
+    // word relabelled to its local index (record i of this rank), and the local
+    // read offsets: with a packed occurrence table, inside the partition sort's
+    // first pass (RecvGen: the received records are read once, not rewritten
+    // first -- 8 serial shards of the bench shape, emit + sort per shard
+    // profiles/r05/sharded; SA_RECV_FUSED=0: the separate pass, A/B runs)
+    static const bool fuse_env = !getenv("SA_RECV_FUSED") || atoi(getenv("SA_RECV_FUSED")) != 0;
+    const bool fused = fuse_env && packed && n > 0;
+    RecvGen RG{};
+    if (fused) {
+        RG.seg = dseg; RG.P = (uint32_t)P; RG.starts = (const uint32_t *)c->d_starts.p;
+        RG.occ_off = (const uint64_t *)c->d_gocc.p; RG.npr = c->gnpr;
+        RG.npr_magic = c->gnpr >= 2 ? ~0ull / c->gnpr + 1 : 0ull;
+        RG.len = (const int32_t *)c->d_glen.p; RG.lbase = (const uint32_t *)c->d_lbase.p;
+        RG.lrank = (const uint32_t *)c->d_lrank.p; RG.k = c->set.kmer_size; RG.lb = c->lb;
+        RG.loff = loff; RG.n_reads = N;
+    } else {
         StageScope st(c, SA_STAGE_EMIT);
-        // read id and loc rank of every received occurrence; the record's low
-        // word becomes its local index (record i of this rank)
         HIPCHK(launch_prepare_received(keys, n, dseg, (uint32_t)P, (const uint32_t *)c->d_starts.p,
                                        (const uint64_t *)c->d_gocc.p, c->gnpr,
                                        (const int32_t *)c->d_glen.p, (const uint32_t *)c->d_lbase.p,
@@ -2105,7 +2139,7 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint6
     PartArgs PA{};
     unsigned long long big_buckets = 0;
     rc = bucket_stage(c, keys, keys2, vals, vals2, n, loff, N, 0, packed ? nullptr : rl, nullptr, false, stmp, cnt,
-                      PA, big_buckets, c->log_ranks, 0, pv);
+                      PA, big_buckets, c->log_ranks, 0, pv, nullptr, fused ? &RG : nullptr);
     if (rc) return rc;
     PairIn PI{};
     PI.rec = PA.rec; PI.xrec = PA.xrec; PI.lst = PA.lst;
@@ -2113,89 +2147,45 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint6
     E.occ_off = loff;  // occurrences of read a on this rank: [loff[a], loff[a+1])
     E.npr = 0;
     uint64_t np = 0, cap_s = 0;
-    // Every global read has ~1/P of its occurrences here.  Per-read regions
-    // (one wave per read, as the single-device first pass, over the read's
-    // local occurrences [loff[a], loff[a + 1])) with every distinct partial kept
-    // (count >= 1: the filter needs the global sums): the list comes out lead-
-    // descending, so each owner's partials are one contiguous range -- no owner
-    // sort, no per-block output claims.  Regions beyond 32 GB (or
-    // SA_SHARD_MULTI=1, A/B runs): multi-read blocks over ~PCM_TARGET local
-    // occurrences, partials sorted by owner.
-    // (round 4, 8 serial virtual shards of the bench shape: per-read regions
-    // 2.55 ms of pair counting per step against 1.55 for multi-read blocks -- a
-    // read has ~60 local occurrences, too few to pay for a wave's table setup
-    // and region ranking; SA_SHARD_PER_READ=1 runs them for A/B)
-    static const bool per_read_on = getenv("SA_SHARD_PER_READ") && atoi(getenv("SA_SHARD_PER_READ")) != 0;
-    bool per_read = per_read_on && (uint64_t)N * PC_RREG * sizeof(uint2) <= (32ull << 30);
-    uint64_t np_ub = 0;
-    if (per_read) {
-        rc = pair_stage(c, E, PI, false, false, nullptr, N, cnt, np, cap_s, nullptr, 0, nullptr, nullptr, &per_read,
-                        &np_ub, true);
-        if (rc) return rc;
-    }
-    c->part_per_read = per_read;
-    if (per_read) {
-        int32_t *dl, *dt, *dc;
-        uint64_t *q;
-        ENSURE(c->d_bounds, (size_t)c->nranks + 1, &q);
-        {
-            StageScope st(c, SA_STAGE_ORDER);
-            if ((rc = assemble_read_regions(c, N, np, np_ub, cap_s, cnt, &dl, &dt, &dc))) return rc;
-            HIPCHK(launch_desc_owner_bounds(dl, &cnt->rtotal, (const uint32_t *)c->d_starts.p, (uint32_t)c->nranks, q,
-                                            c->stream));
-        }
-        Counters hc;
-        c->part_q.assign((size_t)c->nranks + 1, 0);
-        HIPCHK(hipMemcpyAsync(&hc, cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipMemcpyAsync(c->part_q.data(), q, c->part_q.size() * 8, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
-        resolve_timing(c);
-        for (int o = 0; o < c->nranks; ++o) counts[o] = c->part_q[o] - c->part_q[o + 1];
-        c->part_np = hc.rtotal;
-        c->part_perm = nullptr;
-        c->stats.buckets = shard_sum(hc.bkt_counts) + big_buckets;
-        c->stats.role_pairs = shard_sum(hc.role_pairs);
-        return SA_OK;
-    }
-    // one wave per ~PMW_TARGET local occurrences (SA_SHARD_BLOCKS=1: the
-    // 256-thread multi-read blocks over ~PCM_TARGET, for A/B runs)
-    static const bool blocks_forced = getenv("SA_SHARD_BLOCKS") && atoi(getenv("SA_SHARD_BLOCKS")) != 0;
-    c->multi_wave_items = !blocks_forced;
-    const uint32_t target = c->multi_wave_items ? PMW_TARGET : PCM_TARGET;
+    // Every global read has ~1/P of its occurrences here (~60 of a 500 bp read
+    // at P = 8): one wave per ~PMW_TARGET local occurrences (a few consecutive
+    // reads), every distinct partial kept (count >= 1: the filter needs the
+    // global sums), written straight into the regions of the rank owning its
+    // lead -- the send buffers are then one copy of the regions, owner-major.
+    // (round 4, 8 serial virtual shards of the bench shape: one wave per read
+    // counted in 2.55 ms per step against 1.55 for multi-read items -- a read's
+    // ~60 local occurrences do not pay for a wave's table setup; and partials
+    // sorted by owner after the count cost an order stage of 0.3 ms more)
+    const uint32_t target = PMW_TARGET;
     const uint32_t n_multi = (uint32_t)((n + target - 1) / target) + 1;
     uint32_t *items;
-    ENSURE(c->d_items, (size_t)n_multi + 1, &items);
+    ENSURE(c->d_items, 2 * ((size_t)n_multi + 1), &items);
     HIPCHK(launch_pc_items(loff, N, target, n_multi, items, c->stream));
-    rc = pair_stage(c, E, PI, false, true, nullptr, N, cnt, np, cap_s, items, n_multi);
+    if (P > 1)
+        HIPCHK(launch_pc_item_owners(items, n_multi, (const uint32_t *)c->d_starts.p, (uint32_t)P, items + n_multi + 1,
+                                     c->stream));
+    rc = pair_stage(c, E, PI, false, true, nullptr, N, cnt, np, cap_s, items, n_multi, nullptr, nullptr, nullptr,
+                    nullptr, (uint32_t)P, (const uint32_t *)c->d_starts.p, items + n_multi + 1);
     if (rc) return rc;
-    // partials grouped by the rank owning their lead (one stable pass on the
-    // owner id; the owner's reduce sorts them)
-    uint64_t *ok, *ok2; uint32_t *ov, *ov2; uint8_t *otmp; uint64_t *bounds;
-    ENSURE(c->d_okeys, np, &ok);
-    ENSURE(c->d_okeys2, np, &ok2);
-    ENSURE(c->d_ovals, np, &ov);
-    ENSURE(c->d_ovals2, np, &ov2);
-    ENSURE(c->d_osort, radix_sort_temp_bytes(np), &otmp);
-    ENSURE(c->d_bounds, (size_t)c->nranks + 1, &bounds);
-    const int idb = bits_for(N ? N - 1 : 0);
-    std::vector<uint64_t> b((size_t)c->nranks + 1, 0);
-    {
-        StageScope st(c, SA_STAGE_ORDER);
-        HIPCHK(launch_make_order_keys((const uint32_t *)c->d_pf.p, (const uint32_t *)c->d_ps.p, nullptr, cnt->cursor,
-                                      cap_s, 3, idb, ok, ov, cnt->shard_off, c->stream,
-                                      (const uint32_t *)c->d_starts.p, (uint32_t)c->nranks));
-        HIPCHK(radix_sort(&ok, &ov, &ok2, &ov2, np, 0, std::max(c->log_ranks, 1), otmp, c->stream));
-        if (np) HIPCHK(launch_owner_bounds(ok, np, 0, (uint32_t)c->nranks, bounds, c->stream));
-    }
     Counters hc;
     HIPCHK(hipMemcpyAsync(&hc, cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
-    if (np) HIPCHK(hipMemcpyAsync(b.data(), bounds, b.size() * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     resolve_timing(c);
-    b[c->nranks] = np;
-    for (int o = 0; o < c->nranks; ++o) counts[o] = b[o + 1] - b[o];
-    c->part_np = np;
-    c->part_perm = ov;
+    // owner o's partials: its NSHARD regions (one rank: the plain NSHARD regions)
+    const std::vector<unsigned long long> fill =
+        P > 1 ? c->ocur : std::vector<unsigned long long>(hc.cursor, hc.cursor + NSHARD);
+    c->part_off.assign(fill.size() + 1, 0);
+    for (int o = 0; o < P; ++o) counts[o] = 0;
+    uint64_t acc = 0;
+    for (size_t r = 0; r < fill.size(); ++r) {
+        const uint64_t f = std::min<unsigned long long>(fill[r], cap_s);
+        c->part_off[r] = acc;
+        acc += f;
+        counts[r / NSHARD] += f;
+    }
+    c->part_off[fill.size()] = acc;
+    c->part_np = acc;
+    c->part_cap = cap_s;
     c->stats.buckets = shard_sum(hc.bkt_counts) + big_buckets;
     c->stats.role_pairs = shard_sum(hc.role_pairs);
     return SA_OK;
@@ -2206,29 +2196,18 @@ int sa_dist_partials(sa_ctx *c, void *fst, void *snd, void *cnt_out) {
     if (!c->dist) return fail(c, SA_E_STATE, "sa_dist_init first");
     if (c->part_np && (!fst || !snd || !cnt_out)) return SA_E_ARG;
     (void)hipSetDevice(c->device);
-    if (c->part_per_read) {
-        // owners ascending: owner o's partials [part_q[o + 1], part_q[o]) of the
-        // lead-descending list go to out[oo[o] ..]
-        const uint32_t P = (uint32_t)c->nranks;
-        std::vector<uint64_t> oq(2 * ((size_t)P + 1));
-        uint64_t acc = 0;
-        for (uint32_t o = 0; o <= P; ++o) {
-            oq[o] = c->part_q[o];
-            oq[P + 1 + o] = acc;
-            if (o < P) acc += c->part_q[o] - c->part_q[o + 1];
-        }
-        uint64_t *doq;
-        ENSURE(c->d_pq, oq.size(), &doq);
-        HIPCHK(hipMemcpyAsync(doq, oq.data(), oq.size() * 8, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(launch_copy_partials((const int32_t *)c->d_lead.p, (const int32_t *)c->d_trail.p,
-                                    (const int32_t *)c->d_count.p, c->part_np, doq, P, (uint32_t *)fst, (uint32_t *)snd,
-                                    (uint32_t *)cnt_out, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
-        return SA_OK;
-    }
-    HIPCHK(launch_gather_partials(c->part_perm, c->part_np, (const uint32_t *)c->d_pf.p, (const uint32_t *)c->d_ps.p,
-                                  (const uint32_t *)c->d_pc.p, (uint32_t *)fst, (uint32_t *)snd, (uint32_t *)cnt_out,
-                                  c->stream));
+    // the owner regions, concatenated owner-major: the send buffers of exchange 2
+    const uint32_t nreg = (uint32_t)c->part_off.size() - 1;
+    uint64_t *doff;
+    ENSURE(c->d_pq, c->part_off.size(), &doff);
+    HIPCHK(hipMemcpyAsync(doff, c->part_off.data(), c->part_off.size() * 8, hipMemcpyHostToDevice, c->stream));
+    const unsigned long long *dcur = nreg > NSHARD ? (const unsigned long long *)c->d_ocur.p : nullptr;
+    Counters *cnt;
+    ENSURE(c->d_cnt, 1, &cnt);
+    if (!dcur) dcur = cnt->cursor;
+    HIPCHK(launch_copy_owner_regions((const uint32_t *)c->d_pf.p, (const uint32_t *)c->d_ps.p,
+                                     (const uint32_t *)c->d_pc.p, c->part_cap, nreg, dcur, doff, (uint32_t *)fst,
+                                     (uint32_t *)snd, (uint32_t *)cnt_out, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return SA_OK;
 }

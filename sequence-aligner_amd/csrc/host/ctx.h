@@ -117,14 +117,14 @@ struct sa_ctx {
     uint32_t gnpr = 0;               // uniform k-mers per read over all reads (0: mixed)
     int32_t gmaxL = 0, gminL = 0;
     uint64_t part_np = 0;            // partial pairs after sa_dist_count
-    uint32_t *part_perm = nullptr;   // their ascending-lead order (region-space indices)
-    // per-read mode (part_perm unused): the partials are d_lead / d_trail /
-    // d_count, lead descending; owner o's are [part_q[o + 1], part_q[o])
-    bool part_per_read = false;
-    bool multi_wave_items = true;    // sharded pair count: wave per item (else 256-thread blocks)
-    std::vector<uint64_t> part_q;
+    // ... in owner-major regions of part_cap entries (d_pf / d_ps / d_pc; fill
+    // in d_ocur / ocur, or the Counters cursors with one rank): region r's go
+    // to part_off[r] of the send buffers
+    unsigned long long part_cap = 0;
+    std::vector<uint64_t> part_off;
+    std::vector<unsigned long long> ocur;
     DBuf d_gocc, d_seg, d_rl, d_srl, d_srl2, d_loff, d_starts, d_bounds, d_gcodes, d_gwoff, d_glen, d_gbad, d_psum, d_pkeep, d_ppos;
-    DBuf d_scan, d_bigtot, d_items, d_pq;
+    DBuf d_scan, d_bigtot, d_items, d_pq, d_ocur;
     DBuf d_lr;                       // owner-side reduce by lead: counts, offsets, cursors, kept, kept scan
     // k-mer table statistics (sa_kmer_histogram)
     DBuf d_hk0, d_hk1, d_hflag, d_hidx, d_hpos, d_htmp, d_hist, d_hovf, d_hsmall;

@@ -121,16 +121,6 @@ __global__ void owner_bounds_kernel(const uint64_t *keys, uint64_t n, int shift,
     bounds[o] = lo;
 }
 
-__global__ void gather_partials_kernel(const uint32_t *perm, uint64_t n, const uint32_t *fst, const uint32_t *snd,
-                                       const uint32_t *cnt, uint32_t *of, uint32_t *os, uint32_t *oc) {
-    const uint64_t i = (uint64_t)blockIdx.x * DT + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t j = perm[i];
-    of[i] = fst[j];
-    os[i] = snd[j];
-    oc[i] = cnt[j];
-}
-
 // received partials -> keys in the wide canonical order (lead desc, trail asc)
 __global__ void reduce_keys_kernel(const uint32_t *fst, const uint32_t *snd, uint64_t n, int idb, uint64_t *keys,
                                    uint32_t *vals) {
@@ -475,59 +465,26 @@ hipError_t launch_owner_bounds(const uint64_t *keys, uint64_t n, int shift, uint
     return hipGetLastError();
 }
 
-// per-read partials (lead descending, 1-based ids, *n_dev entries): q[o] =
-// entries whose 0-based lead is >= starts[o], o in [0, P] -- owner o's partials
-// are [q[o + 1], q[o])
-__global__ void desc_owner_bounds_kernel(const int32_t *lead, const uint32_t *n_dev, const uint32_t *starts,
-                                         uint32_t P, uint64_t *q) {
-    const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
-    if (o > P) return;
-    const uint32_t t = starts[o];
-    uint64_t lo = 0, hi = *n_dev;  // first i with lead[i] - 1 < t
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if ((uint32_t)(lead[mid] - 1) >= t) lo = mid + 1; else hi = mid;
+// the owner regions concatenated: one block per region, its entries in order
+__global__ void copy_owner_regions_kernel(const uint32_t *fst, const uint32_t *snd, const uint32_t *cnt,
+                                          unsigned long long cap_s, const unsigned long long *cursor,
+                                          const uint64_t *off, uint32_t *of, uint32_t *os, uint32_t *oc) {
+    const uint32_t r = blockIdx.x;
+    const unsigned long long m = min(cursor[r], cap_s), src = (unsigned long long)r * cap_s;
+    const uint64_t dst = off[r];
+    for (unsigned long long j = threadIdx.x; j < m; j += DT) {
+        of[dst + j] = fst[src + j];
+        os[dst + j] = snd[src + j];
+        oc[dst + j] = cnt[src + j];
     }
-    q[o] = lo;
 }
 
-hipError_t launch_desc_owner_bounds(const int32_t *lead, const uint32_t *n_dev, const uint32_t *starts, uint32_t P,
-                                    uint64_t *q, hipStream_t s) {
-    hipLaunchKernelGGL(desc_owner_bounds_kernel, dim3((P + 1 + 255) / 256), dim3(256), 0, s, lead, n_dev, starts, P, q);
-    return hipGetLastError();
-}
-
-// the send buffers of exchange 2 from the per-read partials: owners ascending
-// (owner o's partials at out[oo[o] ..], taken from [q[o + 1], q[o]) of the
-// lead-descending list), ids back to 0-based; oq = {q[0..P], oo[0..P]}
-__global__ void copy_partials_kernel(const int32_t *lead, const int32_t *trail, const int32_t *count, uint64_t n,
-                                     const uint64_t *oq, uint32_t P, uint32_t *of, uint32_t *os, uint32_t *oc) {
-    const uint64_t i = (uint64_t)blockIdx.x * DT + threadIdx.x;
-    if (i >= n) return;
-    const uint64_t *q = oq, *oo = oq + P + 1;
-    uint32_t lo = 0, hi = P;  // largest o with oo[o] <= i
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (oo[mid] <= i) lo = mid; else hi = mid;
-    }
-    const uint64_t j = q[lo + 1] + (i - oo[lo]);
-    of[i] = (uint32_t)(lead[j] - 1);
-    os[i] = (uint32_t)(trail[j] - 1);
-    oc[i] = (uint32_t)count[j];
-}
-
-hipError_t launch_copy_partials(const int32_t *lead, const int32_t *trail, const int32_t *count, uint64_t n,
-                                const uint64_t *oq, uint32_t P, uint32_t *of, uint32_t *os, uint32_t *oc,
-                                hipStream_t s) {
-    if (!n) return hipSuccess;
-    hipLaunchKernelGGL(copy_partials_kernel, grid_for(n), dim3(DT), 0, s, lead, trail, count, n, oq, P, of, os, oc);
-    return hipGetLastError();
-}
-
-hipError_t launch_gather_partials(const uint32_t *perm, uint64_t n, const uint32_t *fst, const uint32_t *snd,
-                                  const uint32_t *cnt, uint32_t *of, uint32_t *os, uint32_t *oc, hipStream_t s) {
-    if (!n) return hipSuccess;
-    hipLaunchKernelGGL(gather_partials_kernel, grid_for(n), dim3(DT), 0, s, perm, n, fst, snd, cnt, of, os, oc);
+hipError_t launch_copy_owner_regions(const uint32_t *fst, const uint32_t *snd, const uint32_t *cnt,
+                                     unsigned long long cap_s, uint32_t n_regions, const unsigned long long *cursor,
+                                     const uint64_t *off, uint32_t *of, uint32_t *os, uint32_t *oc, hipStream_t s) {
+    if (!n_regions) return hipSuccess;
+    hipLaunchKernelGGL(copy_owner_regions_kernel, dim3(n_regions), dim3(DT), 0, s, fst, snd, cnt, cap_s, cursor, off,
+                       of, os, oc);
     return hipGetLastError();
 }
 

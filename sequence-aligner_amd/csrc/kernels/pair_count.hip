@@ -58,6 +58,16 @@ __device__ __forceinline__ uint32_t pc_hash(uint32_t p) {
     return (p * 0x9E3779B1u) >> (32 - __builtin_ctz((unsigned)TAB));
 }
 
+// the rank owning read a: largest o with starts[o] <= a (owners ranks, starts[owners] = reads)
+__device__ __forceinline__ uint32_t owner_of(const uint32_t *starts, uint32_t owners, uint32_t a) {
+    uint32_t lo = 0, hi = owners;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (starts[mid] <= a) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
 // Elements (role pairs) of a chunk are enumerated in windows of PC_WIN; eo[e]
 // = 1 + the occurrence holding element w0 + e, filled by the thread owning the
 // occurrence (its element range is in its registers: no scan, one barrier).
@@ -473,7 +483,9 @@ __global__ __launch_bounds__(PcShape<TAB>::NT) void pair_count_kernel(EmitParams
     //     wave scans, one claim per block, two barriers per chunk
     constexpr int PER = TAB / NT;
     constexpr int CH = PER < 32 ? PER : 32;
-    const unsigned long long region = (unsigned long long)shard * o.cap_s;
+    // (sharded: the regions of the rank owning read a)
+    const uint32_t rslot = o.owners > 1 ? owner_of(o.owner_starts, o.owners, a) * NSHARD + shard : shard;
+    const unsigned long long region = (unsigned long long)rslot * o.cap_s;
     const int lane = tid & 63, wvi = tid >> 6;
     for (int c0 = 0; c0 < PER; c0 += CH) {
         uint32_t keep = 0;
@@ -504,7 +516,7 @@ __global__ __launch_bounds__(PcShape<TAB>::NT) void pair_count_kernel(EmitParams
             if (q < wvi) ex += v;
         }
         if (total == 0) continue;  // uniform: every thread sees the same total
-        if (tid == 0) S.emit_base[buf] = (uint32_t)atomicAdd(&o.cursor[shard], (unsigned long long)total);
+        if (tid == 0) S.emit_base[buf] = (uint32_t)atomicAdd(&o.cursor[rslot], (unsigned long long)total);
         __syncthreads();
         const unsigned long long base = (unsigned long long)S.emit_base[buf] + ex;
         uint32_t k = 0;
@@ -872,192 +884,17 @@ hipError_t launch_pair_count(const EmitParams &e, const PairIn &in, const PairPa
     return hipErrorInvalidValue;
 }
 
-// ---------------------------------------------------------------------------
-// Multi-read blocks (sharded hash stage).  With P ranks every rank counts
-// partial pairs for ALL global reads over its 1/P of the buckets, so a read has
-// ~L/P local occurrences and one-read blocks would be mostly barrier latency
-// (P x 100k blocks of ~60 occurrences at P = 8).  Here a block takes the range
-// of consecutive reads [item_start[b], item_start[b+1]) holding ~PCM_TARGET
-// local occurrences and keys its LDS table by (a, partner) in 64 bits;
-// enumeration and emission are as above.  A block whose table fills appends
-// its reads to the overflow list: they are recounted one read per block.
-// ---------------------------------------------------------------------------
-constexpr int PCM_TAB = 1024;
+// Multi-read items (sharded hash stage): keys are (read, partner) in 64 bits
 constexpr unsigned long long PCM_EMPTY = ~0ull;
-
-struct PcmShared {
-    unsigned long long key[PCM_TAB];
-    uint32_t cnt[PCM_TAB];
-    uint32_t pref[PC_CHUNK + 1];
-    uint4 rec[PC_CHUNK];
-    uint32_t aid[PC_CHUNK];    // read of each occurrence of the chunk
-    uint16_t eo[PC_WIN];       // element -> occurrence (+1) of the current window (as in pair_count_kernel)
-    uint32_t lds4[PC_THREADS / 64];
-    uint32_t fill, overflow, out_base;
-};
 
 __device__ __forceinline__ uint32_t pcm_hash(unsigned long long k) {
     const uint32_t x = ((uint32_t)k * 0x9E3779B1u) ^ ((uint32_t)(k >> 32) * 0x85EBCA77u);
-    return x >> (32 - 10);  // log2(PCM_TAB)
-}
-
-__device__ __forceinline__ void pcm_insert(PcmShared &S, unsigned long long key, uint32_t w) {
-    constexpr uint32_t FILL_MAX = PCM_TAB * 3 / 4;
-    uint32_t slot = pcm_hash(key);
-    for (int probe = 0; probe < PC_PROBE_MAX; ++probe) {  // bounded as in pc_insert
-        unsigned long long old = lds_relaxed(&S.key[slot]);  // final once set (pc_insert)
-        if (old == PCM_EMPTY) old = atomicCAS(&S.key[slot], PCM_EMPTY, key);
-        if (old == PCM_EMPTY || old == key) {
-            if (old == PCM_EMPTY && atomicAdd(&S.fill, 1u) >= FILL_MAX) S.overflow = 1;
-            atomicAdd(&S.cnt[slot], w);
-            return;
-        }
-        slot = (slot + 1) & (PCM_TAB - 1);
-    }
-    S.overflow = 1;
-}
-
-__global__ __launch_bounds__(PC_THREADS) void pair_count_multi_kernel(EmitParams e, PairIn in, PairParams p,
-                                                                      PairOut o, const uint32_t *item_start) {
-    extern __shared__ __align__(16) uint8_t smem[];
-    PcmShared &S = *reinterpret_cast<PcmShared *>(smem);
-    const int tid = threadIdx.x;
-    const uint32_t bid = blockIdx.x;
-    if (bid >= p.n_items) return;
-    const uint32_t ra = item_start[bid], rb = item_start[bid + 1];
-    if (ra >= rb) return;  // whole block: before any barrier
-    for (int i = tid; i < PCM_TAB; i += PC_THREADS) {
-        S.key[i] = PCM_EMPTY;
-        S.cnt[i] = 0;
-    }
-    if (tid == 0) { S.fill = 0; S.overflow = 0; }
-    const uint64_t g0 = e.occ_off[ra];
-    const uint32_t nocc = (uint32_t)(e.occ_off[rb] - g0);
-    unsigned long long role_pairs = 0;
-    __syncthreads();
-
-    for (uint32_t c0 = 0; c0 < nocc; c0 += PC_CHUNK) {
-        const uint32_t cn = min((uint32_t)PC_CHUNK, nocc - c0);
-        constexpr int PER = PC_CHUNK / PC_THREADS;
-        uint32_t mytot[PER];
-#pragma unroll
-        for (int j = 0; j < PER; ++j) {
-            const uint32_t oi = tid * PER + j;  // thread-contiguous
-            uint32_t tot = 0;
-            if (oi < cn) {
-                const uint64_t g = g0 + c0 + oi;
-                const uint4 rc = load_rec(in, g);
-                S.rec[oi] = rc;
-                tot = (rc.y & 0x3FFFFFFFu) + rc.w;
-                uint32_t lo = ra, hi = rb;  // owning read: largest r with occ_off[r] <= g
-                while (hi - lo > 1) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (e.occ_off[mid] <= g) lo = mid; else hi = mid;
-                }
-                S.aid[oi] = lo;
-            }
-            mytot[j] = tot;
-        }
-        uint32_t sum = 0;
-#pragma unroll
-        for (int j = 0; j < PER; ++j) sum += mytot[j];
-        uint32_t total;
-        uint32_t ex = pc_block_excl_scan(sum, S.lds4, &total);
-        uint32_t myex[PER];
-#pragma unroll
-        for (int j = 0; j < PER; ++j) {
-            const uint32_t oi = tid * PER + j;
-            if (oi <= cn) S.pref[oi] = ex;
-            myex[j] = ex;
-            ex += mytot[j];
-        }
-        if (tid == PC_THREADS - 1 && cn == PC_CHUNK) S.pref[PC_CHUNK] = total;
-        role_pairs += total;
-
-        // lane-interleaved enumeration over windows, as in pair_count_kernel
-        for (uint32_t w0 = 0; w0 < total; w0 += PC_WIN) {
-            __syncthreads();  // pref / rec / aid written; the previous window's eo consumed
-            if (S.overflow) break;  // (an overflowed table: totals only, the reads are recounted)
-#pragma unroll
-            for (int j = 0; j < PER; ++j) {
-                const uint32_t e0 = max(myex[j], w0), e1 = min(myex[j] + mytot[j], w0 + (uint32_t)PC_WIN);
-                const uint16_t v = (uint16_t)(tid * PER + j + 1);
-                for (uint32_t el = e0; el < e1; ++el) S.eo[el - w0] = v;
-            }
-            __syncthreads();
-            const uint32_t wn = min((uint32_t)PC_WIN, total - w0);
-            for (uint32_t e0 = 0; e0 < wn; e0 += PC_THREADS * PC_BATCH) {
-                uint32_t part[PC_BATCH], wv[PC_BATCH], own[PC_BATCH];
-#pragma unroll
-                for (int bb = 0; bb < PC_BATCH; ++bb) {
-                    part[bb] = 0;
-                    wv[bb] = 0;  // 0: no role pair in this slot
-                    own[bb] = 0;
-                    const uint32_t el = e0 + bb * PC_THREADS + tid;
-                    if (el < wn) {
-                        const uint32_t oi = (uint32_t)S.eo[el] - 1u;
-                        const uint32_t off = w0 + el - S.pref[oi];
-                        const uint4 rc = S.rec[oi];
-                        const uint32_t nE = rc.y & 0x3FFFFFFFu;
-                        own[bb] = S.aid[oi];
-                        part[bb] = in.lst[rec_entry(rc, off)];
-                        wv[bb] = off < nE ? rc.y >> 30 : 1u;
-                    }
-                }
-#pragma unroll
-                for (int bb = 0; bb < PC_BATCH; ++bb) {
-                    if (wv[bb] == 0 || part[bb] == own[bb]) continue;  // same read (KmerTable.scala:61-63)
-                    pcm_insert(S, ((unsigned long long)own[bb] << 32) | part[bb], wv[bb]);
-                }
-                if (S.overflow) break;
-            }
-        }
-        __syncthreads();
-    }
-
-    const uint32_t shard = bid % NSHARD;
-    if (tid == 0 && role_pairs) atomicAdd(&o.role_pairs[shard], role_pairs);
-    if (S.overflow) {  // recount these reads one per block (2,048 slots, then the split)
-        if (tid == 0) S.out_base = atomicAdd(o.overflow_n, rb - ra);
-        __syncthreads();
-        for (uint32_t r = tid; r < rb - ra; r += PC_THREADS) o.overflow_list[S.out_base + r] = (ra + r) << 6;
-        return;
-    }
-    if (tid == 0) atomicAdd(&o.distinct[shard], (unsigned long long)S.fill);
-    constexpr int PERT = PCM_TAB / PC_THREADS;
-    uint32_t keep = 0;
-#pragma unroll
-    for (int j = 0; j < PERT; ++j) {
-        const uint32_t sl = tid * PERT + j;
-        const uint32_t c = S.cnt[sl];
-        if (S.key[sl] != PCM_EMPTY && (p.emit_all || ((int32_t)c >= p.min_coll && (int32_t)c <= p.max_coll)))
-            keep |= 1u << j;
-    }
-    uint32_t total;
-    uint32_t ex = pc_block_excl_scan(__popc(keep), S.lds4, &total);
-    if (total == 0) return;
-    if (tid == 0) S.out_base = (uint32_t)atomicAdd(&o.cursor[shard], (unsigned long long)total);
-    __syncthreads();
-    const unsigned long long base = (unsigned long long)S.out_base + ex;
-    const unsigned long long region = (unsigned long long)shard * o.cap_s;
-    uint32_t k = 0;
-#pragma unroll
-    for (int j = 0; j < PERT; ++j) {
-        if (!(keep & (1u << j))) continue;
-        const uint32_t sl = tid * PERT + j;
-        const unsigned long long lat = base + k++;
-        if (lat < o.cap_s) {
-            const unsigned long long at = region + lat;
-            o.fst[at] = (uint32_t)(S.key[sl] >> 32);
-            o.snd[at] = (uint32_t)S.key[sl];
-            o.cnt[at] = S.cnt[sl];
-        }
-    }
+    return x >> (32 - 10);
 }
 
 // ---------------------------------------------------------------------------
-// Multi-read items, one WAVE each (sharded hash stage, round 4).  The block
-// form above runs ~16 block barriers per 512-occurrence item; here a 256-thread
+// Multi-read items, one WAVE each (sharded hash stage, round 4).  A 256-thread
+// block form ran ~16 block barriers per 512-occurrence item; here a 256-thread
 // block carries four items of ~PMW_TARGET local occurrences (a few reads), one
 // per wave, with the single-device wave kernel's hand-offs (wave barriers,
 // marker + max-scan element map, per-occurrence list bases) and a wave-private
@@ -1065,8 +902,11 @@ __global__ __launch_bounds__(PC_THREADS) void pair_count_multi_kernel(EmitParams
 // (count >= 1: the filter needs the global sums).  Output claims are made once
 // per BLOCK: the four waves' kept counts are scanned at one block barrier and
 // one device atomic claims the block's range (a claim per item made the wave
-// form slower than the blocks in round 3).  An item whose table fills appends
-// its reads to the overflow list for the recount tiers.
+// form slower than the blocks in round 3).  With several ranks (PairOut::owners)
+// the claim is per block AND owner of the lead, into that owner's regions, so
+// the partials leave grouped by destination rank with no sort (a block's reads
+// are consecutive, so nearly every block has one owner).  An item whose table
+// fills appends its reads to the overflow list for the recount tiers.
 // ---------------------------------------------------------------------------
 constexpr int PMW_WAVES = 4;
 constexpr int PMW_TAB = 256;
@@ -1085,8 +925,15 @@ struct PmwShared {  // one per wave
     uint32_t fill, overflow, kept, pad;
 };
 
+#ifndef PMW_FASTPATH
+#define PMW_FASTPATH 0  // (8 serial shards: pairs 1.455-1.468 ms without, 1.481-1.501 with)
+#endif
 __device__ __forceinline__ void pmw_insert(PmwShared &S, unsigned long long key, uint32_t w) {
     uint32_t slot = pcm_hash(key) >> 2;  // (pcm_hash: 10 bits)
+    if (PMW_FASTPATH && lds_relaxed(&S.key[slot]) == key) {  // the home-slot hit: no probe loop
+        atomicAdd(&S.cnt[slot], w);
+        return;
+    }
     for (int probe = 0; probe < PMW_TAB / 4; ++probe) {
         unsigned long long old = lds_relaxed(&S.key[slot]);  // final once set
         if (old == PCM_EMPTY) old = atomicCAS(&S.key[slot], PCM_EMPTY, key);
@@ -1104,13 +951,14 @@ __global__ __launch_bounds__(PMW_WAVES * 64) void pair_count_multi_wave_kernel(E
                                                                                 PairOut o,
                                                                                 const uint32_t *item_start) {
     __shared__ PmwShared SH[PMW_WAVES];
-    __shared__ uint32_t wkept[PMW_WAVES], blk_base;
+    __shared__ uint32_t wkept[PMW_WAVES], wlast[PMW_WAVES], blk_base;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     PmwShared &S = SH[wv];
     const uint32_t item = blockIdx.x * PMW_WAVES + wv;
     // (no early return: every wave reaches the block's output claim)
     const bool live = item < p.n_items;
     const uint32_t ra = live ? item_start[item] : 0u, rb = live ? item_start[item + 1] : 0u;
+    const uint32_t own2 = live && o.owners > 1 ? o.item_owner[item] : 0u;  // (lo | hi << 16, pc_item_owners)
     for (int i = lane; i < PMW_TAB; i += 64) {
         S.key[i] = PCM_EMPTY;
         S.cnt[i] = 0;
@@ -1244,40 +1092,70 @@ __global__ __launch_bounds__(PMW_WAVES * 64) void pair_count_multi_wave_kernel(E
         for (uint32_t r = ra; r < rb; ++r) o.overflow_list[at + (r - ra)] = r << 6;
     }
     // kept keys of this wave (none when it overflowed), then one claim per block
+    // and owner: the block's reads [first, last] span the owners [o_lo, o_hi]
     uint32_t keep = 0;
 #pragma unroll
     for (int j = 0; j < PMW_TAB / 64; ++j) {
         const uint32_t sl = lane * (PMW_TAB / 64) + j;
         if (live && !over && S.key[sl] != PCM_EMPTY) keep |= 1u << j;
     }
-    const uint32_t mine = __popc(keep);
-    const uint32_t winc = wave_incl_add(mine);
-    if (lane == 63) wkept[wv] = winc;
     if (live && !over && lane == 0) atomicAdd(&o.distinct[shard], (unsigned long long)lds_relaxed(&S.fill));
-    __syncthreads();
-    uint32_t btot = 0, wex = 0;
-#pragma unroll
-    for (int q = 0; q < PMW_WAVES; ++q) {
-        const uint32_t x = wkept[q];
-        if (q < wv) wex += x;
-        btot += x;
-    }
-    if (threadIdx.x == 0) blk_base = btot ? (uint32_t)atomicAdd(&o.cursor[shard], (unsigned long long)btot) : 0u;
-    __syncthreads();
-    if (!mine) return;
-    const unsigned long long region = (unsigned long long)shard * o.cap_s;
-    unsigned long long lat = (unsigned long long)blk_base + wex + (winc - mine);
-#pragma unroll
-    for (int j = 0; j < PMW_TAB / 64; ++j) {
-        if (!(keep & (1u << j))) continue;
-        const uint32_t sl = lane * (PMW_TAB / 64) + j;
-        if (lat < o.cap_s) {
-            const unsigned long long at = region + lat;
-            o.fst[at] = (uint32_t)(S.key[sl] >> 32);
-            o.snd[at] = (uint32_t)S.key[sl];
-            o.cnt[at] = S.cnt[sl];
+    uint32_t o_lo = 0, o_hi = 0;
+    if (o.owners > 1) {
+        if (lane == 0) {
+            wkept[wv] = live && ra < rb ? (own2 & 0xFFFFu) : 0xFFFFFFFFu;
+            wlast[wv] = live && ra < rb ? (own2 >> 16) : 0u;
         }
-        ++lat;
+        __syncthreads();
+        o_lo = 0xFFFFFFFFu;
+#pragma unroll
+        for (int q = 0; q < PMW_WAVES; ++q) {
+            o_lo = min(o_lo, wkept[q]);
+            o_hi = max(o_hi, wlast[q]);
+        }
+        if (o_lo == 0xFFFFFFFFu) o_lo = o_hi = 0;  // (no reads in the block: nothing kept)
+        __syncthreads();  // wkept is reused for the counts below
+    }
+    for (uint32_t ow = o_lo; ow <= o_hi; ++ow) {
+        uint32_t km = keep;
+        if (o_lo != o_hi && km) {  // a block across an owner boundary (rare): this owner's keys
+#pragma unroll
+            for (int j = 0; j < PMW_TAB / 64; ++j) {
+                const uint32_t sl = lane * (PMW_TAB / 64) + j;
+                if (((km >> j) & 1u) && owner_of(o.owner_starts, o.owners, (uint32_t)(S.key[sl] >> 32)) != ow)
+                    km &= ~(1u << j);
+            }
+        }
+        const uint32_t mine = __popc(km);
+        const uint32_t winc = wave_incl_add(mine);
+        if (lane == 63) wkept[wv] = winc;
+        __syncthreads();
+        uint32_t btot = 0, wex = 0;
+#pragma unroll
+        for (int q = 0; q < PMW_WAVES; ++q) {
+            const uint32_t x = wkept[q];
+            if (q < wv) wex += x;
+            btot += x;
+        }
+        const uint32_t rslot = ow * NSHARD + shard;
+        if (threadIdx.x == 0) blk_base = btot ? (uint32_t)atomicAdd(&o.cursor[rslot], (unsigned long long)btot) : 0u;
+        __syncthreads();
+        if (mine) {
+            const unsigned long long region = (unsigned long long)rslot * o.cap_s;
+            unsigned long long lat = (unsigned long long)blk_base + wex + (winc - mine);
+#pragma unroll
+            for (int j = 0; j < PMW_TAB / 64; ++j) {
+                if (!(km & (1u << j))) continue;
+                const uint32_t sl = lane * (PMW_TAB / 64) + j;
+                if (lat < o.cap_s) {
+                    const unsigned long long at = region + lat;
+                    o.fst[at] = (uint32_t)(S.key[sl] >> 32);
+                    o.snd[at] = (uint32_t)S.key[sl];
+                    o.cnt[at] = S.cnt[sl];
+                }
+                ++lat;
+            }
+        }
     }
 }
 
@@ -1291,15 +1169,6 @@ hipError_t launch_pair_count_multi_wave(const EmitParams &e, const PairIn &in, c
     return hipGetLastError();
 }
 
-hipError_t launch_pair_count_multi(const EmitParams &e, const PairIn &in, const PairParams &p, PairOut &o,
-                                   const uint32_t *item_start, uint32_t n_items, hipStream_t s) {
-    if (n_items == 0) return hipSuccess;
-    const size_t lds = sizeof(PcmShared);
-    (void)hipFuncSetAttribute((const void *)pair_count_multi_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    hipLaunchKernelGGL(pair_count_multi_kernel, dim3(n_items), dim3(PC_THREADS), lds, s, e, in, p, o, item_start);
-    return hipGetLastError();
-}
 
 // item j = reads [first read with occ_off >= j * target, same for j + 1)
 __global__ void pc_items_kernel(const uint64_t *occ_off, uint32_t n_reads, uint32_t target, uint32_t n_items,
@@ -1314,6 +1183,24 @@ __global__ void pc_items_kernel(const uint64_t *occ_off, uint32_t n_reads, uint3
         if (occ_off[mid] < t) lo = mid + 1; else hi = mid;
     }
     item_start[j] = lo;
+}
+
+// owners of item j's first and last read, lo | hi << 16 (sharded emission: no
+// search on the pair counter's critical path)
+__global__ void pc_item_owners_kernel(const uint32_t *item_start, uint32_t n_items, const uint32_t *starts,
+                                      uint32_t owners, uint32_t *item_owner) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_items) return;
+    const uint32_t ra = item_start[j], rb = item_start[j + 1];
+    item_owner[j] = ra < rb ? owner_of(starts, owners, ra) | (owner_of(starts, owners, rb - 1) << 16) : 0xFFFFu;
+}
+
+hipError_t launch_pc_item_owners(const uint32_t *item_start, uint32_t n_items, const uint32_t *starts, uint32_t owners,
+                                 uint32_t *item_owner, hipStream_t s) {
+    if (!n_items) return hipSuccess;
+    hipLaunchKernelGGL(pc_item_owners_kernel, dim3((n_items + 255) / 256), dim3(256), 0, s, item_start, n_items, starts,
+                       owners, item_owner);
+    return hipGetLastError();
 }
 
 hipError_t launch_pc_items(const uint64_t *occ_off, uint32_t n_reads, uint32_t target, uint32_t n_items,

@@ -281,14 +281,42 @@ struct RsShared {
 
 // (wave_peers: sa_internal.h)
 
-// VALS = false: key-only sort (records that carry their payload in the key)
-template <bool VALS, int RS_ITEMS, bool GEN = false>
+// a received record's read and loc rank (RecvGen; source s holds record i)
+__device__ __forceinline__ void recv_decode(const RecvGen &g, uint32_t s, uint64_t rec, uint32_t &r, uint32_t &lr) {
+    const uint32_t local = (uint32_t)rec;
+    uint32_t pos;
+    if (g.npr) {
+        // local / npr as the high word of local * magic (exact for local, npr < 2^32)
+        const uint32_t q = g.npr == 1 ? local : (uint32_t)__umul64hi((unsigned long long)local, g.npr_magic);
+        r = g.starts[s] + q;
+        pos = local - q * g.npr;
+    } else {
+        const uint64_t go = g.seg[g.P + 1 + s] + local;
+        uint32_t lo = g.starts[s], up = g.starts[s + 1];  // largest r with occ_off[r] <= go
+        while (up - lo > 1) {
+            const uint32_t mid = (lo + up) >> 1;
+            if (g.occ_off[mid] <= go) lo = mid; else up = mid;
+        }
+        r = lo;
+        pos = (uint32_t)(go - g.occ_off[r]);
+    }
+    lr = g.lrank[(g.npr ? g.lbase[g.npr - 1] : g.lbase[g.len[r] - g.k]) + pos];
+}
+// the source of record i: the last s with seg[s] <= i, from a lower bound s0
+__device__ __forceinline__ uint32_t recv_source(const RecvGen &g, uint32_t s0, uint64_t i) {
+    while (s0 + 1 < g.P && g.seg[s0 + 1] <= i) ++s0;
+    return s0;
+}
+
+// VALS = false: key-only sort (records that carry their payload in the key).
+// RECV: the values are generated from the keys (RecvGen, first pass only)
+template <bool VALS, int RS_ITEMS, bool GEN = false, bool RECV = false>
 __global__ __launch_bounds__(RsDown<RS_ITEMS>::THREADS) void rs_downsweep_kernel(const uint64_t *kin,
                                                                                  const uint32_t *vin, uint64_t *kout,
                                                                                  uint32_t *vout, uint64_t n, int shift,
                                                                                  const uint32_t *hist,
                                                                                  uint32_t nblocks, KeyGen kg,
-                                                                                 int nt_out) {
+                                                                                 int nt_out, RecvGen rg) {
     using D = RsDown<RS_ITEMS>;
     constexpr int RS_TILE = D::TILE, RS_SUB = D::SUB, RS_SLICES = D::SLICES, WAVES = D::WAVES, NT = D::THREADS;
     extern __shared__ __align__(16) uint8_t rs_smem[];
@@ -306,7 +334,45 @@ __global__ __launch_bounds__(RsDown<RS_ITEMS>::THREADS) void rs_downsweep_kernel
         const uint64_t i = sub + (uint64_t)j * 64 + lane;
         if constexpr (GEN) k[j] = i < n ? gen_key(kg, i) : ~0ull;
         else k[j] = i < n ? rs_load_key(kin + i) : ~0ull;
-        v[j] = (VALS && i < n) ? vin[i] : 0u;
+        if constexpr (!RECV) v[j] = (VALS && i < n) ? vin[i] : 0u;
+    }
+    if constexpr (RECV) {
+        // decode: the sub-tile's first source by a wave-uniform search, then
+        // stepped forward per slice and per lane past segment boundaries
+        uint32_t s = 0, hi = rg.P;
+        while (hi - s > 1) {
+            const uint32_t mid = (s + hi) >> 1;
+            if (rg.seg[mid] <= sub) s = mid; else hi = mid;
+        }
+        s = (uint32_t)__builtin_amdgcn_readfirstlane((int)s);
+        // read of the element before the sub-tile (loff boundaries at its start)
+        uint32_t rprev = 0xFFFFFFFFu;  // "read -1" before record 0
+        if (sub > 0 && sub <= n) {
+            const uint64_t ip = sub - 1;
+            uint32_t sp = s;
+            while (sp > 0 && rg.seg[sp] > ip) --sp;
+            uint32_t lrp;
+            recv_decode(rg, sp, rs_load_key(kin + ip), rprev, lrp);
+        }
+#pragma unroll
+        for (int j = 0; j < RS_SLICES; ++j) {
+            const uint64_t i = sub + (uint64_t)j * 64 + lane;
+            const bool valid = i < n;
+            s = (uint32_t)__builtin_amdgcn_readfirstlane((int)recv_source(rg, s, sub + (uint64_t)j * 64));
+            uint32_t r = 0, lr = 0;
+            if (valid) recv_decode(rg, recv_source(rg, s, i), k[j], r, lr);
+            v[j] = (r << rg.lb) | lr;
+            if (valid) k[j] = (k[j] & 0xFFFFFFFF00000000ull) | (uint32_t)i;
+            // loff[a] = i for the reads (read(i - 1), read(i)] (read(-1) = -1)
+            uint32_t prev = (uint32_t)__shfl_up((int)r, 1, 64);
+            if (lane == 0) prev = rprev;
+            rprev = (uint32_t)__builtin_amdgcn_readlane((int)r, 63);
+            if (valid) {
+                for (uint32_t a = prev + 1u; a <= r; ++a) rg.loff[a] = i;
+                if (i + 1 == n)  // the reads after the last record
+                    for (uint32_t a = r + 1u; a <= rg.n_reads; ++a) rg.loff[a] = n;
+            }
+        }
     }
 #pragma unroll
     for (int j = 0; j < RS_SLICES; ++j) {
@@ -493,7 +559,7 @@ static hipError_t rs_pass_keys(const uint64_t *kin, uint64_t *kout, uint64_t n, 
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((rs_downsweep_kernel<false, RS_ITEMS, GEN>), dim3((uint32_t)nb),
                        dim3(RsDown<RS_ITEMS>::THREADS), sizeof(SK), s, kin, nullptr, kout, nullptr, n, shift,
-                       (const uint32_t *)hist, (uint32_t)nb, kg, nt_out ? 1 : 0);
+                       (const uint32_t *)hist, (uint32_t)nb, kg, nt_out ? 1 : 0, RecvGen{});
     return hipGetLastError();
 }
 
@@ -536,11 +602,39 @@ hipError_t radix_sort(uint64_t **keys, uint32_t **vals, uint64_t **keys_alt, uin
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL((rs_downsweep_kernel<true, RS_ITEMS_VALS>), dim3((uint32_t)nb),
                            dim3(RsDown<RS_ITEMS_VALS>::THREADS), sizeof(SV), s, *keys, *vals, *keys_alt, *vals_alt, n,
-                           shift, (const uint32_t *)hist, (uint32_t)nb, KeyGen{}, 0);
+                           shift, (const uint32_t *)hist, (uint32_t)nb, KeyGen{}, 0, RecvGen{});
         uint32_t *tv = *vals; *vals = *vals_alt; *vals_alt = tv;
         uint64_t *tk = *keys; *keys = *keys_alt; *keys_alt = tk;
     }
     return hipGetLastError();
+}
+
+hipError_t radix_sort_recv(const RecvGen &g, uint64_t **keys, uint32_t **vals, uint64_t **keys_alt,
+                           uint32_t **vals_alt, uint64_t n, int lo, int hi, void *tmp, hipStream_t s) {
+    if (n == 0 || hi <= lo) return hipErrorInvalidValue;  // (the caller relabels without a sort)
+    constexpr int TV = RsTile<RS_ITEMS_VALS>::TILE;
+    using SV = RsShared<true, TV, RsDown<RS_ITEMS_VALS>::WAVES>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void *)rs_downsweep_kernel<true, RS_ITEMS_VALS, false, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(SV));
+        attr_set = true;
+    }
+    const uint64_t nb = (n + TV - 1) / TV;
+    uint32_t *hist = (uint32_t *)tmp;
+    void *stmp = (void *)(hist + 256 * nb);
+    // first pass: raw received records in, relabelled keys + generated values out
+    hipLaunchKernelGGL((rs_upsweep_kernel<RS_ITEMS_VALS>), dim3((uint32_t)nb), dim3(RsUp<RS_ITEMS_VALS>::THREADS), 0, s,
+                       *keys, n, lo, hist, (uint32_t)nb, KeyGen{});
+    hipError_t e = rs_offsets(hist, nb, stmp, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((rs_downsweep_kernel<true, RS_ITEMS_VALS, false, true>), dim3((uint32_t)nb),
+                       dim3(RsDown<RS_ITEMS_VALS>::THREADS), sizeof(SV), s, *keys, (const uint32_t *)nullptr, *keys_alt,
+                       *vals_alt, n, lo, (const uint32_t *)hist, (uint32_t)nb, KeyGen{}, 0, g);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    { uint32_t *tv = *vals; *vals = *vals_alt; *vals_alt = tv; }
+    { uint64_t *tk = *keys; *keys = *keys_alt; *keys_alt = tk; }
+    return lo + 8 < hi ? radix_sort(keys, vals, keys_alt, vals_alt, n, lo + 8, hi, tmp, s) : hipSuccess;
 }
 
 __global__ void gen_keys_kernel(KeyGen g, uint64_t n, uint64_t *keys) {

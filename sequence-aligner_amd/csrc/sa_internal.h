@@ -257,6 +257,12 @@ struct PairOut {
     // dispatch order (lead descending) is then one scan + one copy, no sort
     uint2 *rreg;                 // {trail, count}
     uint32_t *rcnt;
+    // sharded path (owners > 1): the partials leave grouped by the rank owning
+    // their lead -- region (owner * NSHARD + shard) of cap_s entries, cursor
+    // [owners * NSHARD]; owner o holds the reads [owner_starts[o], owner_starts[o + 1])
+    uint32_t owners;
+    const uint32_t *owner_starts;
+    const uint32_t *item_owner;  // multi-read items: owners of the item's first | last read << 16
 };
 constexpr uint32_t PC_RREG = 192;  // = the first pass's fill limit (256 slots at 3/4)
 // fill limit of the recount tiers' tables (2,048 slots and up, bucketed
@@ -325,6 +331,31 @@ hipError_t radix_sort_gen(const KeyGen &g, uint64_t **keys, uint64_t **keys_alt,
 hipError_t radix_sort_kv64(uint64_t **keys, uint64_t **vals, uint64_t **keys_alt, uint64_t **vals_alt, uint64_t n,
                            int lo, int hi, void *tmp, hipStream_t s);
 
+// Received records of the sharded path (sa_dist_count): record i in receive
+// order is mix << 32 | its occurrence index local to its source rank.  The
+// first pass of radix_sort_recv decodes each as it loads -- the record's read
+// and loc rank become its value (read << lb | loc rank), its low word becomes i
+// -- and writes the local read offsets loff[a] (first i with read >= a, a in
+// [0, n_reads]): the relabelling pass (prepare_received) folded into the sort
+struct RecvGen {
+    const uint64_t *seg;      // [2P + 1]: seg[s] first record of source s (seg[P] = n); seg[P + 1 + s]
+                              // the global occurrence index of source s's first k-mer
+    uint32_t P;
+    const uint32_t *starts;   // [P + 1] first global read of each source
+    const uint64_t *occ_off;  // global occurrence offsets (mixed lengths)
+    uint32_t npr;             // uniform k-mers per read (0: mixed)
+    unsigned long long npr_magic;
+    const int32_t *len;
+    const uint32_t *lbase, *lrank;
+    int32_t k;
+    int lb;
+    uint64_t *loff;
+    uint32_t n_reads;
+};
+// (key, u32 value) radix sort of received records, values generated (RecvGen)
+hipError_t radix_sort_recv(const RecvGen &g, uint64_t **keys, uint32_t **vals, uint64_t **keys_alt,
+                           uint32_t **vals_alt, uint64_t n, int lo, int hi, void *tmp, hipStream_t s);
+
 // exclusive scan of u32 (in place allowed), returns total in *total_dev
 size_t scan_temp_bytes(uint64_t n);
 hipError_t exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *total_dev,
@@ -342,18 +373,16 @@ hipError_t build_strict_index(const uint64_t *skeys, const uint32_t *svals, uint
 
 hipError_t launch_pair_count(const EmitParams &e, const PairIn &in, const PairParams &p, PairOut &o,
                              const uint32_t *read_list, uint32_t n_blocks, hipStream_t s);
-// sharded path: one block per range of reads with ~PCM_TARGET local occurrences
+// sharded path: one WAVE per range of reads with ~PMW_TARGET local occurrences
 // (launch_pc_items builds item_start[n_items + 1] from the occurrence offsets)
-constexpr uint32_t PCM_TARGET = 512;
-// ... or one WAVE per range of ~PMW_TARGET local occurrences (round 4)
 #ifndef SA_PMW_TARGET
 #define SA_PMW_TARGET 128
 #endif
 constexpr uint32_t PMW_TARGET = SA_PMW_TARGET;
 hipError_t launch_pair_count_multi_wave(const EmitParams &e, const PairIn &in, const PairParams &p, PairOut &o,
                                         const uint32_t *item_start, uint32_t n_items, hipStream_t s);
-hipError_t launch_pair_count_multi(const EmitParams &e, const PairIn &in, const PairParams &p, PairOut &o,
-                                   const uint32_t *item_start, uint32_t n_items, hipStream_t s);
+hipError_t launch_pc_item_owners(const uint32_t *item_start, uint32_t n_items, const uint32_t *starts, uint32_t owners,
+                                 uint32_t *item_owner, hipStream_t s);
 hipError_t launch_pc_items(const uint64_t *occ_off, uint32_t n_reads, uint32_t target, uint32_t n_items,
                            uint32_t *item_start, hipStream_t s);
 
@@ -526,13 +555,11 @@ hipError_t launch_local_offsets(const uint2 *rl, const uint32_t *pv, int lb, uin
                                 uint64_t *loff, hipStream_t s);
 hipError_t launch_owner_bounds(const uint64_t *keys, uint64_t n, int shift, uint32_t P, uint64_t *bounds,
                                hipStream_t s);
-hipError_t launch_desc_owner_bounds(const int32_t *lead, const uint32_t *n_dev, const uint32_t *starts, uint32_t P,
-                                    uint64_t *q, hipStream_t s);
-hipError_t launch_copy_partials(const int32_t *lead, const int32_t *trail, const int32_t *count, uint64_t n,
-                                const uint64_t *oq, uint32_t P, uint32_t *of, uint32_t *os, uint32_t *oc,
-                                hipStream_t s);
-hipError_t launch_gather_partials(const uint32_t *perm, uint64_t n, const uint32_t *fst, const uint32_t *snd,
-                                  const uint32_t *cnt, uint32_t *of, uint32_t *os, uint32_t *oc, hipStream_t s);
+// the owner regions of the partials (PairOut::owners), concatenated in region
+// order (owner-major): region r's min(cursor[r], cap_s) entries to out + off[r]
+hipError_t launch_copy_owner_regions(const uint32_t *fst, const uint32_t *snd, const uint32_t *cnt,
+                                     unsigned long long cap_s, uint32_t n_regions, const unsigned long long *cursor,
+                                     const uint64_t *off, uint32_t *of, uint32_t *os, uint32_t *oc, hipStream_t s);
 hipError_t launch_reduce_keys(const uint32_t *fst, const uint32_t *snd, uint64_t n, int idb, uint64_t *keys,
                               uint32_t *vals, hipStream_t s);
 hipError_t launch_reduce_heads(const uint64_t *skeys, const uint32_t *sidx, uint64_t n, const uint32_t *cnt,

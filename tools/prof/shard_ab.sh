@@ -1,24 +1,15 @@
 #!/bin/bash
-# Sharded-path tests, then 8 serial virtual shards of the bench shape under the
-# variants in $VARIANTS ("dir[:ENV=v,...]" as tools/prof/ab.sh), alternating;
-# one bench line each -> gpurun_out/shab_<n>_<i>.json
+# Same-box A/B of the sharded path: 8 serial virtual shards of the bench shape
+# (bench.py --shards 8 --serial-shards), per-shard stage ms per variant.
+#   VARIANTS="dir[:ENV=v[,ENV=v]] ..."  REPS=2  ARGS=extra bench args
 set -u
-mkdir -p gpurun_out
-if [ "${SKIP_TESTS:-0}" != 1 ]; then
-timeout -k 10 600 python -u -m pytest tests/test_gpu_sharded.py tests/test_gpu_parity.py tests/test_gpu_scale.py -x -v \
-    --timeout 300 --timeout-method thread -k "shard" > gpurun_out/t_shard.log 2>&1
-echo "tests rc=$?" >> gpurun_out/steps.txt
-fi
-for i in 1 2; do
-  n=0
-  for v in $VARIANTS; do
-    n=$((n + 1))
-    dir=${v%%:*}; envs="X=1"
-    [ "$dir" != "$v" ] && envs=$(echo "${v#*:}" | tr ',' ' ')
-    env SA_OVERLAP_LIB=$PWD/sequence-aligner_amd/$dir/libsa_overlap.so $envs timeout -k 10 200 python bench.py \
-        --no-cpu-baseline --shards 8 --serial-shards --steps 3 --warmup 1 --align-steps 1 > gpurun_out/shab_${n}_$i.log 2>&1 \
-        || { echo "shab $v rc=$?" >> gpurun_out/steps.txt; exit 1; }
-    echo "$v $(grep '^{' gpurun_out/shab_${n}_$i.log | tail -1 | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); s=d["stage_ms_per_step"]; print(d["ms_per_step"], s["emit"], s["sort"], s["buckets"], s["pairs"], s["order"])')" >> gpurun_out/shab.txt
-  done
+O=gpurun_out/shard_ab
+mkdir -p $O
+for i in $(seq 1 ${REPS:-2}); do
+ for v in $VARIANTS; do
+  dir=${v%%:*}; envs=""
+  [ "$dir" != "$v" ] && envs=$(echo "${v#*:}" | tr ',' ' ')
+  env SA_OVERLAP_LIB=$PWD/sequence-aligner_amd/$dir/libsa_overlap.so $envs timeout -k 10 180 python bench.py --shards 8 --serial-shards --steps 4 --warmup 1 --no-cpu-baseline --align-steps 1 ${ARGS:-} > $O/run.log 2>&1 || { echo "fail $v"; tail -5 $O/run.log; exit 1; }
+  echo "$v $(grep '^{' $O/run.log | tail -1 | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); s=d["stage_ms_per_step"]; print(d["ms_per_step"], " ".join("%s=%.3f" % (k, v) for k, v in s.items()))')" | tee -a $O/ab.txt
+ done
 done
-echo "shab rc=0" >> gpurun_out/steps.txt
