@@ -1128,7 +1128,8 @@ int device_build(sa_ctx *c, bool readback) {
     HIPCHK(fork_side(c, c->ev_fork));
     HIPCHK(radix_sort(&rk0, &ro0, &rk1, &ro1, nr, SA_LOCALITY_LO, 32, rtmp, c->side));
     HIPCHK(hipEventRecord(c->ev_join, c->side));
-    const uint32_t *read_order = ro0;
+    static const bool no_loc = getenv("SA_NO_LOCALITY") && atoi(getenv("SA_NO_LOCALITY")) != 0;  // (A/B)
+    const uint32_t *read_order = no_loc ? nullptr : ro0;
     PartArgs PA{};
     unsigned long long big_buckets = 0;
     // wide ids: no readback between the bucket build and the pair counter (its
@@ -2127,6 +2128,9 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint6
         RG.len = (const int32_t *)c->d_glen.p; RG.lbase = (const uint32_t *)c->d_lbase.p;
         RG.lrank = (const uint32_t *)c->d_lrank.p; RG.k = c->set.kmer_size; RG.lb = c->lb;
         RG.loff = loff; RG.n_reads = N;
+        PartArgs sc{};  // (the uniform-length loc-rank identity, as the bucket build checks it)
+        set_part_shortcuts(c, sc, c->gnpr);
+        RG.lr_ident = sc.lr_ident;
     } else {
         StageScope st(c, SA_STAGE_EMIT);
         HIPCHK(launch_prepare_received(keys, n, dseg, (uint32_t)P, (const uint32_t *)c->d_starts.p,
@@ -2205,9 +2209,11 @@ int sa_dist_partials(sa_ctx *c, void *fst, void *snd, void *cnt_out) {
     Counters *cnt;
     ENSURE(c->d_cnt, 1, &cnt);
     if (!dcur) dcur = cnt->cursor;
+    uint64_t max_fill = 0;
+    for (uint32_t r = 0; r < nreg; ++r) max_fill = std::max<uint64_t>(max_fill, c->part_off[r + 1] - c->part_off[r]);
     HIPCHK(launch_copy_owner_regions((const uint32_t *)c->d_pf.p, (const uint32_t *)c->d_ps.p,
                                      (const uint32_t *)c->d_pc.p, c->part_cap, nreg, dcur, doff, (uint32_t *)fst,
-                                     (uint32_t *)snd, (uint32_t *)cnt_out, c->stream));
+                                     (uint32_t *)snd, (uint32_t *)cnt_out, max_fill, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return SA_OK;
 }

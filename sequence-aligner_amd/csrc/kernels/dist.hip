@@ -465,26 +465,35 @@ hipError_t launch_owner_bounds(const uint64_t *keys, uint64_t n, int shift, uint
     return hipGetLastError();
 }
 
-// the owner regions concatenated: one block per region, its entries in order
+// the owner regions concatenated: block (x, r) copies entries [x CC, (x + 1) CC)
+// of region r (a grid of chunks, not one block per region: the regions hold
+// ~20k partials each at the bench shape, too few blocks to fill the chip)
+constexpr uint32_t CC = 4 * DT;
 __global__ void copy_owner_regions_kernel(const uint32_t *fst, const uint32_t *snd, const uint32_t *cnt,
                                           unsigned long long cap_s, const unsigned long long *cursor,
                                           const uint64_t *off, uint32_t *of, uint32_t *os, uint32_t *oc) {
-    const uint32_t r = blockIdx.x;
+    const uint32_t r = blockIdx.y;
     const unsigned long long m = min(cursor[r], cap_s), src = (unsigned long long)r * cap_s;
     const uint64_t dst = off[r];
-    for (unsigned long long j = threadIdx.x; j < m; j += DT) {
-        of[dst + j] = fst[src + j];
-        os[dst + j] = snd[src + j];
-        oc[dst + j] = cnt[src + j];
+    const unsigned long long j0 = (unsigned long long)blockIdx.x * CC;
+#pragma unroll
+    for (uint32_t q = 0; q < CC / DT; ++q) {
+        const unsigned long long j = j0 + q * DT + threadIdx.x;
+        if (j < m) {
+            of[dst + j] = fst[src + j];
+            os[dst + j] = snd[src + j];
+            oc[dst + j] = cnt[src + j];
+        }
     }
 }
 
 hipError_t launch_copy_owner_regions(const uint32_t *fst, const uint32_t *snd, const uint32_t *cnt,
                                      unsigned long long cap_s, uint32_t n_regions, const unsigned long long *cursor,
-                                     const uint64_t *off, uint32_t *of, uint32_t *os, uint32_t *oc, hipStream_t s) {
-    if (!n_regions) return hipSuccess;
-    hipLaunchKernelGGL(copy_owner_regions_kernel, dim3(n_regions), dim3(DT), 0, s, fst, snd, cnt, cap_s, cursor, off,
-                       of, os, oc);
+                                     const uint64_t *off, uint32_t *of, uint32_t *os, uint32_t *oc,
+                                     uint64_t max_fill, hipStream_t s) {
+    if (!n_regions || !max_fill) return hipSuccess;
+    const dim3 grid((uint32_t)((max_fill + CC - 1) / CC), n_regions);
+    hipLaunchKernelGGL(copy_owner_regions_kernel, grid, dim3(DT), 0, s, fst, snd, cnt, cap_s, cursor, off, of, os, oc);
     return hipGetLastError();
 }
 

@@ -281,15 +281,21 @@ struct RsShared {
 
 // (wave_peers: sa_internal.h)
 
-// a received record's read and loc rank (RecvGen; source s holds record i)
-__device__ __forceinline__ void recv_decode(const RecvGen &g, uint32_t s, uint64_t rec, uint32_t &r, uint32_t &lr) {
+// a received record's read and loc rank (RecvGen; source s holds record i;
+// st0 = starts[s0] of the slice's source s0, loaded once per slice)
+__device__ __forceinline__ void recv_decode(const RecvGen &g, uint32_t s, uint32_t s0, uint32_t st0, uint64_t rec,
+                                            uint32_t &r, uint32_t &lr) {
     const uint32_t local = (uint32_t)rec;
     uint32_t pos;
     if (g.npr) {
         // local / npr as the high word of local * magic (exact for local, npr < 2^32)
         const uint32_t q = g.npr == 1 ? local : (uint32_t)__umul64hi((unsigned long long)local, g.npr_magic);
-        r = g.starts[s] + q;
+        r = (s == s0 ? st0 : g.starts[s]) + q;
         pos = local - q * g.npr;
+        if (g.lr_ident) {
+            lr = pos;
+            return;
+        }
     } else {
         const uint64_t go = g.seg[g.P + 1 + s] + local;
         uint32_t lo = g.starts[s], up = g.starts[s + 1];  // largest r with occ_off[r] <= go
@@ -352,15 +358,16 @@ __global__ __launch_bounds__(RsDown<RS_ITEMS>::THREADS) void rs_downsweep_kernel
             uint32_t sp = s;
             while (sp > 0 && rg.seg[sp] > ip) --sp;
             uint32_t lrp;
-            recv_decode(rg, sp, rs_load_key(kin + ip), rprev, lrp);
+            recv_decode(rg, sp, sp, rg.starts[sp], rs_load_key(kin + ip), rprev, lrp);
         }
 #pragma unroll
         for (int j = 0; j < RS_SLICES; ++j) {
             const uint64_t i = sub + (uint64_t)j * 64 + lane;
             const bool valid = i < n;
             s = (uint32_t)__builtin_amdgcn_readfirstlane((int)recv_source(rg, s, sub + (uint64_t)j * 64));
+            const uint32_t st0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)rg.starts[s]);
             uint32_t r = 0, lr = 0;
-            if (valid) recv_decode(rg, recv_source(rg, s, i), k[j], r, lr);
+            if (valid) recv_decode(rg, recv_source(rg, s, i), s, st0, k[j], r, lr);
             v[j] = (r << rg.lb) | lr;
             if (valid) k[j] = (k[j] & 0xFFFFFFFF00000000ull) | (uint32_t)i;
             // loff[a] = i for the reads (read(i - 1), read(i)] (read(-1) = -1)

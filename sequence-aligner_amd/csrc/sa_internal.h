@@ -351,6 +351,7 @@ struct RecvGen {
     int lb;
     uint64_t *loff;
     uint32_t n_reads;
+    int lr_ident;             // uniform lengths whose loc rank is the position (no table lookup)
 };
 // (key, u32 value) radix sort of received records, values generated (RecvGen)
 hipError_t radix_sort_recv(const RecvGen &g, uint64_t **keys, uint32_t **vals, uint64_t **keys_alt,
@@ -559,7 +560,8 @@ hipError_t launch_owner_bounds(const uint64_t *keys, uint64_t n, int shift, uint
 // order (owner-major): region r's min(cursor[r], cap_s) entries to out + off[r]
 hipError_t launch_copy_owner_regions(const uint32_t *fst, const uint32_t *snd, const uint32_t *cnt,
                                      unsigned long long cap_s, uint32_t n_regions, const unsigned long long *cursor,
-                                     const uint64_t *off, uint32_t *of, uint32_t *os, uint32_t *oc, hipStream_t s);
+                                     const uint64_t *off, uint32_t *of, uint32_t *os, uint32_t *oc,
+                                     uint64_t max_fill, hipStream_t s);
 hipError_t launch_reduce_keys(const uint32_t *fst, const uint32_t *snd, uint64_t n, int idb, uint64_t *keys,
                               uint32_t *vals, hipStream_t s);
 hipError_t launch_reduce_heads(const uint64_t *skeys, const uint32_t *sidx, uint64_t n, const uint32_t *cnt,
