@@ -137,13 +137,15 @@ __device__ __forceinline__ void lds_radix_sort(SH &S, uint32_t n, int bits) {
         const int nbits = bits - shift < 8 ? bits - shift : 8;
         const uint32_t dmask = (1u << nbits) - 1u;
         reinterpret_cast<uint4 *>(S.cnt[w])[lane] = make_uint4(0, 0, 0, 0);
+        // per element: the key, and its load slot | rank among equal digits << 16
+        // in one register (ranks < 2 CAP); the digit is recomputed from the key
         unsigned long long k[SL];
-        uint32_t gv[SL], rk[SL], dg[SL];
+        uint32_t gr[SL];
 #pragma unroll
         for (int j = 0; j < SL; ++j) {
             const uint32_t i = w * SUB + j * 64 + lane;
             k[j] = i < n ? S.key[i] : 0ull;
-            gv[j] = i < n ? S.oi[i] : 0u;
+            gr[j] = i < n ? S.oi[i] : 0u;
         }
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -151,10 +153,9 @@ __device__ __forceinline__ void lds_radix_sort(SH &S, uint32_t n, int bits) {
             const uint32_t i = w * SUB + j * 64 + lane;
             const bool valid = i < n;
             const uint32_t d = (uint32_t)(k[j] >> shift) & dmask;
-            dg[j] = d;
             const uint64_t peer = wave_peers(d, valid, nbits);
             const uint32_t before = valid ? S.cnt[w][d] : 0u;
-            rk[j] = before + __popcll(peer & lt_mask);
+            gr[j] |= (before + __popcll(peer & lt_mask)) << 16;
             __builtin_amdgcn_wave_barrier();
             if (valid && (peer & lt_mask) == 0) S.cnt[w][d] = before + __popcll(peer);
             __builtin_amdgcn_wave_barrier();
@@ -181,9 +182,9 @@ __device__ __forceinline__ void lds_radix_sort(SH &S, uint32_t n, int bits) {
         for (int j = 0; j < SL; ++j) {
             const uint32_t i = w * SUB + j * 64 + lane;
             if (i < n) {
-                const uint32_t pos = S.ofs[w][dg[j]] + rk[j];
+                const uint32_t pos = S.ofs[w][(uint32_t)(k[j] >> shift) & dmask] + (gr[j] >> 16);
                 S.key[pos] = k[j];
-                S.oi[pos] = (uint16_t)gv[j];
+                S.oi[pos] = (uint16_t)gr[j];
             }
         }
         __syncthreads();  // scatter complete; the counts may be cleared
@@ -277,16 +278,15 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
     const uint32_t b0 = tid * IT;
     uint32_t md_c = 0, ed_c = 0, last_bh = 0, last_gh = 0, first_gh = 0xFFFFFFFFu, first_bh = 0xFFFFFFFFu;
     uint32_t n_bh = 0, n_gh = 0;
-    uint32_t tagv[IT];
+    uint32_t tagp = 0;          // item j's tag bits at 4 j (one register for the IT tags)
     uint32_t fbh = 0, fgh = 0;  // bit j: item b0 + j heads a bucket / a loc group (kept for the outputs)
 #pragma unroll
     for (int j = 0; j < IT; ++j) {
         const uint32_t s = b0 + j;
-        tagv[j] = 0;
         if (s < n) {
             const unsigned long long k = S.key[s];
             const uint32_t t = part_tag(A, (uint32_t)(k & lbm));
-            tagv[j] = t;
+            tagp |= t << (4 * j);
             const bool bh = s == 0 || (S.key[s - 1] >> lb) != (k >> lb);
             const bool gh = s == 0 || S.key[s - 1] != k;
             fbh |= bh ? 1u << j : 0u;
@@ -348,7 +348,7 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
         for (int j = 0; j < IT; ++j) {
             const uint32_t s = b0 + j;
             if (s <= n) { S.mdx[s] = m; S.edx[s] = e; }
-            const uint32_t t = tagv[j];
+            const uint32_t t = (tagp >> (4 * j)) & 15u;
             m += (t & TAG_MD) ? 1u : 0u;
             e += ((t & TAG_ST) ? 1u : 0u) + ((t & TAG_EN) ? 1u : 0u);
         }
@@ -356,20 +356,13 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
     }
     __syncthreads();
     PB_STAMP(A, p, 3);
-    // next group head and next bucket head per item (suffix within the thread,
-    // then gh_next / bh_next)
-    uint32_t nextg[IT], nextb[IT];
-    {
-        uint32_t nx = gh_next, nb_ = bh_next;
-#pragma unroll
-        for (int j = IT - 1; j >= 0; --j) {
-            const uint32_t s = b0 + j;
-            nextg[j] = nx;
-            nextb[j] = nb_;
-            if ((fgh >> j) & 1u) nx = s;
-            if ((fbh >> j) & 1u) nb_ = s;
-        }
-    }
+    // next group head and next bucket head of item j: the thread's next head
+    // bit above j (fgh / fbh), else gh_next / bh_next -- recomputed where used,
+    // not held in 2 IT registers
+    auto next_head = [&](uint32_t f, int j, uint32_t nxt) -> uint32_t {
+        const uint32_t above = f >> (j + 1);
+        return above ? b0 + (uint32_t)j + 1u + (uint32_t)__builtin_ctz(above) : nxt;
+    };
     // ---- outputs --------------------------------------------------------
     // The partition's list slice [3 ps, 3 ps + ltot) is assembled in LDS (the
     // key array is free once the heads are found; 2 CAP words hold any default
@@ -394,7 +387,7 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
         const bool isb = (fbh >> j) & 1u, isg = (fgh >> j) & 1u;
         if (isb) bh = s;
         if (isg) gh = s;
-        const uint32_t t = tagv[j];
+        const uint32_t t = (tagp >> (4 * j)) & 15u;
         const uint32_t slot = S.oi[s];
         const uint32_t code = S.g[slot];
         uint32_t r, g;
@@ -407,7 +400,7 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
         }
         const uint32_t st = (t & TAG_ST) ? 1u : 0u, en = (t & TAG_EN) ? 1u : 0u, md = (t & TAG_MD) ? 1u : 0u;
         // split point of the bucket [bh, nextb): its md entries end at c
-        const uint64_t c = 3ull * ps + S.mdx[nextb[j]] + S.edx[bh];
+        const uint64_t c = 3ull * ps + S.mdx[next_head(fbh, j, bh_next)] + S.edx[bh];
         const uint64_t mpos = c - 1u - (S.mdx[s] - S.mdx[bh]), epos = c + (S.edx[s] - S.edx[bh]);
         if (staged) {
             if (md) stg[mpos - lbase] = r;
@@ -420,7 +413,7 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
         }
         const uint32_t me = st + en;
         const uint32_t nE = me ? (S.mdx[gh] - S.mdx[bh]) : 0u;        // <= CAP: no escape here
-        const uint32_t nD = md ? (S.edx[nextg[j]] - S.edx[bh]) : 0u;  // <= 2 CAP
+        const uint32_t nD = md ? (S.edx[next_head(fgh, j, gh_next)] - S.edx[bh]) : 0u;  // <= 2 CAP
         A.rec[g] = encode_rec(c, nE, nD, me);
 #ifdef SA_PB_PROBE_DUP
         if (A.rec_dup) A.rec_dup[g] = encode_rec(c, nE, nD, me);  // (probe: twice the scattered stores)
@@ -706,11 +699,27 @@ hipError_t launch_part_starts(const PartArgs &a, uint64_t n, int shift, hipStrea
 
 // one tier of the bucket build: CAP 1,024 over every partition, 2,048 / 4,096
 // over the lists the bounds kernel / the 2,048 tier made
+// Main-pass blocks per CU, set by their LDS (MI355X: 160 KB per CU).  Fewer
+// resident blocks than the registers allow measured faster: the 1,024-record
+// blocks share the CUs with the split / 2,048-record tiers on the side stream,
+// and their scattered record stores contend in the MALL.  Same box, 3 pairs,
+// bench shape (profiles/r05/ab/ab_pb_blocks_per_cu.txt): 7 (the register limit)
+// 1.183-1.189 ms, 6 1.177-1.187, 5 1.136-1.143, 4 1.309-1.310
+#ifndef SA_PB_BLOCKS_PER_CU
+#define SA_PB_BLOCKS_PER_CU 5
+#endif
+constexpr size_t PB_CU_LDS = 160 * 1024;
+inline size_t pb_main_lds(size_t need) {
+    const size_t cap = SA_PB_BLOCKS_PER_CU > 0 ? PB_CU_LDS / SA_PB_BLOCKS_PER_CU : 0;
+    return cap > need ? cap : need;
+}
+
 hipError_t launch_part_build(const PartArgs &a, bool strict, int cap, hipStream_t s) {
     if (!a.np) return hipSuccess;
 #define PB_LAUNCH(CAPV, GRID, ST, MAINV)                                                                   \
     do {                                                                                                 \
-        const size_t lds = part_lds<CAPV>() + (a.rl || a.pv ? 4 * (size_t)(CAPV) : 0);                   \
+        size_t lds = part_lds<CAPV>() + (a.rl || a.pv ? 4 * (size_t)(CAPV) : 0);                       \
+        if (MAINV) lds = pb_main_lds(lds);                                                               \
         (void)hipFuncSetAttribute((const void *)part_build_kernel<CAPV, ST, MAINV>,                      \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                 \
         hipLaunchKernelGGL((part_build_kernel<CAPV, ST, MAINV>), dim3(GRID), dim3(PbShape<CAPV>::NT), lds, s, a); \
