@@ -863,7 +863,11 @@ hipError_t launch_pair_count(const EmitParams &e, const PairIn &in, const PairPa
         const uint32_t nb = (p.n_items + PW_WAVES - 1) / PW_WAVES;
         const uint32_t grid = p.xcd_swizzle ? (nb + 7) & ~7u : nb;
         if (!p.max_blocks || grid <= p.max_blocks) {
-            hipLaunchKernelGGL(pair_count_wave_kernel, dim3(grid), dim3(PW_WAVES * 64), 0, s, e, in, p, o, read_list,
+            static const size_t pw_dyn = occ_lds("SA_OCC_PW", sizeof(PwShared) * PW_WAVES, 0);  // (A/B)
+            if (pw_dyn)
+                (void)hipFuncSetAttribute((const void *)pair_count_wave_kernel,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)pw_dyn);
+            hipLaunchKernelGGL(pair_count_wave_kernel, dim3(grid), dim3(PW_WAVES * 64), pw_dyn, s, e, in, p, o, read_list,
                                grid);
             return hipGetLastError();
         }

@@ -726,7 +726,8 @@ hipError_t launch_part_build(const PartArgs &a, bool strict, int cap, hipStream_
     } while (0)
     const uint32_t mid_grid = a.np < 1024u ? a.np : 1024u;
     if (cap == 1) {  // the split tier (non-strict, records without sorted values)
-        const size_t lds = part_lds<1024>() + (a.rl || a.pv ? 4 * (size_t)1024 : 0);
+        const size_t lds0 = part_lds<1024>() + (a.rl || a.pv ? 4 * (size_t)1024 : 0);
+        const size_t lds = occ_lds("SA_OCC_SPLIT", lds0, lds0);  // (A/B)
         (void)hipFuncSetAttribute((const void *)part_split_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds);
         hipLaunchKernelGGL(part_split_kernel, dim3(2 * (a.np < SPLIT_MAX ? a.np : SPLIT_MAX)), dim3(PbShape<1024>::NT),

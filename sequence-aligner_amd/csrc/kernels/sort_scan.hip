@@ -553,10 +553,11 @@ template <int RS_ITEMS, bool GEN = false>
 static hipError_t rs_pass_keys(const uint64_t *kin, uint64_t *kout, uint64_t n, int shift, uint32_t *hist,
                                void *stmp, hipStream_t s, const KeyGen &kg = KeyGen{}, bool nt_out = false) {
     using SK = RsShared<false, RsTile<RS_ITEMS>::TILE, RsDown<RS_ITEMS>::WAVES>;
+    static const size_t sk_lds = occ_lds("SA_OCC_RS", sizeof(SK), sizeof(SK));  // (A/B)
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void *)rs_downsweep_kernel<false, RS_ITEMS, GEN>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(SK));
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sk_lds);
         attr_set = true;
     }
     const uint64_t nb = (n + RsTile<RS_ITEMS>::TILE - 1) / RsTile<RS_ITEMS>::TILE;
@@ -565,7 +566,7 @@ static hipError_t rs_pass_keys(const uint64_t *kin, uint64_t *kout, uint64_t n, 
     hipError_t e = rs_offsets(hist, nb, stmp, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((rs_downsweep_kernel<false, RS_ITEMS, GEN>), dim3((uint32_t)nb),
-                       dim3(RsDown<RS_ITEMS>::THREADS), sizeof(SK), s, kin, nullptr, kout, nullptr, n, shift,
+                       dim3(RsDown<RS_ITEMS>::THREADS), sk_lds, s, kin, nullptr, kout, nullptr, n, shift,
                        (const uint32_t *)hist, (uint32_t)nb, kg, nt_out ? 1 : 0, RecvGen{});
     return hipGetLastError();
 }

@@ -235,6 +235,18 @@ struct PairParams {
     int32_t early;
 };
 
+// A/B knob (environment SA_OCC_<NAME> = b > 0): the LDS a block allocates,
+// padded so that at most b blocks fit one CU (MI355X: 160 KB of LDS per CU);
+// `used` = the block's LDS without padding, returns the dynamic size to launch
+// with (its own dynamic part `dyn` plus the pad)
+inline size_t occ_lds(const char *env, size_t used, size_t dyn) {
+    const char *v = getenv(env);
+    const int b = v ? atoi(v) : 0;
+    if (b <= 0) return dyn;
+    const size_t cap = (160u * 1024u) / (size_t)b;
+    return cap > used ? dyn + (cap - used) : dyn;
+}
+
 // Device-wide counters are sharded NSHARD ways (shard = blockIdx % NSHARD) and
 // block-reduced first: same-address device atomics from every block serialise
 // at one L2 channel (MI355X_MICROARCH.md, fan-in row).
