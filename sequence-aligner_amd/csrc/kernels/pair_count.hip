@@ -77,8 +77,8 @@ constexpr int PC_WIN = 2048;
 // one block fits a CU: it runs 1,024 threads (16 waves to hide the partner
 // gathers, not 4), 1,024-occurrence chunks and 6,144-element windows (6
 // partner loads in flight per thread: the packed tier's LDS holds 12 KB of
-// window map beside its 128 KB table; 8 would pass the 160 KB); the smaller
-// tables keep 256 threads.
+// window map beside its 128 KB table; 8 would pass the 160 KB; the two-word
+// 16,384-slot table keeps 4); the smaller tables keep 256 threads.
 #ifndef PC_HUGE_CHUNK
 #define PC_HUGE_CHUNK 1024
 #endif
@@ -89,8 +89,10 @@ template <int TAB> struct PcShape {
     static constexpr int NT = TAB >= PC_TAB_HUGE ? 1024 : PC_THREADS;
     static constexpr bool PACKED = TAB >= PC_TAB_HUGE2;
     static constexpr int CHUNK = TAB >= PC_TAB_HUGE ? PC_HUGE_CHUNK : PC_CHUNK;
-    static constexpr int WIN = TAB >= PC_TAB_HUGE ? 1024 * PC_HUGE_BATCH : PC_WIN;
-    static constexpr int BATCH = TAB >= PC_TAB_HUGE ? PC_HUGE_BATCH : PC_BATCH;
+    // (the two-word 16,384-slot table fills 128 KB with keys and counts: 4 loads,
+    // 4,096-element windows, or the block passes 160 KB of LDS)
+    static constexpr int BATCH = TAB >= PC_TAB_HUGE2 ? PC_HUGE_BATCH : TAB >= PC_TAB_HUGE ? 4 : PC_BATCH;
+    static constexpr int WIN = TAB >= PC_TAB_HUGE ? 1024 * BATCH : PC_WIN;
 };
 
 template <int TAB>
@@ -543,6 +545,7 @@ __global__ __launch_bounds__(PcShape<TAB>::NT) void pair_count_kernel(EmitParams
 
 template <int TAB>
 static size_t pc_lds_bytes(bool strict) {
+    static_assert(sizeof(PcShared<TAB>) <= 160 * 1024, "a pair-count block must fit the CU's 160 KB of LDS");
     size_t s = (sizeof(PcShared<TAB>) + 15) & ~size_t(15);
     if (strict) s += sizeof(PcSharedStrict<TAB>);
     return s;
