@@ -1467,9 +1467,22 @@ int device_align(sa_ctx *c, bool readback) {
             const bool x2 = lw == 16 && exact && P.cost_bits == 8 && P.gap_open <= 0 && P.gap_extend <= 0 &&
                             -(int64_t)P.gap_open < 65536 && -(int64_t)P.gap_extend < 65536 &&
                             cmax * (int64_t)maxL + 255 < 65536;
-            if (x2)
-                HIPCHK(launch_dovetail_p1x2(AR, dl, dt, nd, P, p1, k0, v0, &cnt->err, cnt->cells, c->stream));
-            else
+            if (x2) {
+                // row segments when the waves are few enough for the last round to matter: units of
+                // 1 / nseg of a wave, ~20+ per SIMD (1,024 SIMDs), at most 8, rows >= 32 per segment
+                const uint32_t ng = dovetail_p1x2_groups(nd);
+                int32_t nseg = (int32_t)std::min<uint64_t>(8, (20 * 1024 + ng - 1) / ng);
+                nseg = std::max(1, std::min(nseg, (int32_t)(maxL / 32)));
+                if (const char *e = getenv("SA_P1_SEGS")) nseg = atoi(e);  // A/B: 0 = one-segment kernel
+                if (nseg >= 1) {
+                    uint32_t *tf, *st = nullptr;
+                    ENSURE(c->d_p1tf, (uint64_t)ng + 1, &tf);
+                    if (nseg > 1) ENSURE(c->d_p1st, dovetail_p1x2_state_words(nd), &st);
+                    HIPCHK(launch_dovetail_p1x2_seg(AR, dl, dt, nd, P, p1, k0, v0, &cnt->err, cnt->cells, nseg, tf, st,
+                                                    c->stream));
+                } else
+                    HIPCHK(launch_dovetail_p1x2(AR, dl, dt, nd, P, p1, k0, v0, &cnt->err, cnt->cells, c->stream));
+            } else
                 HIPCHK(launch_dovetail_p1(AR, dl, dt, nd, P, lw, exact, p1, k0, v0, &cnt->err, cnt->cells,
                                           c->stream));
             HIPCHK(radix_sort(&k0, &v0, &k1, &v1, nd, 0, 20, tmp, c->stream));
@@ -1509,6 +1522,7 @@ int device_align(sa_ctx *c, bool readback) {
         const char *msg = err == SA_E_NON_ACGT ? "non-ACGT base in an aligned region (HOXD MatchError)"
                         : err == SA_E_SHORT_READ ? "trail shorter than the band width (StringIndexOutOfBounds)"
                         : err == SA_E_DEGENERATE ? "no positive phase-1 cell (degenerate backtrack)"
+                        : err == SA_E_HIP ? "phase-1 row-segment hand-off timed out"
                         : "alignment limit exceeded";
         return fail(c, err, msg);
     }
@@ -1610,7 +1624,7 @@ void sa_ctx_destroy(sa_ctx *c) {
                     &c->d_gmds, &c->d_gede, &c->d_ogid, &c->d_bkttmp, &c->d_mdidx, &c->d_edidx, &c->d_occidx,
                     &c->d_bnst, &c->d_brank, &c->d_bhash, &c->d_bfirst, &c->d_pf, &c->d_ps, &c->d_pc, &c->d_pr,
                     &c->d_ovl, &c->d_cnt, &c->d_okeys, &c->d_ovals, &c->d_okeys2, &c->d_ovals2, &c->d_osort,
-                    &c->d_lead, &c->d_trail, &c->d_count, &c->d_aln, &c->d_p1, &c->d_tb, &c->d_rkey, &c->d_rkey2, &c->d_rord, &c->d_rord2, &c->d_rtmp, &c->d_gocc, &c->d_seg, &c->d_rl, &c->d_srl, &c->d_srl2, &c->d_loff, &c->d_starts, &c->d_bounds, &c->d_gcodes, &c->d_gwoff, &c->d_glen, &c->d_gbad, &c->d_psum, &c->d_pkeep, &c->d_ppos, &c->d_scan, &c->d_pstart, &c->d_biglist, &c->d_rec,
+                    &c->d_lead, &c->d_trail, &c->d_count, &c->d_aln, &c->d_p1, &c->d_p1tf, &c->d_p1st, &c->d_tb, &c->d_rkey, &c->d_rkey2, &c->d_rord, &c->d_rord2, &c->d_rtmp, &c->d_gocc, &c->d_seg, &c->d_rl, &c->d_srl, &c->d_srl2, &c->d_loff, &c->d_starts, &c->d_bounds, &c->d_gcodes, &c->d_gwoff, &c->d_glen, &c->d_gbad, &c->d_psum, &c->d_pkeep, &c->d_ppos, &c->d_scan, &c->d_pstart, &c->d_biglist, &c->d_rec,
                     &c->d_srec, &c->d_bnmd, &c->d_ishead, &c->d_bnst2, &c->d_tmd, &c->d_ted, &c->d_tmdi,
                     &c->d_tedi, &c->d_xrec, &c->d_tier, &c->d_ovlrp, &c->d_meta, &c->d_items, &c->d_pq, &c->d_ocur, &c->d_lr, &c->d_bigtot, &c->d_hk0, &c->d_hk1, &c->d_hflag,
                     &c->d_hidx, &c->d_hpos, &c->d_htmp, &c->d_hist, &c->d_hovf, &c->d_hsmall,

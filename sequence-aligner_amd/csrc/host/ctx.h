@@ -97,7 +97,7 @@ struct sa_ctx {
     uint32_t *bkt_rank_dev = nullptr;
     DBuf d_pf, d_ps, d_pc, d_pr, d_ovl, d_cnt;
     DBuf d_okeys, d_ovals, d_okeys2, d_ovals2, d_osort;
-    DBuf d_lead, d_trail, d_count, d_aln, d_p1, d_tb, d_ltb, d_lmax;
+    DBuf d_lead, d_trail, d_count, d_aln, d_p1, d_p1tf, d_p1st, d_tb, d_ltb, d_lmax;
     DBuf d_rkey, d_rkey2, d_rord, d_rord2, d_rtmp;
     DBuf d_rreg, d_rcnt, d_rex;  // per-read pair regions, counts, their exclusive scan
     // per-read mode: the recounted reads' pairs sorted (lead, trail, count) and

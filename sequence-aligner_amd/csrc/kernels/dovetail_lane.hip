@@ -452,40 +452,57 @@ __device__ __forceinline__ u16x2 pk_dif(u16x2 a, u16x2 b) { return pk(upk(a) - u
 // a + b per half where neither half reaches 2^16 (no carry crosses)
 __device__ __forceinline__ u16x2 pk_sum(u16x2 a, u16x2 b) { return pk(upk(a) + upk(b)); }
 
-__global__ __launch_bounds__(256) void dovetail_p1x2_kernel(DevReads rd, const int32_t *lead, const int32_t *trail,
-                                                            uint64_t npairs, AlignParams P, int32_t *p1,
-                                                            uint64_t *rows2_key, uint32_t *order, int32_t *err,
-                                                            unsigned long long *cells_total) {
+// Phase-1 lane state between row segments (dovetail_p1x2_seg_kernel): Tc, Q, O per
+// column, best, borg -- u32 words, word r of lane l at [r * 64 + l] of the wave's slot.
+// The next segment may run on another XCD (its own L2): the words move as device-scope
+// relaxed atomics -- loads and stores that go past the non-coherent L2 one instruction at
+// a time -- instead of release / acquire fences, whose L2 write-back and invalidate of the
+// whole cache per hand-off cost more than the segments saved.
+constexpr int P1X2_STATE = 3 * 15 + 2;
+__device__ __forceinline__ uint32_t st_ld(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_st(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Lane t's two pairs over rows [seg * R + 1, (seg + 1) * R] of its wave's rmax rows
+// (R = rmax / nseg rounded up to even); st = the wave's state slot when nseg > 1.
+__device__ __forceinline__ void p1x2_run(const DevReads &rd, const int32_t *lead, const int32_t *trail,
+                                         uint64_t npairs, const AlignParams &P, int32_t *p1, uint64_t *rows2_key,
+                                         uint32_t *order, int32_t *err, unsigned long long *cells_total,
+                                         const uint64_t t, const int32_t seg, const int32_t nseg, uint32_t *st) {
     constexpr int LW = 16;
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
     const uint64_t pairA = 2 * t, pairB = 2 * t + 1;
     const bool haveA = pairA < npairs, haveB = pairB < npairs;
+    const bool last = seg == nseg - 1;
     LanePair qa{0, 0, 0, 0, 0, -100, rd.codes, rd.codes}, qb = qa;
     if (haveA) {
         qa = lane_pair<LW, true>(rd, lead, trail, pairA, P);
-        if (qa.status < 0) set_err(err, qa.status);
+        if (qa.status < 0 && last) set_err(err, qa.status);
     }
     if (haveB) {
         qb = lane_pair<LW, true>(rd, lead, trail, pairB, P);
-        if (qb.status < 0) set_err(err, qb.status);
+        if (qb.status < 0 && last) set_err(err, qb.status);
     }
-    // biased column packs: byte x = cost(x, b) + 128 for B base b of column j
-    auto colpack = [&](int bb) {
+    // biased row packs (uniform): byte b = cost(a, b) + 128 for A base a of the row.  Each
+    // row picks its pack per pair; each column's v_perm selector (a per-lane constant) picks
+    // byte b_j of pair A's pack and byte b_j' of pair B's -- 15 selector registers, not 30
+    // column packs, which keeps the kernel at <= 128 VGPRs (4 waves per SIMD).
+    auto rowpack = [&](int a) {
         uint32_t v = 0;
 #pragma unroll
-        for (int x = 0; x < 4; ++x) v |= (uint32_t)((P.cost[x * 4 + bb] + 128) & 255) << (8 * x);
+        for (int b = 0; b < 4; ++b) v |= (uint32_t)((P.cost[a * 4 + b] + 128) & 255) << (8 * b);
         return v;
     };
-    const uint32_t cq0 = colpack(0), cq1 = colpack(1), cq2 = colpack(2), cq3 = colpack(3);
+    const uint32_t cr0 = rowpack(0), cr1 = rowpack(1), cr2 = rowpack(2), cr3 = rowpack(3);
     const uint32_t bwA = qa.status == 0 ? gld(qa.Bw, 0) : 0u, bwB = qb.status == 0 ? gld(qb.Bw, 0) : 0u;
-    uint32_t cbA[LW - 1], cbB[LW - 1];
+    uint32_t csel[LW - 1];  // [bA_j, 0, 4 + bB_j, 0] (0x0C selects a zero byte)
 #pragma unroll
     for (int j = 1; j < LW; ++j) {
         const uint32_t ba = (bwA >> (30 - 2 * (j - 1))) & 3u, bb = (bwB >> (30 - 2 * (j - 1))) & 3u;
-        const uint32_t a01 = (ba & 1) ? cq1 : cq0, a23 = (ba & 1) ? cq3 : cq2;
-        const uint32_t b01 = (bb & 1) ? cq1 : cq0, b23 = (bb & 1) ? cq3 : cq2;
-        cbA[j - 1] = (ba & 2) ? a23 : a01;
-        cbB[j - 1] = (bb & 2) ? b23 : b01;
+        csel[j - 1] = ba | 0x00000C00u | ((4u + bb) << 16) | 0x0C000000u;
     }
     const u16x2 gO = pk((uint32_t)in_vgpr((int32_t)((uint32_t)(-P.gap_open) * 0x10001u)));
     const u16x2 gE = pk((uint32_t)in_vgpr((int32_t)((uint32_t)(-P.gap_extend) * 0x10001u)));
@@ -493,31 +510,48 @@ __global__ __launch_bounds__(256) void dovetail_p1x2_kernel(DevReads rd, const i
     const u16x2 one = pk((uint32_t)in_vgpr((int32_t)0x00010001));
     u16x2 Tc[LW - 1], Q[LW - 1];
     uint32_t O[LW - 1];
-#pragma unroll
-    for (int j = 0; j < LW - 1; ++j) { Tc[j] = 0; Q[j] = 0; O[j] = 0x00010001u; }  // origin (row 0, col != 0)
     u16x2 best = 0;
     uint32_t borg = 0;
+    if (seg == 0) {
+#pragma unroll
+        for (int j = 0; j < LW - 1; ++j) { Tc[j] = 0; Q[j] = 0; O[j] = 0x00010001u; }  // origin (row 0, col != 0)
+    } else {
+#pragma unroll
+        for (int j = 0; j < LW - 1; ++j) {
+            Tc[j] = pk(st_ld(st + j * 64 + lane));
+            Q[j] = pk(st_ld(st + (15 + j) * 64 + lane));
+            O[j] = st_ld(st + (30 + j) * 64 + lane);
+        }
+        best = pk(st_ld(st + 45 * 64 + lane));
+        borg = st_ld(st + 46 * 64 + lane);
+    }
     const int32_t rowsA = qa.status == 0 ? qa.LA : 0, rowsB = qb.status == 0 ? qb.LA : 0;
     int32_t rmax = max(rowsA, rowsB);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) rmax = max(rmax, __shfl_xor(rmax, off, 64));
     rmax = __builtin_amdgcn_readfirstlane(rmax);
+    const int32_t R = nseg == 1 ? rmax : (((rmax + nseg - 1) / nseg) + 1) & ~1;
+    const int32_t i0 = seg * R + 1, i1 = min(rmax, (seg + 1) * R);
     const int32_t awlA = max((qa.LA + 15) / 16 - 1, 0), awlB = max((qb.LA + 15) / 16 - 1, 0);
-    uint32_t awA = qa.Aw[0], awnA = qa.Aw[min(1, awlA)];
-    uint32_t awB = qb.Aw[0], awnB = qb.Aw[min(1, awlB)];
+    const int32_t w0 = (i0 - 1) >> 4;  // the A word of row i0, and the next
+    uint32_t awA = qa.Aw[min(w0, awlA)], awnA = qa.Aw[min(w0 + 1, awlA)];
+    uint32_t awB = qb.Aw[min(w0, awlB)], awnB = qb.Aw[min(w0 + 1, awlB)];
     __builtin_amdgcn_s_waitcnt(0);
     auto row = [&](const int32_t i) {
         const uint32_t act = (i <= rowsA ? 0x0000FFFFu : 0u) | (i <= rowsB ? 0xFFFF0000u : 0u);
         const uint32_t sh = 30 - 2 * ((i - 1) & 15);
         const uint32_t aA = (awA >> sh) & 3u, aB = (awB >> sh) & 3u;
-        const uint32_t sel = aA | 0x00000C00u | ((4u + aB) << 16) | 0x0C000000u;  // [cA, 0, cB, 0]
+        // bit-selects, not a ternary chain: that became a private lookup table (scratch)
+        const uint32_t mA1 = 0u - (aA & 1u), mA2 = 0u - (aA >> 1), mB1 = 0u - (aB & 1u), mB2 = 0u - (aB >> 1);
+        const uint32_t rA = bsel3(mA2, bsel3(mA1, cr3, cr2), bsel3(mA1, cr1, cr0));
+        const uint32_t rB = bsel3(mB2, bsel3(mB1, cr3, cr2), bsel3(mB1, cr1, cr0));
         u16x2 Tdiag = 0, Zl = 0, Xl = 0;
         uint32_t Odiag = (uint32_t)((i - 1) << 1) * 0x10001u;
         uint32_t Ol = (uint32_t)(i << 1) * 0x10001u;
         const uint32_t self = (uint32_t)((i << 1) | 1) * 0x10001u;
 #pragma unroll
         for (int j = 0; j < LW - 1; ++j) {
-            const u16x2 cpk = pk(__builtin_amdgcn_perm(cbB[j], cbA[j], sel));
+            const u16x2 cpk = pk(__builtin_amdgcn_perm(rB, rA, csel[j]));
             const u16x2 M = pk_subs(pk_sum(Tdiag, cpk), bias);
             const u16x2 Y = pk_subs(Q[j], gE);
             const u16x2 X = pk_subs(pk_max(Zl, Xl), gE);
@@ -542,12 +576,23 @@ __global__ __launch_bounds__(256) void dovetail_p1x2_kernel(DevReads rd, const i
         awnA = gld(qa.Aw, min((i >> 4) + 1, awlA));
         awnB = gld(qb.Aw, min((i >> 4) + 1, awlB));
     };
-    int32_t i = 1;
-    for (; i < rmax; i += 2) {  // two rows per iteration (by hand: #pragma unroll gives up here)
+    int32_t i = i0;
+    for (; i < i1; i += 2) {  // two rows per iteration (by hand: #pragma unroll gives up here)
         row(i);
         row(i + 1);
     }
-    if (i == rmax) row(i);
+    if (i == i1) row(i);
+    if (!last) {
+#pragma unroll
+        for (int j = 0; j < LW - 1; ++j) {
+            st_st(st + j * 64 + lane, upk(Tc[j]));
+            st_st(st + (15 + j) * 64 + lane, upk(Q[j]));
+            st_st(st + (30 + j) * 64 + lane, O[j]);
+        }
+        st_st(st + 45 * 64 + lane, upk(best));
+        st_st(st + 46 * 64 + lane, borg);
+        return;
+    }
     unsigned long long cells = 0;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -577,6 +622,57 @@ __global__ __launch_bounds__(256) void dovetail_p1x2_kernel(DevReads rd, const i
         order[pair] = (uint32_t)pair;
     }
     add_cells(cells, cells_total);
+}
+
+__global__ __launch_bounds__(256) void dovetail_p1x2_kernel(DevReads rd, const int32_t *lead, const int32_t *trail,
+                                                            uint64_t npairs, AlignParams P, int32_t *p1,
+                                                            uint64_t *rows2_key, uint32_t *order, int32_t *err,
+                                                            unsigned long long *cells_total) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    p1x2_run(rd, lead, trail, npairs, P, p1, rows2_key, order, err, cells_total, t, 0, 1, nullptr);
+}
+
+// Phase 1 in row segments (tail balance).  Every lane does the same instruction stream, so a
+// wave of 128 pairs costs the same issue time however many pairs it holds: ~5,350 waves over
+// 1,024 SIMDs quantize to 6 rounds for 5.23 of work.  Here each one-wave workgroup takes a
+// ticket u (one device atomic): wave group g = u % ngroups, row segment s = u / ngroups.
+// Tickets are handed out in order, so every segment-(s - 1) ticket went to a resident or
+// finished workgroup before any segment-s ticket exists -- the wait below cannot deadlock.
+// Segment s > 0 waits for flags[g] == s (bounded: SA_E_HIP after ~2^24 polls), loads the
+// lanes' state, runs its rows and hands on; the last segment writes the results.  Units of
+// 1 / nseg of a wave let the dispatcher even out the SIMDs' issue time.
+__global__ __launch_bounds__(64) void dovetail_p1x2_seg_kernel(DevReads rd, const int32_t *lead, const int32_t *trail,
+                                                               uint64_t npairs, AlignParams P, int32_t *p1,
+                                                               uint64_t *rows2_key, uint32_t *order, int32_t *err,
+                                                               unsigned long long *cells_total, uint32_t ngroups,
+                                                               int32_t nseg, uint32_t *ticket, uint32_t *flags,
+                                                               uint32_t *state) {
+    const int lane = threadIdx.x;
+    uint32_t u = 0;
+    if (lane == 0) u = atomicAdd(ticket, 1u);
+    u = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)__shfl((int)u, 0, 64));
+    const uint32_t g = u % ngroups;
+    const int32_t s = (int32_t)(u / ngroups);
+    uint32_t *st = state + (uint64_t)g * P1X2_STATE * 64;
+    if (s > 0) {
+        if (lane == 0) {
+            uint32_t polls = 0;
+            while (st_ld(flags + g) < (uint32_t)s) {
+                __builtin_amdgcn_s_sleep(4);
+                if (++polls > (1u << 24)) { set_err(err, -7); break; }  // SA_E_HIP
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the state loads stay after the flag's
+    }
+    p1x2_run(rd, lead, trail, npairs, P, p1, rows2_key, order, err, cells_total, (uint64_t)g * 64 + lane, s, nseg,
+             st);
+    if (s < nseg - 1) {
+        __builtin_amdgcn_s_waitcnt(0);  // every state store acknowledged at device scope ...
+        __builtin_amdgcn_wave_barrier();
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        if (lane == 0) st_st(flags + g, (uint32_t)(s + 1));  // ... before the flag
+    }
 }
 
 // Phase 2 (BioLibs.scala:691-819) + Alignment/Overlap validity, one pair per
@@ -1065,6 +1161,23 @@ hipError_t launch_dovetail_p1x2(const DevReads &r, const int32_t *lead, const in
     const uint64_t lanes = (n + 1) / 2;
     hipLaunchKernelGGL(dovetail_p1x2_kernel, dim3((uint32_t)((lanes + 255) / 256)), dim3(256), 0, s, r, lead, trail,
                        n, p, p1, rows2_key, order, err, cells);
+    return hipGetLastError();
+}
+
+uint32_t dovetail_p1x2_groups(uint64_t n) { return (uint32_t)(((n + 1) / 2 + 63) / 64); }
+size_t dovetail_p1x2_state_words(uint64_t n) { return (size_t)dovetail_p1x2_groups(n) * P1X2_STATE * 64; }
+
+hipError_t launch_dovetail_p1x2_seg(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
+                                    const AlignParams &p, int32_t *p1, uint64_t *rows2_key, uint32_t *order,
+                                    int32_t *err, unsigned long long *cells, int32_t nseg, uint32_t *ticket_flags,
+                                    uint32_t *state, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const uint32_t ng = dovetail_p1x2_groups(n);
+    // ticket_flags: 1 + ng words, zeroed here
+    hipError_t e = hipMemsetAsync(ticket_flags, 0, (size_t)(1 + ng) * 4, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(dovetail_p1x2_seg_kernel, dim3((uint32_t)((uint64_t)ng * nseg)), dim3(64), 0, s, r, lead,
+                       trail, n, p, p1, rows2_key, order, err, cells, ng, nseg, ticket_flags, ticket_flags + 1, state);
     return hipGetLastError();
 }
 

@@ -518,6 +518,15 @@ hipError_t launch_dovetail_p1(const DevReads &r, const int32_t *lead, const int3
 hipError_t launch_dovetail_p1x2(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
                                 const AlignParams &p, int32_t *p1, uint64_t *rows2_key, uint32_t *order, int32_t *err,
                                 unsigned long long *cells, hipStream_t s);
+// phase 1 (two pairs per lane) in nseg row segments of every 64-lane group, one ticketed
+// one-wave workgroup per (segment, group): ticket_flags = 1 + dovetail_p1x2_groups(n) u32,
+// state = dovetail_p1x2_state_words(n) u32 (unused when nseg == 1)
+uint32_t dovetail_p1x2_groups(uint64_t n);
+size_t dovetail_p1x2_state_words(uint64_t n);
+hipError_t launch_dovetail_p1x2_seg(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
+                                    const AlignParams &p, int32_t *p1, uint64_t *rows2_key, uint32_t *order,
+                                    int32_t *err, unsigned long long *cells, int32_t nseg, uint32_t *ticket_flags,
+                                    uint32_t *state, hipStream_t s);
 hipError_t launch_dovetail_p2(const DevReads &r, const int32_t *lead, const int32_t *trail, uint64_t n,
                               const AlignParams &p, int lw, bool exact, const int32_t *p1, const uint32_t *order,
                               DevAlignment *out, int32_t *err, hipStream_t s);

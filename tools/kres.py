@@ -21,6 +21,6 @@ for line in r.stderr.splitlines():
     elif cur is not None:
         cur[k] = v
 for c in rows:
-    print("%-70.70s vgpr %4s agpr %3s sspill %4s vspill %4s occ %2s lds %6s" % (
+    print("%-70.70s vgpr %4s agpr %3s sspill %4s vspill %4s scratch %4s occ %2s lds %6s" % (
         c["name"].replace("sa::", ""), c.get("VGPRs"), c.get("AGPRs"), c.get("SGPRs Spill"), c.get("VGPRs Spill"),
-        c.get("Occupancy [waves/SIMD]"), c.get("LDS Size [bytes/block]")))
+        c.get("ScratchSize [bytes/lane]"), c.get("Occupancy [waves/SIMD]"), c.get("LDS Size [bytes/block]")))
