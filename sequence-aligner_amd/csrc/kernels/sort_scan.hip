@@ -129,7 +129,13 @@ constexpr int RS_THREADS = 256;
 // tiles 0.69 ms), 16 where values ride along (their LDS staging at 8,192 keys
 // would leave one workgroup per CU)
 constexpr int RS_ITEMS_KEYS = 32;
-constexpr int RS_ITEMS_VALS = 32;  // (8 serial shards of the bench shape: 12-byte records' sort 1.32 -> 1.20 ms per shard)
+#ifndef SA_RS_ITEMS_VALS  // (A/B builds)
+#define SA_RS_ITEMS_VALS 32
+#endif
+// 12-byte records, 8,192-key tiles (8 serial shards of the bench shape: the records' sort
+// 1.32 -> 1.20 ms per shard against 4,096; values staged in the key slots after the keys
+// went out, two workgroups per CU: 1.35 -> 1.16 ms)
+constexpr int RS_ITEMS_VALS = SA_RS_ITEMS_VALS;
 constexpr int RS_ITEMS_KV = 16;    // 16-byte records: 4,096-key tiles of 4 waves
 template <int ITEMS> struct RsTile {
     static constexpr int TILE = RS_THREADS * ITEMS;
@@ -269,10 +275,11 @@ struct RsDown {
     static constexpr int WAVES = TILE / 1024, THREADS = WAVES * 64, SUB = 1024, SLICES = SUB / 64;
 };
 
+// (with values the key slots take the staged values after the keys went out: the
+// tile keeps a key-only footprint -- 2 workgroups per CU at 8,192 keys, not 1)
 template <bool VALS, int RS_TILE, int WAVES>
 struct RsShared {
     unsigned long long key[RS_TILE];
-    uint32_t val[VALS ? RS_TILE : 1];
     uint32_t cnt[WAVES][256];      // per-wave digit counts
     uint32_t lofs[256];            // tile-local start of each digit run
     uint32_t gofs[256];            // global start of each digit run
@@ -281,24 +288,33 @@ struct RsShared {
 
 // (wave_peers: sa_internal.h)
 
+// The sources' table (seg[0 .. 2P], starts[0 .. P]) staged in LDS once per block when
+// P <= RS_RECV_PMAX: the per-slice and per-lane source searches then cost LDS reads, not
+// chains of dependent global loads (the pass ran 3x a plain 12-byte pass on them).
+constexpr uint32_t RS_RECV_PMAX = 64;
+struct RecvTab {
+    const uint64_t *seg;
+    const uint32_t *starts;
+};
+
 // a received record's read and loc rank (RecvGen; source s holds record i;
 // st0 = starts[s0] of the slice's source s0, loaded once per slice)
-__device__ __forceinline__ void recv_decode(const RecvGen &g, uint32_t s, uint32_t s0, uint32_t st0, uint64_t rec,
-                                            uint32_t &r, uint32_t &lr) {
+__device__ __forceinline__ void recv_decode(const RecvGen &g, const RecvTab &t, uint32_t s, uint32_t s0, uint32_t st0,
+                                            uint64_t rec, uint32_t &r, uint32_t &lr) {
     const uint32_t local = (uint32_t)rec;
     uint32_t pos;
     if (g.npr) {
         // local / npr as the high word of local * magic (exact for local, npr < 2^32)
         const uint32_t q = g.npr == 1 ? local : (uint32_t)__umul64hi((unsigned long long)local, g.npr_magic);
-        r = (s == s0 ? st0 : g.starts[s]) + q;
+        r = (s == s0 ? st0 : t.starts[s]) + q;
         pos = local - q * g.npr;
         if (g.lr_ident) {
             lr = pos;
             return;
         }
     } else {
-        const uint64_t go = g.seg[g.P + 1 + s] + local;
-        uint32_t lo = g.starts[s], up = g.starts[s + 1];  // largest r with occ_off[r] <= go
+        const uint64_t go = t.seg[g.P + 1 + s] + local;
+        uint32_t lo = t.starts[s], up = t.starts[s + 1];  // largest r with occ_off[r] <= go
         while (up - lo > 1) {
             const uint32_t mid = (lo + up) >> 1;
             if (g.occ_off[mid] <= go) lo = mid; else up = mid;
@@ -309,15 +325,17 @@ __device__ __forceinline__ void recv_decode(const RecvGen &g, uint32_t s, uint32
     lr = g.lrank[(g.npr ? g.lbase[g.npr - 1] : g.lbase[g.len[r] - g.k]) + pos];
 }
 // the source of record i: the last s with seg[s] <= i, from a lower bound s0
-__device__ __forceinline__ uint32_t recv_source(const RecvGen &g, uint32_t s0, uint64_t i) {
-    while (s0 + 1 < g.P && g.seg[s0 + 1] <= i) ++s0;
+__device__ __forceinline__ uint32_t recv_source(const RecvGen &g, const RecvTab &t, uint32_t s0, uint64_t i) {
+    while (s0 + 1 < g.P && t.seg[s0 + 1] <= i) ++s0;
     return s0;
 }
 
 // VALS = false: key-only sort (records that carry their payload in the key).
 // RECV: the values are generated from the keys (RecvGen, first pass only)
+// (launch bounds: 4 waves per SIMD -- two 8-wave workgroups of an 8,192-key tile per CU,
+// as its LDS allows -- so <= 128 VGPRs)
 template <bool VALS, int RS_ITEMS, bool GEN = false, bool RECV = false>
-__global__ __launch_bounds__(RsDown<RS_ITEMS>::THREADS) void rs_downsweep_kernel(const uint64_t *kin,
+__global__ __launch_bounds__(RsDown<RS_ITEMS>::THREADS, 4) void rs_downsweep_kernel(const uint64_t *kin,
                                                                                  const uint32_t *vin, uint64_t *kout,
                                                                                  uint32_t *vout, uint64_t n, int shift,
                                                                                  const uint32_t *hist,
@@ -343,12 +361,21 @@ __global__ __launch_bounds__(RsDown<RS_ITEMS>::THREADS) void rs_downsweep_kernel
         if constexpr (!RECV) v[j] = (VALS && i < n) ? vin[i] : 0u;
     }
     if constexpr (RECV) {
+        __shared__ uint64_t tseg[2 * RS_RECV_PMAX + 1];
+        __shared__ uint32_t tstarts[RS_RECV_PMAX + 1];
+        RecvTab tab{rg.seg, rg.starts};
+        if (rg.P <= RS_RECV_PMAX) {  // (uniform)
+            for (uint32_t q = tid; q <= 2 * rg.P; q += NT) tseg[q] = rg.seg[q];
+            for (uint32_t q = tid; q <= rg.P; q += NT) tstarts[q] = rg.starts[q];
+            __syncthreads();
+            tab = RecvTab{tseg, tstarts};
+        }
         // decode: the sub-tile's first source by a wave-uniform search, then
         // stepped forward per slice and per lane past segment boundaries
         uint32_t s = 0, hi = rg.P;
         while (hi - s > 1) {
             const uint32_t mid = (s + hi) >> 1;
-            if (rg.seg[mid] <= sub) s = mid; else hi = mid;
+            if (tab.seg[mid] <= sub) s = mid; else hi = mid;
         }
         s = (uint32_t)__builtin_amdgcn_readfirstlane((int)s);
         // read of the element before the sub-tile (loff boundaries at its start)
@@ -356,18 +383,18 @@ __global__ __launch_bounds__(RsDown<RS_ITEMS>::THREADS) void rs_downsweep_kernel
         if (sub > 0 && sub <= n) {
             const uint64_t ip = sub - 1;
             uint32_t sp = s;
-            while (sp > 0 && rg.seg[sp] > ip) --sp;
+            while (sp > 0 && tab.seg[sp] > ip) --sp;
             uint32_t lrp;
-            recv_decode(rg, sp, sp, rg.starts[sp], rs_load_key(kin + ip), rprev, lrp);
+            recv_decode(rg, tab, sp, sp, tab.starts[sp], rs_load_key(kin + ip), rprev, lrp);
         }
 #pragma unroll
         for (int j = 0; j < RS_SLICES; ++j) {
             const uint64_t i = sub + (uint64_t)j * 64 + lane;
             const bool valid = i < n;
-            s = (uint32_t)__builtin_amdgcn_readfirstlane((int)recv_source(rg, s, sub + (uint64_t)j * 64));
-            const uint32_t st0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)rg.starts[s]);
+            s = (uint32_t)__builtin_amdgcn_readfirstlane((int)recv_source(rg, tab, s, sub + (uint64_t)j * 64));
+            const uint32_t st0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)tab.starts[s]);
             uint32_t r = 0, lr = 0;
-            if (valid) recv_decode(rg, recv_source(rg, s, i), s, st0, k[j], r, lr);
+            if (valid) recv_decode(rg, tab, recv_source(rg, tab, s, i), s, st0, k[j], r, lr);
             v[j] = (r << rg.lb) | lr;
             if (valid) k[j] = (k[j] & 0xFFFFFFFF00000000ull) | (uint32_t)i;
             // loff[a] = i for the reads (read(i - 1), read(i)] (read(-1) = -1)
@@ -425,20 +452,48 @@ __global__ __launch_bounds__(RsDown<RS_ITEMS>::THREADS) void rs_downsweep_kernel
         const uint64_t i = sub + (uint64_t)j * 64 + lane;
         if (i < n) {
             const uint32_t d = (uint32_t)(k[j] >> shift) & 255u;
-            const uint32_t pos = S.cnt[w][d] + rk[j];
-            S.key[pos] = k[j];
-            if constexpr (VALS) S.val[pos] = v[j];
+            rk[j] += S.cnt[w][d];  // the element's slot in the staged tile
+            S.key[rk[j]] = k[j];
         }
     }
     __syncthreads();
     const uint32_t nt = (uint32_t)min((uint64_t)RS_TILE, n - base);
-    for (uint32_t i = tid; i < nt; i += NT) {
-        const unsigned long long kk = S.key[i];
-        const uint32_t d = (uint32_t)(kk >> shift) & 255u;
-        const uint32_t pos = S.gofs[d] + (i - S.lofs[d]);
-        if (nt_out) __builtin_nontemporal_store(kk, kout + pos);
-        else kout[pos] = kk;
-        if constexpr (VALS) vout[pos] = S.val[i];
+    if constexpr (!VALS) {
+        for (uint32_t i = tid; i < nt; i += NT) {
+            const unsigned long long kk = S.key[i];
+            const uint32_t d = (uint32_t)(kk >> shift) & 255u;
+            const uint32_t pos = S.gofs[d] + (i - S.lofs[d]);
+            if (nt_out) __builtin_nontemporal_store(kk, kout + pos);
+            else kout[pos] = kk;
+        }
+    } else {
+        // keys out, each thread keeping its slots' output positions; then the values
+        // take the slots and follow to the same positions
+        constexpr int PER = RS_TILE / NT;
+        uint32_t gp[PER];
+#pragma unroll
+        for (int m = 0; m < PER; ++m) {
+            const uint32_t i = tid + m * NT;
+            gp[m] = 0;
+            if (i < nt) {
+                const unsigned long long kk = S.key[i];
+                const uint32_t d = (uint32_t)(kk >> shift) & 255u;
+                gp[m] = S.gofs[d] + (i - S.lofs[d]);
+                if (nt_out) __builtin_nontemporal_store(kk, kout + gp[m]);
+                else kout[gp[m]] = kk;
+            }
+        }
+        __syncthreads();
+        uint32_t *sv = reinterpret_cast<uint32_t *>(S.key);
+#pragma unroll
+        for (int j = 0; j < RS_SLICES; ++j)
+            if (sub + (uint64_t)j * 64 + lane < n) sv[rk[j]] = v[j];
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < PER; ++m) {
+            const uint32_t i = tid + m * NT;
+            if (i < nt) vout[gp[m]] = sv[i];
+        }
     }
 }
 
