@@ -405,7 +405,9 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
                  const uint64_t *occ_off, uint32_t n_reads, uint32_t npr, const uint2 *rl,
                  const int32_t *len, bool strict, void *stmp, Counters *cnt, PartArgs &PA,
                  unsigned long long &big_buckets, int skip_bits = 0, int phase = 0, const uint32_t *pv = nullptr,
-                 const KeyGen *kgen = nullptr, const RecvGen *recv = nullptr) {
+                 const KeyGen *kgen = nullptr, const RecvGen *recv = nullptr, bool counters_zeroed = false) {
+    // counters_zeroed: the caller cleared the whole Counters block just before (its
+    // partition-list counts then need no clear of their own)
     // phase 0: everything; 1: sort + LDS tiers, no readback (the caller's
     // first pair-count pass aborts on big_n); 2: only the global path of the
     // partitions phase 1 listed (keys / PA as phase 1 left them)
@@ -531,7 +533,7 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
             ENSURE(c->d_brank, n + 1, &c->bkt_rank_dev);
             HIPCHK(hipMemsetAsync(PA.is_head, 0, n + 1, c->stream));
         }
-        if (!c->counters_fresh)  // (a fresh Counters block is all zero already)
+        if (!counters_zeroed)
             HIPCHK(hipMemsetAsync(&cnt->mid_n, 0, 3 * sizeof(uint32_t), c->stream));  // mid_n, mid2_n, fb_n
         {
             // the bounds kernel lists the partitions above 1,024 records; their
@@ -649,7 +651,10 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
                const uint32_t *read_order, uint32_t n_items, Counters *cnt, uint64_t &np, uint64_t &cap_s_out,
                const uint32_t *item_start = nullptr, uint32_t n_multi = 0, const uint32_t *abort_flag = nullptr,
                bool *aborted = nullptr, bool *per_read = nullptr, uint64_t *distinct_ub = nullptr,
-               uint32_t owners = 1, const uint32_t *owner_starts = nullptr, const uint32_t *item_owner = nullptr) {
+               uint32_t owners = 1, const uint32_t *owner_starts = nullptr, const uint32_t *item_owner = nullptr,
+               bool counters_zeroed = false) {
+    // counters_zeroed: the caller cleared the whole Counters block and nothing has counted
+    // since (the cursors and the overflow count then need no clear of their own)
     // per_read (in: allowed; out: used): the first pass writes each read's
     // dispatched pairs, trail-ascending, into a fixed region of PC_RREG slots
     // (wide ids, dispatched pairs only, one device); a read whose table
@@ -766,11 +771,10 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
         O.rcnt = rcnt;
         // (cursor, role pairs, dummy, distinct: a pass re-run after an abort or
         // in the shared-region mode counts from zero)
-        if (!c->counters_fresh) {  // (the first pass after the build's Counters clear skips these)
+        if (!counters_zeroed) {
             HIPCHK(hipMemsetAsync(cnt->cursor, 0, 4 * NSHARD * sizeof(unsigned long long), c->stream));
             HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(uint32_t), c->stream));
         }
-        c->counters_fresh = false;
         if (owners > 1) HIPCHK(hipMemsetAsync(dcur, 0, (size_t)R * 8, c->stream));
         if (!skip_first) {
             StageScope st(c, SA_STAGE_PAIRS);
@@ -1051,8 +1055,7 @@ int device_build(sa_ctx *c, bool readback) {
     EmitParams E = emit_params(c);
     Counters *cnt;
     ENSURE(c->d_cnt, 1, &cnt);
-    HIPCHK(hipMemsetAsync(cnt, 0, sizeof(Counters), c->stream));
-    c->counters_fresh = true;
+    HIPCHK(hipMemsetAsync(cnt, 0, sizeof(Counters), c->stream));  // (the first bucket and pair stages rely on it)
 
     uint64_t *keys, *keys2; uint32_t *vals, *vals2; void *stmp;
     ENSURE(c->d_keys, n, &keys);
@@ -1137,7 +1140,7 @@ int device_build(sa_ctx *c, bool readback) {
     const int bphase = strict ? 0 : 1;
     rc = bucket_stage(c, keys, keys2, vals, vals2, n, (const uint64_t *)c->d_occ_off.p, nr, c->uniform_npr,
                       orl, (const int32_t *)c->d_len.p, strict, stmp, cnt, PA, big_buckets, 0, bphase, nullptr,
-                      use_kgen ? &kg : nullptr);
+                      use_kgen ? &kg : nullptr, nullptr, true);
     if (rc) return rc;
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
     if (strict) {
@@ -1197,7 +1200,7 @@ int device_build(sa_ctx *c, bool readback) {
     bool per_read = per_read_ok;
     uint64_t np_ub = 0;
     rc = pair_stage(c, E, PI, strict, emit_all, read_order, nr, cnt, np, cap_s, nullptr, 0,
-                    bphase == 1 ? &cnt->big_n : nullptr, &aborted, &per_read, &np_ub);
+                    bphase == 1 ? &cnt->big_n : nullptr, &aborted, &per_read, &np_ub, 1, nullptr, nullptr, true);
     if (rc) return rc;
     if (aborted) {  // partitions above 4,096 records (high-copy repeats): build them, count again
         rc = bucket_stage(c, keys, keys2, vals, vals2, n, (const uint64_t *)c->d_occ_off.p, nr, c->uniform_npr,
@@ -2105,8 +2108,7 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint6
     if (n >= 0xFFFFFFF0ull) return fail(c, SA_E_OVERFLOW, "more than 2^32 - 16 k-mers received on one rank");
     Counters *cnt;
     ENSURE(c->d_cnt, 1, &cnt);
-    HIPCHK(hipMemsetAsync(cnt, 0, sizeof(Counters), c->stream));
-    c->counters_fresh = true;
+    HIPCHK(hipMemsetAsync(cnt, 0, sizeof(Counters), c->stream));  // (the bucket and pair stages rely on it)
     // received records are in global occurrence order (sources in rank order,
     // each in occurrence order): local index i <-> i-th owned occurrence
     uint2 *rl; uint32_t *vals, *vals2; uint64_t *loff, *keys2, *dseg; uint8_t *stmp;
@@ -2157,7 +2159,7 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint6
     PartArgs PA{};
     unsigned long long big_buckets = 0;
     rc = bucket_stage(c, keys, keys2, vals, vals2, n, loff, N, 0, packed ? nullptr : rl, nullptr, false, stmp, cnt,
-                      PA, big_buckets, c->log_ranks, 0, pv, nullptr, fused ? &RG : nullptr);
+                      PA, big_buckets, c->log_ranks, 0, pv, nullptr, fused ? &RG : nullptr, true);
     if (rc) return rc;
     PairIn PI{};
     PI.rec = PA.rec; PI.xrec = PA.xrec; PI.lst = PA.lst;
@@ -2183,7 +2185,7 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint6
         HIPCHK(launch_pc_item_owners(items, n_multi, (const uint32_t *)c->d_starts.p, (uint32_t)P, items + n_multi + 1,
                                      c->stream));
     rc = pair_stage(c, E, PI, false, true, nullptr, N, cnt, np, cap_s, items, n_multi, nullptr, nullptr, nullptr,
-                    nullptr, (uint32_t)P, (const uint32_t *)c->d_starts.p, items + n_multi + 1);
+                    nullptr, (uint32_t)P, (const uint32_t *)c->d_starts.p, items + n_multi + 1, true);
     if (rc) return rc;
     Counters hc;
     HIPCHK(hipMemcpyAsync(&hc, cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));

@@ -137,9 +137,6 @@ struct sa_ctx {
     int aligner = SA_ALIGNER_LINEAR;  // SA_OPT_ALIGNER (--linear-align / --quadratic-align)
     uint64_t local_batch_bytes = 16ull << 30;  // traceback-code budget of one quadratic launch
     bool built = false, aligned = false;
-    // the device Counters were just zeroed on the stream and nothing has counted
-    // into the pair-count or tier-list fields since: their own clears can be skipped
-    bool counters_fresh = false;
 #ifdef SA_PB_STAMPS
     uint64_t *stamps_dev = nullptr;  // (timing probe builds, partition.hip PB_STAMP)
     uint32_t stamps_np = 0;
