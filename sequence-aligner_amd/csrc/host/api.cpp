@@ -302,7 +302,7 @@ DevReads dev_reads(sa_ctx *c) {
 }
 
 EmitParams emit_params(sa_ctx *c) {
-    EmitParams e;
+    EmitParams e{};
     e.k = c->set.kmer_size;
     e.m = c->m;
     e.lb = c->lb;
@@ -344,6 +344,12 @@ int ensure_prepared(sa_ctx *c) {
 // the packed reads (radix_sort_gen), so they are never written and re-read
 // unsorted, and pack_emit only packs and writes the locality keys.
 // SA_KEYGEN=0 keeps the stored records (A/B)
+// the pack kernel counts the first radix pass's digits (SA_HIST_IN_PACK=0: the upsweep does)
+static bool hist_in_pack() {
+    static const bool on = !getenv("SA_HIST_IN_PACK") || atoi(getenv("SA_HIST_IN_PACK")) != 0;  // (A/B)
+    return on;
+}
+
 static bool make_keygen(const sa_ctx *c, const EmitParams &E, uint64_t n, KeyGen &kg) {
     static const bool env_on = !getenv("SA_KEYGEN") || atoi(getenv("SA_KEYGEN")) != 0;
     const size_t nr = c->woff.empty() ? 0 : c->woff.size() - 1;
@@ -401,6 +407,15 @@ static void set_part_shortcuts(const sa_ctx *c, PartArgs &PA, uint32_t npr) {
 // mix, then one LDS workgroup per partition (part_build), the global scan path
 // for partitions too large for LDS.  Read ids come from rid[val] when given
 // (distributed mode), else from the occurrence offsets.
+// partition bits of the bucket build for n records (see bucket_stage)
+static int part_bits(uint64_t n) {
+    const uint64_t part_target = 700;
+    int PB = 1;
+    while (PB < 24 && (part_target << PB) < n) ++PB;
+    if (PB > 16 && (n >> 16) <= 900) PB = 16;
+    return PB;
+}
+
 int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, uint32_t *vals2, uint64_t n,
                  const uint64_t *occ_off, uint32_t n_reads, uint32_t npr, const uint2 *rl,
                  const int32_t *len, bool strict, void *stmp, Counters *cnt, PartArgs &PA,
@@ -422,10 +437,7 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
     // (round 4, same-box A/B at the bench shape: ~1,100-1,400-record partitions
     // with the 2,048-record tier as the main pass -- 8 waves per block -- built
     // buckets in 1.53-1.55 ms against 1.15 for ~700-record ones on the 1,024 tier)
-    const uint64_t part_target = 700;
-    int PB = 1;
-    while (PB < 24 && (part_target << PB) < n) ++PB;
-    if (PB > 16 && (n >> 16) <= 900) PB = 16;
+    const int PB = part_bits(n);
     const uint32_t nparts = 1u << PB;
     const int kbits = 32 + c->lb;  // LDS sort key: mix << lb | loc rank
     uint2 *srl = nullptr;
@@ -771,7 +783,7 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
         O.rcnt = rcnt;
         // (cursor, role pairs, dummy, distinct: a pass re-run after an abort or
         // in the shared-region mode counts from zero)
-        if (!counters_zeroed) {
+        if (!counters_zeroed || attempt > 0) {  // (a re-run attempt counts from zero)
             HIPCHK(hipMemsetAsync(cnt->cursor, 0, 4 * NSHARD * sizeof(unsigned long long), c->stream));
             HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(uint32_t), c->stream));
         }
@@ -1116,7 +1128,11 @@ int device_build(sa_ctx *c, bool readback) {
     const bool use_kgen = fused && make_keygen(c, E, n, kg);
     {
         StageScope st(c, SA_STAGE_EMIT);
-        if (fused) HIPCHK(launch_pack_emit(R, E, use_kgen ? nullptr : keys, c->stream));
+        if (use_kgen && hist_in_pack()) {  // + the first radix pass's tile histogram
+            E.hist = (uint32_t *)stmp;
+            E.hist_shift = kg.hist_shift = 64 - part_bits(n);
+            HIPCHK(launch_pack_emit_hist(R, E, n, c->stream));
+        } else if (fused) HIPCHK(launch_pack_emit(R, E, use_kgen ? nullptr : keys, c->stream));
         else HIPCHK(launch_kmer_emit(R, E, keys, vals, c->stream));
     }
     // reads in locality order (overlapping reads adjacent) for pair_count: by
@@ -2050,7 +2066,11 @@ int sa_dist_emit(sa_ctx *c, void *send_recs, uint64_t *counts) {
     const bool use_kgen = fused && make_keygen(c, E, n, kg);
     {
         StageScope st(c, SA_STAGE_EMIT);
-        if (fused) HIPCHK(launch_pack_emit(R, E, use_kgen ? nullptr : keys, c->stream));
+        if (use_kgen && c->log_ranks > 0 && hist_in_pack()) {  // + the owner pass's tile histogram
+            E.hist = (uint32_t *)stmp;
+            E.hist_shift = kg.hist_shift = 64 - c->log_ranks;
+            HIPCHK(launch_pack_emit_hist(R, E, n, c->stream));
+        } else if (fused) HIPCHK(launch_pack_emit(R, E, use_kgen ? nullptr : keys, c->stream));
         else HIPCHK(launch_kmer_emit(R, E, keys, nullptr, c->stream));
     }
     // owner = top log2(P) bits of the mixed hash: one stable radix pass groups

@@ -190,6 +190,90 @@ __global__ __launch_bounds__(256) void pack_emit_kernel(DevReads r, EmitParams e
     }
 }
 
+// pack_emit_kernel's work for generated records (keys == nullptr) plus the first radix
+// pass's tile histogram (radix_sort_gen's upsweep, which would generate every record once
+// more): block t owns the records [t T, (t + 1) T) of one key-only tile.  It packs every read
+// overlapping them, writes words, bad position and locality key only for the reads whose
+// first k-mer is its own (each read has exactly one such block), and counts its own k-mers'
+// digits in LDS: hist[t * 256 + d], no global atomics.  Uniform lengths (npr k-mers per read).
+template <int T>
+__global__ __launch_bounds__(256) void pack_emit_hist_kernel(DevReads r, EmitParams e, uint64_t n) {
+    __shared__ uint32_t cnt[4][256];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (uint32_t q = tid; q < 4 * 256; q += 256) (&cnt[0][0])[q] = 0;
+    __syncthreads();
+    const int shift = 32 - 2 * e.m;
+    const int dsh = e.hist_shift - 32;  // the digit in the hash word (hist_shift >= 32)
+    const uint64_t t0 = (uint64_t)blockIdx.x * T, t1 = min(t0 + T, n);
+    const uint32_t npr = e.npr;
+    const uint32_t r0 = (uint32_t)(t0 / npr), r1 = (uint32_t)((t1 - 1) / npr);
+    for (uint32_t rd = r0 + w; rd <= r1; rd += 4) {
+        const uint64_t b0 = r.boff[rd];
+        const int32_t L = (int32_t)(r.boff[rd + 1] - b0);
+        const int32_t nw = (L + 15) >> 4;  // <= 64 (host-checked)
+        const uint64_t g0 = (uint64_t)rd * npr;
+        const bool own = g0 >= t0;  // the read's first k-mer is in this tile
+        int32_t first_bad = INT32_MAX;
+        uint32_t word = 0;
+        if ((int32_t)lane < nw) {
+            const int32_t p0 = (int32_t)lane << 4;
+            const uint64_t a = b0 + (uint64_t)p0;
+            const uint32_t *wp = reinterpret_cast<const uint32_t *>(r.ascii + (a & ~3ull));
+            const uint32_t sh = (uint32_t)(a & 3u);
+            uint32_t d[5];
+#pragma unroll
+            for (int j = 0; j < 5; ++j) d[j] = wp[j];
+            const int32_t valid = min(16, L - p0);
+            uint32_t badm = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t x = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
+                uint32_t bm;
+                const uint32_t c = codes4(x, bm);
+#pragma unroll
+                for (int b = 0; b < 4; ++b) word |= ((c >> (2 * b)) & 3u) << (30 - 2 * (4 * j + b));
+                badm |= bm << (4 * j);
+            }
+            const uint32_t vmask = valid >= 16 ? 0xFFFFu : ((1u << valid) - 1u);
+            word &= valid >= 16 ? 0xFFFFFFFFu : ~(0xFFFFFFFFu >> (2 * valid));
+            badm &= vmask;
+            if (badm) first_bad = p0 + (int32_t)__builtin_ctz(badm);
+            if (own) r.codes[r.woff[rd] + lane] = word;
+        }
+        if (own) {
+            for (int off = 32; off > 0; off >>= 1) {
+                const int32_t o = __shfl_xor(first_bad, off, 64);
+                first_bad = o < first_bad ? o : first_bad;
+            }
+            if (lane == 0) r.bad[rd] = first_bad;
+        }
+        // own reads: every k-mer (locality key); the others: only this tile's k-mers
+        const int32_t nk = (int32_t)npr;
+        const int32_t lo_i = own ? 0 : (int32_t)(t0 - g0);
+        const int32_t hi_i = (int32_t)min<uint64_t>((uint64_t)nk, own ? (uint64_t)nk : t1 - g0);
+        uint32_t kmin = 0xFFFFFFFFu;
+        for (int32_t i0 = lo_i & ~63; i0 < hi_i; i0 += 64) {  // wave-uniform trip count (shuffles)
+            const int32_t i = i0 + (int32_t)lane;
+            const int q = (i >> 4) & 63, s2 = i & 15;
+            const uint32_t wa = (uint32_t)__shfl((int)word, q, 64), wb = (uint32_t)__shfl((int)word, (q + 1) & 63, 64);
+            if (i < lo_i || i >= hi_i) continue;
+            uint32_t x = s2 == 0 ? wa : ((wa << (2 * s2)) | (wb >> (32 - 2 * s2)));
+            x = shift == 32 ? 0u : (x >> shift);
+            x ^= (x >> 1) & 0x55555555u;
+            const uint32_t h = mix32(x);
+            kmin = min(kmin, h);
+            const uint64_t g = g0 + (uint64_t)i;
+            if (g >= t0 && g < t1) atomicAdd(&cnt[w][(h >> dsh) & 255u], 1u);
+        }
+        if (own && e.rkey) {
+            for (int off = 32; off > 0; off >>= 1) kmin = min(kmin, (uint32_t)__shfl_xor(kmin, off, 64));
+            if (lane == 0) { e.rkey[rd] = kmin; e.rord[rd] = rd; }
+        }
+    }
+    __syncthreads();
+    e.hist[(uint64_t)blockIdx.x * 256 + tid] = cnt[0][tid] + cnt[1][tid] + cnt[2][tid] + cnt[3][tid];
+}
+
 static uint32_t grid_for_waves(uint64_t waves) {
     uint64_t blocks = (waves + 3) / 4;
     if (blocks > 8192) blocks = 8192;
@@ -206,6 +290,14 @@ hipError_t launch_kmer_emit(const DevReads &r, const EmitParams &p, uint64_t *ke
                             hipStream_t s) {
     if (r.n == 0) return hipSuccess;
     hipLaunchKernelGGL(kmer_emit_kernel, dim3(grid_for_waves(r.n)), dim3(256), 0, s, r, p, keys, vals);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_emit_hist(const DevReads &r, const EmitParams &p, uint64_t n, hipStream_t s) {
+    constexpr uint32_t T = 8192;  // = radix_key_tile() (sort_scan.hip; checked by the caller)
+    if (r.n == 0 || n == 0) return hipSuccess;
+    if (!p.npr || !p.hist || p.hist_shift < 32 || radix_key_tile() != T) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(pack_emit_hist_kernel<T>, dim3((uint32_t)((n + T - 1) / T)), dim3(256), 0, s, r, p, n);
     return hipGetLastError();
 }
 

@@ -604,9 +604,13 @@ size_t radix_sort_temp_bytes(uint64_t n) {  // (the smallest tile: the most tile
 }
 
 // one key-only pass at RS_ITEMS keys per lane-slot of a tile
+uint32_t radix_key_tile() { return RsTile<RS_ITEMS_KEYS>::TILE; }
+
+// (counted = true: hist already holds this pass's tile counts -- launch_pack_emit_hist)
 template <int RS_ITEMS, bool GEN = false>
 static hipError_t rs_pass_keys(const uint64_t *kin, uint64_t *kout, uint64_t n, int shift, uint32_t *hist,
-                               void *stmp, hipStream_t s, const KeyGen &kg = KeyGen{}, bool nt_out = false) {
+                               void *stmp, hipStream_t s, const KeyGen &kg = KeyGen{}, bool nt_out = false,
+                               bool counted = false) {
     using SK = RsShared<false, RsTile<RS_ITEMS>::TILE, RsDown<RS_ITEMS>::WAVES>;
     static const size_t sk_lds = occ_lds("SA_OCC_RS", sizeof(SK), sizeof(SK));  // (A/B)
     static bool attr_set = false;
@@ -616,8 +620,9 @@ static hipError_t rs_pass_keys(const uint64_t *kin, uint64_t *kout, uint64_t n, 
         attr_set = true;
     }
     const uint64_t nb = (n + RsTile<RS_ITEMS>::TILE - 1) / RsTile<RS_ITEMS>::TILE;
-    hipLaunchKernelGGL((rs_upsweep_kernel<RS_ITEMS, GEN>), dim3((uint32_t)nb), dim3(RsUp<RS_ITEMS>::THREADS), 0, s,
-                       kin, n, shift, hist, (uint32_t)nb, kg);
+    if (!counted)
+        hipLaunchKernelGGL((rs_upsweep_kernel<RS_ITEMS, GEN>), dim3((uint32_t)nb), dim3(RsUp<RS_ITEMS>::THREADS), 0,
+                           s, kin, n, shift, hist, (uint32_t)nb, kg);
     hipError_t e = rs_offsets(hist, nb, stmp, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((rs_downsweep_kernel<false, RS_ITEMS, GEN>), dim3((uint32_t)nb),
@@ -722,7 +727,8 @@ hipError_t radix_sort_gen(const KeyGen &g, uint64_t **keys, uint64_t **keys_alt,
     const bool nt0 = nt_env && lo + 8 >= hi;
     hipError_t e = n >= RS_BIG_TILE_KEYS
                        ? rs_pass_keys<2 * RS_ITEMS_KEYS, true>(nullptr, *keys, n, lo, hist, stmp, s, g, nt0)
-                       : rs_pass_keys<RS_ITEMS_KEYS, true>(nullptr, *keys, n, lo, hist, stmp, s, g, nt0);
+                       : rs_pass_keys<RS_ITEMS_KEYS, true>(nullptr, *keys, n, lo, hist, stmp, s, g, nt0,
+                                                           g.hist_shift == lo);
     if (e != hipSuccess) return e;
     for (int shift = lo + 8; shift < hi; shift += 8) {
         const bool nt = nt_env && shift + 8 >= hi;

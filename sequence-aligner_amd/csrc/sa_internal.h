@@ -38,6 +38,10 @@ struct EmitParams {
     // mixed lengths without pos_bits codes: per-occurrence {read, loc rank}
     // table (nullable), so the bucket build finds both with one load
     uint2 *occ_rl;
+    // uniform lengths (KeyGen): the first radix pass's tile histogram, counted by the
+    // pack kernel from the hashes it computes anyway (launch_pack_emit_hist; nullptr: off)
+    uint32_t *hist;
+    int hist_shift;            // the pass's digit: bits [hist_shift, hist_shift + 8) of the record
 };
 
 // bijective 32-bit mix of the seqHash: equal mix <=> equal hash, so a bucket
@@ -79,6 +83,8 @@ struct KeyGen {
     uint32_t npr;              // k-mers per read (>= 1)
     uint64_t npr_magic;        // floor((2^64 - 1) / npr) + 1 (npr >= 2)
     int shift;                 // 32 - 2 min(16, k)
+    int hist_shift = -1;       // >= 0: the tile histogram of the pass at this shift is already
+                               // in the sort's temp (launch_pack_emit_hist): no upsweep
 };
 __device__ __forceinline__ uint64_t gen_key(const KeyGen &g, uint64_t i) {
     const uint32_t r = g.npr == 1 ? (uint32_t)i : (uint32_t)__umul64hi((unsigned long long)i, g.npr_magic);
@@ -325,6 +331,10 @@ struct DevAlignment {            // mirrors sa_alignment
 hipError_t launch_pack_reads(const DevReads &r, hipStream_t s);
 // pack + emit in one pass (reads of <= 1,024 bases)
 hipError_t launch_pack_emit(const DevReads &r, const EmitParams &p, uint64_t *keys, hipStream_t s);
+// pack_emit without records (KeyGen) that also writes p.hist (the first key-only radix
+// pass's tile histogram at p.hist_shift, tiles of radix_key_tile() records); n = records
+uint32_t radix_key_tile();
+hipError_t launch_pack_emit_hist(const DevReads &r, const EmitParams &p, uint64_t n, hipStream_t s);
 hipError_t launch_kmer_emit(const DevReads &r, const EmitParams &p, uint64_t *keys, uint32_t *vals,
                             hipStream_t s);
 
