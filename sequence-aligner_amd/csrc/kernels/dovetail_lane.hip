@@ -880,8 +880,15 @@ struct BandX2 {
     uint32_t acc[16];
     u16x2 best;
     uint32_t bpos;
-    int32_t ap[2], bp[2];
-    uint32_t awd[2], pa[2], bw[2], pb[2];
+    // A words realigned to the pair's phase-2 start ds: ra = A bases [ds + 16 m, +16) for the
+    // rows 16 m + 1 .. 16 m + 16, so every lane changes word on the same rows; aw1 / aw2 the
+    // next two aligned words (aw2's load issued 16 rows before it is used), as = ds mod 16,
+    // aj the next aligned word to load.  B positions (9 + u - 1 on row u) are the same for
+    // every lane: bw the current word, bw1 the next (loaded 16 rows ahead).  No word load is
+    // waited on within 16 rows of its issue -- the row loop's loads were once every row and
+    // their vmcnt waits also drained the code stores issued before them.
+    uint32_t ra[2], aw1[2], aw2[2], bw[2], bw1[2];
+    int32_t as[2], aj[2];
 };
 
 __device__ __forceinline__ uint32_t x2_sel(uint32_t b0, uint32_t b1) {
@@ -907,9 +914,10 @@ __device__ __forceinline__ void band_row_x2(BandX2 &S, const int32_t u, const ui
                                             const int32_t awl0, const int32_t awl1, const int32_t bwl0,
                                             const int32_t bwl1, const uint32_t *dummy, uint32_t *tb, uint64_t nl) {
     uint32_t cp[2];
+    const int ash = 30 - 2 * ((u - 1) & 15);  // (uniform)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-        const uint32_t a = (S.awd[h] >> (30 - 2 * (S.ap[h] & 15))) & 3u;
+        const uint32_t a = (S.ra[h] >> ash) & 3u;
         const uint32_t c01 = (a & 1) ? cpa[1] : cpa[0], c23 = (a & 1) ? cpa[3] : cpa[2];
         cp[h] = (a & 2) ? c23 : c01;
     }
@@ -946,18 +954,31 @@ __device__ __forceinline__ void band_row_x2(BandX2 &S, const int32_t u, const ui
         Xl = X;
     }
     uint32_t bnew[2];
+    const int32_t bp = 8 + u;  // this row's new B position (uniform)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-        const LanePair &q = h ? q1 : q0;
-        const int32_t awl = h ? awl1 : awl0, bwl = h ? bwl1 : bwl0, LB = h ? LB1 : LB0;
-        ++S.ap[h];
-        S.awd[h] = (S.ap[h] & 15) == 0 ? S.pa[h] : S.awd[h];
-        S.pa[h] = gld((((S.ap[h] + 1) & 15) == 0) ? q.Aw + min((S.ap[h] + 1) >> 4, awl) : dummy, 0);
-        bnew[h] = S.bp[h] < LB ? (S.bw[h] >> (30 - 2 * (S.bp[h] & 15))) & 3u : 0u;
-        ++S.bp[h];
-        S.bw[h] = (S.bp[h] & 15) == 0 ? S.pb[h] : S.bw[h];
-        S.pb[h] = gld((((S.bp[h] + 1) & 15) == 0) ? q.Bw + min((S.bp[h] + 1) >> 4, bwl) : dummy, 0);
+        const int32_t LB = h ? LB1 : LB0;
+        bnew[h] = bp < LB ? (S.bw[h] >> (30 - 2 * (bp & 15))) & 3u : 0u;
     }
+    if (((bp + 1) & 15) == 0) {  // (uniform) the next row starts B word (bp + 1) >> 4
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const LanePair &q = h ? q1 : q0;
+            S.bw[h] = S.bw1[h];
+            S.bw1[h] = gld(q.Bw, min(((bp + 1) >> 4) + 1, h ? bwl1 : bwl0));
+        }
+    }
+    if ((u & 15) == 0) {  // (uniform) the next row starts realigned A word u >> 4
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const LanePair &q = h ? q1 : q0;
+            S.ra[h] = S.as[h] == 0 ? S.aw1[h] : __builtin_amdgcn_alignbit(S.aw1[h], S.aw2[h], 32 - 2 * S.as[h]);
+            S.aw1[h] = S.aw2[h];
+            S.aw2[h] = gld(q.Aw, min(S.aj[h], h ? awl1 : awl0));
+            ++S.aj[h];
+        }
+    }
+    (void)dummy;
 #pragma unroll
     for (int k = 0; k < 15; ++k) S.sel[k] = S.sel[k + 1];
     S.sel[15] = x2_sel(bnew[0], bnew[1]);
@@ -1040,12 +1061,17 @@ __global__ __launch_bounds__(256) void dovetail_p2tbx2_kernel(DevReads rd, const
     for (int h = 0; h < 2; ++h) {
         awl[h] = max((q[h].LA + 15) / 16 - 1, 0);
         bwl[h] = max((LBh[h] + 15) / 16 - 1, 0);
-        S.bp[h] = LW - zr;
-        S.bw[h] = q[h].Bw[min(S.bp[h] >> 4, bwl[h])];
-        S.pb[h] = q[h].Bw[min((S.bp[h] >> 4) + 1, bwl[h])];
-        S.ap[h] = ds[h];
-        S.awd[h] = q[h].Aw[min(S.ap[h] >> 4, awl[h])];
-        S.pa[h] = q[h].Aw[min((S.ap[h] >> 4) + 1, awl[h])];
+        // row 1's B position LW - zr = 9 lies in word 0
+        S.bw[h] = q[h].Bw[0];
+        S.bw1[h] = q[h].Bw[min(1, bwl[h])];
+        // realigned A word 0 = bases [ds, ds + 16) from aligned words j0, j0 + 1
+        const int32_t j0 = ds[h] >> 4;
+        S.as[h] = ds[h] & 15;
+        const uint32_t w0 = q[h].Aw[min(j0, awl[h])];
+        S.aw1[h] = q[h].Aw[min(j0 + 1, awl[h])];
+        S.aw2[h] = q[h].Aw[min(j0 + 2, awl[h])];
+        S.aj[h] = j0 + 3;
+        S.ra[h] = S.as[h] == 0 ? w0 : __builtin_amdgcn_alignbit(w0, S.aw1[h], 32 - 2 * S.as[h]);
     }
     uint32_t *tb = tbbuf + tl;
     __builtin_amdgcn_s_waitcnt(0);
