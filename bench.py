@@ -479,7 +479,8 @@ def main():
     # over the hot loops' static mix (tools/isa_mix.py): lane-ops/s the SIMDs can
     # issue for THIS instruction mix; the 2-cycle figure stays beside it as nominal.
     mix, mix_src = isa_mix()
-    kern = (("sa::dovetail_p1x2_kernel", "dovetail_p1x2"), ("sa::dovetail_p2tbx2_kernel", "dovetail_p2tbx2"))
+    # (phase 1 is dovetail_p1x2_seg_kernel since round 5, dovetail_p1x2_kernel before: one prefix)
+    kern = (("sa::dovetail_p1x2_", "dovetail_p1x2"), ("sa::dovetail_p2tbx2_kernel", "dovetail_p2tbx2"))
     valu_k = [pmc_sum(rows, (kn,), "SQ_INSTS_VALU_avg") for kn, _ in kern]
     valu = sum(valu_k) if None not in valu_k else None
     valu_ach = valu * 64 / (al_ms * 1e-3) / 1e12 if valu is not None and al_ms > 0 else None

@@ -26,7 +26,8 @@ SRC = os.path.join(ROOT, "sequence-aligner_amd", "csrc", "kernels", "dovetail_la
 CHEAP = ("v_add_u32", "v_sub_u32", "v_subrev_u32", "v_and_b32", "v_or_b32", "v_xor_b32", "v_bitop3_b32",
          "v_lshrrev_b32", "v_ashrrev_i32", "v_max_u16", "v_add_u16", "v_sub_u16", "v_mov_b32")
 COST_CHEAP, COST_FULL = 2.55, 4.35
-KERNELS = {"dovetail_p1x2": "_ZN2sa20dovetail_p1x2_kernel", "dovetail_p2tbx2": "_ZN2sa22dovetail_p2tbx2_kernel"}
+# (phase 1 runs as dovetail_p1x2_seg_kernel since round 5: the same row loop as dovetail_p1x2_kernel)
+KERNELS = {"dovetail_p1x2": "_ZN2sa24dovetail_p1x2_seg_kernel", "dovetail_p2tbx2": "_ZN2sa22dovetail_p2tbx2_kernel"}
 
 
 def main(out):
