@@ -471,9 +471,6 @@ __device__ __forceinline__ void part_build_one(const PartArgs &A, const uint32_t
 // block is spent reading the bounds of a partition already built while holding
 // 44 / 84 KB of LDS, and a partition of ~1,100 records is sorted over 2,048
 // slots, not 4,096 (the tail of the stage is one such block's latency).
-#ifndef SA_PB_PERSIST
-#define SA_PB_PERSIST 0  // (A/B builds: n > 0 = main pass as n x 256 persistent blocks)
-#endif
 template <int CAP, bool STRICT, bool MAIN>
 __global__ __launch_bounds__(PbShape<CAP>::NT) void part_build_kernel(PartArgs A) {
     extern __shared__ __align__(16) uint8_t smem_raw[];
@@ -483,20 +480,10 @@ __global__ __launch_bounds__(PbShape<CAP>::NT) void part_build_kernel(PartArgs A
         // the main pass: one block per partition (two per block, the second's
         // records loading while the first is built, measured no faster: 1.32 ms
         // either way, profiles/r04/ab/ab_tier_order_pair_build.txt)
-#if SA_PB_PERSIST
-        for (uint32_t p = blockIdx.x; p < A.np; p += gridDim.x) {  // (A/B: persistent blocks)
-            __syncthreads();
-            PartLoad<CAP> L;
-            PB_STAMP(A, p, 0);
-            part_load<CAP>(A, p, L);
-            part_build_one<CAP, STRICT>(A, p, S, Sr, L);
-        }
-#else
         PartLoad<CAP> L;
         PB_STAMP(A, blockIdx.x, 0);
         part_load<CAP>(A, blockIdx.x, L);
         part_build_one<CAP, STRICT>(A, blockIdx.x, S, Sr, L);
-#endif
     } else {
         // (split tier: the partitions it handed on, then the mid-list entries past its grid)
         const bool fb = CAP < 4096 && A.split;
@@ -746,12 +733,7 @@ hipError_t launch_part_build(const PartArgs &a, bool strict, int cap, hipStream_
         hipLaunchKernelGGL(part_split_kernel, dim3(2 * (a.np < SPLIT_MAX ? a.np : SPLIT_MAX)), dim3(PbShape<1024>::NT),
                            lds, s, a);
     } else if (cap == 1024) {
-#if SA_PB_PERSIST
-        const uint32_t g1 = a.np < (uint32_t)(SA_PB_PERSIST * 256) ? a.np : (uint32_t)(SA_PB_PERSIST * 256);
-#else
-        const uint32_t g1 = a.np;
-#endif
-        if (strict) PB_LAUNCH(1024, g1, true, true); else PB_LAUNCH(1024, g1, false, true);
+        if (strict) PB_LAUNCH(1024, a.np, true, true); else PB_LAUNCH(1024, a.np, false, true);
     } else if (cap == 2048) {
         if (strict) PB_LAUNCH(2048, mid_grid, true, false); else PB_LAUNCH(2048, mid_grid, false, false);
     } else {
