@@ -121,3 +121,15 @@ def test_two_pairs_per_lane_kernels(oracle_mod, cost):
     reads = H.mutate(H.synth_reads(200, 490, 4000, gc=0.45, seed=21, mixed=(470, 497)), rng, 3)
     assert 467 <= min(map(len, reads)) and max(map(len, reads)) <= 500
     check(oracle_mod, reads, c, False, kmer_size=12)
+
+
+@pytest.mark.parametrize("segs", ["0", "1", "2", "5", "8"])
+def test_phase1_row_segments(oracle_mod, monkeypatch, segs):
+    """Phase 1 of the two-pairs-per-lane aligner in row segments (dovetail_p1x2_seg_kernel,
+    DESIGN.md 4.6): the lanes' state handed between ticketed one-wave workgroups through
+    device-scope atomics.  Every segment count -- 0 is the one-segment kernel -- gives the
+    oracle's alignments, on reads of 467..500 bp (pairs of different lengths in one wave)."""
+    monkeypatch.setenv("SA_P1_SEGS", segs)
+    rng = np.random.default_rng(22)
+    reads = H.mutate(H.synth_reads(240, 490, 4000, gc=0.45, seed=22, mixed=(467, 500)), rng, 3)
+    check(oracle_mod, reads, HOXD70, False, kmer_size=12)
