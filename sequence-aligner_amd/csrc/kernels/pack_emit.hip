@@ -196,8 +196,9 @@ __global__ __launch_bounds__(256) void pack_emit_kernel(DevReads r, EmitParams e
 // overlapping them, writes words, bad position and locality key only for the reads whose
 // first k-mer is its own (each read has exactly one such block), and counts its own k-mers'
 // digits in LDS: hist[t * 256 + d], no global atomics.  Uniform lengths (npr k-mers per read).
-// (NW waves per block, TPB tiles: one tile over 8 waves -- ~2 reads of 500 bp each -- keeps
-// the most waves in flight; 4 tiles over 4 waves measured slower, 0.146 vs 0.122 ms)
+// (NW waves per block, TPB tiles per block; same box at the bench shape, emit ms: one tile
+// over 4 waves 0.122, over 8 waves 0.124, over 16 waves 0.135, 4 tiles over 4 waves 0.146 --
+// profiles/r05/ab/ab_hist_in_pack.txt)
 template <int T, int TPB, int NW>
 __global__ __launch_bounds__(NW * 64) void pack_emit_hist_kernel(DevReads r, EmitParams e, uint64_t n) {
     __shared__ uint32_t cnt[TPB][256];
@@ -303,7 +304,7 @@ hipError_t launch_kmer_emit(const DevReads &r, const EmitParams &p, uint64_t *ke
 #define SA_PEH_TPB 1
 #endif
 #ifndef SA_PEH_NW
-#define SA_PEH_NW 8
+#define SA_PEH_NW 4
 #endif
 hipError_t launch_pack_emit_hist(const DevReads &r, const EmitParams &p, uint64_t n, hipStream_t s) {
     constexpr uint32_t T = 8192;  // = radix_key_tile() (sort_scan.hip; checked by the caller)
