@@ -625,7 +625,7 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
             const uint32_t ps = starts[p], pn = starts[p + 1] - starts[p];
             // (mix << lb | loc rank, g) pairs of the range into keys2 / vals, then
             // sort the bits below the partition id (the records in keys are spent)
-            HIPCHK(launch_convert_records(keys + ps, pn, PA, keys2 + ps, vals + ps, c->stream));
+            HIPCHK(launch_convert_records(keys + ps, pn, PA, keys2 + ps, vals + ps, ps, c->stream));
             uint64_t *k0 = keys2 + ps, *k1 = keys + ps;
             uint32_t *v0 = vals + ps, *v1 = vals2 + ps;
             HIPCHK(radix_sort(&k0, &v0, &k1, &v1, pn, 0, kbits - skip_bits - PB, btmp, c->stream));
@@ -2178,8 +2178,10 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint6
     }
     PartArgs PA{};
     unsigned long long big_buckets = 0;
+    // phase 1: no readback between the bucket build and the pair counter, whose pass aborts
+    // when a partition still needs the global path (phase 2 below), as on one device
     rc = bucket_stage(c, keys, keys2, vals, vals2, n, loff, N, 0, packed ? nullptr : rl, nullptr, false, stmp, cnt,
-                      PA, big_buckets, c->log_ranks, 0, pv, nullptr, fused ? &RG : nullptr, true);
+                      PA, big_buckets, c->log_ranks, 1, pv, nullptr, fused ? &RG : nullptr, true);
     if (rc) return rc;
     PairIn PI{};
     PI.rec = PA.rec; PI.xrec = PA.xrec; PI.lst = PA.lst;
@@ -2204,9 +2206,19 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint6
     if (P > 1)
         HIPCHK(launch_pc_item_owners(items, n_multi, (const uint32_t *)c->d_starts.p, (uint32_t)P, items + n_multi + 1,
                                      c->stream));
-    rc = pair_stage(c, E, PI, false, true, nullptr, N, cnt, np, cap_s, items, n_multi, nullptr, nullptr, nullptr,
+    bool aborted = false;
+    rc = pair_stage(c, E, PI, false, true, nullptr, N, cnt, np, cap_s, items, n_multi, &cnt->big_n, &aborted, nullptr,
                     nullptr, (uint32_t)P, (const uint32_t *)c->d_starts.p, items + n_multi + 1, true);
     if (rc) return rc;
+    if (aborted) {  // partitions above 4,096 records (high-copy repeats): build them, count again
+        rc = bucket_stage(c, keys, keys2, vals, vals2, n, loff, N, 0, packed ? nullptr : rl, nullptr, false, stmp,
+                          cnt, PA, big_buckets, c->log_ranks, 2, pv);
+        if (rc) return rc;
+        PI.xrec = PA.xrec;
+        rc = pair_stage(c, E, PI, false, true, nullptr, N, cnt, np, cap_s, items, n_multi, nullptr, nullptr, nullptr,
+                        nullptr, (uint32_t)P, (const uint32_t *)c->d_starts.p, items + n_multi + 1);
+        if (rc) return rc;
+    }
     Counters hc;
     HIPCHK(hipMemcpyAsync(&hc, cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));

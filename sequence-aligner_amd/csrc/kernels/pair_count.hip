@@ -961,8 +961,11 @@ __global__ __launch_bounds__(PMW_WAVES * 64) void pair_count_multi_wave_kernel(E
     __shared__ uint32_t wkept[PMW_WAVES], wlast[PMW_WAVES], blk_base;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     PmwShared &S = SH[wv];
+    // big partitions still to build (bucket_stage phase 1): the whole block exits before
+    // its first barrier -- the flag was set before this launch, every thread reads the same
+    if (p.abort && *p.abort) return;
     const uint32_t item = blockIdx.x * PMW_WAVES + wv;
-    // (no early return: every wave reaches the block's output claim)
+    // (no early return below: every wave reaches the block's output claim)
     const bool live = item < p.n_items;
     const uint32_t ra = live ? item_start[item] : 0u, rb = live ? item_start[item + 1] : 0u;
     const uint32_t own2 = live && o.owners > 1 ? o.item_owner[item] : 0u;  // (lo | hi << 16, pc_item_owners)

@@ -743,21 +743,25 @@ hipError_t launch_part_build(const PartArgs &a, bool strict, int cap, hipStream_
     return hipGetLastError();
 }
 
+// (rec8 = the sorted records from position ps on.  With sorted packed values -- the sharded
+// path, A.spv -- record i's value is spv[ps + i], as in the LDS tiers: the unsorted table A.pv
+// shares its buffer with the sort and holds sorted values by now.  ovals may alias spv's
+// range: each thread reads its value before it writes)
 __global__ void convert_records_kernel(const uint64_t *rec8, uint32_t n, PartArgs A, uint64_t *okeys,
-                                       uint32_t *ovals) {
+                                       uint32_t *ovals, uint32_t ps) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint32_t code, r;
     okeys[i] = record_key(rec8[i], A, code, r, A.rl ? A.rl + (uint32_t)rec8[i] : nullptr,
-                          A.pv ? A.pv + (uint32_t)rec8[i] : nullptr);
+                          A.spv ? A.spv + ps + i : (A.pv ? A.pv + (uint32_t)rec8[i] : nullptr));
     // the global scan path indexes by occurrence: decode a (read, pos) code
     ovals[i] = A.pos_bits ? A.meta[code >> A.pos_bits].x + (code & ((1u << A.pos_bits) - 1u)) : code;
 }
 
 hipError_t launch_convert_records(const uint64_t *rec8, uint32_t n, const PartArgs &a, uint64_t *okeys,
-                                  uint32_t *ovals, hipStream_t s) {
+                                  uint32_t *ovals, uint32_t ps, hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(convert_records_kernel, dim3((n + 255) / 256), dim3(256), 0, s, rec8, n, a, okeys, ovals);
+    hipLaunchKernelGGL(convert_records_kernel, dim3((n + 255) / 256), dim3(256), 0, s, rec8, n, a, okeys, ovals, ps);
     return hipGetLastError();
 }
 

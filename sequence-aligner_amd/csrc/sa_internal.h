@@ -481,7 +481,7 @@ hipError_t launch_part_starts(const PartArgs &a, uint64_t n, int shift, hipStrea
 hipError_t launch_part_build(const PartArgs &a, bool strict, int cap, hipStream_t s);
 // 8-byte records of one big partition -> (mix << lb | locrank, g) for the global scan path
 hipError_t launch_convert_records(const uint64_t *rec8, uint32_t n, const PartArgs &a, uint64_t *okeys,
-                                  uint32_t *ovals, hipStream_t s);
+                                  uint32_t *ovals, uint32_t ps, hipStream_t s);
 // big partition at sorted offset ps: its temporary (ascending, partition-
 // relative) md / edge lists of the global scan moved into the combined layout
 // (and the strict list indices with them), then the per-occurrence records

@@ -46,9 +46,11 @@ def workload(seed, repeat=False):
     rng = np.random.default_rng(seed)
     reads = H.mutate(H.synth_reads(1500, 300, 20000, gc=0.5, seed=seed, mixed=(250, 340)), rng, 3)
     st = dict(kmer_size=15, min_collisions=5, id_mode=sao.SA_IDS_WIDE)
-    if repeat:  # a 15-mer in 2,400 reads: multi-read pair-count blocks overflow and recount
+    if repeat:  # a 15-mer in 2,400 reads: multi-read pair-count blocks overflow and recount;
+        # in 5,000 (repeat="big"): a partition past 4,096 records on its owner shard -- the
+        # first pair-count pass aborts and the global bucket path runs (bucket_stage phase 2)
         motif = "ACGTTGCAACGTAGC"
-        for i in range(2400):
+        for i in range(5000 if repeat == "big" else 2400):
             s_ = "".join("ACGT"[x] for x in rng.integers(0, 4, 120))
             p_ = 5 if i % 2 == 0 else 55
             reads.append(s_[:p_] + motif + s_[p_ + 15:])
@@ -56,7 +58,7 @@ def workload(seed, repeat=False):
     return reads, st
 
 
-@pytest.mark.parametrize("P,repeat", [(2, False), (4, False), (8, False), (4, True)])
+@pytest.mark.parametrize("P,repeat", [(2, False), (4, False), (8, False), (4, True), (4, "big")])
 def test_virtual_shards_match_single_gpu(P, repeat):
     reads, st = workload(90 + P, repeat)
     ref = run(reads, **st)
