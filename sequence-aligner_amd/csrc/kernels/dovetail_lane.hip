@@ -537,8 +537,14 @@ __device__ __forceinline__ void p1x2_run(const DevReads &rd, const int32_t *lead
     uint32_t awA = qa.Aw[min(w0, awlA)], awnA = qa.Aw[min(w0 + 1, awlA)];
     uint32_t awB = qb.Aw[min(w0, awlB)], awnB = qb.Aw[min(w0 + 1, awlB)];
     __builtin_amdgcn_s_waitcnt(0);
-    auto row = [&](const int32_t i) {
-        const uint32_t act = (i <= rowsA ? 0x0000FFFFu : 0u) | (i <= rowsB ? 0xFFFF0000u : 0u);
+    // rows every lane's pairs still have (i <= rmin, the wave's shortest) skip the row mask
+    int32_t rmin = min(rowsA, rowsB);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) rmin = min(rmin, __shfl_xor(rmin, off, 64));
+    rmin = __builtin_amdgcn_readfirstlane(rmin);
+    auto row = [&](const int32_t i, auto masked) {
+        const uint32_t act = !decltype(masked)::value ? 0xFFFFFFFFu
+                             : (i <= rowsA ? 0x0000FFFFu : 0u) | (i <= rowsB ? 0xFFFF0000u : 0u);
         const uint32_t sh = 30 - 2 * ((i - 1) & 15);
         const uint32_t aA = (awA >> sh) & 3u, aB = (awB >> sh) & 3u;
         // bit-selects, not a ternary chain: that became a private lookup table (scratch)
@@ -577,11 +583,15 @@ __device__ __forceinline__ void p1x2_run(const DevReads &rd, const int32_t *lead
         awnB = gld(qb.Aw, min((i >> 4) + 1, awlB));
     };
     int32_t i = i0;
-    for (; i < i1; i += 2) {  // two rows per iteration (by hand: #pragma unroll gives up here)
-        row(i);
-        row(i + 1);
+    const int32_t iu = min(i1, rmin);  // rows [i0, iu] unmasked, (iu, i1] masked
+    const std::false_type unm{};
+    const std::true_type msk{};
+    for (; i < iu; i += 2) {  // two rows per iteration (by hand: #pragma unroll gives up here)
+        row(i, unm);
+        row(i + 1, unm);
     }
-    if (i == i1) row(i);
+    if (i == iu) { row(i, unm); ++i; }
+    for (; i <= i1; ++i) row(i, msk);
     if (!last) {
 #pragma unroll
         for (int j = 0; j < LW - 1; ++j) {
