@@ -3,7 +3,7 @@
 # 8 serial virtual shards, configs[4] k = 12 slice line.  Stops at the first failing step.
 set -u
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/r05final2
+O=$R/gpurun_out/${TAG:-r05final2}
 mkdir -p $O
 cd $R
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread --durations=10 > $O/gpu_tests.log 2>&1
