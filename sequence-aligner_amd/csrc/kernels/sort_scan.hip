@@ -637,11 +637,40 @@ static hipError_t rs_pass_keys(const uint64_t *kin, uint64_t *kout, uint64_t n, 
 // (48.6M keys) they measured slower than 8,192 (0.53 vs 0.50 ms)
 constexpr uint64_t RS_BIG_TILE_KEYS = 1ull << 27;
 
+// 12-byte (key, u32 value) passes at ITEMS keys per lane-slot of a tile: 8,192-key tiles, and
+// 16,384 past 2^27 records (as the key-only passes: runs of ~64 keys per digit for an output far
+// beyond the MALL)
+template <int ITEMS>
+static hipError_t rs_sort_vals(uint64_t **keys, uint32_t **vals, uint64_t **keys_alt, uint32_t **vals_alt,
+                               uint64_t n, int lo, int hi, void *tmp, hipStream_t s) {
+    constexpr int TV = RsTile<ITEMS>::TILE;
+    using SV = RsShared<true, TV, RsDown<ITEMS>::WAVES>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void *)rs_downsweep_kernel<true, ITEMS>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(SV));
+        attr_set = true;
+    }
+    uint32_t *hist = (uint32_t *)tmp;
+    const uint64_t nb = (n + TV - 1) / TV;
+    void *stmp = (void *)(hist + 256 * nb);
+    for (int shift = lo; shift < hi; shift += 8) {
+        hipLaunchKernelGGL((rs_upsweep_kernel<ITEMS>), dim3((uint32_t)nb), dim3(RsUp<ITEMS>::THREADS), 0, s, *keys, n,
+                           shift, hist, (uint32_t)nb, KeyGen{});
+        hipError_t e = rs_offsets(hist, nb, stmp, s);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL((rs_downsweep_kernel<true, ITEMS>), dim3((uint32_t)nb), dim3(RsDown<ITEMS>::THREADS),
+                           sizeof(SV), s, *keys, *vals, *keys_alt, *vals_alt, n, shift, (const uint32_t *)hist,
+                           (uint32_t)nb, KeyGen{}, 0, RecvGen{});
+        uint32_t *tv = *vals; *vals = *vals_alt; *vals_alt = tv;
+        uint64_t *tk = *keys; *keys = *keys_alt; *keys_alt = tk;
+    }
+    return hipGetLastError();
+}
+
 hipError_t radix_sort(uint64_t **keys, uint32_t **vals, uint64_t **keys_alt, uint32_t **vals_alt,
                       uint64_t n, int lo, int hi, void *tmp, hipStream_t s) {
     if (n <= 1 || hi <= lo) return hipSuccess;
-    constexpr int TV = RsTile<RS_ITEMS_VALS>::TILE;
-    using SV = RsShared<true, TV, RsDown<RS_ITEMS_VALS>::WAVES>;
     const bool with_vals = vals != nullptr && *vals != nullptr;
     uint32_t *hist = (uint32_t *)tmp;
     if (!with_vals) {
@@ -655,53 +684,46 @@ hipError_t radix_sort(uint64_t **keys, uint32_t **vals, uint64_t **keys_alt, uin
         }
         return hipGetLastError();
     }
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void *)rs_downsweep_kernel<true, RS_ITEMS_VALS>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(SV));
-        attr_set = true;
-    }
-    const uint64_t nb = (n + TV - 1) / TV;
-    void *stmp = (void *)(hist + 256 * nb);
-    for (int shift = lo; shift < hi; shift += 8) {
-        hipLaunchKernelGGL((rs_upsweep_kernel<RS_ITEMS_VALS>), dim3((uint32_t)nb), dim3(RsUp<RS_ITEMS_VALS>::THREADS), 0,
-                           s, *keys, n, shift, hist, (uint32_t)nb, KeyGen{});
-        hipError_t e = rs_offsets(hist, nb, stmp, s);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL((rs_downsweep_kernel<true, RS_ITEMS_VALS>), dim3((uint32_t)nb),
-                           dim3(RsDown<RS_ITEMS_VALS>::THREADS), sizeof(SV), s, *keys, *vals, *keys_alt, *vals_alt, n,
-                           shift, (const uint32_t *)hist, (uint32_t)nb, KeyGen{}, 0, RecvGen{});
-        uint32_t *tv = *vals; *vals = *vals_alt; *vals_alt = tv;
-        uint64_t *tk = *keys; *keys = *keys_alt; *keys_alt = tk;
-    }
-    return hipGetLastError();
+    return n >= RS_BIG_TILE_KEYS ? rs_sort_vals<2 * RS_ITEMS_VALS>(keys, vals, keys_alt, vals_alt, n, lo, hi, tmp, s)
+                                 : rs_sort_vals<RS_ITEMS_VALS>(keys, vals, keys_alt, vals_alt, n, lo, hi, tmp, s);
 }
 
-hipError_t radix_sort_recv(const RecvGen &g, uint64_t **keys, uint32_t **vals, uint64_t **keys_alt,
-                           uint32_t **vals_alt, uint64_t n, int lo, int hi, void *tmp, hipStream_t s) {
-    if (n == 0 || hi <= lo) return hipErrorInvalidValue;  // (the caller relabels without a sort)
-    constexpr int TV = RsTile<RS_ITEMS_VALS>::TILE;
-    using SV = RsShared<true, TV, RsDown<RS_ITEMS_VALS>::WAVES>;
+template <int ITEMS>
+static hipError_t rs_recv_pass(const RecvGen &g, uint64_t **keys, uint32_t **vals, uint64_t **keys_alt,
+                               uint32_t **vals_alt, uint64_t n, int lo, void *tmp, hipStream_t s) {
+    constexpr int TV = RsTile<ITEMS>::TILE;
+    using SV = RsShared<true, TV, RsDown<ITEMS>::WAVES>;
     static bool attr_set = false;
     if (!attr_set) {
-        (void)hipFuncSetAttribute((const void *)rs_downsweep_kernel<true, RS_ITEMS_VALS, false, true>,
+        (void)hipFuncSetAttribute((const void *)rs_downsweep_kernel<true, ITEMS, false, true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(SV));
         attr_set = true;
     }
     const uint64_t nb = (n + TV - 1) / TV;
     uint32_t *hist = (uint32_t *)tmp;
     void *stmp = (void *)(hist + 256 * nb);
-    // first pass: raw received records in, relabelled keys + generated values out
-    hipLaunchKernelGGL((rs_upsweep_kernel<RS_ITEMS_VALS>), dim3((uint32_t)nb), dim3(RsUp<RS_ITEMS_VALS>::THREADS), 0, s,
-                       *keys, n, lo, hist, (uint32_t)nb, KeyGen{});
+    // raw received records in, relabelled keys + generated values out
+    hipLaunchKernelGGL((rs_upsweep_kernel<ITEMS>), dim3((uint32_t)nb), dim3(RsUp<ITEMS>::THREADS), 0, s, *keys, n, lo,
+                       hist, (uint32_t)nb, KeyGen{});
     hipError_t e = rs_offsets(hist, nb, stmp, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((rs_downsweep_kernel<true, RS_ITEMS_VALS, false, true>), dim3((uint32_t)nb),
-                       dim3(RsDown<RS_ITEMS_VALS>::THREADS), sizeof(SV), s, *keys, (const uint32_t *)nullptr, *keys_alt,
-                       *vals_alt, n, lo, (const uint32_t *)hist, (uint32_t)nb, KeyGen{}, 0, g);
+    hipLaunchKernelGGL((rs_downsweep_kernel<true, ITEMS, false, true>), dim3((uint32_t)nb), dim3(RsDown<ITEMS>::THREADS),
+                       sizeof(SV), s, *keys, (const uint32_t *)nullptr, *keys_alt, *vals_alt, n, lo,
+                       (const uint32_t *)hist, (uint32_t)nb, KeyGen{}, 0, g);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     { uint32_t *tv = *vals; *vals = *vals_alt; *vals_alt = tv; }
     { uint64_t *tk = *keys; *keys = *keys_alt; *keys_alt = tk; }
+    return hipSuccess;
+}
+
+hipError_t radix_sort_recv(const RecvGen &g, uint64_t **keys, uint32_t **vals, uint64_t **keys_alt,
+                           uint32_t **vals_alt, uint64_t n, int lo, int hi, void *tmp, hipStream_t s) {
+    if (n == 0 || hi <= lo) return hipErrorInvalidValue;  // (the caller relabels without a sort)
+    // first pass: the received records decoded and relabelled (RecvGen); then as radix_sort
+    const hipError_t e = n >= RS_BIG_TILE_KEYS
+                             ? rs_recv_pass<2 * RS_ITEMS_VALS>(g, keys, vals, keys_alt, vals_alt, n, lo, tmp, s)
+                             : rs_recv_pass<RS_ITEMS_VALS>(g, keys, vals, keys_alt, vals_alt, n, lo, tmp, s);
+    if (e != hipSuccess) return e;
     return lo + 8 < hi ? radix_sort(keys, vals, keys_alt, vals_alt, n, lo + 8, hi, tmp, s) : hipSuccess;
 }
 
