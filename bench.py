@@ -76,6 +76,10 @@ def synth_workload(n_reads, read_len, genome_len, gc, seed, shard=0, min_len=Non
                           np.where(bit == 1, ord("T"), ord("A"))).astype(np.uint8)
         rs = (seed ^ 0xABCDEF) + 7919 * shard
         starts = (splitmix64(rs, n_reads) % (np.uint64(genome_len + 1) - lens.astype(np.uint64))).astype(np.int64)
+    if os.environ.get("SA_BENCH_SORTED_READS") == "1" and lens.min() == lens.max():
+        # (experiment only, never the metric's workload: each shard's reads in genome order,
+        # i.e. read ids already in locality order -- DESIGN.md 8, item 1)
+        starts = np.sort(starts)
     offsets = np.zeros(n_reads + 1, dtype=np.uint64)
     offsets[1:] = np.cumsum(lens)
     if lens.min() == lens.max():
