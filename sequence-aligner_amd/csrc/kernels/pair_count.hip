@@ -917,9 +917,21 @@ __device__ __forceinline__ uint32_t pcm_hash(unsigned long long k) {
 // ---------------------------------------------------------------------------
 constexpr int PMW_WAVES = 4;
 constexpr int PMW_TAB = 256;
-constexpr int PMW_CHUNK = 128;              // occurrences per chunk (2 per lane)
+#ifndef SA_PMW_CHUNK  // (A/B builds)
+#define SA_PMW_CHUNK 64
+#endif
+#ifndef SA_PMW_MIN_WAVES
+#define SA_PMW_MIN_WAVES 1
+#endif
+// occurrences per chunk, 1 per lane (2 per lane: 21.6 -> 26.7 KB of LDS per block, 7 -> 5 waves
+// per SIMD; 8 serial shards of the bench shape, pairs 1.350 -> 1.325 ms with 1 per lane,
+// profiles/r05/sharded/ab_pmw_chunk.txt)
+constexpr int PMW_CHUNK = SA_PMW_CHUNK;
 constexpr int PMW_OCC = PMW_CHUNK / 64;
-constexpr int PMW_BATCH = 8;                // partner gathers in flight per lane
+#ifndef SA_PMW_BATCH
+#define SA_PMW_BATCH 8
+#endif
+constexpr int PMW_BATCH = SA_PMW_BATCH;     // partner gathers in flight per lane
 constexpr int PMW_WIN = 64 * PMW_BATCH;     // elements per window
 constexpr uint32_t PMW_FILL_MAX = PMW_TAB * 3 / 4;
 
@@ -954,7 +966,7 @@ __device__ __forceinline__ void pmw_insert(PmwShared &S, unsigned long long key,
     S.overflow = 1;
 }
 
-__global__ __launch_bounds__(PMW_WAVES * 64) void pair_count_multi_wave_kernel(EmitParams e, PairIn in, PairParams p,
+__global__ __launch_bounds__(PMW_WAVES * 64, SA_PMW_MIN_WAVES) void pair_count_multi_wave_kernel(EmitParams e, PairIn in, PairParams p,
                                                                                 PairOut o,
                                                                                 const uint32_t *item_start) {
     __shared__ PmwShared SH[PMW_WAVES];
