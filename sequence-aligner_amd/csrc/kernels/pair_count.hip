@@ -935,12 +935,17 @@ constexpr int PMW_BATCH = SA_PMW_BATCH;     // partner gathers in flight per lan
 constexpr int PMW_WIN = 64 * PMW_BATCH;     // elements per window
 constexpr uint32_t PMW_FILL_MAX = PMW_TAB * 3 / 4;
 
+#ifndef SA_PMW_RB_MAX
+#define SA_PMW_RB_MAX 64  // (A/B builds: 0 = the owning read by a search in global memory)
+#endif
+constexpr int PMW_RB_MAX = SA_PMW_RB_MAX > 0 ? SA_PMW_RB_MAX : 1;
 struct PmwShared {  // one per wave
     unsigned long long key[PMW_TAB];
     uint32_t cnt[PMW_TAB];
     uint4 rec[PMW_CHUNK];     // {list entry of element 0 (u64), edge-role end, edge weight}
     uint32_t aid[PMW_CHUNK];  // read of each occurrence of the chunk
     uint16_t eo[PMW_WIN];
+    uint32_t rbo[PMW_RB_MAX];  // the item's read starts relative to its first occurrence
     uint32_t fill, overflow, kept, pad;
 };
 
@@ -990,6 +995,10 @@ __global__ __launch_bounds__(PMW_WAVES * 64, SA_PMW_MIN_WAVES) void pair_count_m
     const uint32_t nocc = ra < rb ? (uint32_t)(e.occ_off[rb] - g0) : 0u;
     unsigned long long role_pairs = 0;
     bool over = false;
+    // the item's read boundaries staged in LDS (one coalesced load): each occurrence finds its
+    // read there, not by dependent loads of occ_off
+    const bool rb_lds = SA_PMW_RB_MAX > 0 && rb - ra + 1 <= (uint32_t)PMW_RB_MAX;  // (wave-uniform)
+    if (rb_lds && (uint32_t)lane <= rb - ra) S.rbo[lane] = (uint32_t)(e.occ_off[ra + lane] - g0);
     __builtin_amdgcn_wave_barrier();
     for (uint32_t c0 = 0; c0 < nocc; c0 += PMW_CHUNK) {
         const uint32_t cn = min((uint32_t)PMW_CHUNK, nocc - c0);
@@ -1006,12 +1015,22 @@ __global__ __launch_bounds__(PMW_WAVES * 64, SA_PMW_MIN_WAVES) void pair_count_m
                 const uint64_t g = g0 + c0 + oi;
                 rcj[j] = load_rec(in, g);
                 mytot[j] = (rcj[j].y & 0x3FFFFFFFu) + rcj[j].w;
-                // owning read: largest r with occ_off[r] <= g (a few cached loads;
-                // the item's boundaries broadcast from registers measured slower)
+                // owning read: largest r with occ_off[r] <= g (in LDS, or a few cached
+                // loads; the item's boundaries broadcast from registers measured slower)
                 uint32_t lo = ra, hi = rb;
-                while (hi - lo > 1) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (e.occ_off[mid] <= g) lo = mid; else hi = mid;
+                if (rb_lds) {
+                    const uint32_t rel = c0 + oi;
+                    uint32_t l = 0, h = rb - ra;
+                    while (h - l > 1) {
+                        const uint32_t mid = (l + h) >> 1;
+                        if (S.rbo[mid] <= rel) l = mid; else h = mid;
+                    }
+                    lo = ra + l;
+                } else {
+                    while (hi - lo > 1) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (e.occ_off[mid] <= g) lo = mid; else hi = mid;
+                    }
                 }
                 own[j] = lo;
             }
