@@ -794,7 +794,7 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
                 PairParams PM = P;
                 PM.n_items = n_multi;
                 PM.table = 1024;
-                HIPCHK(launch_pair_count_multi_wave(E, PI, PM, O, item_start, n_multi, c->stream));
+                HIPCHK(launch_pair_count_multi_wave(E, PI, PM, O, item_start, n_multi, n_items, c->stream));
             } else {
                 HIPCHK(launch_pair_count(E, PI, P, O, read_order, read_order ? ((n_items + 7) & ~7u) : n_items,
                                          c->stream));

@@ -920,8 +920,8 @@ constexpr int PMW_TAB = 256;
 #ifndef SA_PMW_CHUNK  // (A/B builds)
 #define SA_PMW_CHUNK 64
 #endif
-#ifndef SA_PMW_MIN_WAVES
-#define SA_PMW_MIN_WAVES 1
+#ifndef SA_PMW_MIN_WAVES  // (8 waves per SIMD: <= 64 VGPRs, with the 32-bit keys' 18.5 KB of LDS per
+#define SA_PMW_MIN_WAVES 8  // block -- 8 serial shards, pairs 1.261 -> 1.230 ms, ab_pmw_k32.txt)
 #endif
 // occurrences per chunk, 1 per lane (2 per lane: 21.6 -> 26.7 KB of LDS per block, 7 -> 5 waves
 // per SIMD; 8 serial shards of the bench shape, pairs 1.350 -> 1.325 ms with 1 per lane,
@@ -939,8 +939,35 @@ constexpr uint32_t PMW_FILL_MAX = PMW_TAB * 3 / 4;
 #define SA_PMW_RB_MAX 64  // (A/B builds: 0 = the owning read by a search in global memory)
 #endif
 constexpr int PMW_RB_MAX = SA_PMW_RB_MAX > 0 ? SA_PMW_RB_MAX : 1;
+// Table keys: (read, partner) as read << 32 | partner, or -- when every global read id fits 26
+// bits -- as (read - the item's first read) << 26 | partner in 32 bits (items of <= 64 reads;
+// a wider item goes to the recount tiers): half the key LDS and 32-bit LDS atomics
+constexpr int PMW_K32_PBITS = 26;
+template <typename K> struct PmwKey;
+template <> struct PmwKey<unsigned long long> {
+    static constexpr unsigned long long EMPTY = ~0ull;
+    __device__ static unsigned long long make(uint32_t r, uint32_t ra, uint32_t part) {
+        (void)ra;
+        return ((unsigned long long)r << 32) | part;
+    }
+    __device__ static uint32_t lead(unsigned long long k, uint32_t ra) { (void)ra; return (uint32_t)(k >> 32); }
+    __device__ static uint32_t part(unsigned long long k) { return (uint32_t)k; }
+    __device__ static uint32_t slot(unsigned long long k) {
+        const uint32_t x = ((uint32_t)k * 0x9E3779B1u) ^ ((uint32_t)(k >> 32) * 0x85EBCA77u);
+        return x >> (32 - 8);
+    }
+};
+template <> struct PmwKey<uint32_t> {
+    static constexpr uint32_t EMPTY = 0xFFFFFFFFu;  // (never a key: partners < 2^26 - 1)
+    __device__ static uint32_t make(uint32_t r, uint32_t ra, uint32_t part) { return ((r - ra) << PMW_K32_PBITS) | part; }
+    __device__ static uint32_t lead(uint32_t k, uint32_t ra) { return ra + (k >> PMW_K32_PBITS); }
+    __device__ static uint32_t part(uint32_t k) { return k & ((1u << PMW_K32_PBITS) - 1u); }
+    __device__ static uint32_t slot(uint32_t k) { return (k * 0x9E3779B1u) >> (32 - 8); }
+};
+
+template <typename K>
 struct PmwShared {  // one per wave
-    unsigned long long key[PMW_TAB];
+    K key[PMW_TAB];
     uint32_t cnt[PMW_TAB];
     uint4 rec[PMW_CHUNK];     // {list entry of element 0 (u64), edge-role end, edge weight}
     uint32_t aid[PMW_CHUNK];  // read of each occurrence of the chunk
@@ -952,17 +979,19 @@ struct PmwShared {  // one per wave
 #ifndef PMW_FASTPATH
 #define PMW_FASTPATH 0  // (8 serial shards: pairs 1.455-1.468 ms without, 1.481-1.501 with)
 #endif
-__device__ __forceinline__ void pmw_insert(PmwShared &S, unsigned long long key, uint32_t w) {
-    uint32_t slot = pcm_hash(key) >> 2;  // (pcm_hash: 10 bits)
+template <typename K>
+__device__ __forceinline__ void pmw_insert(PmwShared<K> &S, K key, uint32_t w) {
+    constexpr K EMPTY = PmwKey<K>::EMPTY;
+    uint32_t slot = PmwKey<K>::slot(key);
     if (PMW_FASTPATH && lds_relaxed(&S.key[slot]) == key) {  // the home-slot hit: no probe loop
         atomicAdd(&S.cnt[slot], w);
         return;
     }
     for (int probe = 0; probe < PMW_TAB / 4; ++probe) {
-        unsigned long long old = lds_relaxed(&S.key[slot]);  // final once set
-        if (old == PCM_EMPTY) old = atomicCAS(&S.key[slot], PCM_EMPTY, key);
-        if (old == PCM_EMPTY || old == key) {
-            if (old == PCM_EMPTY && atomicAdd(&S.fill, 1u) >= PMW_FILL_MAX) S.overflow = 1;
+        K old = lds_relaxed(&S.key[slot]);  // final once set
+        if (old == EMPTY) old = atomicCAS(&S.key[slot], EMPTY, key);
+        if (old == EMPTY || old == key) {
+            if (old == EMPTY && atomicAdd(&S.fill, 1u) >= PMW_FILL_MAX) S.overflow = 1;
             atomicAdd(&S.cnt[slot], w);
             return;
         }
@@ -971,13 +1000,15 @@ __device__ __forceinline__ void pmw_insert(PmwShared &S, unsigned long long key,
     S.overflow = 1;
 }
 
+template <typename K>
 __global__ __launch_bounds__(PMW_WAVES * 64, SA_PMW_MIN_WAVES) void pair_count_multi_wave_kernel(EmitParams e, PairIn in, PairParams p,
                                                                                 PairOut o,
                                                                                 const uint32_t *item_start) {
-    __shared__ PmwShared SH[PMW_WAVES];
+    using KK = PmwKey<K>;
+    __shared__ PmwShared<K> SH[PMW_WAVES];
     __shared__ uint32_t wkept[PMW_WAVES], wlast[PMW_WAVES], blk_base;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    PmwShared &S = SH[wv];
+    PmwShared<K> &S = SH[wv];
     // big partitions still to build (bucket_stage phase 1): the whole block exits before
     // its first barrier -- the flag was set before this launch, every thread reads the same
     if (p.abort && *p.abort) return;
@@ -987,10 +1018,12 @@ __global__ __launch_bounds__(PMW_WAVES * 64, SA_PMW_MIN_WAVES) void pair_count_m
     const uint32_t ra = live ? item_start[item] : 0u, rb = live ? item_start[item + 1] : 0u;
     const uint32_t own2 = live && o.owners > 1 ? o.item_owner[item] : 0u;  // (lo | hi << 16, pc_item_owners)
     for (int i = lane; i < PMW_TAB; i += 64) {
-        S.key[i] = PCM_EMPTY;
+        S.key[i] = KK::EMPTY;
         S.cnt[i] = 0;
     }
-    if (lane == 0) { S.fill = 0; S.overflow = 0; }
+    // (32-bit keys hold the read as an offset of 6 bits: a wider item is recounted by the tiers)
+    const bool too_wide = sizeof(K) == 4 && rb - ra > 64u;
+    if (lane == 0) { S.fill = 0; S.overflow = too_wide ? 1u : 0u; }
     const uint64_t g0 = ra < rb ? e.occ_off[ra] : 0ull;
     const uint32_t nocc = ra < rb ? (uint32_t)(e.occ_off[rb] - g0) : 0u;
     unsigned long long role_pairs = 0;
@@ -1120,7 +1153,7 @@ __global__ __launch_bounds__(PMW_WAVES * 64, SA_PMW_MIN_WAVES) void pair_count_m
 #pragma unroll
             for (int bb = 0; bb < PMW_BATCH; ++bb) {
                 if (wt[bb] == 0 || part[bb] == ow[bb]) continue;  // same read (KmerTable.scala:61-63)
-                pmw_insert(S, ((unsigned long long)ow[bb] << 32) | part[bb], wt[bb]);
+                pmw_insert<K>(S, KK::make(ow[bb], ra, part[bb]), wt[bb]);
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -1138,7 +1171,7 @@ __global__ __launch_bounds__(PMW_WAVES * 64, SA_PMW_MIN_WAVES) void pair_count_m
 #pragma unroll
     for (int j = 0; j < PMW_TAB / 64; ++j) {
         const uint32_t sl = lane * (PMW_TAB / 64) + j;
-        if (live && !over && S.key[sl] != PCM_EMPTY) keep |= 1u << j;
+        if (live && !over && S.key[sl] != KK::EMPTY) keep |= 1u << j;
     }
     if (live && !over && lane == 0) atomicAdd(&o.distinct[shard], (unsigned long long)lds_relaxed(&S.fill));
     uint32_t o_lo = 0, o_hi = 0;
@@ -1163,7 +1196,7 @@ __global__ __launch_bounds__(PMW_WAVES * 64, SA_PMW_MIN_WAVES) void pair_count_m
 #pragma unroll
             for (int j = 0; j < PMW_TAB / 64; ++j) {
                 const uint32_t sl = lane * (PMW_TAB / 64) + j;
-                if (((km >> j) & 1u) && owner_of(o.owner_starts, o.owners, (uint32_t)(S.key[sl] >> 32)) != ow)
+                if (((km >> j) & 1u) && owner_of(o.owner_starts, o.owners, KK::lead(S.key[sl], ra)) != ow)
                     km &= ~(1u << j);
             }
         }
@@ -1190,8 +1223,8 @@ __global__ __launch_bounds__(PMW_WAVES * 64, SA_PMW_MIN_WAVES) void pair_count_m
                 const uint32_t sl = lane * (PMW_TAB / 64) + j;
                 if (lat < o.cap_s) {
                     const unsigned long long at = region + lat;
-                    o.fst[at] = (uint32_t)(S.key[sl] >> 32);
-                    o.snd[at] = (uint32_t)S.key[sl];
+                    o.fst[at] = KK::lead(S.key[sl], ra);
+                    o.snd[at] = KK::part(S.key[sl]);
                     o.cnt[at] = S.cnt[sl];
                 }
                 ++lat;
@@ -1200,13 +1233,21 @@ __global__ __launch_bounds__(PMW_WAVES * 64, SA_PMW_MIN_WAVES) void pair_count_m
     }
 }
 
+#ifndef SA_PMW_K32
+#define SA_PMW_K32 1  // (A/B builds: 0 = 64-bit keys always)
+#endif
 hipError_t launch_pair_count_multi_wave(const EmitParams &e, const PairIn &in, const PairParams &p, PairOut &o,
-                                        const uint32_t *item_start, uint32_t n_items, hipStream_t s) {
+                                        const uint32_t *item_start, uint32_t n_items, uint32_t n_reads,
+                                        hipStream_t s) {
     if (n_items == 0) return hipSuccess;
     PairParams q = p;
     q.n_items = n_items;
-    hipLaunchKernelGGL(pair_count_multi_wave_kernel, dim3((n_items + PMW_WAVES - 1) / PMW_WAVES), dim3(PMW_WAVES * 64),
-                       0, s, e, in, q, o, item_start);
+    const dim3 grid((n_items + PMW_WAVES - 1) / PMW_WAVES), block(PMW_WAVES * 64);
+    if (SA_PMW_K32 && n_reads < (1u << PMW_K32_PBITS) - 1u)  // every partner id fits 26 bits
+        hipLaunchKernelGGL(pair_count_multi_wave_kernel<uint32_t>, grid, block, 0, s, e, in, q, o, item_start);
+    else
+        hipLaunchKernelGGL(pair_count_multi_wave_kernel<unsigned long long>, grid, block, 0, s, e, in, q, o,
+                           item_start);
     return hipGetLastError();
 }
 

@@ -403,7 +403,7 @@ hipError_t launch_pair_count(const EmitParams &e, const PairIn &in, const PairPa
 #endif
 constexpr uint32_t PMW_TARGET = SA_PMW_TARGET;
 hipError_t launch_pair_count_multi_wave(const EmitParams &e, const PairIn &in, const PairParams &p, PairOut &o,
-                                        const uint32_t *item_start, uint32_t n_items, hipStream_t s);
+                                        const uint32_t *item_start, uint32_t n_items, uint32_t n_reads, hipStream_t s);
 hipError_t launch_pc_item_owners(const uint32_t *item_start, uint32_t n_items, const uint32_t *starts, uint32_t owners,
                                  uint32_t *item_owner, hipStream_t s);
 hipError_t launch_pc_items(const uint64_t *occ_off, uint32_t n_reads, uint32_t target, uint32_t n_items,
