@@ -933,6 +933,7 @@ constexpr int PMW_OCC = PMW_CHUNK / 64;
 #endif
 constexpr int PMW_BATCH = SA_PMW_BATCH;     // partner gathers in flight per lane
 constexpr int PMW_WIN = 64 * PMW_BATCH;     // elements per window
+static_assert(PMW_BATCH % 8 == 0, "the window's element offsets move as uint4 pairs: 8 per lane step");
 constexpr uint32_t PMW_FILL_MAX = PMW_TAB * 3 / 4;
 
 #ifndef SA_PMW_RB_MAX
