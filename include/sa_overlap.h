@@ -168,12 +168,24 @@ enum sa_option {
                                   Applies to the launches that walk a read / item list
                                   (every build passes one); a list-less launch larger
                                   than the slice fails with SA_E_HIP */
-    SA_OPT_FIRST_PASS = 8      /* pair counter's first pass (wide ids): 0 auto (default: a
+    SA_OPT_FIRST_PASS = 8,     /* pair counter's first pass (wide ids): 0 auto (default: a
                                   sample of every 64th read runs it first when there are
                                   >= 2^18 reads; if >= 95 % of the sample overflows its
                                   256-slot tables, every read goes straight to the big
                                   recount tier), 1 always run it, 2 always skip it (a
                                   test hook for the dense path) */
+    SA_OPT_PASS_BUDGET_MB = 9, /* sharded context: MiB of partial (lead, trail, count)
+                                  entries (12 B each, counted by their upper bound) one
+                                  shard may produce per lead-range pass; the shards then
+                                  count, exchange and reduce 1/npass of every owner's leads
+                                  per pass (sa_dist_plan).  0 (default): half of the free
+                                  device memory after the bucket build, shared by the
+                                  shards on the device, at ~40 B per entry */
+    SA_OPT_LEAN_MEMORY = 10    /* sharded context: free each shard's scratch between stages
+                                  (sort / bucket scratch after the bucket build, exchange
+                                  buffers after use, reduce scratch after each pass) so
+                                  that virtual shards of a large read set fit one device;
+                                  costs re-allocations every build */
 };
 
 /* Project4's fdAlign switch (Project4.scala:187-192, :585-604).
@@ -260,6 +272,12 @@ int sa_ctx_create_rank(const sa_settings *s, int device, int rank, int nranks, c
 /* Bytes this process's shards sent to other shards (exchanges 1 and 2, read
  * all-gather) since the context was created. */
 uint64_t sa_exchanged_bytes(const sa_ctx *ctx);
+/* The last sharded build of this process's shards: its lead-range passes (1 unless the
+ * partials' bound passed SA_OPT_PASS_BUDGET_MB), the partial (lead, trail, count)
+ * entries its shards counted over all passes (the exchange-2 volume, 12 B each), and
+ * their upper bound (sa_dist_buckets).  Any pointer may be NULL; SA_E_ARG on a
+ * single-device context. */
+int sa_get_shard_info(const sa_ctx *ctx, uint32_t *npass, uint64_t *partials, uint64_t *bound);
 
 /* ---- Per-shard entry points, one process (context) per GPU ----
  * What a sharded context runs on each shard; exposed for callers that move the
@@ -272,6 +290,12 @@ uint64_t sa_exchanged_bytes(const sa_ctx *ctx);
  *   sa_dist_emit      -> exchange 1 (8-byte k-mer records, grouped by owner rank)
  *   sa_dist_count     -> sa_dist_partials -> exchange 2 (partial pair counts)
  *   sa_dist_reduce    (this rank's leads: sum, [min,max] filter, dispatch)
+ * or, with the partials bounded per lead-range pass (read sets whose partials do
+ * not fit HBM at once, e.g. configs[4] at k = 12):
+ *   sa_dist_emit      -> exchange 1
+ *   sa_dist_buckets   -> sa_dist_plan (every rank; npass = the max over ranks)
+ *   for pass = npass - 1 down to 0:
+ *     sa_dist_count_pass -> sa_dist_partials -> exchange 2 -> sa_dist_reduce_pass
  * and, for alignment, sa_dist_codes -> all-gather -> sa_dist_set_reads, then
  * sa_align / sa_device_align / sa_get_ovl over this rank's leads.  The
  * library works on its own non-blocking HIP stream: device buffers handed in
@@ -299,6 +323,25 @@ int sa_dist_partials(sa_ctx *ctx, void *fst, void *snd, void *cnt);
 /* Partials received in exchange 2: sum, filter, dispatch this rank's leads
  * (wide canonical order: lead descending, trail ascending). */
 int sa_dist_reduce(sa_ctx *ctx, const void *fst, const void *snd, const void *cnt, uint64_t n);
+/* Lead-range passes.  sa_dist_buckets: the first half of sa_dist_count (the records
+ * received in exchange 1 -> this rank's buckets, built once); *bound = an upper bound
+ * of the partials this rank can produce (the partner-list elements of its
+ * occurrences, KmerTable.scala:85-149).  sa_dist_plan: the fewest passes whose every
+ * pass stays within `budget` partial entries on this rank (1 when the bound fits);
+ * ranks must agree on one pass count -- take the max over ranks.  Pass p of npass
+ * covers, for every owner rank r, leads [s_r + len_r * p / npass,
+ * s_r + len_r * (p + 1) / npass) of its reads [s_r, s_r + len_r).
+ * sa_dist_count_pass: that pass's partials (counts[nranks] per lead owner, then
+ * sa_dist_partials as above).  sa_dist_reduce_pass: this rank's leads of the pass,
+ * appended to the dispatch; run the passes from npass - 1 down to 0 (pass npass - 1
+ * starts a new dispatch, pass 0 completes it), so the dispatch stays lead-descending.
+ * sa_dist_count == sa_dist_buckets + sa_dist_count_pass(0, 1); sa_dist_reduce ==
+ * sa_dist_reduce_pass(0, 1). */
+int sa_dist_buckets(sa_ctx *ctx, void *recv_recs, const uint64_t *recv_counts, uint64_t *bound);
+int sa_dist_plan(sa_ctx *ctx, uint64_t budget, uint32_t *npass);
+int sa_dist_count_pass(sa_ctx *ctx, uint32_t pass, uint32_t npass, uint64_t *counts);
+int sa_dist_reduce_pass(sa_ctx *ctx, const void *fst, const void *snd, const void *cnt, uint64_t n, uint32_t pass,
+                        uint32_t npass);
 /* This rank's packed reads (2-bit words, u32[*nwords]) and first-invalid
  * positions (int32 per read); NULL buffers query *nwords only. */
 int sa_dist_codes(sa_ctx *ctx, void *codes, void *bad, uint64_t *nwords);

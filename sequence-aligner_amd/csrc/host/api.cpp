@@ -664,7 +664,7 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
                const uint32_t *item_start = nullptr, uint32_t n_multi = 0, const uint32_t *abort_flag = nullptr,
                bool *aborted = nullptr, bool *per_read = nullptr, uint64_t *distinct_ub = nullptr,
                uint32_t owners = 1, const uint32_t *owner_starts = nullptr, const uint32_t *item_owner = nullptr,
-               bool counters_zeroed = false) {
+               bool counters_zeroed = false, const uint32_t *item_end = nullptr) {
     // counters_zeroed: the caller cleared the whole Counters block and nothing has counted
     // since (the cursors and the overflow count then need no clear of their own)
     // per_read (in: allowed; out: used): the first pass writes each read's
@@ -775,6 +775,7 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
         O.owners = owners;
         O.owner_starts = owner_starts;
         O.item_owner = item_owner;
+        O.item_end = item_end;
         O.cap_s = cap_s;
         O.role_pairs = cnt->role_pairs;
         O.overflow_n = &cnt->overflow_n;
@@ -809,7 +810,10 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
         if (owners > 1) { if (int rc_c = read_cur()) return rc_c; }
         else memcpy(cur.data(), hp->cursor, NSHARD * 8);
         ovn = skip_first ? n_items : hp->overflow_n;
-        const uint32_t abv = P.abort && !skip_first ? hp->big_n : 0u;
+        // big partitions still to build: the first pass exited at once -- and with the
+        // first pass skipped (SA_OPT_FIRST_PASS = 2) the tiers below would read records
+        // the global path has not written yet, so the skip mode aborts the same way
+        const uint32_t abv = P.abort ? hp->big_n : 0u;
         unsigned long long dist_h[NSHARD];
         memcpy(dist_h, hp->distinct, sizeof(dist_h));
         if (abv) {
@@ -896,7 +900,10 @@ int pair_stage(sa_ctx *c, const EmitParams &E, const PairIn &PI, bool strict, bo
             // after 1/4 5.79; 8/8 after 1/8 5.48 s (profiles/r05/c4ab)
             static const int early_env = getenv("SA_EARLY_STOP") ? atoi(getenv("SA_EARLY_STOP")) : 8;
             static const int early_frac = getenv("SA_EARLY_FRAC") ? std::max(1, atoi(getenv("SA_EARLY_FRAC"))) : 8;
-            PT.early = table >= 16384 && fest && early_env > 0 ? (early_env & 255) | (early_frac << 8) : 0;
+            // (not at the finest split: with no finer class left, a projection that
+            // over-reads would push a read that fits into `failed` -> SA_E_OVERFLOW)
+            PT.early = table >= 16384 && fest && split < 64 && early_env > 0 ? (early_env & 255) | (early_frac << 8)
+                                                                             : 0;
             PairOut OT = O;
             // (skip mode: the split-1 big-tier pass is every read's first pass)
             OT.role_pairs = skip_first && split == 1 && table >= 16384 ? cnt->role_pairs : cnt->role_pairs_dummy;
@@ -1541,7 +1548,7 @@ int device_align(sa_ctx *c, bool readback) {
         const char *msg = err == SA_E_NON_ACGT ? "non-ACGT base in an aligned region (HOXD MatchError)"
                         : err == SA_E_SHORT_READ ? "trail shorter than the band width (StringIndexOutOfBounds)"
                         : err == SA_E_DEGENERATE ? "no positive phase-1 cell (degenerate backtrack)"
-                        : err == SA_E_HIP ? "phase-1 row-segment hand-off timed out"
+                        : err == SA_E_HIP ? "phase-1 row-segment hand-off timed out or read inconsistent state"
                         : "alignment limit exceeded";
         return fail(c, err, msg);
     }
@@ -1588,6 +1595,33 @@ int single_align(sa_ctx *c, bool readback) {
     (void)hipSetDevice(c->device);
     return device_align(c, readback);
 }
+
+namespace sa {
+void dist_release(sa_ctx *c, int what) {
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    auto rel = [](std::initializer_list<DBuf *> bs) {
+        for (DBuf *b : bs) {
+            if (b->p) (void)hipFree(b->p);
+            b->p = nullptr;
+            b->bytes = 0;
+        }
+    };
+    if (what & DIST_RELEASE_BUCKET_SCRATCH)
+        rel({&c->d_keys, &c->d_keys2, &c->d_vals, &c->d_vals2, &c->d_sorttmp, &c->d_rl, &c->d_srl, &c->d_srl2,
+             &c->d_ogid, &c->d_bkttmp, &c->d_tmd, &c->d_ted, &c->d_bmdo, &c->d_bedo, &c->d_bstart, &c->d_gbid,
+             &c->d_gmds, &c->d_gede});
+    if (what & DIST_RELEASE_PAIR_OUTPUT) rel({&c->d_pf, &c->d_ps, &c->d_pc});
+    if (what & DIST_RELEASE_REDUCE_SCRATCH)
+        rel({&c->d_okeys, &c->d_okeys2, &c->d_ovals, &c->d_ovals2, &c->d_osort, &c->d_psum, &c->d_pkeep, &c->d_ppos,
+             &c->d_lr, &c->d_scan});
+    if (what & DIST_RELEASE_BUCKETS) {
+        rel({&c->d_rec, &c->d_md, &c->d_xrec, &c->d_pbound, &c->d_pitems, &c->d_items, &c->d_tier, &c->d_ovl,
+             &c->d_ovlrp});
+        c->dist_bkt = false;
+    }
+}
+}  // namespace sa
 
 // ===========================================================================
 // C ABI
@@ -1648,7 +1682,8 @@ void sa_ctx_destroy(sa_ctx *c) {
                     &c->d_tedi, &c->d_xrec, &c->d_tier, &c->d_ovlrp, &c->d_meta, &c->d_items, &c->d_pq, &c->d_ocur, &c->d_lr, &c->d_bigtot, &c->d_hk0, &c->d_hk1, &c->d_hflag,
                     &c->d_hidx, &c->d_hpos, &c->d_htmp, &c->d_hist, &c->d_hovf, &c->d_hsmall,
                     &c->d_ltb, &c->d_lmax, &c->d_rreg, &c->d_rcnt, &c->d_rex,
-                    &c->d_shl, &c->d_sht, &c->d_shc, &c->d_rsh};
+                    &c->d_shl, &c->d_sht, &c->d_shc, &c->d_rsh, &c->d_pbound, &c->d_pbown, &c->d_prange,
+                    &c->d_pioff, &c->d_pitems};
     for (DBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     for (auto &p : c->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
@@ -1929,7 +1964,10 @@ int sa_set_option(sa_ctx *c, int option, int64_t value) {
         c->first_pass = (int)value;
         break;
     case SA_OPT_SERIAL_SHARDS:
-        if (!c->multi) return fail(c, SA_E_ARG, "SA_OPT_SERIAL_SHARDS needs a sharded context");
+    case SA_OPT_PASS_BUDGET_MB:
+    case SA_OPT_LEAN_MEMORY:
+        if (!c->multi) return fail(c, SA_E_ARG, "this option needs a sharded context");
+        if (value < 0) return fail(c, SA_E_ARG, "option value must be >= 0");
         return multi_set_option(c, option, value);
     default: return fail(c, SA_E_ARG, "unknown option");
     }
@@ -2108,9 +2146,43 @@ int sa_dist_emit(sa_ctx *c, void *send_recs, uint64_t *counts) {
     return SA_OK;
 }
 
-int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint64_t *counts) {
-    if (!c || !counts || !recv_counts) return SA_E_ARG;
+extern "C++" {  // (host helpers of the pass functions below: C++ linkage)
+// Owner r's leads in pass `pass` of npass (lead-range passes): [s + len * pass / npass,
+// s + len * (pass + 1) / npass) of its reads [s, s + len).  Every rank derives the same
+// ranges from the same starts, so the partials of a pass meet at their owners complete.
+static void pass_range(const sa_ctx *c, int r, uint32_t pass, uint32_t npass, uint32_t &a, uint32_t &b) {
+    const uint32_t s = c->dstarts[r];
+    const uint64_t len = c->dstarts[r + 1] - s;
+    a = s + (uint32_t)(len * pass / npass);
+    b = s + (uint32_t)(len * (pass + 1) / npass);
+}
+
+// grow a device buffer keeping its first `keep` elements (the reduce passes append)
+template <class T>
+int ensure_keep(sa_ctx *c, DBuf &b, size_t count, size_t keep, T **out) {
+    const size_t need = std::max<size_t>(count, 1) * sizeof(T);
+    if (b.bytes < need) {
+        void *p = nullptr;
+        const size_t alloc = need + need / 4;
+        hipError_t e = hipMalloc(&p, alloc);
+        if (e != hipSuccess) return fail(c, SA_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+        if (keep && b.p) HIPCHK(hipMemcpyAsync(p, b.p, keep * sizeof(T), hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (b.p) (void)hipFree(b.p);
+        b.p = p;
+        b.bytes = alloc;
+    }
+    *out = (T *)b.p;
+    return SA_OK;
+}
+
+}  // extern "C++"
+
+int sa_dist_buckets(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint64_t *bound) {
+    if (!c || !recv_counts) return SA_E_ARG;
     if (!c->dist) return fail(c, SA_E_STATE, "sa_dist_init first");
+    c->dist_bkt = false;
+    c->pbcum.clear();
     const int P = c->nranks;
     // seg[s] = first received record of source s; seg[P + 1 + s] = the global
     // occurrence index of source s's first k-mer (its records carry local ones)
@@ -2155,7 +2227,10 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint6
     // first -- 8 serial shards of the bench shape, emit + sort per shard
     // profiles/r05/sharded; SA_RECV_FUSED=0: the separate pass, A/B runs)
     static const bool fuse_env = !getenv("SA_RECV_FUSED") || atoi(getenv("SA_RECV_FUSED")) != 0;
-    const bool fused = fuse_env && packed && n > 0;
+    // The fused pass counts digits on the raw received keys but ranks the relabelled ones
+    // (low word = local index): the two agree only while the first pass's digit lies in
+    // the high word, i.e. its shift 64 - log_ranks - PB >= 32 (PB up to 23: log_ranks <= 9)
+    const bool fused = fuse_env && packed && n > 0 && 64 - c->log_ranks - part_bits(n) >= 32;
     RecvGen RG{};
     if (fused) {
         RG.seg = dseg; RG.P = (uint32_t)P; RG.starts = (const uint32_t *)c->d_starts.p;
@@ -2178,17 +2253,100 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint6
     }
     PartArgs PA{};
     unsigned long long big_buckets = 0;
-    // phase 1: no readback between the bucket build and the pair counter, whose pass aborts
-    // when a partition still needs the global path (phase 2 below), as on one device
+    // phase 1: no readback between the bucket build and the bound kernel, which
+    // exits at once when a partition still needs the global path (phase 2 below)
     rc = bucket_stage(c, keys, keys2, vals, vals2, n, loff, N, 0, packed ? nullptr : rl, nullptr, false, stmp, cnt,
                       PA, big_buckets, c->log_ranks, 1, pv, nullptr, fused ? &RG : nullptr, true);
     if (rc) return rc;
     PairIn PI{};
     PI.rec = PA.rec; PI.xrec = PA.xrec; PI.lst = PA.lst;
-    EmitParams E = emit_params(c);
-    E.occ_off = loff;  // occurrences of read a on this rank: [loff[a], loff[a+1])
-    E.npr = 0;
-    uint64_t np = 0, cap_s = 0;
+    // per-read upper bounds of the partials (the pass plan), per lead owner on the host
+    uint64_t *pb; unsigned long long *pown;
+    ENSURE(c->d_pbound, (size_t)N + 1, &pb);
+    ENSURE(c->d_pbown, (size_t)P + 1, &pown);
+    const uint32_t *dst = (const uint32_t *)c->d_starts.p;
+    HIPCHK(launch_read_bound(loff, N, PI, dst, (uint32_t)P, pb, pown, c->stream, &cnt->big_n));
+    Counters *hp;
+    if (int rc_p = pinned_counters(c, &hp)) return rc_p;
+    c->pbown.assign((size_t)P + 1, 0);
+    HIPCHK(hipMemcpyAsync(hp, cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(c->pbown.data(), pown, ((size_t)P + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const unsigned long long lds_buckets = shard_sum(hp->bkt_counts);
+    if (hp->big_n) {  // partitions above 4,096 records (high-copy repeats): the global path, then the bounds
+        rc = bucket_stage(c, keys, keys2, vals, vals2, n, loff, N, 0, packed ? nullptr : rl, nullptr, false, stmp,
+                          cnt, PA, big_buckets, c->log_ranks, 2, pv);
+        if (rc) return rc;
+        PI.xrec = PA.xrec;
+        HIPCHK(launch_read_bound(loff, N, PI, dst, (uint32_t)P, pb, pown, c->stream));
+        HIPCHK(hipMemcpyAsync(c->pbown.data(), pown, ((size_t)P + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    resolve_timing(c);
+    c->dist_in = PI;
+    c->dist_recv = n;
+    c->dist_bkt = true;
+    c->dist_npass = 1;
+    c->stats.buckets = lds_buckets + big_buckets;
+    c->stats.role_pairs = 0;
+    c->stats.pairs = 0;
+    c->stats.dispatched = 0;
+    if (bound) *bound = c->pbown[P];
+    return SA_OK;
+}
+
+int sa_dist_plan(sa_ctx *c, uint64_t budget, uint32_t *npass) {
+    if (!c || !npass) return SA_E_ARG;
+    if (!c->dist_bkt) return fail(c, SA_E_STATE, "sa_dist_buckets first");
+    const int P = c->nranks;
+    const uint64_t total = c->pbown[P];
+    budget = std::max<uint64_t>(budget, 1);
+    if (total <= budget) {
+        c->dist_npass = *npass = 1;
+        return SA_OK;
+    }
+    (void)hipSetDevice(c->device);
+    const uint32_t N = (uint32_t)c->dlen.size();
+    if (c->pbcum.size() != (size_t)N + 1) {  // the per-read bounds, prefix-summed on the host
+        std::vector<uint64_t> b(N);
+        if (N) HIPCHK(hipMemcpy(b.data(), c->d_pbound.p, (size_t)N * 8, hipMemcpyDeviceToHost));
+        c->pbcum.assign((size_t)N + 1, 0);
+        for (uint32_t i = 0; i < N; ++i) c->pbcum[i + 1] = c->pbcum[i] + b[i];
+    }
+    uint64_t maxlen = 1;
+    for (int r = 0; r < P; ++r) maxlen = std::max<uint64_t>(maxlen, c->dstarts[r + 1] - c->dstarts[r]);
+    // the largest pass of an np-pass plan on this rank (every owner's range of the pass)
+    auto worst = [&](uint64_t np) {
+        uint64_t w = 0;
+        for (uint64_t p = 0; p < np; ++p) {
+            uint64_t t = 0;
+            for (int r = 0; r < P; ++r) {
+                uint32_t a, b;
+                pass_range(c, r, (uint32_t)p, (uint32_t)np, a, b);
+                t += c->pbcum[b] - c->pbcum[a];
+            }
+            w = std::max(w, t);
+        }
+        return w;
+    };
+    uint64_t np = std::min<uint64_t>(maxlen, (total + budget - 1) / budget);
+    while (np < maxlen && worst(np) > budget) np = std::min<uint64_t>(maxlen, np + std::max<uint64_t>(1, np / 8));
+    if (np > 0xFFFFFFFull) return fail(c, SA_E_OVERFLOW, "lead-range pass plan: too many passes");
+    c->dist_npass = *npass = (uint32_t)np;
+    return SA_OK;
+}
+
+int sa_dist_count_pass(sa_ctx *c, uint32_t pass, uint32_t npass, uint64_t *counts) {
+    if (!c || !counts || npass == 0 || pass >= npass) return SA_E_ARG;
+    if (!c->dist_bkt) return fail(c, SA_E_STATE, "sa_dist_buckets first");
+    (void)hipSetDevice(c->device);
+    const int P = c->nranks;
+    const uint32_t N = (uint32_t)c->dlen.size();
+    const uint64_t n = c->dist_recv;
+    Counters *cnt;
+    ENSURE(c->d_cnt, 1, &cnt);
+    const uint64_t *loff = (const uint64_t *)c->d_loff.p;
+    const uint32_t *dst = (const uint32_t *)c->d_starts.p;
     // Every global read has ~1/P of its occurrences here (~60 of a 500 bp read
     // at P = 8): one wave per ~PMW_TARGET local occurrences (a few consecutive
     // reads), every distinct partial kept (count >= 1: the filter needs the
@@ -2199,26 +2357,47 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint6
     // ~60 local occurrences do not pay for a wave's table setup; and partials
     // sorted by owner after the count cost an order stage of 0.3 ms more)
     const uint32_t target = PMW_TARGET;
-    const uint32_t n_multi = (uint32_t)((n + target - 1) / target) + 1;
-    uint32_t *items;
-    ENSURE(c->d_items, 2 * ((size_t)n_multi + 1), &items);
-    HIPCHK(launch_pc_items(loff, N, target, n_multi, items, c->stream));
-    if (P > 1)
-        HIPCHK(launch_pc_item_owners(items, n_multi, (const uint32_t *)c->d_starts.p, (uint32_t)P, items + n_multi + 1,
-                                     c->stream));
-    bool aborted = false;
-    rc = pair_stage(c, E, PI, false, true, nullptr, N, cnt, np, cap_s, items, n_multi, &cnt->big_n, &aborted, nullptr,
-                    nullptr, (uint32_t)P, (const uint32_t *)c->d_starts.p, items + n_multi + 1, true);
-    if (rc) return rc;
-    if (aborted) {  // partitions above 4,096 records (high-copy repeats): build them, count again
-        rc = bucket_stage(c, keys, keys2, vals, vals2, n, loff, N, 0, packed ? nullptr : rl, nullptr, false, stmp,
-                          cnt, PA, big_buckets, c->log_ranks, 2, pv);
-        if (rc) return rc;
-        PI.xrec = PA.xrec;
-        rc = pair_stage(c, E, PI, false, true, nullptr, N, cnt, np, cap_s, items, n_multi, nullptr, nullptr, nullptr,
-                        nullptr, (uint32_t)P, (const uint32_t *)c->d_starts.p, items + n_multi + 1);
-        if (rc) return rc;
+    uint32_t n_multi = 0;
+    uint32_t *istart, *iend = nullptr, *iown = nullptr;
+    uint64_t own_max = 0;  // the largest owner's bound of this pass's partials
+    if (npass == 1) {  // every read: items over all local occurrences, no readback
+        n_multi = (uint32_t)((n + target - 1) / target) + 1;
+        ENSURE(c->d_items, 2 * ((size_t)n_multi + 1), &istart);
+        HIPCHK(launch_pc_items(loff, N, target, n_multi, istart, c->stream));
+        iown = istart + n_multi + 1;
+        for (int r = 0; r < P; ++r) own_max = std::max<uint64_t>(own_max, c->pbown[r]);
+    } else {  // this pass's lead range of every owner
+        std::vector<uint32_t> rg(2 * (size_t)P);
+        const bool cum = c->pbcum.size() == (size_t)N + 1;
+        for (int r = 0; r < P; ++r) {
+            pass_range(c, r, pass, npass, rg[2 * r], rg[2 * r + 1]);
+            own_max = std::max<uint64_t>(own_max, cum ? c->pbcum[rg[2 * r + 1]] - c->pbcum[rg[2 * r]] : c->pbown[r]);
+        }
+        uint32_t *drg, *ioff;
+        ENSURE(c->d_prange, rg.size(), &drg);
+        ENSURE(c->d_pioff, (size_t)P + 1, &ioff);
+        HIPCHK(hipMemcpyAsync(drg, rg.data(), rg.size() * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(launch_pass_items_count(loff, drg, (uint32_t)P, target, ioff, c->stream));
+        HIPCHK(hipMemcpyAsync(&n_multi, ioff + P, 4, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        ENSURE(c->d_pitems, 3 * ((size_t)n_multi + 1), &istart);
+        iend = istart + n_multi + 1;
+        iown = istart + 2 * ((size_t)n_multi + 1);
+        HIPCHK(launch_pass_items_fill(loff, drg, (uint32_t)P, target, ioff, n_multi, istart, iend, c->stream));
     }
+    if (P > 1) HIPCHK(launch_pc_item_owners(istart, n_multi, dst, (uint32_t)P, iown, c->stream, iend));
+    // output room: each owner's NSHARD regions hold 5/4 of that owner's bound spread
+    // evenly (the bound is the partner-list elements, >= the distinct partials); a
+    // region that still fills is grown and the pass recounted (pair_stage)
+    const uint64_t R = (uint64_t)NSHARD * (uint64_t)std::max(P, 1);
+    c->pair_cap = ((own_max + own_max / 4) / NSHARD + 1024) * R;
+    EmitParams E = emit_params(c);
+    E.occ_off = loff;  // occurrences of read a on this rank: [loff[a], loff[a+1])
+    E.npr = 0;
+    uint64_t np = 0, cap_s = 0;
+    int rc = pair_stage(c, E, c->dist_in, false, true, nullptr, N, cnt, np, cap_s, istart, n_multi, nullptr, nullptr,
+                        nullptr, nullptr, (uint32_t)P, dst, iown, false, iend);
+    if (rc) return rc;
     Counters hc;
     HIPCHK(hipMemcpyAsync(&hc, cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -2238,9 +2417,15 @@ int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint6
     c->part_off[fill.size()] = acc;
     c->part_np = acc;
     c->part_cap = cap_s;
-    c->stats.buckets = shard_sum(hc.bkt_counts) + big_buckets;
-    c->stats.role_pairs = shard_sum(hc.role_pairs);
+    if (pass + 1 == npass) c->stats.role_pairs = 0;  // (passes run from the last to the first)
+    c->stats.role_pairs += shard_sum(hc.role_pairs);
     return SA_OK;
+}
+
+int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint64_t *counts) {
+    if (!c || !counts || !recv_counts) return SA_E_ARG;
+    int rc = sa_dist_buckets(c, recv_recs, recv_counts, nullptr);
+    return rc ? rc : sa_dist_count_pass(c, 0, 1, counts);
 }
 
 int sa_dist_partials(sa_ctx *c, void *fst, void *snd, void *cnt_out) {
@@ -2266,14 +2451,29 @@ int sa_dist_partials(sa_ctx *c, void *fst, void *snd, void *cnt_out) {
     return SA_OK;
 }
 
-int sa_dist_reduce(sa_ctx *c, const void *fst, const void *snd, const void *cnt_in, uint64_t n) {
-    if (!c || (n && (!fst || !snd || !cnt_in))) return SA_E_ARG;
+int sa_dist_reduce_pass(sa_ctx *c, const void *fst, const void *snd, const void *cnt_in, uint64_t n, uint32_t pass,
+                        uint32_t npass) {
+    if (!c || (n && (!fst || !snd || !cnt_in)) || npass == 0 || pass >= npass) return SA_E_ARG;
     if (!c->dist) return fail(c, SA_E_STATE, "sa_dist_init first");
     (void)hipSetDevice(c->device);
     const uint32_t N = (uint32_t)c->dlen.size();
     const int idb = bits_for(N ? N - 1 : 0);
     Counters *cnt;
     ENSURE(c->d_cnt, 1, &cnt);
+    // this rank's leads of the pass; passes run from the last (highest leads) to the
+    // first, so each one's dispatch (lead descending) is appended after the previous
+    uint32_t lbase, lend;
+    pass_range(c, c->rank, pass, npass, lbase, lend);
+    const uint32_t nl = lend - lbase;
+    if (pass + 1 == npass) {
+        c->disp_acc = 0;
+        c->stats.pairs = 0;
+        c->stats.dispatched = 0;
+    }
+    const uint64_t acc = c->disp_acc;
+    c->built = c->aligned = false;
+    c->lead.clear(); c->trail.clear(); c->count.clear();
+    c->pfst.clear(); c->psnd.clear(); c->pcnt.clear();
     uint64_t *ok, *ok2; uint32_t *ov, *ov2, *sum, *keep, *pos; uint8_t *otmp, *scan;
     ENSURE(c->d_okeys, n, &ok);
     ENSURE(c->d_okeys2, n, &ok2);
@@ -2283,11 +2483,21 @@ int sa_dist_reduce(sa_ctx *c, const void *fst, const void *snd, const void *cnt_
     ENSURE(c->d_psum, n, &sum);
     ENSURE(c->d_pkeep, n, &keep);
     ENSURE(c->d_ppos, n, &pos);
-    const uint32_t lbase = c->dstarts[c->rank], nl = c->dstarts[c->rank + 1] - lbase;
     ENSURE(c->d_scan, scan_temp_bytes(std::max<uint64_t>(n, nl)), &scan);
     HIPCHK(hipMemsetAsync(cnt->distinct, 0, sizeof(cnt->distinct), c->stream));
     HIPCHK(hipMemsetAsync(cnt->totals, 0, sizeof(cnt->totals), c->stream));
     HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(cnt->overflow_n), c->stream));
+    auto finish = [&](uint32_t nd, unsigned long long ndist) {
+        c->disp_acc = acc + nd;
+        c->n_disp = c->disp_acc;
+        c->stats.pairs += ndist;
+        c->stats.dispatched = c->disp_acc;
+        c->stats.id_mode = SA_IDS_WIDE;
+        c->mode = SA_IDS_WIDE;
+        c->built = pass == 0;  // (the first pass is the last to run)
+        c->aligned = false;
+        return (int)SA_OK;
+    };
     // this rank's leads: per-lead segments of the received partials, summed and
     // filtered in LDS (one wave per lead; one block for a lead with more than
     // 192 distinct partners), then one scan + one copy in lead-descending
@@ -2315,26 +2525,17 @@ int sa_dist_reduce(sa_ctx *c, const void *fst, const void *snd, const void *cnt_
             const uint32_t nd = hp->totals[0];
             const unsigned long long ndist = shard_sum(hp->distinct);
             int32_t *dlead, *dtrail, *dcount;
-            ENSURE(c->d_lead, nd, &dlead);
-            ENSURE(c->d_trail, nd, &dtrail);
-            ENSURE(c->d_count, nd, &dcount);
+            if (int r_ = ensure_keep(c, c->d_lead, acc + nd, acc, &dlead)) return r_;
+            if (int r_ = ensure_keep(c, c->d_trail, acc + nd, acc, &dtrail)) return r_;
+            if (int r_ = ensure_keep(c, c->d_count, acc + nd, acc, &dcount)) return r_;
             {
                 StageScope st(c, SA_STAGE_ORDER);
-                HIPCHK(launch_lead_copy(seg, loff, kcnt, kex, &cnt->totals[0], nl, lbase, dlead, dtrail, dcount,
-                                        c->stream));
+                HIPCHK(launch_lead_copy(seg, loff, kcnt, kex, &cnt->totals[0], nl, lbase, dlead + acc, dtrail + acc,
+                                        dcount + acc, c->stream));
             }
             HIPCHK(hipStreamSynchronize(c->stream));
             resolve_timing(c);
-            c->n_disp = nd;
-            c->lead.clear(); c->trail.clear(); c->count.clear();
-            c->pfst.clear(); c->psnd.clear(); c->pcnt.clear();
-            c->stats.pairs = ndist;
-            c->stats.dispatched = nd;
-            c->stats.id_mode = SA_IDS_WIDE;
-            c->mode = SA_IDS_WIDE;
-            c->built = true;
-            c->aligned = false;
-            return SA_OK;
+            return finish(nd, ndist);
         }
         HIPCHK(hipMemsetAsync(cnt->distinct, 0, sizeof(cnt->distinct), c->stream));
         HIPCHK(hipMemsetAsync(cnt->totals, 0, sizeof(cnt->totals), c->stream));
@@ -2351,24 +2552,19 @@ int sa_dist_reduce(sa_ctx *c, const void *fst, const void *snd, const void *cnt_
     HIPCHK(hipMemcpyAsync(&nd, &cnt->totals[0], 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     int32_t *dlead, *dtrail, *dcount;
-    ENSURE(c->d_lead, nd, &dlead);
-    ENSURE(c->d_trail, nd, &dtrail);
-    ENSURE(c->d_count, nd, &dcount);
-    HIPCHK(launch_reduce_compact(ok, n, idb, sum, keep, pos, dlead, dtrail, dcount, c->stream));
+    if (int r_ = ensure_keep(c, c->d_lead, acc + nd, acc, &dlead)) return r_;
+    if (int r_ = ensure_keep(c, c->d_trail, acc + nd, acc, &dtrail)) return r_;
+    if (int r_ = ensure_keep(c, c->d_count, acc + nd, acc, &dcount)) return r_;
+    HIPCHK(launch_reduce_compact(ok, n, idb, sum, keep, pos, dlead + acc, dtrail + acc, dcount + acc, c->stream));
     Counters hc;
     HIPCHK(hipMemcpyAsync(&hc, cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     resolve_timing(c);
-    c->n_disp = nd;
-    c->lead.clear(); c->trail.clear(); c->count.clear();
-    c->pfst.clear(); c->psnd.clear(); c->pcnt.clear();
-    c->stats.pairs = shard_sum(hc.distinct);
-    c->stats.dispatched = nd;
-    c->stats.id_mode = SA_IDS_WIDE;
-    c->mode = SA_IDS_WIDE;
-    c->built = true;
-    c->aligned = false;
-    return SA_OK;
+    return finish(nd, shard_sum(hc.distinct));
+}
+
+int sa_dist_reduce(sa_ctx *c, const void *fst, const void *snd, const void *cnt_in, uint64_t n) {
+    return sa_dist_reduce_pass(c, fst, snd, cnt_in, n, 0, 1);
 }
 
 int sa_dist_codes(sa_ctx *c, void *codes, void *bad, uint64_t *nwords) {

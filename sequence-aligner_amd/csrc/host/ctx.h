@@ -126,6 +126,18 @@ struct sa_ctx {
     DBuf d_gocc, d_seg, d_rl, d_srl, d_srl2, d_loff, d_starts, d_bounds, d_gcodes, d_gwoff, d_glen, d_gbad, d_psum, d_pkeep, d_ppos;
     DBuf d_scan, d_bigtot, d_items, d_pq, d_ocur;
     DBuf d_lr;                       // owner-side reduce by lead: counts, offsets, cursors, kept, kept scan
+    // lead-range passes (sa_dist_buckets -> sa_dist_plan -> per pass sa_dist_count_pass,
+    // exchange 2, sa_dist_reduce_pass): the buckets are built once, then each pass counts
+    // the partials of 1/npass of every owner's leads, so the partials held at once are
+    // bounded by the pass (SURVEY.md 8(e) exchange 2 at configs[4]'s density)
+    bool dist_bkt = false;                 // buckets of the received records are built
+    sa::PairIn dist_in{};                  // their records and lists (device)
+    uint64_t dist_recv = 0;                // records received
+    std::vector<unsigned long long> pbown; // partial bound per lead owner [nranks], total last
+    std::vector<uint64_t> pbcum;           // host prefix sums of the per-read bounds (multi-pass plans)
+    uint32_t dist_npass = 1;               // the last plan's pass count
+    uint64_t disp_acc = 0;                 // dispatched pairs the reduce passes appended so far
+    DBuf d_pbound, d_pbown, d_prange, d_pioff, d_pitems;
     // k-mer table statistics (sa_kmer_histogram)
     DBuf d_hk0, d_hk1, d_hflag, d_hidx, d_hpos, d_htmp, d_hist, d_hovf, d_hsmall;
     std::vector<uint64_t> hsize, hcount;
@@ -175,4 +187,12 @@ void multi_stage_times(const sa_ctx *c, double *ms, uint64_t *n);
 void multi_reset_stage_times(sa_ctx *c);
 int multi_sync(sa_ctx *c);
 uint64_t multi_exchanged_bytes(const sa_ctx *c);
+// sharded contexts with SA_OPT_LEAN_MEMORY: free a child's scratch between stages (api.cpp)
+enum : int {
+    DIST_RELEASE_BUCKET_SCRATCH = 1,  // emit keys, sort / bucket-build scratch (after sa_dist_buckets)
+    DIST_RELEASE_PAIR_OUTPUT = 2,     // the pair counter's owner regions (after sa_dist_partials)
+    DIST_RELEASE_REDUCE_SCRATCH = 4,  // the owner reduce's scratch (after sa_dist_reduce_pass)
+    DIST_RELEASE_BUCKETS = 8          // records, lists, bounds, items (after the last pass)
+};
+void dist_release(sa_ctx *c, int what);
 }  // namespace sa

@@ -50,6 +50,8 @@ struct Shard {
     DBuf sk, rk, pf, ps, pc, qf, qs, qc, codes, bad, xbuf;
     std::vector<uint64_t> cnt, rcnt;  // per peer: elements sent / received
     uint64_t n_recv = 0, n_part = 0;
+    uint64_t bound = 0;               // upper bound of this shard's partials (sa_dist_buckets)
+    uint32_t npass = 1;               // this shard's pass plan (sa_dist_plan)
     std::string err;
 };
 
@@ -69,6 +71,14 @@ struct sa_multi {
     DBuf gcodes, gbad;              // virtual shards: one all-gathered copy on the device
     double x_ms = 0;                // exchange wall time (SA_STAGE_EXCHANGE)
     uint64_t x_n = 0, x_bytes = 0;
+    // lead-range passes (SA_OPT_PASS_BUDGET_MB; 0 = from the free device memory) and
+    // scratch release between stages (SA_OPT_LEAN_MEMORY)
+    uint64_t budget_mb = 0;
+    bool lean = false;
+    // the last sharded build: passes, partial entries over every shard and pass, and
+    // their upper bound (sa_get_shard_info)
+    uint32_t npass = 1;
+    uint64_t partials = 0, bound = 0;
 };
 
 namespace {
@@ -244,6 +254,27 @@ int exchange_counts(sa_ctx *c) {
 
 bool is_pow2(int x) { return x > 0 && (x & (x - 1)) == 0; }
 
+// Partial entries one shard may produce per lead-range pass: SA_OPT_PASS_BUDGET_MB, or
+// from the free memory of its device after the bucket build.  An entry (counted by its
+// upper bound) takes ~15 B of pair-counter regions, 12 B of send and 12 B of receive
+// buffer and ~28 B of reduce scratch on every shard of the device; with
+// SA_OPT_LEAN_MEMORY only the send and receive buffers of every shard are held at
+// once (regions and scratch one shard at a time).  Within [2^16, 2^31] entries.
+uint64_t pass_budget(const sa_multi *m, const Shard &s) {
+    uint64_t b;
+    if (m->budget_mb) {
+        b = (m->budget_mb << 20) / 12;
+    } else {
+        size_t fr = 0, tot = 0;
+        (void)hipSetDevice(s.device);
+        if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 0;
+        const uint64_t per_dev = m->rccl ? 1 : m->sh.size();  // shards sharing this device
+        const uint64_t per_entry = m->lean ? 24 * per_dev + 43 : 67 * per_dev;
+        b = (uint64_t)((double)fr * 0.6) / per_entry;
+    }
+    return std::min<uint64_t>(std::max<uint64_t>(b, 1ull << 16), 1ull << 31);
+}
+
 void clear_child_reads(sa_ctx *k) {
     k->bases.clear();
     k->boff.assign(1, 0);
@@ -390,44 +421,93 @@ int multi_build(sa_ctx *c, bool readback, int (*single_build)(sa_ctx *, bool)) {
         pl[l].rcnt = s.rcnt; pl[l].roff = prefix(s.rcnt);
     }
     if ((rc = exchange(c, pl, 8))) return rc;
-    // ---- count: buckets of this hash range, partial pairs by lead owner
+    if (m->lean) for (Shard &s : m->sh) release(s.sk, s.device);
+    // ---- buckets of this hash range (built once), the partials' upper bounds
     rc = for_shards(c, [&](Shard &s) {
-        s.cnt.assign(P, 0);
-        int r = sa_dist_count(s.child, s.rk.p, s.rcnt.data(), s.cnt.data());
-        if (r) return r;
-        s.n_part = 0;
-        for (uint64_t v : s.cnt) s.n_part += v;
-        if (grow(s.pf, s.n_part * 4 + 4, s.device) || grow(s.ps, s.n_part * 4 + 4, s.device) ||
-            grow(s.pc, s.n_part * 4 + 4, s.device))
-            return (int)SA_E_NOMEM;
-        return sa_dist_partials(s.child, s.pf.p, s.ps.p, s.pc.p);
+        int r = sa_dist_buckets(s.child, s.rk.p, s.rcnt.data(), &s.bound);
+        if (m->lean) {  // the received records are consumed (they were the sort's keys)
+            release(s.rk, s.device);
+            dist_release(s.child, DIST_RELEASE_BUCKET_SCRATCH);
+        }
+        return r;
     });
     if (rc) return rc;
-    // ---- exchange 2: partials to the shard owning the lead
-    if ((rc = exchange_counts(c))) return rc;
-    for (size_t l = 0; l < m->sh.size(); ++l) {
-        Shard &s = m->sh[l];
-        s.n_recv = 0;
-        for (uint64_t v : s.rcnt) s.n_recv += v;
-        if (grow(s.qf, s.n_recv * 4 + 4, s.device) || grow(s.qs, s.n_recv * 4 + 4, s.device) ||
-            grow(s.qc, s.n_recv * 4 + 4, s.device))
-            return set_err(c, SA_E_NOMEM, "receive buffer");
-        pl[l].scnt = s.cnt; pl[l].soff = prefix(s.cnt);
-        pl[l].rcnt = s.rcnt; pl[l].roff = prefix(s.rcnt);
+    // ---- lead-range passes: every pass holds the partials of 1/npass of every
+    // owner's leads, within the budget on every shard (all ranks agree on npass)
+    std::vector<uint64_t> budget(m->sh.size());
+    for (size_t l = 0; l < m->sh.size(); ++l) budget[l] = pass_budget(m, m->sh[l]);
+    uint32_t npass = 1;
+    rc = for_shards(c, [&](Shard &s) { return sa_dist_plan(s.child, budget[&s - m->sh.data()], &s.npass); });
+    if (rc) return rc;
+    for (Shard &s : m->sh) npass = std::max(npass, s.npass);
+    if (m->rank_mode) {  // the max over ranks
+        Shard &s = m->sh[0];
+        s.cnt.assign(P, npass);
+        if ((rc = exchange_counts(c))) return rc;
+        for (uint64_t v : s.rcnt) npass = std::max<uint32_t>(npass, (uint32_t)v);
     }
-    // (lead, trail, count) arrays in one RCCL group
+    m->npass = npass;
+    m->partials = 0;
+    m->bound = 0;
+    for (Shard &s : m->sh) m->bound += s.bound;
     DBuf Shard::*src[3] = {&Shard::pf, &Shard::ps, &Shard::pc};
     DBuf Shard::*dst[3] = {&Shard::qf, &Shard::qs, &Shard::qc};
-    std::vector<Part> parts(3);
-    for (int a = 0; a < 3; ++a)
+    for (uint32_t pass = npass; pass-- > 0;) {
+        // ---- count: partial pairs of this pass's leads, grouped by lead owner
+        rc = for_shards(c, [&](Shard &s) {
+            s.cnt.assign(P, 0);
+            int r = sa_dist_count_pass(s.child, pass, npass, s.cnt.data());
+            if (r) return r;
+            s.n_part = 0;
+            for (uint64_t v : s.cnt) s.n_part += v;
+            if (grow(s.pf, s.n_part * 4 + 4, s.device) || grow(s.ps, s.n_part * 4 + 4, s.device) ||
+                grow(s.pc, s.n_part * 4 + 4, s.device))
+                return (int)SA_E_NOMEM;
+            r = sa_dist_partials(s.child, s.pf.p, s.ps.p, s.pc.p);
+            if (m->lean) dist_release(s.child, DIST_RELEASE_PAIR_OUTPUT);
+            return r;
+        });
+        if (rc) return rc;
+        for (Shard &s : m->sh) m->partials += s.n_part;
+        // ---- exchange 2: partials to the shard owning the lead
+        if ((rc = exchange_counts(c))) return rc;
         for (size_t l = 0; l < m->sh.size(); ++l) {
-            parts[a].send.push_back((m->sh[l].*src[a]).p);
-            parts[a].recv.push_back((m->sh[l].*dst[a]).p);
+            Shard &s = m->sh[l];
+            s.n_recv = 0;
+            for (uint64_t v : s.rcnt) s.n_recv += v;
+            if (grow(s.qf, s.n_recv * 4 + 4, s.device) || grow(s.qs, s.n_recv * 4 + 4, s.device) ||
+                grow(s.qc, s.n_recv * 4 + 4, s.device))
+                return set_err(c, SA_E_NOMEM, "receive buffer");
+            pl[l].scnt = s.cnt; pl[l].soff = prefix(s.cnt);
+            pl[l].rcnt = s.rcnt; pl[l].roff = prefix(s.rcnt);
         }
-    if ((rc = exchange_parts(c, pl, parts, 4))) return rc;
-    // ---- reduce + filter: this shard's leads
-    rc = for_shards(c, [&](Shard &s) { return sa_dist_reduce(s.child, s.qf.p, s.qs.p, s.qc.p, s.n_recv); });
-    if (rc) return rc;
+        // (lead, trail, count) arrays in one RCCL group
+        std::vector<Part> parts(3);
+        for (int a = 0; a < 3; ++a)
+            for (size_t l = 0; l < m->sh.size(); ++l) {
+                parts[a].send.push_back((m->sh[l].*src[a]).p);
+                parts[a].recv.push_back((m->sh[l].*dst[a]).p);
+            }
+        if ((rc = exchange_parts(c, pl, parts, 4))) return rc;
+        if (m->lean)
+            for (Shard &s : m->sh)
+                for (int a = 0; a < 3; ++a) release(s.*src[a], s.device);
+        // ---- reduce + filter: this shard's leads of the pass, appended
+        rc = for_shards(c, [&](Shard &s) {
+            int r = sa_dist_reduce_pass(s.child, s.qf.p, s.qs.p, s.qc.p, s.n_recv, pass, npass);
+            if (m->lean) {
+                for (int a = 0; a < 3; ++a) release(s.*dst[a], s.device);
+                dist_release(s.child, DIST_RELEASE_REDUCE_SCRATCH);
+            }
+            return r;
+        });
+        if (rc) return rc;
+    }
+    if (m->lean)
+        for (Shard &s : m->sh) {
+            (void)hipSetDevice(s.device);
+            dist_release(s.child, DIST_RELEASE_BUCKETS);
+        }
     c->stats = sa_stats{};
     uint64_t nd = 0;
     for (Shard &s : m->sh) {
@@ -654,6 +734,14 @@ int multi_set_option(sa_ctx *c, int option, int64_t value) {
         c->multi->serial = value != 0;
         return SA_OK;
     }
+    if (option == SA_OPT_PASS_BUDGET_MB) {
+        c->multi->budget_mb = (uint64_t)value;
+        return SA_OK;
+    }
+    if (option == SA_OPT_LEAN_MEMORY) {
+        c->multi->lean = value != 0;
+        return SA_OK;
+    }
     for (Shard &s : c->multi->sh) {
         int rc = sa_set_option(s.child, option, value);
         if (rc) return set_err(c, rc, sa_last_error(s.child));
@@ -698,6 +786,14 @@ uint64_t multi_exchanged_bytes(const sa_ctx *c) { return c->multi ? c->multi->x_
 // C ABI: constructors
 // ---------------------------------------------------------------------------
 extern "C" {
+
+int sa_get_shard_info(const sa_ctx *c, uint32_t *npass, uint64_t *partials, uint64_t *bound) {
+    if (!c || !c->multi) return SA_E_ARG;
+    if (npass) *npass = c->multi->npass;
+    if (partials) *partials = c->multi->partials;
+    if (bound) *bound = c->multi->bound;
+    return SA_OK;
+}
 
 int sa_rccl_unique_id(void *id, size_t cap) {
     if (!id || cap < sizeof(ncclUniqueId)) return SA_E_ARG;

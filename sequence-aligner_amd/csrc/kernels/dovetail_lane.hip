@@ -458,7 +458,17 @@ __device__ __forceinline__ u16x2 pk_sum(u16x2 a, u16x2 b) { return pk(upk(a) + u
 // relaxed atomics -- loads and stores that go past the non-coherent L2 one instruction at
 // a time -- instead of release / acquire fences, whose L2 write-back and invalidate of the
 // whole cache per hand-off cost more than the segments saved.
-constexpr int P1X2_STATE = 3 * 15 + 2;
+// Hardware assumption (gfx950), not a C++ memory-model guarantee: the producer's
+// s_waitcnt(0) before its flag store means every sc1 state store has been acknowledged by
+// the device-coherent level, and the consumer issues its sc1 state loads only after it
+// has seen the flag, so they cannot return older values.  A later compiler or target
+// could weaken that, so the hand-off is checked: word 47 of a lane's slot is a checksum
+// of the other 47 words and of the segment they are for, and a consumer that reads a
+// mismatch reports SA_E_HIP (err -7) instead of aligning from stale state.
+constexpr int P1X2_WORDS = 3 * 15 + 2;
+constexpr int P1X2_STATE = P1X2_WORDS + 1;
+__device__ __forceinline__ uint32_t p1x2_seal(uint32_t h, uint32_t w) { return ((h << 5) | (h >> 27)) ^ w; }
+__device__ __forceinline__ uint32_t p1x2_seal_init(int32_t seg) { return 0x9E3779B1u * (uint32_t)(seg + 1); }
 __device__ __forceinline__ uint32_t st_ld(const uint32_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -516,14 +526,21 @@ __device__ __forceinline__ void p1x2_run(const DevReads &rd, const int32_t *lead
 #pragma unroll
         for (int j = 0; j < LW - 1; ++j) { Tc[j] = 0; Q[j] = 0; O[j] = 0x00010001u; }  // origin (row 0, col != 0)
     } else {
+        uint32_t hT = p1x2_seal_init(seg), hQ = 0, hO = 0;
 #pragma unroll
         for (int j = 0; j < LW - 1; ++j) {
-            Tc[j] = pk(st_ld(st + j * 64 + lane));
-            Q[j] = pk(st_ld(st + (15 + j) * 64 + lane));
+            const uint32_t t = st_ld(st + j * 64 + lane), q = st_ld(st + (15 + j) * 64 + lane);
             O[j] = st_ld(st + (30 + j) * 64 + lane);
+            Tc[j] = pk(t);
+            Q[j] = pk(q);
+            hT = p1x2_seal(hT, t);
+            hQ = p1x2_seal(hQ, q);
+            hO = p1x2_seal(hO, O[j]);
         }
         best = pk(st_ld(st + 45 * 64 + lane));
         borg = st_ld(st + 46 * 64 + lane);
+        const uint32_t chk = st_ld(st + P1X2_WORDS * 64 + lane);
+        if (p1x2_seal(p1x2_seal(hT ^ hQ ^ hO, upk(best)), borg) != chk) set_err(err, -7);  // SA_E_HIP
     }
     const int32_t rowsA = qa.status == 0 ? qa.LA : 0, rowsB = qb.status == 0 ? qb.LA : 0;
     int32_t rmax = max(rowsA, rowsB);
@@ -593,14 +610,19 @@ __device__ __forceinline__ void p1x2_run(const DevReads &rd, const int32_t *lead
     if (i == iu) { row(i, unm); ++i; }
     for (; i <= i1; ++i) row(i, msk);
     if (!last) {
+        uint32_t hT = p1x2_seal_init(seg + 1), hQ = 0, hO = 0;
 #pragma unroll
         for (int j = 0; j < LW - 1; ++j) {
             st_st(st + j * 64 + lane, upk(Tc[j]));
             st_st(st + (15 + j) * 64 + lane, upk(Q[j]));
             st_st(st + (30 + j) * 64 + lane, O[j]);
+            hT = p1x2_seal(hT, upk(Tc[j]));
+            hQ = p1x2_seal(hQ, upk(Q[j]));
+            hO = p1x2_seal(hO, O[j]);
         }
         st_st(st + 45 * 64 + lane, upk(best));
         st_st(st + 46 * 64 + lane, borg);
+        st_st(st + P1X2_WORDS * 64 + lane, p1x2_seal(p1x2_seal(hT ^ hQ ^ hO, upk(best)), borg));
         return;
     }
     unsigned long long cells = 0;

@@ -1016,7 +1016,9 @@ __global__ __launch_bounds__(PMW_WAVES * 64, SA_PMW_MIN_WAVES) void pair_count_m
     const uint32_t item = blockIdx.x * PMW_WAVES + wv;
     // (no early return below: every wave reaches the block's output claim)
     const bool live = item < p.n_items;
-    const uint32_t ra = live ? item_start[item] : 0u, rb = live ? item_start[item + 1] : 0u;
+    // (lead-range passes: the pass's items carry their own ends -- its ranges leave gaps)
+    const uint32_t ra = live ? item_start[item] : 0u,
+                   rb = live ? (o.item_end ? o.item_end[item] : item_start[item + 1]) : 0u;
     const uint32_t own2 = live && o.owners > 1 ? o.item_owner[item] : 0u;  // (lo | hi << 16, pc_item_owners)
     for (int i = lane; i < PMW_TAB; i += 64) {
         S.key[i] = KK::EMPTY;
@@ -1270,19 +1272,134 @@ __global__ void pc_items_kernel(const uint64_t *occ_off, uint32_t n_reads, uint3
 
 // owners of item j's first and last read, lo | hi << 16 (sharded emission: no
 // search on the pair counter's critical path)
-__global__ void pc_item_owners_kernel(const uint32_t *item_start, uint32_t n_items, const uint32_t *starts,
-                                      uint32_t owners, uint32_t *item_owner) {
+__global__ void pc_item_owners_kernel(const uint32_t *item_start, const uint32_t *item_end, uint32_t n_items,
+                                      const uint32_t *starts, uint32_t owners, uint32_t *item_owner) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n_items) return;
-    const uint32_t ra = item_start[j], rb = item_start[j + 1];
+    const uint32_t ra = item_start[j], rb = item_end ? item_end[j] : item_start[j + 1];
     item_owner[j] = ra < rb ? owner_of(starts, owners, ra) | (owner_of(starts, owners, rb - 1) << 16) : 0xFFFFu;
 }
 
 hipError_t launch_pc_item_owners(const uint32_t *item_start, uint32_t n_items, const uint32_t *starts, uint32_t owners,
-                                 uint32_t *item_owner, hipStream_t s) {
+                                 uint32_t *item_owner, hipStream_t s, const uint32_t *item_end) {
     if (!n_items) return hipSuccess;
-    hipLaunchKernelGGL(pc_item_owners_kernel, dim3((n_items + 255) / 256), dim3(256), 0, s, item_start, n_items, starts,
-                       owners, item_owner);
+    // owners travel as lo | hi << 16 (the multi-wave kernel decodes & 0xFFFF, >> 16);
+    // sa_dist_init caps nranks at 256, this keeps the packing honest on its own
+    if (owners == 0 || owners > 0xFFFFu) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(pc_item_owners_kernel, dim3((n_items + 255) / 256), dim3(256), 0, s, item_start, item_end,
+                       n_items, starts, owners, item_owner);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Lead-range passes of the sharded count (sa_dist_count_pass).  A pass counts the
+// partials of the leads in nr read ranges rg[2r] .. rg[2r + 1] (one range per lead
+// owner), so the partials held at once are bounded by the pass, not by the read set.
+// Its items are the ranges' reads cut every `target` local occurrences exactly as
+// pc_items_kernel cuts all reads; range r's items are [ioff[r], ioff[r + 1]).
+// ---------------------------------------------------------------------------
+__global__ void pass_items_count_kernel(const uint64_t *occ_off, const uint32_t *rg, uint32_t nr, uint32_t target,
+                                        uint32_t *ioff) {
+    if (threadIdx.x || blockIdx.x) return;  // nr <= 256 ranges: one serial scan
+    uint32_t acc = 0;
+    for (uint32_t r = 0; r < nr; ++r) {
+        ioff[r] = acc;
+        const uint64_t n = occ_off[rg[2 * r + 1]] - occ_off[rg[2 * r]];
+        acc += (uint32_t)((n + target - 1) / target);
+    }
+    ioff[nr] = acc;
+}
+
+// first read x in [a, b] with occ_off[x] >= v (occ_off[b] >= v)
+__device__ __forceinline__ uint32_t occ_lower_bound(const uint64_t *occ_off, uint32_t a, uint32_t b, uint64_t v) {
+    while (a < b) {
+        const uint32_t mid = a + ((b - a) >> 1);
+        if (occ_off[mid] < v) a = mid + 1; else b = mid;
+    }
+    return a;
+}
+
+__global__ void pass_items_fill_kernel(const uint64_t *occ_off, const uint32_t *rg, uint32_t nr, uint32_t target,
+                                       const uint32_t *ioff, uint32_t n_items, uint32_t *istart, uint32_t *iend) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_items) return;
+    uint32_t lo = 0, hi = nr;  // the range holding item j: largest r with ioff[r] <= j
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (ioff[mid] <= j) lo = mid; else hi = mid;
+    }
+    const uint32_t t = j - ioff[lo], ni = ioff[lo + 1] - ioff[lo];
+    const uint32_t a = rg[2 * lo], b = rg[2 * lo + 1];
+    const uint64_t base = occ_off[a];
+    istart[j] = t == 0 ? a : occ_lower_bound(occ_off, a, b, base + (uint64_t)t * target);
+    iend[j] = t + 1 == ni ? b : occ_lower_bound(occ_off, a, b, base + (uint64_t)(t + 1) * target);
+}
+
+hipError_t launch_pass_items_count(const uint64_t *occ_off, const uint32_t *rg, uint32_t nr, uint32_t target,
+                                   uint32_t *ioff, hipStream_t s) {
+    if (nr == 0 || nr > 256) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(pass_items_count_kernel, dim3(1), dim3(64), 0, s, occ_off, rg, nr, target, ioff);
+    return hipGetLastError();
+}
+
+hipError_t launch_pass_items_fill(const uint64_t *occ_off, const uint32_t *rg, uint32_t nr, uint32_t target,
+                                  const uint32_t *ioff, uint32_t n_items, uint32_t *istart, uint32_t *iend,
+                                  hipStream_t s) {
+    if (!n_items) return hipSuccess;
+    hipLaunchKernelGGL(pass_items_fill_kernel, dim3((n_items + 255) / 256), dim3(256), 0, s, occ_off, rg, nr, target,
+                       ioff, n_items, istart, iend);
+    return hipGetLastError();
+}
+
+// Upper bound of the partials each read can lead on this rank: its local occurrences'
+// partner-list elements (every element is at most one distinct (lead, partner) key,
+// KmerTable.scala:57-80), bound[a].  Sums per lead owner into own[o] (o < owners) and the
+// total into own[owners]: the host plans the lead-range passes from them.
+// abort (nullable): big partitions still to build (bucket_stage phase 1) -- their records
+// are not written yet, so every block exits at once and the host runs this again later
+__global__ __launch_bounds__(256) void read_bound_kernel(const uint64_t *occ_off, uint32_t n_reads, PairIn in,
+                                                         const uint32_t *starts, uint32_t owners, uint64_t *bound,
+                                                         unsigned long long *own, const uint32_t *abort) {
+    if (abort && *abort) return;
+    const uint32_t a = blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t s = 0;
+    if (a < n_reads) {
+        const uint64_t g1 = occ_off[a + 1];
+        for (uint64_t g = occ_off[a]; g < g1; ++g) {
+            const uint4 r = load_rec(in, g);
+            s += (r.y & 0x3FFFFFFFu) + r.w;
+        }
+        bound[a] = s;
+    }
+    // one atomic per wave and owner: a wave's reads are consecutive, so nearly
+    // always one owner (the first and last lane agree)
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane((int)a);
+    const uint32_t ow0 = first < n_reads ? owner_of(starts, owners, first) : 0u;
+    const uint32_t lastr = min(first + 63u, n_reads ? n_reads - 1u : 0u);
+    const uint32_t ow1 = first < n_reads ? owner_of(starts, owners, lastr) : 0u;
+    uint64_t t = s;
+    if (ow0 == ow1) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
+        if (lane == 0 && first < n_reads) {
+            atomicAdd(&own[ow0], (unsigned long long)t);
+            atomicAdd(&own[owners], (unsigned long long)t);
+        }
+    } else if (a < n_reads && s) {
+        atomicAdd(&own[owner_of(starts, owners, a)], (unsigned long long)s);
+        atomicAdd(&own[owners], (unsigned long long)s);
+    }
+}
+
+hipError_t launch_read_bound(const uint64_t *occ_off, uint32_t n_reads, const PairIn &in, const uint32_t *starts,
+                             uint32_t owners, uint64_t *bound, unsigned long long *own, hipStream_t s,
+                             const uint32_t *abort) {
+    if (owners == 0 || owners > 256) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(own, 0, ((size_t)owners + 1) * sizeof(unsigned long long), s);
+    if (e != hipSuccess || !n_reads) return e;
+    hipLaunchKernelGGL(read_bound_kernel, dim3((n_reads + 255) / 256), dim3(256), 0, s, occ_off, n_reads, in, starts,
+                       owners, bound, own, abort);
     return hipGetLastError();
 }
 

@@ -281,6 +281,9 @@ struct PairOut {
     uint32_t owners;
     const uint32_t *owner_starts;
     const uint32_t *item_owner;  // multi-read items: owners of the item's first | last read << 16
+    // multi-read items with their own ends (lead-range passes: the pass's read ranges leave
+    // gaps, so item j is [item_start[j], item_end[j])); null: item_start[j + 1]
+    const uint32_t *item_end;
 };
 constexpr uint32_t PC_RREG = 192;  // = the first pass's fill limit (256 slots at 3/4)
 // fill limit of the recount tiers' tables (2,048 slots and up, bucketed
@@ -405,7 +408,20 @@ constexpr uint32_t PMW_TARGET = SA_PMW_TARGET;
 hipError_t launch_pair_count_multi_wave(const EmitParams &e, const PairIn &in, const PairParams &p, PairOut &o,
                                         const uint32_t *item_start, uint32_t n_items, uint32_t n_reads, hipStream_t s);
 hipError_t launch_pc_item_owners(const uint32_t *item_start, uint32_t n_items, const uint32_t *starts, uint32_t owners,
-                                 uint32_t *item_owner, hipStream_t s);
+                                 uint32_t *item_owner, hipStream_t s, const uint32_t *item_end = nullptr);
+// lead-range passes (sa_dist_count_pass): items over the reads of nr ranges rg[2r] ..
+// rg[2r + 1] only (ioff: nr + 1 u32, the count kernel's exclusive item offsets, ioff[nr] =
+// items), then their starts and ends
+hipError_t launch_pass_items_count(const uint64_t *occ_off, const uint32_t *rg, uint32_t nr, uint32_t target,
+                                   uint32_t *ioff, hipStream_t s);
+hipError_t launch_pass_items_fill(const uint64_t *occ_off, const uint32_t *rg, uint32_t nr, uint32_t target,
+                                  const uint32_t *ioff, uint32_t n_items, uint32_t *istart, uint32_t *iend,
+                                  hipStream_t s);
+// per-read upper bound of the partials each read leads on this rank (bound[n_reads]),
+// summed per lead owner into own[0 .. owners) and in all into own[owners]
+hipError_t launch_read_bound(const uint64_t *occ_off, uint32_t n_reads, const PairIn &in, const uint32_t *starts,
+                             uint32_t owners, uint64_t *bound, unsigned long long *own, hipStream_t s,
+                             const uint32_t *abort = nullptr);
 hipError_t launch_pc_items(const uint64_t *occ_off, uint32_t n_reads, uint32_t target, uint32_t n_items,
                            uint32_t *item_start, hipStream_t s);
 

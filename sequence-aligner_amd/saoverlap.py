@@ -24,6 +24,7 @@ LIB_PATH = os.environ.get("SA_OVERLAP_LIB") or os.path.join(HERE, "build", "libs
 SA_IDS_AUTO, SA_IDS_STRICT, SA_IDS_WIDE = 0, 1, 2
 SA_OPT_KEEP_PAIRS, SA_OPT_TIMING, SA_OPT_ALIGN_KERNEL, SA_OPT_ALIGNER, SA_OPT_LOCAL_BATCH_MB = 1, 2, 3, 4, 5
 SA_OPT_SERIAL_SHARDS, SA_OPT_LAUNCH_SLICE, SA_OPT_FIRST_PASS = 6, 7, 8
+SA_OPT_PASS_BUDGET_MB, SA_OPT_LEAN_MEMORY = 9, 10   # sharded contexts: lead-range passes, scratch release
 SA_ALIGNER_LINEAR, SA_ALIGNER_QUADRATIC = 0, 1   # --linear-align / --quadratic-align
 SA_STATS_PER_READ_REGIONS, SA_STATS_RECOUNTED = 1, 2    # sa_stats.flags bits of the last build
 ALIGN_AUTO, ALIGN_GROUP, ALIGN_LANE, ALIGN_LANE_SUMMARY = 0, 1, 2, 3
@@ -40,7 +41,8 @@ EXPORTS = ("sa_default_settings", "sa_ctx_create", "sa_ctx_destroy", "sa_last_er
            "sa_get_stats", "sa_get_stage_times", "sa_reset_stage_times", "sa_device_build", "sa_device_align",
            "sa_sync", "sa_dist_init", "sa_dist_local_kmers", "sa_dist_emit", "sa_dist_count", "sa_dist_partials",
            "sa_dist_reduce", "sa_dist_codes", "sa_dist_set_reads", "sa_ctx_create_multi", "sa_rccl_unique_id",
-           "sa_ctx_create_rank", "sa_exchanged_bytes")
+           "sa_ctx_create_rank", "sa_exchanged_bytes", "sa_dist_buckets", "sa_dist_plan", "sa_dist_count_pass",
+           "sa_dist_reduce_pass", "sa_get_shard_info")
 RCCL_ID_BYTES = 128
 
 
@@ -111,6 +113,11 @@ def lib():
         L.sa_ctx_create_rank.argtypes = [P(Settings), C.c_int, C.c_int, C.c_int, C.c_char_p, P(vp)]
         L.sa_exchanged_bytes.argtypes = [vp]
         L.sa_exchanged_bytes.restype = C.c_uint64
+        L.sa_dist_buckets.argtypes = [vp, vp, P(C.c_uint64), P(C.c_uint64)]
+        L.sa_dist_plan.argtypes = [vp, C.c_uint64, P(C.c_uint32)]
+        L.sa_dist_count_pass.argtypes = [vp, C.c_uint32, C.c_uint32, P(C.c_uint64)]
+        L.sa_dist_reduce_pass.argtypes = [vp, vp, vp, vp, C.c_uint64, C.c_uint32, C.c_uint32]
+        L.sa_get_shard_info.argtypes = [vp, P(C.c_uint32), P(C.c_uint64), P(C.c_uint64)]
         _lib = L
     return _lib
 
@@ -162,7 +169,8 @@ class Overlapper:
 
     def __init__(self, device=0, timing=False, keep_pairs=False, align_kernel=ALIGN_AUTO,
                  aligner=SA_ALIGNER_LINEAR, local_batch_mb=None, gpus=1, shards=1, rank=None, nranks=None,
-                 rccl_id=None, serial_shards=False, launch_slice=0, first_pass=0, **kw):
+                 rccl_id=None, serial_shards=False, launch_slice=0, first_pass=0, pass_budget_mb=0,
+                 lean_memory=False, **kw):
         self.s = settings(**kw)
         h = C.c_void_p()
         if rank is not None:
@@ -191,6 +199,10 @@ class Overlapper:
             self._chk(lib().sa_set_option(h, SA_OPT_LAUNCH_SLICE, launch_slice))
         if first_pass:
             self._chk(lib().sa_set_option(h, SA_OPT_FIRST_PASS, first_pass))
+        if pass_budget_mb:
+            self._chk(lib().sa_set_option(h, SA_OPT_PASS_BUDGET_MB, pass_budget_mb))
+        if lean_memory:
+            self._chk(lib().sa_set_option(h, SA_OPT_LEAN_MEMORY, 1))
 
     def kmer_histogram(self):
         """(uniques, {bucket size: number of hashes}) -- KmerTable.uniqueKmers /
@@ -328,6 +340,14 @@ class Overlapper:
         """Bytes sent to other shards so far (sharded contexts)."""
         return int(lib().sa_exchanged_bytes(self.h))
 
+    def shard_info(self):
+        """The last sharded build: {npass, partials, bound} (sa_get_shard_info) --
+        its lead-range passes, the partial entries counted over all shards and passes
+        (exchange 2's volume, 12 B each) and their upper bound."""
+        npass, parts, bound = C.c_uint32(), C.c_uint64(), C.c_uint64()
+        self._chk(lib().sa_get_shard_info(self.h, C.byref(npass), C.byref(parts), C.byref(bound)))
+        return {"npass": npass.value, "partials": parts.value, "bound": bound.value}
+
     # ---- sharded hash stage (include/sa_overlap.h, sa_dist_*); buffers are
     # device pointers (ints), e.g. torch_tensor.data_ptr() on this context's GPU
     def dist_init(self, rank, nranks, starts, lengths):
@@ -362,6 +382,28 @@ class Overlapper:
 
     def dist_reduce(self, fst, snd, cnt, n):
         self._chk(lib().sa_dist_reduce(self.h, fst, snd, cnt, n))
+
+    # lead-range passes (bounded partials): buckets once, then per pass (npass - 1 down
+    # to 0) count -> partials -> exchange 2 -> reduce_pass
+    def dist_buckets(self, recv_recs, recv_counts):
+        """Returns the upper bound of this rank's partials."""
+        rc = (C.c_uint64 * self.nranks)(*[int(x) for x in recv_counts])
+        b = C.c_uint64()
+        self._chk(lib().sa_dist_buckets(self.h, recv_recs, rc, C.byref(b)))
+        return b.value
+
+    def dist_plan(self, budget):
+        n = C.c_uint32()
+        self._chk(lib().sa_dist_plan(self.h, int(budget), C.byref(n)))
+        return n.value
+
+    def dist_count_pass(self, p, npass):
+        cnt = self._counts()
+        self._chk(lib().sa_dist_count_pass(self.h, p, npass, cnt))
+        return np.array(cnt[:], dtype=np.int64)
+
+    def dist_reduce_pass(self, fst, snd, cnt, n, p, npass):
+        self._chk(lib().sa_dist_reduce_pass(self.h, fst, snd, cnt, n, p, npass))
 
     def dist_codes(self, codes=None, bad=None):
         nw = C.c_uint64()

@@ -74,7 +74,10 @@ class NumpyWorker:
         en = self.tail <= loc
         return st, md, en
 
-    def count(self, recv_recs, recv_counts):
+    def buckets(self, recv_recs, recv_counts):
+        """This rank's buckets and their partial pairs (all leads), plus every
+        read's upper bound of the partials it leads here: its role pairs as fst,
+        same-read ones included (>= its distinct partials)."""
         n = int(np.sum(recv_counts))
         recs = recv_recs[:n].numpy().view(np.uint64)
         src = np.repeat(np.arange(self.P), np.asarray(recv_counts, dtype=np.int64))
@@ -89,6 +92,7 @@ class NumpyWorker:
             buckets.setdefault(h, []).append((r, loc))
         pairs = {}
         rp = 0
+        self.rbound = np.zeros(len(self.lengths), dtype=np.int64)
         for occ in buckets.values():
             st, md, en = [], [], []
             for r, loc in occ:
@@ -105,17 +109,48 @@ class NumpyWorker:
                 for ra, la in edge_list:
                     for rb, lb in md:
                         rp += 1
+                        fst, snd = (ra, rb) if la > lb else (rb, ra)  # tie: md occurrence first
+                        self.rbound[fst] += 1
                         if ra == rb:
                             continue
-                        fst, snd = (ra, rb) if la > lb else (rb, ra)  # tie: md occurrence first
                         pairs[(fst, snd)] = pairs.get((fst, snd), 0) + 1
         self.role_pairs = rp
-        items = sorted(pairs.items())
+        self._pairs = sorted(pairs.items())
+        return int(self.rbound.sum())
+
+    def _range(self, r, p, npass):
+        s, ln = int(self.starts[r]), int(self.starts[r + 1] - self.starts[r])
+        return s + ln * p // npass, s + ln * (p + 1) // npass
+
+    def plan(self, budget):
+        """The fewest passes whose every pass's bound on this rank is <= budget
+        (sa_dist_plan)."""
+        total = int(self.rbound.sum())
+        if total <= budget:
+            return 1
+        cum = np.concatenate([[0], np.cumsum(self.rbound)])
+        maxlen = max(1, int(np.max(np.diff(self.starts))))
+
+        def worst(np_):
+            return max(sum(int(cum[b] - cum[a]) for a, b in (self._range(r, p, np_) for r in range(self.P)))
+                       for p in range(np_))
+        np_ = min(maxlen, -(-total // budget))
+        while np_ < maxlen and worst(np_) > budget:
+            np_ = min(maxlen, np_ + max(1, np_ // 8))
+        return np_
+
+    def count_pass(self, p, npass):
+        rg = [self._range(r, p, npass) for r in range(self.P)]
+        items = [(k, c) for k, c in self._pairs if any(a <= k[0] < b for a, b in rg)]
         self._pf = np.array([a for (a, _), _ in items], dtype=np.int32)
         self._ps = np.array([b for (_, b), _ in items], dtype=np.int32)
         self._pc = np.array([c for _, c in items], dtype=np.int32)
         owner = np.searchsorted(self.starts, self._pf, side="right") - 1
         return np.bincount(owner, minlength=self.P).astype(np.int64)
+
+    def count(self, recv_recs, recv_counts):
+        self.buckets(recv_recs, recv_counts)
+        return self.count_pass(0, 1)
 
     def partials(self, fst, snd, cnt):
         n = len(self._pf)
@@ -124,17 +159,26 @@ class NumpyWorker:
             snd[:n].copy_(_t(self._ps))
             cnt[:n].copy_(_t(self._pc))
 
-    def reduce(self, fst, snd, cnt, n):
+    def reduce_pass(self, fst, snd, cnt, n, p, npass):
+        """This rank's leads of pass p, appended (passes run npass - 1 down to 0)."""
         f, s, c = fst[:n].numpy(), snd[:n].numpy(), cnt[:n].numpy()
+        a0, a1 = self._range(self.rank, p, npass)
         tot = {}
         for a, b, x in zip(f.tolist(), s.tolist(), c.tolist()):
+            assert a0 <= a < a1, "a partial outside this pass's leads"
             tot[(a, b)] = tot.get((a, b), 0) + x
         keep = sorted(((a, b, x) for (a, b), x in tot.items() if self.min_c <= x <= self.max_c),
                       key=lambda t: (-t[0], t[1]))
-        self.lead = np.array([a + 1 for a, _, _ in keep], dtype=np.int32)
-        self.trail = np.array([b + 1 for _, b, _ in keep], dtype=np.int32)
-        self.dcount = np.array([x for _, _, x in keep], dtype=np.int32)
-        self.distinct = len(tot)
+        if p == npass - 1:
+            self.lead = self.trail = self.dcount = np.zeros(0, dtype=np.int32)
+            self.distinct = 0
+        self.lead = np.concatenate([self.lead, np.array([a + 1 for a, _, _ in keep], dtype=np.int32)])
+        self.trail = np.concatenate([self.trail, np.array([b + 1 for _, b, _ in keep], dtype=np.int32)])
+        self.dcount = np.concatenate([self.dcount, np.array([x for _, _, x in keep], dtype=np.int32)])
+        self.distinct += len(tot)
+
+    def reduce(self, fst, snd, cnt, n):
+        self.reduce_pass(fst, snd, cnt, n, 0, 1)
 
     def stats(self):
         return {"role_pairs": self.role_pairs, "dispatched": len(self.lead)}

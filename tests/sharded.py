@@ -33,7 +33,13 @@ descending rank order gives the single-GPU wide-id output exactly.
 
 A worker implements the per-rank compute on buffers the orchestrator owns:
 `HipWorker` wraps saoverlap.Overlapper (device pointers of torch tensors on
-this rank's GPU); tests/ provides a numpy model with the same methods.
+this rank's GPU); tests/dist_model.py is a numpy model with the same methods.
+
+Lead-range passes (build(budget=...)): for read sets whose partials do not fit
+at once, each pass p of npass counts, exchanges and reduces only the leads
+[s_r + len_r * p // npass, s_r + len_r * (p + 1) // npass) of every owner r;
+the ranks agree on npass (the largest of their plans) and run the passes from
+the last to the first, so each rank's dispatch stays lead-descending.
 """
 import numpy as np
 import torch
@@ -65,6 +71,19 @@ class HipWorker:
 
     def reduce(self, fst, snd, cnt, n):
         self.ov.dist_reduce(fst.data_ptr(), snd.data_ptr(), cnt.data_ptr(), n)
+
+    # lead-range passes (sa_dist_buckets / _plan / _count_pass / _reduce_pass)
+    def buckets(self, recv_recs, recv_counts):
+        return self.ov.dist_buckets(recv_recs.data_ptr(), recv_counts)
+
+    def plan(self, budget):
+        return self.ov.dist_plan(budget)
+
+    def count_pass(self, p, npass):
+        return self.ov.dist_count_pass(p, npass)
+
+    def reduce_pass(self, fst, snd, cnt, n, p, npass):
+        self.ov.dist_reduce_pass(fst.data_ptr(), snd.data_ptr(), cnt.data_ptr(), n, p, npass)
 
     def code_words(self):
         return self.ov.dist_codes()
@@ -134,7 +153,11 @@ class ShardedOverlapper:
         recv.copy_(r_h)
 
     # -- one build step ---------------------------------------------------------
-    def build(self):
+    def build(self, budget=None):
+        """One step; with `budget` (partial entries per rank and pass) the count runs
+        in lead-range passes: buckets once, every rank plans its passes, the ranks
+        take the largest pass count, then per pass (npass - 1 down to 0) count ->
+        exchange 2 -> reduce, each appending its leads' dispatch."""
         w = self.w
         n = w.local_kmers()
         sk = self._buf("sk", n, torch.int64)
@@ -144,7 +167,19 @@ class ShardedOverlapper:
         rk = self._buf("rk", nr, torch.int64)
         self._a2a(rk, sk, rcounts, counts)
         self._ready()
-        pcounts = w.count(rk, rcounts)
+        if budget is None:
+            self._exchange2(w.count(rk, rcounts), w.reduce)
+            self.npass = 1
+            return
+        self.bound = w.buckets(rk, rcounts)
+        mine = w.plan(budget)
+        self.npass = npass = int(self._a2a_counts([mine] * self.P).max())  # every rank's plan: the max
+        for p in range(npass - 1, -1, -1):
+            self._exchange2(w.count_pass(p, npass),
+                            lambda qf, qs, qc, nq, p=p: w.reduce_pass(qf, qs, qc, nq, p, npass))
+
+    def _exchange2(self, pcounts, reduce):
+        w = self.w
         npart = int(np.sum(pcounts))
         pf = self._buf("pf", npart, torch.int32)
         ps = self._buf("ps", npart, torch.int32)
@@ -159,7 +194,7 @@ class ShardedOverlapper:
         self._a2a(qs, ps, rp, pcounts)
         self._a2a(qc, pc, rp, pcounts)
         self._ready()
-        w.reduce(qf, qs, qc, nq)
+        reduce(qf, qs, qc, nq)
 
     # -- reads for alignment: all-gather of the packed words ---------------------
     def gather_reads(self):

@@ -344,7 +344,7 @@ def test_bench_scale_properties():
     assert (np.diff(d1[1])[same] > 0).all()
 
 
-def _hip_rank_main(rank, P, port, reads, starts, st, outdir):
+def _hip_rank_main(rank, P, port, reads, starts, st, outdir, budget=None):
     import torch
     import torch.distributed as dist
 
@@ -359,26 +359,30 @@ def _hip_rank_main(rank, P, port, reads, starts, st, outdir):
         ov = sao_.Overlapper(id_mode=sao_.SA_IDS_WIDE, **st)
         ov.add_reads(reads[starts[rank]:starts[rank + 1]])
         so = ShardedOverlapper(HipWorker(ov), rank, P, starts, [len(r) for r in reads], "cuda:0")
-        so.build()
-        so.build()  # buffers reused
+        so.build(budget)
+        so.build(budget)  # buffers reused
         lead, trail, count = ov.dispatch()
         so.gather_reads()
         ov.align()
         s = ov.stats()
         np.savez(os.path.join(outdir, "h%d.npz" % rank), lead=lead, trail=trail, count=count, al=ov.alignments(),
-                 ovl=np.frombuffer(ov.ovl(), dtype=np.uint8), rp=np.int64(s["role_pairs"]))
+                 ovl=np.frombuffer(ov.ovl(), dtype=np.uint8), rp=np.int64(s["role_pairs"]),
+                 npass=np.int64(so.npass))
         ov.close()
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("P,repeat", [(2, False), (4, False), (2, True)])
-def test_sharded_hip_matches_single_gpu(P, repeat, tmp_path):
+@pytest.mark.parametrize("P,repeat,budget", [(2, False, None), (4, False, None), (2, True, None),
+                                             (4, False, 40000), (2, True, 40000)])
+def test_sharded_hip_matches_single_gpu(P, repeat, budget, tmp_path):
     """P processes share the GPU (gloo, host-staged exchanges) and run the
     sharded stage on the HIP path: the ranks' dispatch, alignments and .ovl in
     descending rank order equal the single-context wide-id run exactly.  The
     repeat case (a 15-mer in 2,400 reads) overflows the multi-read blocks'
-    tables, so those reads are recounted one per block."""
+    tables, so those reads are recounted one per block.  With a budget the
+    count runs in lead-range passes through the per-rank C ABI
+    (sa_dist_buckets / _plan / _count_pass / _reduce_pass)."""
     import socket
 
     import torch.multiprocessing as mp
@@ -396,7 +400,7 @@ def test_sharded_hip_matches_single_gpu(P, repeat, tmp_path):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    mp.spawn(_hip_rank_main, args=(P, port, reads, cut, st, str(tmp_path)), nprocs=P)
+    mp.spawn(_hip_rank_main, args=(P, port, reads, cut, st, str(tmp_path), budget), nprocs=P)
     res = [np.load(os.path.join(str(tmp_path), "h%d.npz" % r)) for r in range(P)]
     order = list(range(P - 1, -1, -1))
     ref = gpu_run(reads=reads, wide=True, keep_pairs=False, **st)
@@ -408,6 +412,8 @@ def test_sharded_hip_matches_single_gpu(P, repeat, tmp_path):
     np.testing.assert_array_equal(np.concatenate([res[r]["al"] for r in order]), ref.alignments())
     assert b"".join(res[r]["ovl"].tobytes() for r in order) == ref.ovl()
     assert sum(int(x["rp"]) for x in res) == ref.stats()["role_pairs"]
+    npass = {int(x["npass"]) for x in res}
+    assert len(npass) == 1 and (npass.pop() > 1) == (budget is not None)
 
 
 @pytest.mark.parametrize("mixed,k", [((100, 1000), 15), ((600, 1500), 14)])

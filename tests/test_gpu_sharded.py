@@ -69,6 +69,48 @@ def test_virtual_shards_match_single_gpu(P, repeat):
     assert got.exchanged_bytes() > 0
 
 
+@pytest.mark.parametrize("P,repeat,lean", [(4, False, False), (8, False, True), (4, "big", True)])
+def test_virtual_shards_lead_range_passes(P, repeat, lean):
+    """A 1 MiB partial budget (87k entries per shard and pass; the shards' bound
+    is several times that) makes the sharded count run in lead-range passes:
+    buckets built once, then per pass every shard counts the partials of 1/npass
+    of every owner's leads, exchange 2 and the reduce append that slice of the
+    dispatch.  Output = the single device's, bit for bit (dispatch, alignments,
+    .ovl, stats), with and without SA_OPT_LEAN_MEMORY (scratch freed between
+    stages), twice on one context."""
+    reads, st = workload(110 + P, repeat)
+    ref = run(reads, **st)
+    got = run(reads, shards=P, build_twice=True, pass_budget_mb=1, lean_memory=lean, **st)
+    info = got.shard_info()
+    assert info["npass"] > 2 and info["bound"] > 3 * 87381, info
+    assert info["partials"] >= ref.stats()["pairs"]  # every distinct pair met on >= 1 shard
+    assert_same(got, ref)
+
+
+def test_first_pass_modes_with_big_partition(oracle_mod):
+    """One device, a 15-mer in 5,000 reads (a partition past 4,096 records: the
+    global bucket path, bucket_stage phase 2): the pair counter's first pass run
+    (SA_OPT_FIRST_PASS = 1), skipped (2) and probed (0) give the oracle's
+    dispatch.  The skip mode must wait for the global path like the first pass
+    does (it used to count from records not yet written)."""
+    reads, st = workload(96, "big")
+    r = oracle_mod.Run(reads=reads, settings=oracle_mod.default_settings(
+        kmer_size=st["kmer_size"], min_collisions=st["min_collisions"]), wide=True, skip_align=True)
+    outs = []
+    for mode in (1, 2, 0):
+        ov = sao.Overlapper(first_pass=mode, **st)
+        ov.add_reads(reads)
+        ov.build()
+        lead, trail, _ = ov.dispatch()
+        np.testing.assert_array_equal(lead, r.lead)
+        np.testing.assert_array_equal(trail, r.trail)
+        outs.append(ov.stats())
+        ov.close()
+    for s in outs[1:]:
+        for k in ("kmers", "buckets", "role_pairs", "pairs", "dispatched"):
+            assert s[k] == outs[0][k], k
+
+
 def test_virtual_shards_device_only_path():
     """sa_device_build / sa_device_align on a sharded context, results fetched after."""
     reads, st = workload(97)
@@ -135,6 +177,20 @@ def test_rank_mode_one_rank_rccl(tmp_path):
     path2 = str(tmp_path / "r2.ovl")
     ov.write_ovl(path2)
     assert open(path2, "rb").read() == ref.ovl()
+
+
+def test_rank_mode_lead_range_passes():
+    """One-rank RCCL context in lead-range passes: the pass count is agreed over
+    RCCL (every rank's plan, the max) and every pass's partials go through the
+    RCCL exchange to self."""
+    reads, st = workload(105)
+    ref = run(reads, **st)
+    ov = sao.Overlapper(rank=0, nranks=1, rccl_id=sao.rccl_unique_id(), pass_budget_mb=1, **st)
+    ov.add_reads(reads)
+    ov.build()
+    ov.align()
+    assert ov.shard_info()["npass"] > 2
+    assert_same(ov, ref)
 
 
 @pytest.mark.parametrize("shards", [1, 4])
