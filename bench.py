@@ -62,38 +62,54 @@ def synth_lengths(n_reads, read_len, min_len, seed, shard=0):
     return (min_len + (z % np.uint64(read_len - min_len + 1))).astype(np.int64)
 
 
-def synth_workload(n_reads, read_len, genome_len, gc, seed, shard=0, min_len=None):
-    """Genome: base i from splitmix64(seed) (GC with probability gc); reads start
-    uniformly in [0, G-L] (splitmix64((seed ^ 0xABCDEF) + 7919 * shard): shard
-    r of a multi-GPU run samples its own reads of the same genome), forward
-    strand, error-free; lengths from synth_lengths."""
-    lens = synth_lengths(n_reads, read_len, min_len, seed, shard)
+def synth_genome(genome_len, gc, seed):
+    """Base i from splitmix64(seed) output i + 1: G/C with probability gc (then the
+    low bit picks G or C), else T/A (oracle.synth_genome is the same in C)."""
     with np.errstate(over="ignore"):
         z = splitmix64(seed, genome_len)
         u = (z >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
         bit = (z & np.uint64(1)).astype(np.uint8)
-        genome = np.where(u < gc, np.where(bit == 1, ord("G"), ord("C")),
-                          np.where(bit == 1, ord("T"), ord("A"))).astype(np.uint8)
+        return np.where(u < gc, np.where(bit == 1, ord("G"), ord("C")),
+                        np.where(bit == 1, ord("T"), ord("A"))).astype(np.uint8)
+
+
+def synth_layout(n_reads, read_len, genome_len, seed, shard=0, min_len=None):
+    """Read starts (uniform in [0, G - L], splitmix64((seed ^ 0xABCDEF) + 7919 *
+    shard)) and lengths (synth_lengths)."""
+    lens = synth_lengths(n_reads, read_len, min_len, seed, shard)
+    with np.errstate(over="ignore"):
         rs = (seed ^ 0xABCDEF) + 7919 * shard
         starts = (splitmix64(rs, n_reads) % (np.uint64(genome_len + 1) - lens.astype(np.uint64))).astype(np.int64)
+    return starts, lens
+
+
+def synth_workload(n_reads, read_len, genome_len, gc, seed, shard=0, min_len=None, genome=None):
+    """Genome: synth_genome(seed); reads start uniformly in [0, G-L]
+    (splitmix64((seed ^ 0xABCDEF) + 7919 * shard): shard r of a multi-GPU run
+    samples its own reads of the same genome), forward strand, error-free;
+    lengths from synth_lengths.  Returns (bases, offsets)."""
+    if genome is None:
+        genome = synth_genome(genome_len, gc, seed)
+    starts, lens = synth_layout(n_reads, read_len, genome_len, seed, shard, min_len)
     if os.environ.get("SA_BENCH_SORTED_READS") == "1" and lens.min() == lens.max():
         # (experiment only, never the metric's workload: each shard's reads in genome order,
         # i.e. read ids already in locality order -- DESIGN.md 8, item 1)
         starts = np.sort(starts)
     offsets = np.zeros(n_reads + 1, dtype=np.uint64)
     offsets[1:] = np.cumsum(lens)
-    if lens.min() == lens.max():
-        idx = starts[:, None] + np.arange(read_len, dtype=np.int64)[None, :]
-        return genome[idx].reshape(-1), offsets
     # each read is the first len bases of a read_len window at its start (the
     # genome padded so every window exists); chunks of reads bound host memory
     win = np.lib.stride_tricks.sliding_window_view(np.concatenate([genome, np.zeros(read_len, np.uint8)]),
                                                    read_len)
-    keep = np.arange(read_len, dtype=np.int64)[None, :]
     out = np.empty(int(offsets[-1]), dtype=np.uint8)
+    uniform = lens.min() == lens.max()
+    keep = np.arange(read_len, dtype=np.int64)[None, :]
     for r0 in range(0, n_reads, 1 << 19):
         r1 = min(n_reads, r0 + (1 << 19))
-        out[int(offsets[r0]):int(offsets[r1])] = win[starts[r0:r1]][keep < lens[r0:r1, None]]
+        if uniform:
+            out[int(offsets[r0]):int(offsets[r1])] = win[starts[r0:r1]][:, :read_len].reshape(-1)
+        else:
+            out[int(offsets[r0]):int(offsets[r1])] = win[starts[r0:r1]][keep < lens[r0:r1, None]]
     return out, offsets
 
 

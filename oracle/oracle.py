@@ -76,6 +76,10 @@ def lib():
         L.orc_max_threads.restype = C.c_int
         L.orc_lead_rows.argtypes = [C.c_char_p, P(C.c_uint64), C.c_uint32, P(Settings), P(C.c_int32), C.c_size_t,
                                     C.c_int, P(C.c_uint64), P(P(C.c_int32)), P(P(C.c_int32))]
+        L.orc_lead_stats.argtypes = [C.c_char_p, P(C.c_uint64), P(C.c_int32), C.c_uint32, P(Settings), P(C.c_int32),
+                                     C.c_size_t, C.c_int, C.c_int, P(C.c_uint64)]
+        L.orc_synth_genome.argtypes = [C.c_uint64, C.c_uint64, C.c_double, C.c_void_p, C.c_int]
+        L.orc_synth_genome.restype = None
         L.orc_free.argtypes = [C.c_void_p]
         L.orc_free.restype = None
         _lib = L
@@ -229,6 +233,32 @@ def lead_rows(bases, offsets, leads, settings=None, threads=0):
     lib().orc_free(C.cast(sp, C.c_void_p))
     lib().orc_free(C.cast(cp, C.c_void_p))
     return ro.astype(np.int64), snd, cnt
+
+
+def lead_stats(genome, starts, lens, leads, settings=None, threads=0, log_ranks=0):
+    """Per sampled lead (orc_lead_stats), over reads genome[starts[r]:starts[r] +
+    lens[r]]: an (n_leads, 4) int64 array of distinct partners, role pairs with the
+    lead as fst, partials over 2^log_ranks hash-range owners, dispatched partners."""
+    s = settings or default_settings()
+    st = np.ascontiguousarray(starts, dtype=np.uint64)
+    ln = np.ascontiguousarray(lens, dtype=np.int32)
+    ld = np.ascontiguousarray(leads, dtype=np.int32)
+    out = np.zeros((len(ld), 4), dtype=np.uint64)
+    P = C.POINTER
+    rc = lib().orc_lead_stats(genome, st.ctypes.data_as(P(C.c_uint64)), ln.ctypes.data_as(P(C.c_int32)), len(st),
+                              C.byref(s), ld.ctypes.data_as(P(C.c_int32)), len(ld), threads, log_ranks,
+                              out.ctypes.data_as(P(C.c_uint64)))
+    if rc:
+        raise OracleError(rc)
+    return out.astype(np.int64)
+
+
+def synth_genome(seed, n, gc=0.5, threads=0):
+    """bench.synth_workload's genome as bytes (orc_synth_genome: one C pass,
+    not numpy's temporaries -- configs[4]'s 1.375 Gbp)."""
+    buf = C.create_string_buffer(n)
+    lib().orc_synth_genome(seed, n, gc, buf, threads)
+    return buf.raw[:n]
 
 
 def max_threads():

@@ -1178,11 +1178,33 @@ static void read_hashes(const char *sq, int64_t L, int k, uint32_t *out) {
     }
 }
 
-int orc_lead_rows(const char *bases, const uint64_t *offsets, uint32_t n, const orc_settings *s,
-                  const int32_t *leads, size_t n_leads, int threads, uint64_t *row_off, int32_t **snd_out,
-                  int32_t **cnt_out) {
-    *snd_out = NULL;
-    *cnt_out = NULL;
+/* reads as (base + start[r], len[r]) -- reads cut from one genome, the projection's
+ * configs[3] / [4] sets without materialising them -- or back to back (off) */
+typedef struct { const char *base; const uint64_t *off; const uint64_t *start; const int32_t *len; } rd_src;
+static inline const char *rd_seq(const rd_src *R, uint32_t r) { return R->base + (R->start ? R->start[r] : R->off[r]); }
+static inline int64_t rd_len(const rd_src *R, uint32_t r) {
+    return R->start ? (int64_t)R->len[r] : (int64_t)(R->off[r + 1] - R->off[r]);
+}
+/* the sharded path's owner rank of a k-mer: the top log_ranks bits of mix32(seqHash)
+ * (sa_internal.h mix32, the device's record key) */
+static inline uint32_t owner_of_hash(uint32_t h, int log_ranks) {
+    if (log_ranks <= 0) return 0;
+    h ^= h >> 16; h *= 0x7feb352du;
+    h ^= h >> 15; h *= 0x846ca68bu;
+    h ^= h >> 16;
+    return h >> (32 - log_ranks);
+}
+
+/* rows (snd_out / cnt_out non-null): the PairData rows of the sampled leads;
+ * stats (st non-null, 4 per lead): distinct partners, role pairs with fst = the
+ * lead, partials = distinct (partner, owner rank) of those role pairs when the
+ * buckets are owned by 2^log_ranks ranks, dispatched partners ([min, max]) */
+static int lead_scan(const rd_src *R, uint32_t n, const orc_settings *s, const int32_t *leads, size_t n_leads,
+                     int threads, uint64_t *row_off, int32_t **snd_out, int32_t **cnt_out, int log_ranks,
+                     uint64_t *st) {
+    if (snd_out) *snd_out = NULL;
+    if (cnt_out) *cnt_out = NULL;
+    if (log_ranks > 6) return ORC_E_INPUT;  /* owner masks are 64 bits */
     const int nt = threads > 0 ? threads : orc_max_threads();
     const int k = s->kmer_size;
     const int w = k < 16 ? k : 16;
@@ -1195,15 +1217,15 @@ int orc_lead_rows(const char *bases, const uint64_t *offsets, uint32_t n, const 
     uint32_t *rank = (uint32_t *)malloc((nwords + 1) * sizeof(uint32_t));
     int64_t maxL = 0;
     for (uint32_t r = 0; r < n; r++)
-        if ((int64_t)(offsets[r + 1] - offsets[r]) > maxL) maxL = (int64_t)(offsets[r + 1] - offsets[r]);
+        if (rd_len(R, r) > maxL) maxL = rd_len(R, r);
     if (!bits || !rank) { free(bits); free(rank); return ORC_E_NOMEM; }
     /* pass 1: the sampled leads' hashes */
     {
         uint32_t *hs = (uint32_t *)malloc(((size_t)maxL + 1) * sizeof(uint32_t));
         for (size_t i = 0; i < n_leads && hs; i++) {
             const uint32_t r = (uint32_t)leads[i] - 1u;
-            const int64_t L = (int64_t)(offsets[r + 1] - offsets[r]);
-            read_hashes(bases + offsets[r], L, k, hs);
+            const int64_t L = rd_len(R, r);
+            read_hashes(rd_seq(R, r), L, k, hs);
             for (int64_t p = 0; p + k <= L; p++) bits[hs[p] >> 6] |= 1ull << (hs[p] & 63);
         }
         if (!hs) { free(bits); free(rank); return ORC_E_NOMEM; }
@@ -1234,9 +1256,9 @@ int orc_lead_rows(const char *bases, const uint64_t *offsets, uint32_t n, const 
             uint32_t *hs = (uint32_t *)malloc(((size_t)maxL + 1) * sizeof(uint32_t));
 #pragma omp for schedule(dynamic, 1024)
             for (uint32_t r = 0; r < n; r++) {
-                const int64_t L = (int64_t)(offsets[r + 1] - offsets[r]);
+                const int64_t L = rd_len(R, r);
                 if (!hs || L < k) continue;
-                read_hashes(bases + offsets[r], L, k, hs);
+                read_hashes(rd_seq(R, r), L, k, hs);
                 for (int64_t p = 0; p + k <= L; p++) {
                     const uint32_t h = hs[p];
                     if (!IS_HIT(h)) continue;
@@ -1264,27 +1286,30 @@ int orc_lead_rows(const char *bases, const uint64_t *offsets, uint32_t n, const 
 #pragma omp parallel num_threads(nt)
         {
             int32_t *acc = (int32_t *)calloc((size_t)n + 1, sizeof(int32_t));
+            uint64_t *om = st ? (uint64_t *)calloc((size_t)n + 1, sizeof(uint64_t)) : NULL;
             uint32_t *hs = (uint32_t *)malloc(((size_t)maxL + 1) * sizeof(uint32_t));
             ivec touched = {0};
-            int lrc = (!acc || !hs) ? ORC_E_NOMEM : ORC_OK;
+            int lrc = (!acc || !hs || (st && !om)) ? ORC_E_NOMEM : ORC_OK;
 #pragma omp for schedule(dynamic, 1)
             for (size_t li = 0; li < n_leads; li++) {
                 if (lrc) continue;
                 const uint32_t r = (uint32_t)leads[li] - 1u;
-                const int64_t L = (int64_t)(offsets[r + 1] - offsets[r]);
+                const int64_t L = rd_len(R, r);
                 const float dr = (float)(L - k);
-                read_hashes(bases + offsets[r], L, k, hs);
+                read_hashes(rd_seq(R, r), L, k, hs);
                 touched.n = 0;
+                uint64_t rp_lead = 0;
                 for (int64_t p = 0; p + k <= L; p++) {
                     const float lo = (float)p / dr;
                     const int o_st = lo <= head, o_md = midLead <= lo && lo <= midTail, o_en = tail <= lo;
                     const int o_ed = o_st + o_en;
                     if (!o_ed && !o_md) continue;
                     const uint32_t b = HIT_RANK(hs[p]);
+                    const uint64_t obit = st ? 1ull << owner_of_hash(hs[p], log_ranks) : 0ull;
                     for (uint64_t x = bstart[b]; x < bstart[b + 1]; x++) {
                         const uint32_t q = occ[2 * x];
                         if (q == r) continue;
-                        const float le = (float)occ[2 * x + 1] / (float)((int64_t)(offsets[q + 1] - offsets[q]) - k);
+                        const float le = (float)occ[2 * x + 1] / (float)(rd_len(R, q) - k);
                         const int e_md = midLead <= le && le <= midTail;
                         const int e_ed = (le <= head) + (tail <= le);
                         int add = 0;
@@ -1293,7 +1318,24 @@ int orc_lead_rows(const char *bases, const uint64_t *offsets, uint32_t n, const 
                         if (!add) continue;
                         if (acc[q] == 0 && iv_push(&touched, (int32_t)q)) { lrc = ORC_E_NOMEM; break; }
                         acc[q] += add;
+                        rp_lead += (uint64_t)add;
+                        if (st) om[q] |= obit;
                     }
+                }
+                if (st) {  /* per-lead statistics instead of rows */
+                    uint64_t parts = 0, nd = 0;
+                    for (size_t z = 0; z < touched.n; z++) {
+                        const int32_t q = touched.v[z];
+                        parts += (uint64_t)__builtin_popcountll(om[q]);
+                        nd += s->min_collisions <= acc[q] && acc[q] <= s->max_collisions;
+                        acc[q] = 0;
+                        om[q] = 0;
+                    }
+                    st[4 * li] = touched.n;
+                    st[4 * li + 1] = rp_lead;
+                    st[4 * li + 2] = parts;
+                    st[4 * li + 3] = nd;
+                    continue;
                 }
                 int32_t *sv = (int32_t *)malloc((touched.n + 1) * sizeof(int32_t));
                 int32_t *cv = (int32_t *)malloc((touched.n + 1) * sizeof(int32_t));
@@ -1304,14 +1346,14 @@ int orc_lead_rows(const char *bases, const uint64_t *offsets, uint32_t n, const 
                 for (size_t z = 0; z < touched.n; z++) { cv[z] = acc[sv[z]]; acc[sv[z]] = 0; sv[z] += 1; }
                 rs[li] = sv; rcn[li] = cv; rn[li] = touched.n;
             }
-            free(acc); free(hs); free(touched.v);
+            free(acc); free(om); free(hs); free(touched.v);
             if (lrc) {
 #pragma omp critical
                 rc = lrc;
             }
         }
         free(occ);
-        if (!rc) {
+        if (!rc && !st) {
             row_off[0] = 0;
             for (size_t li = 0; li < n_leads; li++) row_off[li + 1] = row_off[li] + rn[li];
             *snd_out = (int32_t *)malloc((row_off[n_leads] + 1) * sizeof(int32_t));
@@ -1328,8 +1370,36 @@ int orc_lead_rows(const char *bases, const uint64_t *offsets, uint32_t n, const 
 #undef HIT_RANK
 #undef IS_HIT
     free(bits); free(rank); free(bstart);
-    if (rc) { free(*snd_out); free(*cnt_out); *snd_out = *cnt_out = NULL; }
+    if (rc && snd_out) { free(*snd_out); free(*cnt_out); *snd_out = *cnt_out = NULL; }
     return rc;
+}
+
+int orc_lead_rows(const char *bases, const uint64_t *offsets, uint32_t n, const orc_settings *s,
+                  const int32_t *leads, size_t n_leads, int threads, uint64_t *row_off, int32_t **snd_out,
+                  int32_t **cnt_out) {
+    const rd_src R = {bases, offsets, NULL, NULL};
+    return lead_scan(&R, n, s, leads, n_leads, threads, row_off, snd_out, cnt_out, 0, NULL);
+}
+
+int orc_lead_stats(const char *genome, const uint64_t *starts, const int32_t *lens, uint32_t n, const orc_settings *s,
+                   const int32_t *leads, size_t n_leads, int threads, int log_ranks, uint64_t *stats) {
+    const rd_src R = {genome, NULL, starts, lens};
+    return lead_scan(&R, n, s, leads, n_leads, threads, NULL, NULL, NULL, log_ranks, stats);
+}
+
+/* synth genome base i (bench.synth_workload): z = splitmix64 output i + 1 of `seed`;
+ * u = (z >> 11) * 2^-53 < gc ? (z & 1 ? 'G' : 'C') : (z & 1 ? 'T' : 'A') */
+void orc_synth_genome(uint64_t seed, uint64_t n, double gc, char *out, int threads) {
+    const int nt = threads > 0 ? threads : orc_max_threads();
+#pragma omp parallel for num_threads(nt) schedule(static)
+    for (int64_t i = 0; i < (int64_t)n; i++) {
+        uint64_t z = seed + (uint64_t)(i + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        const double u = (double)(z >> 11) * (1.0 / 9007199254740992.0);
+        out[i] = u < gc ? ((z & 1) ? 'G' : 'C') : ((z & 1) ? 'T' : 'A');
+    }
 }
 
 void orc_free(void *p) { free(p); }

@@ -95,6 +95,17 @@ int orc_run_wide_mt(orc_ctx *c, const orc_settings *s, int threads, uint64_t *ro
 int orc_lead_rows(const char *bases, const uint64_t *offsets, uint32_t n_reads, const orc_settings *s,
                   const int32_t *leads, size_t n_leads, int threads, uint64_t *row_off, int32_t **snd_out,
                   int32_t **cnt_out);
+/* Projection statistics of the sampled leads over reads cut from one genome (read r =
+ * genome[starts[r] .. starts[r] + lens[r])): per lead 4 values in stats[4 i ..] --
+ * distinct partners, role pairs with fst = the lead, partials (distinct (partner,
+ * owner rank) over 2^log_ranks hash-range owners, log_ranks <= 6: what the sharded
+ * count of that lead writes in all) and dispatched partners.  Same semantics as
+ * orc_lead_rows. */
+int orc_lead_stats(const char *genome, const uint64_t *starts, const int32_t *lens, uint32_t n_reads,
+                   const orc_settings *s, const int32_t *leads, size_t n_leads, int threads, int log_ranks,
+                   uint64_t *stats);
+/* bench.synth_workload's genome (splitmix64 `seed`, GC fraction gc) into out[n] */
+void orc_synth_genome(uint64_t seed, uint64_t n, double gc, char *out, int threads);
 void orc_free(void *p);
 
 /* Results of orc_run (arrays owned by ctx, valid until destroy/next run). */

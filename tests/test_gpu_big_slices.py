@@ -264,3 +264,134 @@ def test_dense_first_pass_modes_match_sampled_oracle(oracle_mod):
     print("dense k=10: %d pairs, %d dispatched; sampled leads %d rows (max %d partners)"
           % (st["pairs"], st["dispatched"], len(snd), int(np.diff(ro).max())))
     assert int(np.diff(ro).max()) > 24576  # some sampled lead is past one big table
+
+
+# ---------------------------------------------------------------------------
+# round 6: the 8-GPU configs at their REAL density
+# ---------------------------------------------------------------------------
+def sampled_rows_check(oracle_mod, bases, o, k, lead, trail, count, leads):
+    """The dispatch rows of the sampled leads equal the oracle's PairData rows of
+    those leads filtered by [7, 222]; the whole dispatch is lead-descending,
+    trail-ascending.  Returns (PairData rows, dispatched rows) of the sample."""
+    dl = np.diff(lead.astype(np.int64))
+    assert (dl <= 0).all()
+    assert (np.diff(trail.astype(np.int64))[dl == 0] > 0).all()
+    s = oracle_mod.default_settings(kmer_size=k)
+    ro, snd, cnt = oracle_mod.lead_rows(bases, o, leads, settings=s, threads=0)
+    keep = (cnt >= s.min_collisions) & (cnt <= s.max_collisions)
+    neg = -lead.astype(np.int64)
+    lo = np.searchsorted(neg, -leads.astype(np.int64), "left")
+    hi = np.searchsorted(neg, -leads.astype(np.int64), "right")
+    sel = np.concatenate([np.arange(a, b) for a, b in zip(lo, hi)])
+    np.testing.assert_array_equal(lead[sel], np.repeat(leads, np.diff(ro))[keep])
+    np.testing.assert_array_equal(trail[sel], snd[keep])
+    np.testing.assert_array_equal(count[sel], cnt[keep])
+    return len(snd), sel
+
+
+def test_configs3_real_density_eight_shards(oracle_mod):
+    """configs[3]'s actual read set on one MI355X: 10M x 500 bp from a 250 Mbp
+    genome (seed 4, 20x; 4.86e9 k-mers), k = 15, over 8 virtual shards -- each
+    shard receives a configs[3] rank's 607.5M records at the config's own k-mer
+    density (~1.3 random genomic occurrences per 15-mer code x 20x coverage).
+    The shards run one after another with SA_OPT_LEAN_MEMORY (8 shards' bucket
+    structures stay resident; sort and exchange scratch is freed between stages)
+    and the count runs in lead-range passes sized from the free memory.  Checked:
+    ~2,000 sampled leads' dispatch rows and counts against the oracle's PairData
+    rows (orc_lead_rows), the dispatch order, the k-mer total, the sampled
+    leads' alignments against orc_align_batch, and the partials the shards
+    exchanged against the oracle's projection of the same read set
+    (orc_lead_stats, tools/project_partials.py)."""
+    n, G = 10_000_000, 250_000_000
+    b, o = bench.synth_workload(n, 500, G, 0.5, seed=4)
+    bases = b.tobytes()
+    del b
+    t0 = time.time()
+    ov = sao.Overlapper(shards=8, kmer_size=15, id_mode=sao.SA_IDS_WIDE, serial_shards=True, lean_memory=True,
+                        timing=True)
+    ov.add_packed(bases, o)
+    ov.device_build()
+    t_first = time.time() - t0
+    st = ov.stats()
+    info = ov.shard_info()
+    xb = ov.exchanged_bytes()
+    # a second build, timed per shard (serial shards: each stage time is one shard's)
+    ov.reset_stage_times()
+    t0 = time.time()
+    ov.device_build()
+    t_second = time.time() - t0
+    times = {s: round(ms, 3) for s, (ms, nl) in ov.stage_times().items() if nl}
+    assert ov.stats()["dispatched"] == st["dispatched"]
+    lead, trail, count = ov.dispatch()
+    assert st["kmers"] == n * 486 and len(lead) == st["dispatched"]
+    leads = sampled_leads(n, np.full(n, 500))
+    t0 = time.time()
+    rows, sel = sampled_rows_check(oracle_mod, bases, o, 15, lead, trail, count, leads)
+    t_orc = time.time() - t0
+    # the sampled leads' alignments (device) against the oracle's
+    ov.device_align()
+    al = ov.alignments()[sel]
+    s = oracle_mod.default_settings(kmer_size=15)
+    ref = oracle_mod.align_batch(bases, o, lead[sel], trail[sel], settings=s, threads=0)
+    for name in ALIGN_CMP:
+        np.testing.assert_array_equal(al[:, sao.ALIGN_FIELDS.index(name)], ref[:, oracle_mod.ALIGN_FIELDS.index(name)],
+                                      err_msg=name)
+    ov.close()
+    # the projection's estimate of the same read set's partials (sampled leads, oracle)
+    starts = bench.synth_layout(n, 500, G, 4)[0]
+    proj = oracle_mod.lead_stats(oracle_mod.synth_genome(4, G, 0.5), starts, np.full(n, 500, np.int32), leads,
+                                 settings=s, threads=0, log_ranks=3)
+    est = proj[:, 2].mean() * n
+    print("configs[3] real density, 8 shards: %d dispatched, %d passes, partials %d (projected %.4g), bound %d; "
+          "first build %.1f s, second %.1f s; per-shard stages %s; sampled %d leads / %d rows / %d dispatched; "
+          "oracle %.1f s" % (st["dispatched"], info["npass"], info["partials"], est, info["bound"], t_first, t_second,
+                             times, len(leads), rows, len(sel), t_orc))
+    assert abs(info["partials"] / est - 1) < 0.05
+    assert len(sel) > 5000 and rows > len(sel)
+    record("c3_real_density_8shards", {
+        "reads": n, "read_len": 500, "genome_bp": G, "seed": 4, "k": 15, "shards": 8, "stats": st,
+        "npass": info["npass"], "partials_total": info["partials"], "partials_per_shard": info["partials"] / 8,
+        "partial_bound_total": info["bound"], "partials_projected_by_oracle": est,
+        "exchanged_bytes_first_build": xb, "first_build_s": t_first, "second_build_s": t_second,
+        "per_shard_stage_ms_sum_over_8_serial_shards": times, "sampled_leads": int(len(leads)),
+        "sampled_pairdata_rows": rows, "sampled_dispatched_rows": int(len(sel)),
+        "note": "serial virtual shards, SA_OPT_LEAN_MEMORY, pass budget from free memory; stage times are the "
+                "sum over the 8 shards of one build (divide by 8 for one shard)"})
+
+
+def test_configs4_shape_k12_eight_shards_in_passes(oracle_mod):
+    """configs[4]'s k = 12 pass on the sharded path (SA_E_NOMEM in round 5 from
+    1M reads: every distinct partial was held at once): 1M mixed 100-1,000 bp
+    reads, 8 virtual shards, the count in lead-range passes sized from the free
+    memory.  The dispatch equals the single device's element for element, and
+    the sampled leads' rows equal the oracle's PairData rows."""
+    n, k = 1_000_000, 12
+    b, o = bench.synth_workload(n, 1000, int(n * 550 / 20.0), 0.5, seed=12, min_len=100)
+    bases = b.tobytes()
+    del b
+    one = sao.Overlapper(kmer_size=k, id_mode=sao.SA_IDS_WIDE)
+    one.add_packed(bases, o)
+    one.build()
+    ref = one.dispatch()
+    rst = one.stats()
+    one.close()
+    t0 = time.time()
+    ov = sao.Overlapper(shards=8, kmer_size=k, id_mode=sao.SA_IDS_WIDE)
+    ov.add_packed(bases, o)
+    ov.build()
+    t_sh = time.time() - t0
+    st, info = ov.stats(), ov.shard_info()
+    got = ov.dispatch()
+    ov.close()
+    for x, y in zip(got, ref):
+        np.testing.assert_array_equal(x, y)
+    for key in ("kmers", "role_pairs", "pairs", "dispatched"):
+        assert st[key] == rst[key], key
+    leads = sampled_leads(n, np.diff(o.astype(np.int64)), count=800, seed=9)
+    rows, sel = sampled_rows_check(oracle_mod, bases, o, k, *got, leads)
+    print("configs[4] shape k=12, 1M reads, 8 shards: %d passes, partials %d (bound %d), distinct %d, dispatched %d; "
+          "sharded build %.1f s; sampled %d rows / %d dispatched" % (info["npass"], info["partials"], info["bound"],
+                                                                    st["pairs"], st["dispatched"], t_sh, rows, len(sel)))
+    assert info["partials"] > st["pairs"]
+    record("c4shape_k12_1M_8shards", {"reads": n, "k": k, "shards": 8, "stats": st, "shard_info": info,
+                                      "sharded_build_s": t_sh, "sampled_rows": rows, "sampled_dispatched": int(len(sel))})

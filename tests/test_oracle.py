@@ -218,3 +218,78 @@ def test_degenerate_and_dud_cases(oracle_mod):
     # B's prefix absent from A's band -> dud
     a = oracle_mod.align_pair("ACGT" * 20, "GGGGACGTACGTACGT" * 2, settings=oracle_mod.default_settings(kmer_size=12))
     assert a["is_dud"] == 1 and a["valid"] == 0
+
+
+def _mix32(h):
+    h ^= h >> 16
+    h = (h * 0x7FEB352D) & 0xFFFFFFFF
+    h ^= h >> 15
+    h = (h * 0x846CA68B) & 0xFFFFFFFF
+    return h ^ (h >> 16)
+
+
+def test_lead_stats_match_rows_and_brute_force(oracle_mod):
+    """orc_lead_stats (the projection of configs[3] / [4]'s per-rank partials):
+    on reads cut from one genome by (start, length) it gives, per lead, the
+    number of its PairData rows, the sum of their counts (its role pairs as
+    fst), its dispatched rows -- all equal to orc_lead_rows on the same reads
+    materialised -- and its partials over 2^L hash-range owners, equal to a
+    brute-force count of distinct (partner, owner of the k-mer) over its role
+    pairs (owner = top L bits of mix32(seqHash), the device's record key)."""
+    import bench
+    G, n, k = 4000, 160, 11
+    genome = oracle_mod.synth_genome(9, G, 0.5)
+    starts, lens = bench.synth_layout(n, 120, G, 9, min_len=40)
+    reads = [genome[int(a):int(a) + int(b)].decode() for a, b in zip(starts, lens)]
+    s = oracle_mod.default_settings(kmer_size=k, min_collisions=2)
+    leads = np.arange(1, n + 1, dtype=np.int32)
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    ro, snd, cnt = oracle_mod.lead_rows("".join(reads).encode(), off, leads, settings=s, threads=2)
+    rows = np.diff(ro)
+    owner = np.repeat(np.arange(n), rows)
+
+    def seg_sum(v):
+        out = np.zeros(n, dtype=np.int64)
+        np.add.at(out, owner, v.astype(np.int64))
+        return out
+    for L in (0, 1, 3):
+        st = oracle_mod.lead_stats(genome, starts, lens, leads, settings=s, threads=2, log_ranks=L)
+        np.testing.assert_array_equal(st[:, 0], rows)
+        np.testing.assert_array_equal(st[:, 1], seg_sum(cnt))
+        np.testing.assert_array_equal(st[:, 3], seg_sum((cnt >= 2) & (cnt <= 222)))
+        if L == 0:
+            np.testing.assert_array_equal(st[:, 2], rows)
+    # brute force at L = 2 (KmerTable.scala:57-80 role pairs, keyed by the k-mer's owner)
+    f32 = np.float32
+    code = {"A": 0, "C": 1, "T": 2, "G": 3}
+    occ = {}
+    for r, rd in enumerate(reads):
+        d = len(rd) - k
+        for i in range(len(rd) - k + 1):
+            h = 0
+            for ch in rd[i:i + k]:
+                h = ((h << 2) ^ code[ch]) & 0xFFFFFFFF
+            loc = f32(i) / f32(d) if d > 0 else f32("nan")
+            occ.setdefault(h, []).append((r, loc))
+    parts = np.zeros(n, dtype=np.int64)
+    seen = set()
+    for h, lst in occ.items():
+        own = _mix32(h) >> 30
+        tag = [(r, l, l <= f32(0.4), f32(0.3) <= l <= f32(0.7), f32(0.6) <= l) for r, l in lst if not np.isnan(l)]
+        for ra, la, sa, ma, ea in tag:
+            for rb, lb, sb, mb, eb in tag:
+                if ra == rb:
+                    continue
+                if ((sa or ea) and mb and la > lb) or (ma and (sb or eb) and not lb > la):
+                    if (ra, rb, own) not in seen:
+                        seen.add((ra, rb, own))
+                        parts[ra] += 1
+    st = oracle_mod.lead_stats(genome, starts, lens, leads, settings=s, threads=2, log_ranks=2)
+    np.testing.assert_array_equal(st[:, 2], parts)
+    assert (st[:, 2] > st[:, 0]).any()
+
+
+def test_synth_genome_is_the_bench_genome(oracle_mod):
+    import bench
+    for seed, gc in ((1, 0.5), (5, 0.17)):
+        assert oracle_mod.synth_genome(seed, 200000, gc) == bench.synth_genome(200000, gc, seed).tobytes()
