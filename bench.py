@@ -113,6 +113,75 @@ def synth_workload(n_reads, read_len, genome_len, gc, seed, shard=0, min_len=Non
     return out, offsets
 
 
+def end_to_end(sao, fasta_path, k, reps=5, cli=None):
+    """calc-overlaps from host FASTA bytes to a written .ovl (SURVEY.md 8(d) timing
+    protocol; Project4.scala:56-60 -> :795-825) through the C ABI, each repetition
+    on a fresh context in this (HIP-initialised) process: median of `reps` of the
+    total and of each part -- ctx create, FASTA parse (readSeq), the build
+    (upload = read metadata + H2D, the device stages, the strict Trove replay,
+    dispatch D2H), the alignment (device, alignment D2H, .ovl formatting) and the
+    file write -- the parts from the library's own stage clocks (device stages:
+    HIP events; host stages: wall clock).  With `cli`, the sa-overlap process's
+    wall time on the same file too (process start and HIP initialisation
+    included)."""
+    import subprocess
+    import tempfile
+    runs = []
+    out = os.path.join(tempfile.gettempdir(), "sa_e2e_%d.ovl" % os.getpid())
+    ovl = b""
+    for _ in range(reps):
+        r = {}
+        t0 = time.perf_counter()
+        ov = sao.Overlapper(kmer_size=k, timing=True)
+        r["ctx_create"] = time.perf_counter() - t0
+        t1 = time.perf_counter()
+        ov.read_fasta(fasta_path)
+        r["fasta_parse"] = time.perf_counter() - t1
+        t1 = time.perf_counter()
+        ov.build()
+        r["build"] = time.perf_counter() - t1
+        t1 = time.perf_counter()
+        ov.align()
+        r["align"] = time.perf_counter() - t1
+        t1 = time.perf_counter()
+        ov.write_ovl(out)
+        r["write"] = time.perf_counter() - t1
+        r["total"] = time.perf_counter() - t0
+        st = ov.stage_times()
+        for name, (ms, n) in st.items():
+            if n:
+                r["stage_" + name] = ms / 1e3
+        stats = ov.stats()
+        ov.close()
+        runs.append(r)
+    ovl = open(out, "rb").read()
+    os.unlink(out)
+    keys = sorted({k_ for r in runs for k_ in r})
+    med = {k_: float(np.median([r.get(k_, 0.0) for r in runs])) for k_ in keys}
+    res = {"total_s": round(med["total"], 4), "reps": reps,
+           "breakdown_ms": {k_: round(v * 1e3, 3) for k_, v in med.items() if k_ != "total"},
+           "id_mode": "strict" if stats["id_mode"] == sao.SA_IDS_STRICT else "wide",
+           "dispatched": int(stats["dispatched"]), "ovl_records": int(stats["ovl_records"]), "ovl_bytes": len(ovl)}
+    if cli:
+        t0 = time.perf_counter()
+        rc = subprocess.run([cli, "-i", fasta_path, "-o", out, "-k", str(k)], capture_output=True, timeout=600)
+        res["cli_wall_s"] = round(time.perf_counter() - t0, 3)
+        res["cli_identical"] = rc.returncode == 0 and open(out, "rb").read() == ovl
+        if os.path.exists(out):
+            os.unlink(out)
+    return res, ovl
+
+
+def write_fasta(path, bases, offsets):
+    """Reads as FASTA (one line each, headers r1..rN): readSeq's input format."""
+    with open(path, "wb") as f:
+        b = memoryview(bases)
+        for i in range(len(offsets) - 1):
+            f.write(b">r%d\n" % (i + 1))
+            f.write(b[int(offsets[i]):int(offsets[i + 1])])
+            f.write(b"\n")
+
+
 DEFAULT_WORKLOAD = "n100000_L500_k15"
 
 
@@ -533,6 +602,7 @@ def main():
     # ---- CPU baselines (rank 0, N = 1): the C oracle on this box's cores ---
     cpu = None
     config0 = None
+    config2_e2e = None
     if rank == 0 and n_gpus == 1 and mode == "single" and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
@@ -600,18 +670,25 @@ def main():
         t0 = time.perf_counter()
         rc0 = oracle.Run(reads=cr, settings=oracle.default_settings(kmer_size=15))
         t_c0 = time.perf_counter() - t0
-        t0 = time.perf_counter()
-        o0 = sao.Overlapper(kmer_size=15)
-        o0.add_reads(cr)
-        o0.build()
-        o0.align()
-        g_ovl = o0.ovl()
-        t_g0 = time.perf_counter() - t0
-        o0.close()
+        import tempfile
+        cli = os.path.join(ROOT, "sequence-aligner_amd", "build", "sa-overlap")
+        fa0 = os.path.join(tempfile.gettempdir(), "sa_c_ruddii_%d.seq" % os.getpid())
+        cb = b"".join(cr)
+        write_fasta(fa0, cb, np.concatenate([[0], np.cumsum([len(x) for x in cr])]))
+        e2e0, g_ovl = end_to_end(sao, fa0, 15, reps=5, cli=cli if os.path.exists(cli) else None)
+        os.unlink(fa0)
         config0 = {"workload": "configs[0]: c_ruddii reconstructed 32,000 x 100 bp reads, k=15, strict ids, "
-                               "FASTA reads in host memory -> .ovl bytes",
-                   "cpu_port_1_thread_s": round(t_c0, 3), "gpu_end_to_end_s": round(t_g0, 4),
+                               "FASTA file -> .ovl file",
+                   "cpu_port_1_thread_s": round(t_c0, 3), "gpu_end_to_end_s": e2e0["total_s"],
+                   "gpu_end_to_end": e2e0,
                    "ovl_records": g_ovl.count(b"{OVL"), "ovl_identical": g_ovl == rc0.ovl}
+        # configs[2] end to end: the bench's 100k reads as a FASTA file -> written .ovl
+        fa2 = os.path.join(tempfile.gettempdir(), "sa_bench_%d.seq" % os.getpid())
+        write_fasta(fa2, bases, offsets)
+        e2e2, _ = end_to_end(sao, fa2, args.k, reps=5, cli=cli if os.path.exists(cli) else None)
+        os.unlink(fa2)
+        config2_e2e = dict(e2e2, workload="configs[2]: %d x %d bp reads (this bench's), k=%d, wide ids, FASTA "
+                                           "file -> .ovl file" % (args.reads, args.len, args.k))
 
     note("aligner timed")
     dhash = None
@@ -679,6 +756,7 @@ def main():
             "read_allgather_ms": round(t_gather * 1e3, 3) if t_gather is not None else None,
             "cpu_baseline": cpu,
             "config0": config0,
+            "config2_end_to_end": config2_e2e,
             "check_shards": check,
             "dispatch_hash": dhash,
         }

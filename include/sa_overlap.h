@@ -223,6 +223,13 @@ enum sa_stage {
     SA_STAGE_PACK = 0, SA_STAGE_EMIT, SA_STAGE_SORT, SA_STAGE_BUCKETS, SA_STAGE_PAIRS,
     SA_STAGE_ORDER, SA_STAGE_ALIGN,
     SA_STAGE_EXCHANGE,  /* sharded contexts: inter-shard exchanges (host wall clock) */
+    /* host wall clock of the calc-overlaps path around the device stages (any context) */
+    SA_STAGE_UPLOAD,    /* read metadata + H2D of the reads (first build after reads change) */
+    SA_STAGE_REPLAY,    /* strict ids: Trove replay of KmerData / PairData / DispatchData order,
+                           with its D2H / H2D copies; wide ids + keep_pairs: PairData on the host */
+    SA_STAGE_READBACK,  /* D2H of the dispatch (sa_build_candidates) and alignments */
+    SA_STAGE_FORMAT,    /* .ovl record text (Overlap.print, ObjectStore.scala:127-135) */
+    SA_STAGE_WRITE,     /* sa_write_ovl: the file write */
     SA_NUM_STAGES
 };
 int sa_get_stage_times(const sa_ctx *ctx, double *ms, uint64_t *launches, int n);

@@ -20,6 +20,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -101,6 +102,19 @@ struct StageScope {
             (void)hipEventRecord(b, c->stream);
             c->pending.push_back({stage, a, b});
         }
+    }
+};
+
+// host wall-clock stage (SA_STAGE_UPLOAD .. SA_STAGE_WRITE): the calc-overlaps path's
+// host work around the device stages, recorded whatever SA_OPT_TIMING says
+struct HostScope {
+    sa_ctx *c;
+    int stage;
+    std::chrono::steady_clock::time_point t0;
+    HostScope(sa_ctx *c_, int s) : c(c_), stage(s), t0(std::chrono::steady_clock::now()) {}
+    ~HostScope() {
+        c->stage_ms[stage] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        c->stage_n[stage] += 1;
     }
 };
 
@@ -319,13 +333,14 @@ EmitParams emit_params(sa_ctx *c) {
 }
 
 int ensure_prepared(sa_ctx *c) {
-    if (c->reads_dirty) {
-        int rc = prepare_reads(c);
-        if (rc) return rc;
-        c->reads_dirty = false;
-        c->uploaded = false;
-    }
-    if (!c->uploaded) {
+    if (c->reads_dirty || !c->uploaded) {
+        HostScope hs(c, SA_STAGE_UPLOAD);
+        if (c->reads_dirty) {
+            int rc = prepare_reads(c);
+            if (rc) return rc;
+            c->reads_dirty = false;
+            c->uploaded = false;
+        }
         int rc = upload_reads(c);
         if (rc) return rc;
     }
@@ -1170,6 +1185,7 @@ int device_build(sa_ctx *c, bool readback) {
         // KmerData iteration rank of every bucket: replay its Trove layout over the
         // distinct hashes in first-occurrence order (KmerTable.scala:45-50).  A
         // bucket is named by the sorted position of its head record.
+        HostScope hs(c, SA_STAGE_REPLAY);
         std::vector<uint8_t> head(n);
         std::vector<uint32_t> first(n);
         if (n) {
@@ -1181,8 +1197,6 @@ int device_build(sa_ctx *c, bool readback) {
             if (head[i]) fh.push_back({first[i], (uint32_t)i});
         std::sort(fh.begin(), fh.end());
         TroveLayout kd;
-        std::unordered_map<int32_t, uint32_t> pos_of;
-        pos_of.reserve(fh.size() * 2);
         const int k = c->set.kmer_size, mm = c->m;
         for (auto &x : fh) {
             const uint32_t g = x.first;
@@ -1197,12 +1211,11 @@ int device_build(sa_ctx *c, bool readback) {
                 h ^= ch == 'C' ? 1u : ch == 'T' ? 2u : ch == 'G' ? 3u : 0u;
             }
             (void)k;
-            kd.insert((int32_t)h);
-            pos_of[(int32_t)h] = x.second;
+            kd.insert((int32_t)h, (int32_t)x.second);  // (distinct hashes: every insert is fresh)
         }
         std::vector<uint32_t> rank(n, 0);
         uint32_t rk = 0;
-        kd.for_each([&](int32_t key) { rank[pos_of[key]] = rk++; });
+        kd.for_each_kv([&](int32_t, int32_t pos) { rank[(uint32_t)pos] = rk++; });
         if (rk >= (1u << 26)) return fail(c, SA_E_OVERFLOW, "strict ids: more than 2^26 distinct k-mers");
         if (n) HIPCHK(hipMemcpy(c->bkt_rank_dev, rank.data(), n * 4, hipMemcpyHostToDevice));
     }
@@ -1286,6 +1299,7 @@ int device_build(sa_ctx *c, bool readback) {
     if (!strict && !emit_all) {
         c->n_disp = np;
         if (readback && np) {
+            HostScope hs(c, SA_STAGE_READBACK);
             c->lead.resize(np); c->trail.resize(np); c->count.resize(np);
             HIPCHK(hipMemcpy(c->lead.data(), dlead, np * 4, hipMemcpyDeviceToHost));
             HIPCHK(hipMemcpy(c->trail.data(), dtrail, np * 4, hipMemcpyDeviceToHost));
@@ -1293,6 +1307,7 @@ int device_build(sa_ctx *c, bool readback) {
         }
     } else {
         // every distinct pair came back (strict: in first-insertion order; wide: lead desc)
+        HostScope hs(c, SA_STAGE_REPLAY);
         std::vector<int32_t> f(np), s(np), k(np);
         if (np) {
             HIPCHK(hipMemcpy(f.data(), dlead, np * 4, hipMemcpyDeviceToHost));
@@ -1300,45 +1315,48 @@ int device_build(sa_ctx *c, bool readback) {
             HIPCHK(hipMemcpy(k.data(), dcount, np * 4, hipMemcpyDeviceToHost));
         }
         if (strict) {
-            // PairData: Trove layout of keys (fst<<16)^snd inserted in first-occurrence order
+            // PairData: Trove layout of keys (fst<<16)^snd inserted in first-occurrence
+            // order, each slot carrying its pair's index (the count without a lookup)
             TroveLayout pd;
-            std::vector<std::pair<int32_t, uint32_t>> key_ix(np);
             for (uint64_t i = 0; i < np; ++i) {
                 const int32_t key = (int32_t)(((uint32_t)f[i] << 16) ^ (uint32_t)s[i]);
-                pd.insert(key);
-                key_ix[i] = {key, (uint32_t)i};
+                pd.insert(key, (int32_t)i);
             }
-            std::sort(key_ix.begin(), key_ix.end());
-            auto find = [&](int32_t key) {
-                return std::lower_bound(key_ix.begin(), key_ix.end(), std::make_pair(key, 0u))->second;
-            };
-            // calcDispatchData (KmerTable.scala:155-187) over PairData iteration order
+            // calcDispatchData (KmerTable.scala:155-187) over PairData iteration order:
+            // DispatchData's Trove layout over the leads, each lead's (trail, count)
+            // list in that order.  Decoded leads are 16-bit (key >> 16, E4): a lead's
+            // list slot is looked up in a 65,536-entry table
             TroveLayout dd;
-            std::vector<std::vector<int32_t>> lists;
-            std::unordered_map<int32_t, int32_t> list_of;  // lead -> list index
+            std::vector<std::vector<std::pair<int32_t, int32_t>>> lists;
+            std::vector<int32_t> list_of(1 << 16, -1);  // lead + 32,768 -> list index
             bool id_err = false;
-            pd.for_each([&](int32_t key) {
-                const uint32_t ix = find(key);
-                const int32_t cnt_ = k[ix];
+            pd.for_each_kv([&](int32_t key, int32_t ix) {
+                const int32_t cnt_ = k[(uint32_t)ix];
                 const int32_t a = key >> 16;
                 const int32_t b = (int32_t)((uint32_t)key << 16) >> 16;
                 if (c->keep_pairs) { c->pfst.push_back(a); c->psnd.push_back(b); c->pcnt.push_back(cnt_); }
                 if (c->set.min_collisions <= cnt_ && cnt_ <= c->set.max_collisions) {
-                    if (dd.insert(a)) { list_of[a] = (int32_t)lists.size(); lists.emplace_back(); }
-                    lists[list_of[a]].push_back(b);
+                    int32_t &li = list_of[(uint32_t)(a + 32768) & 0xFFFFu];
+                    if (li < 0) {
+                        dd.insert(a, (int32_t)lists.size());
+                        li = (int32_t)lists.size();
+                        lists.emplace_back();
+                    }
+                    lists[(size_t)li].push_back({b, cnt_});
                     if (a < 1 || a > (int32_t)nr || b < 1 || b > (int32_t)nr) id_err = true;
                 }
             });
             if (id_err)
                 return fail(c, SA_E_ID_RANGE, "strict ids: a dispatched pair decodes to an id outside 1..N "
                                               "(reference NullPointerException, KmerTable.scala:263-265)");
-            dd.for_each([&](int32_t a) {
-                const auto &vec = lists[list_of[a]];
-                for (int32_t b : vec) {
+            size_t nd_ = 0;
+            for (const auto &v : lists) nd_ += v.size();
+            c->lead.reserve(nd_); c->trail.reserve(nd_); c->count.reserve(nd_);
+            dd.for_each_kv([&](int32_t a, int32_t li) {
+                for (const auto &bc : lists[(size_t)li]) {
                     c->lead.push_back(a);
-                    c->trail.push_back(b);
-                    const int32_t key = (int32_t)(((uint32_t)a << 16) ^ (uint32_t)b);
-                    c->count.push_back(k[find(key)]);
+                    c->trail.push_back(bc.first);
+                    c->count.push_back(bc.second);
                 }
             });
         } else {
@@ -1562,23 +1580,48 @@ int device_align(sa_ctx *c, bool readback) {
 // Project4.scala:795-825; Overlap.print, ObjectStore.scala:127-135) for the
 // last alignment, once: sa_align does it at once, after sa_device_align the
 // getters / writer do it on first use (never a previous run's records)
+// decimal text of v at p (Integer.toString), returns the end
+static inline char *put_int(char *p, int32_t v) {
+    uint32_t u = v < 0 ? 0u - (uint32_t)v : (uint32_t)v;
+    if (v < 0) *p++ = '-';
+    char t[12];
+    int n = 0;
+    do { t[n++] = (char)('0' + u % 10); u /= 10; } while (u);
+    while (n) *p++ = t[--n];
+    return p;
+}
+
 int host_results(sa_ctx *c) {
     if (c->host_valid) return SA_OK;
     const uint64_t nd = c->n_disp;
-    c->alns.resize(nd);
-    if (nd) HIPCHK(hipMemcpy(c->alns.data(), c->d_aln.p, nd * sizeof(sa_alignment), hipMemcpyDeviceToHost));
+    {
+        HostScope hs(c, SA_STAGE_READBACK);
+        c->alns.resize(nd);
+        if (nd) HIPCHK(hipMemcpy(c->alns.data(), c->d_aln.p, nd * sizeof(sa_alignment), hipMemcpyDeviceToHost));
+    }
+    HostScope hs(c, SA_STAGE_FORMAT);
+    // "{OVL\nadj:N\nrds:" + lead + "," + trail + "\nscr:0\nahg:" + ahg + "\nbhg:" + bhg + "\n}" + "\n"
+    // (Overlap.print, ObjectStore.scala:127-135; Project4.scala:814-818), at most 88 bytes
     uint64_t rec = 0;
-    c->ovl.clear();
-    char buf[160];
+    for (uint64_t i = 0; i < nd; ++i) rec += (c->alns[i].flags & SA_ALN_OVL_VALID) != 0;
+    c->ovl.resize(rec * 88);
+    char *p = &c->ovl[0], *const p0 = p;
+    static const char H1[] = "{OVL\nadj:N\nrds:", H2[] = "\nscr:0\nahg:", H3[] = "\nbhg:", H4[] = "\n}\n";
     for (uint64_t i = 0; i < nd; ++i) {
         const sa_alignment &a = c->alns[i];
         if (!(a.flags & SA_ALN_OVL_VALID)) continue;
         const int ra = (a.flags & SA_ALN_DUD) ? 0 : a.lead, rb = (a.flags & SA_ALN_DUD) ? 0 : a.trail;
-        const int m = snprintf(buf, sizeof(buf), "{OVL\nadj:N\nrds:%d,%d\nscr:0\nahg:%d\nbhg:%d\n}\n", ra, rb,
-                               a.ahg, a.bhg);
-        c->ovl.append(buf, (size_t)m);
-        ++rec;
+        memcpy(p, H1, sizeof(H1) - 1); p += sizeof(H1) - 1;
+        p = put_int(p, ra);
+        *p++ = ',';
+        p = put_int(p, rb);
+        memcpy(p, H2, sizeof(H2) - 1); p += sizeof(H2) - 1;
+        p = put_int(p, a.ahg);
+        memcpy(p, H3, sizeof(H3) - 1); p += sizeof(H3) - 1;
+        p = put_int(p, a.bhg);
+        memcpy(p, H4, sizeof(H4) - 1); p += sizeof(H4) - 1;
     }
+    c->ovl.resize((size_t)(p - p0));
     c->stats.ovl_records = rec;
     c->host_valid = true;
     return SA_OK;
@@ -1882,6 +1925,7 @@ int sa_write_ovl(sa_ctx *c, const char *path) {
         const int rc = multi_sharded(c) ? multi_host_results(c) : host_results(c);
         if (rc) return rc;
     }
+    HostScope hs(c, SA_STAGE_WRITE);
     FILE *f = path ? fopen(path, "wb") : stdout;  // the file is deleted and recreated (Project4.scala:797-805)
     if (!f) return fail(c, SA_E_INPUT, std::string("cannot write ") + path);
     const size_t w = fwrite(text->data(), 1, text->size(), f);

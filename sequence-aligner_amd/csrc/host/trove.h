@@ -30,11 +30,14 @@ public:
         compute_max_size();
     }
 
-    // put(key, _) for a key not yet present; returns false if it was present.
-    bool insert(int32_t key) {
+    // put(key, val) for a key not yet present; returns false if it was present
+    // (the value is the caller's payload -- e.g. the key's index in its arrays --
+    // and moves with the key through every rehash, so iteration needs no lookup)
+    bool insert(int32_t key, int32_t val = 0) {
         int32_t slot;
         bool fresh = probe_insert(key, &slot);
         if (!fresh) return false;
+        vals_[slot] = val;
         if (consumed_free_) --free_;
         if (++size_ > max_size_ || free_ == 0) {
             rehash(size_ > max_size_ ? next_prime(cap_ << 1) : cap_);
@@ -52,6 +55,12 @@ public:
         for (int32_t i = cap_; i-- > 0;)
             if (full_[i]) f(keys_[i]);
     }
+    // (key, value) in the same order
+    template <class F>
+    void for_each_kv(F f) const {
+        for (int32_t i = cap_; i-- > 0;)
+            if (full_[i]) f(keys_[i], vals_[i]);
+    }
 
     static int32_t next_prime(int32_t desired) {
         int lo = 0, hi = TROVE_NPRIMES - 1;
@@ -68,6 +77,7 @@ private:
     void alloc(int32_t cap) {
         cap_ = cap;
         keys_.assign((size_t)cap, 0);
+        vals_.assign((size_t)cap, 0);
         full_.assign((size_t)cap, 0);
     }
     void compute_max_size() {
@@ -99,9 +109,10 @@ private:
         }
     }
     void rehash(int32_t newcap) {
-        std::vector<int32_t> ok;
+        std::vector<int32_t> ok, ov;
         std::vector<uint8_t> of;
         ok.swap(keys_);
+        ov.swap(vals_);
         of.swap(full_);
         const int32_t oldcap = cap_;
         alloc(newcap);
@@ -109,11 +120,12 @@ private:
             if (of[i]) {
                 int32_t s;
                 probe_insert(ok[i], &s);
+                vals_[s] = ov[i];
             }
         }
     }
 
-    std::vector<int32_t> keys_;
+    std::vector<int32_t> keys_, vals_;
     std::vector<uint8_t> full_;
     int32_t cap_ = 0, size_ = 0, free_ = 0, max_size_ = 0;
     bool consumed_free_ = false;

@@ -28,7 +28,8 @@ SA_OPT_PASS_BUDGET_MB, SA_OPT_LEAN_MEMORY = 9, 10   # sharded contexts: lead-ran
 SA_ALIGNER_LINEAR, SA_ALIGNER_QUADRATIC = 0, 1   # --linear-align / --quadratic-align
 SA_STATS_PER_READ_REGIONS, SA_STATS_RECOUNTED = 1, 2    # sa_stats.flags bits of the last build
 ALIGN_AUTO, ALIGN_GROUP, ALIGN_LANE, ALIGN_LANE_SUMMARY = 0, 1, 2, 3
-STAGES = ("pack", "emit", "sort", "buckets", "pairs", "order", "align", "exchange")
+STAGES = ("pack", "emit", "sort", "buckets", "pairs", "order", "align", "exchange",
+          "upload", "replay", "readback", "format", "write")  # (the last five: host wall clock)
 ERRORS = {-1: "SA_E_ARG", -2: "SA_E_INPUT", -3: "SA_E_NON_ACGT", -4: "SA_E_ID_RANGE", -5: "SA_E_SHORT_READ",
           -6: "SA_E_DEGENERATE", -7: "SA_E_HIP", -8: "SA_E_NOMEM", -9: "SA_E_RCCL", -10: "SA_E_STATE",
           -11: "SA_E_OVERFLOW"}
