@@ -257,9 +257,8 @@ bool is_pow2(int x) { return x > 0 && (x & (x - 1)) == 0; }
 // Partial entries one shard may produce per lead-range pass: SA_OPT_PASS_BUDGET_MB, or
 // from the free memory of its device after the bucket build.  An entry (counted by its
 // upper bound) takes ~15 B of pair-counter regions, 12 B of send and 12 B of receive
-// buffer and ~28 B of reduce scratch on every shard of the device; with
-// SA_OPT_LEAN_MEMORY only the send and receive buffers of every shard are held at
-// once (regions and scratch one shard at a time).  Within [2^16, 2^31] entries.
+// buffer and ~28 B of reduce scratch on every shard of the device, all of them held
+// across the passes.  Within [2^16, 2^31] entries.
 uint64_t pass_budget(const sa_multi *m, const Shard &s) {
     uint64_t b;
     if (m->budget_mb) {
@@ -269,7 +268,7 @@ uint64_t pass_budget(const sa_multi *m, const Shard &s) {
         (void)hipSetDevice(s.device);
         if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 0;
         const uint64_t per_dev = m->rccl ? 1 : m->sh.size();  // shards sharing this device
-        const uint64_t per_entry = m->lean ? 24 * per_dev + 43 : 67 * per_dev;
+        const uint64_t per_entry = 67 * per_dev;
         b = (uint64_t)((double)fr * 0.6) / per_entry;
     }
     return std::min<uint64_t>(std::max<uint64_t>(b, 1ull << 16), 1ull << 31);
@@ -405,7 +404,9 @@ int multi_build(sa_ctx *c, bool readback, int (*single_build)(sa_ctx *, bool)) {
         if (r) return r;
         if (grow(s.sk, n * 8 + 8, s.device)) return (int)SA_E_NOMEM;
         s.cnt.assign(P, 0);
-        return sa_dist_emit(s.child, s.sk.p, s.cnt.data());
+        r = sa_dist_emit(s.child, s.sk.p, s.cnt.data());
+        if (m->lean) dist_release(s.child, DIST_RELEASE_BUCKET_SCRATCH);  // (the emit's sort scratch)
+        return r;
     });
     if (rc) return rc;
     // ---- exchange 1: k-mer records to the shard owning their hash range
@@ -463,9 +464,7 @@ int multi_build(sa_ctx *c, bool readback, int (*single_build)(sa_ctx *, bool)) {
             if (grow(s.pf, s.n_part * 4 + 4, s.device) || grow(s.ps, s.n_part * 4 + 4, s.device) ||
                 grow(s.pc, s.n_part * 4 + 4, s.device))
                 return (int)SA_E_NOMEM;
-            r = sa_dist_partials(s.child, s.pf.p, s.ps.p, s.pc.p);
-            if (m->lean) dist_release(s.child, DIST_RELEASE_PAIR_OUTPUT);
-            return r;
+            return sa_dist_partials(s.child, s.pf.p, s.ps.p, s.pc.p);
         });
         if (rc) return rc;
         for (Shard &s : m->sh) m->partials += s.n_part;
@@ -489,24 +488,22 @@ int multi_build(sa_ctx *c, bool readback, int (*single_build)(sa_ctx *, bool)) {
                 parts[a].recv.push_back((m->sh[l].*dst[a]).p);
             }
         if ((rc = exchange_parts(c, pl, parts, 4))) return rc;
-        if (m->lean)
-            for (Shard &s : m->sh)
-                for (int a = 0; a < 3; ++a) release(s.*src[a], s.device);
         // ---- reduce + filter: this shard's leads of the pass, appended
         rc = for_shards(c, [&](Shard &s) {
-            int r = sa_dist_reduce_pass(s.child, s.qf.p, s.qs.p, s.qc.p, s.n_recv, pass, npass);
-            if (m->lean) {
-                for (int a = 0; a < 3; ++a) release(s.*dst[a], s.device);
-                dist_release(s.child, DIST_RELEASE_REDUCE_SCRATCH);
-            }
-            return r;
+            return sa_dist_reduce_pass(s.child, s.qf.p, s.qs.p, s.qc.p, s.n_recv, pass, npass);
         });
         if (rc) return rc;
     }
+    // lean: the pass buffers live across the passes (allocating and freeing tens of GB
+    // per pass and shard cost more than the passes -- hipFree synchronises), then go
+    // with the bucket structures at the end of the build
     if (m->lean)
         for (Shard &s : m->sh) {
-            (void)hipSetDevice(s.device);
-            dist_release(s.child, DIST_RELEASE_BUCKETS);
+            for (int a = 0; a < 3; ++a) {
+                release(s.*src[a], s.device);
+                release(s.*dst[a], s.device);
+            }
+            dist_release(s.child, DIST_RELEASE_PAIR_OUTPUT | DIST_RELEASE_REDUCE_SCRATCH | DIST_RELEASE_BUCKETS);
         }
     c->stats = sa_stats{};
     uint64_t nd = 0;

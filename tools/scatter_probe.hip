@@ -163,6 +163,20 @@ static void run_nt8(void *) { hipLaunchKernelGGL(scatter_nt8, grid_of(g.n), dim3
 static void run_s4(void *) { hipLaunchKernelGGL(scatter4, grid_of(g.n), dim3(256), 0, 0, g.idx, g.n, (uint32_t *)g.out); }
 static void run_g4(void *) { hipLaunchKernelGGL(gather, grid_of(g.n), dim3(256), 0, 0, g.idx, g.n, g.src, g.sink); }
 
+// Hash-indexed bucket directory probe: item i gathers dir[h(i) & mask]
+// (its bucket's head, one random 4-byte load from a 2^T-entry table) and, with dep = 1,
+// then a second load that depends on it (the first entry of that bucket's list, random in
+// a list of the same size): the minimum a directory costs the pair counter per occurrence
+// in place of the bucket build's scattered 8-byte record store.  Items are generated in
+// the kernel (no index array), so the bytes moved are the gathers' alone.
+__global__ void dir_gather(uint64_t n, const uint32_t *dir, uint32_t mask, int dep, uint32_t *sink) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t v = dir[hash32((uint32_t)i ^ (uint32_t)(i >> 32) * 0x9E3779B1u) & mask];
+    if (dep) v = dir[(v * 2654435761u) & mask];
+    if (v == 0xDEADBEEFu) sink[0] = v;
+}
+
 int main(int argc, char **argv) {
     // argv[1] = "big N": only the 8-byte scatter section at N items (round 3:
     // does the per-store cost grow with the target array -- TLB reach -- at
@@ -210,6 +224,34 @@ int main(int argc, char **argv) {
         }
         printf("n=%llu direct %.3f ms | staged (ipb %u, bins %u x %u shards, %.0f MB each): stage %.3f + scatter %.3f = %.3f ms\n",
                (unsigned long long)n, d, ipb, nbins, ns, 8.0 * (1ull << wshift) / 1e6, t1 / 3, t2 / 3, (t1 + t2) / 3);
+        return 0;
+    }
+    // argv[1] = "dir N T": N directory gathers from a 2^T-entry (4 * 2^T bytes) table,
+    // one load and two dependent loads per item
+    if (argc > 3 && argv[1][0] == 'd') {
+        const uint64_t n = strtoull(argv[2], nullptr, 10);
+        const int T = atoi(argv[3]);
+        uint32_t *dir, *sink;
+        CHK(hipMalloc(&dir, (4ull << T)));
+        CHK(hipMalloc(&sink, 64));
+        hipLaunchKernelGGL(make_idx, grid_of(1ull << T), dim3(256), 0, 0, dir, 1ull << T, 1ull << T, 0u);
+        for (int dep = 0; dep < 2; ++dep) {
+            hipEvent_t a, b;
+            CHK(hipEventCreate(&a)); CHK(hipEventCreate(&b));
+            hipLaunchKernelGGL(dir_gather, grid_of(n), dim3(256), 0, 0, n, dir, (uint32_t)((1ull << T) - 1), dep, sink);
+            CHK(hipDeviceSynchronize());
+            CHK(hipEventRecord(a));
+            for (int r = 0; r < 3; ++r)
+                hipLaunchKernelGGL(dir_gather, grid_of(n), dim3(256), 0, 0, n, dir, (uint32_t)((1ull << T) - 1), dep, sink);
+            CHK(hipEventRecord(b));
+            CHK(hipEventSynchronize(b));
+            float ms = 0;
+            CHK(hipEventElapsedTime(&ms, a, b));
+            ms /= 3;
+            printf("dir n=%llu table 2^%d (%.0f MB): %d load(s) per item %.3f ms (%.3f ms per 48.6M, %.1f G items/s)\n",
+                   (unsigned long long)n, T, 4.0 * (1ull << T) / 1e6, dep + 1, ms, ms * 48.6e6 / n, n / (ms * 1e-3) / 1e9);
+        }
+        CHK(hipFree(dir)); CHK(hipFree(sink));
         return 0;
     }
     // argv[1] = "atom NBLOCKS NBINS NSHARD"
