@@ -1751,6 +1751,7 @@ int sa_add_reads(sa_ctx *c, const char *bases, const uint64_t *offsets, uint32_t
         if (offsets[r + 1] < offsets[r]) return fail(c, SA_E_ARG, "offsets must be non-decreasing");
     }
     c->bases.insert(c->bases.end(), bases + offsets[0], bases + offsets[n]);
+    c->boff.reserve(c->boff.size() + n);
     for (uint32_t r = 0; r < n; ++r) c->boff.push_back(base0 + (offsets[r + 1] - offsets[0]));
     c->reads_dirty = true;
     c->built = c->aligned = false;
@@ -1763,6 +1764,15 @@ int sa_read_fasta(sa_ctx *c, const char *path) {
     std::vector<char> b;
     std::vector<uint64_t> off;
     if (read_fasta(path, b, off) != 0) return fail(c, SA_E_INPUT, std::string("Invalid Sequence File: ") + path);
+    if (off.size() - 1 > 0xFFFFFFFFull) return fail(c, SA_E_OVERFLOW, "more than 2^32 - 1 reads");
+    if (c->bases.empty() && c->boff.size() == 1) {  // the first reads: taken over, not copied
+        c->bases.swap(b);
+        c->boff.swap(off);
+        c->reads_dirty = true;
+        c->built = c->aligned = false;
+        ++c->reads_gen;
+        return SA_OK;
+    }
     return sa_add_reads(c, b.data(), off.data(), (uint32_t)(off.size() - 1));
 }
 

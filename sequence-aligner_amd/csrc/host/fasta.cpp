@@ -17,39 +17,53 @@ namespace sa {
 int read_fasta(const char *path, std::vector<char> &bases, std::vector<uint64_t> &offsets) {
     FILE *f = fopen(path, "rb");
     if (!f) return -1;
+    // the whole file in one read (then whatever a pipe or a growing file still holds)
     std::vector<char> buf;
+    if (fseeko(f, 0, SEEK_END) == 0) {
+        const off_t sz = ftello(f);
+        if (sz > 0) buf.resize((size_t)sz);
+        if (fseeko(f, 0, SEEK_SET) != 0) buf.clear();
+    }
+    buf.resize(buf.empty() ? 0 : fread(buf.data(), 1, buf.size(), f));
     {
         char tmp[1 << 16];
         size_t got;
         while ((got = fread(tmp, 1, sizeof(tmp), f)) > 0) buf.insert(buf.end(), tmp, tmp + got);
     }
     fclose(f);
-    bases.clear();
-    offsets.assign(1, 0);
     const size_t n = buf.size();
-    size_t p = 0;
-    bool first = true;
     if (n == 0) return -1;  // in.readLine() == null -> NPE on line.startsWith
+    bases.resize(n);  // (an upper bound; trimmed below)
+    offsets.assign(1, 0);
+    const char *B = buf.data();
+    char *D = bases.data();
+    size_t nb = 0, p = 0;
+    bool first = true;
     while (p < n) {
-        size_t e = p;
-        while (e < n && buf[e] != '\n' && buf[e] != '\r') ++e;
-        size_t next = e;
-        if (next < n) next += (buf[next] == '\r' && next + 1 < n && buf[next + 1] == '\n') ? 2 : 1;
+        // the line [p, e) and the start of the next: "\n", "\r" and "\r\n" end a line
+        const char *nl = (const char *)memchr(B + p, '\n', n - p);
+        size_t e = nl ? (size_t)(nl - B) : n;
+        size_t next = nl ? e + 1 : n;
+        if (const char *cr = (const char *)memchr(B + p, '\r', e - p)) {
+            e = (size_t)(cr - B);
+            next = e + ((e + 1 < n && B[e + 1] == '\n') ? 2 : 1);
+        }
         if (first) {
-            if (e == p || buf[p] != '>') return -1;
+            if (e == p || B[p] != '>') return -1;
             first = false;
-        } else if (e > p && buf[p] == '>') {
-            offsets.push_back(bases.size());
-        } else {
-            for (size_t q = p; q < e; ++q) {
-                char ch = buf[q];
-                if (ch >= 'a' && ch <= 'z') ch = (char)(ch - 32);
-                bases.push_back(ch);
-            }
+        } else if (e > p && B[p] == '>') {
+            offsets.push_back(nb);
+        } else {  // sequence text, upper-cased (toUpperCase)
+            char *d = D + nb;
+            const size_t len = e - p;
+            memcpy(d, B + p, len);
+            for (size_t q = 0; q < len; ++q) d[q] = (char)(d[q] - ((d[q] >= 'a' && d[q] <= 'z') ? 32 : 0));
+            nb += len;
         }
         p = next;
     }
-    offsets.push_back(bases.size());
+    bases.resize(nb);
+    offsets.push_back(nb);
     return 0;
 }
 

@@ -51,6 +51,7 @@ struct Shard {
     std::vector<uint64_t> cnt, rcnt;  // per peer: elements sent / received
     uint64_t n_recv = 0, n_part = 0;
     uint64_t bound = 0;               // upper bound of this shard's partials (sa_dist_buckets)
+    uint64_t mem_total = 0;           // its device's memory (hipDeviceProp_t::totalGlobalMem)
     uint32_t npass = 1;               // this shard's pass plan (sa_dist_plan)
     std::string err;
 };
@@ -259,19 +260,24 @@ bool is_pow2(int x) { return x > 0 && (x & (x - 1)) == 0; }
 // upper bound) takes ~15 B of pair-counter regions, 12 B of send and 12 B of receive
 // buffer and ~28 B of reduce scratch on every shard of the device, all of them held
 // across the passes.  Within [2^16, 2^31] entries.
+// (The free memory is asked for only when the shards' bounds come near it: hipMemGetInfo
+// costs ~2 ms a call -- 8 serial shards of the bench shape took 35.6 -> 52.1 ms per step
+// with one query per shard and build, profiles/r06/ab/ab_sharded8_meminfo.txt.)
 uint64_t pass_budget(const sa_multi *m, const Shard &s) {
     uint64_t b;
+    const uint64_t cap = 1ull << 31;
     if (m->budget_mb) {
         b = (m->budget_mb << 20) / 12;
     } else {
-        size_t fr = 0, tot = 0;
-        (void)hipSetDevice(s.device);
-        if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 0;
         const uint64_t per_dev = m->rccl ? 1 : m->sh.size();  // shards sharing this device
         const uint64_t per_entry = 67 * per_dev;
+        if ((double)s.bound * per_entry <= 0.15 * (double)s.mem_total) return cap;  // far from the memory: one pass
+        (void)hipSetDevice(s.device);
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 0;
         b = (uint64_t)((double)fr * 0.6) / per_entry;
     }
-    return std::min<uint64_t>(std::max<uint64_t>(b, 1ull << 16), 1ull << 31);
+    return std::min<uint64_t>(std::max<uint64_t>(b, 1ull << 16), cap);
 }
 
 void clear_child_reads(sa_ctx *k) {
@@ -823,6 +829,8 @@ int sa_ctx_create_multi(const sa_settings *s, int n_gpus, int n_shards, sa_ctx *
         rc = sa_ctx_create(s, sh.device, &sh.child);
         if (rc) { sa_ctx_destroy(c); return rc; }
         (void)hipSetDevice(sh.device);
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, sh.device) == hipSuccess) sh.mem_total = prop.totalGlobalMem;
         if (hipStreamCreateWithFlags(&sh.xs, hipStreamNonBlocking) != hipSuccess) { sa_ctx_destroy(c); return SA_E_HIP; }
     }
     if (m->rccl) {
@@ -855,6 +863,8 @@ int sa_ctx_create_rank(const sa_settings *s, int device, int rank, int nranks, c
     rc = sa_ctx_create(s, device, &sh.child);
     if (rc) { sa_ctx_destroy(c); return rc; }
     (void)hipSetDevice(device);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess) sh.mem_total = prop.totalGlobalMem;
     if (hipStreamCreateWithFlags(&sh.xs, hipStreamNonBlocking) != hipSuccess) { sa_ctx_destroy(c); return SA_E_HIP; }
     ncclUniqueId u;
     memcpy(&u, id, sizeof(u));

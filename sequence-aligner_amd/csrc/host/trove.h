@@ -31,13 +31,14 @@ public:
     }
 
     // put(key, val) for a key not yet present; returns false if it was present
-    // (the value is the caller's payload -- e.g. the key's index in its arrays --
-    // and moves with the key through every rehash, so iteration needs no lookup)
+    // (the value is the caller's payload -- e.g. the key's index in its arrays,
+    // >= 0 -- and moves with the key through every rehash, so iteration needs no
+    // lookup)
     bool insert(int32_t key, int32_t val = 0) {
-        int32_t slot;
+        Slot *slot;
         bool fresh = probe_insert(key, &slot);
         if (!fresh) return false;
-        vals_[slot] = val;
+        slot->val = val;
         if (consumed_free_) --free_;
         if (++size_ > max_size_ || free_ == 0) {
             rehash(size_ > max_size_ ? next_prime(cap_ << 1) : cap_);
@@ -53,13 +54,13 @@ public:
     template <class F>
     void for_each(F f) const {
         for (int32_t i = cap_; i-- > 0;)
-            if (full_[i]) f(keys_[i]);
+            if (slots_[i].val >= 0) f(slots_[i].key);
     }
     // (key, value) in the same order
     template <class F>
     void for_each_kv(F f) const {
         for (int32_t i = cap_; i-- > 0;)
-            if (full_[i]) f(keys_[i], vals_[i]);
+            if (slots_[i].val >= 0) f(slots_[i].key, slots_[i].val);
     }
 
     static int32_t next_prime(int32_t desired) {
@@ -74,59 +75,62 @@ public:
     }
 
 private:
+    // key and payload side by side (val < 0: a FREE slot) -- one cache line per probe
+    // (the PairData replay of configs[0]'s 3.1M keys is bound by these misses)
+    struct Slot {
+        int32_t key;
+        int32_t val;
+    };
+    static constexpr int32_t FREE = -1;
     void alloc(int32_t cap) {
         cap_ = cap;
-        keys_.assign((size_t)cap, 0);
-        vals_.assign((size_t)cap, 0);
-        full_.assign((size_t)cap, 0);
+        slots_.assign((size_t)cap, Slot{0, FREE});
     }
     void compute_max_size() {
         const int32_t lf = (int32_t)((float)cap_ * 0.5f);
         max_size_ = cap_ - 1 < lf ? cap_ - 1 : lf;
         free_ = cap_ - size_;
     }
-    bool probe_insert(int32_t key, int32_t *slot) {
+    bool probe_insert(int32_t key, Slot **slot) {
         const int32_t length = cap_;
         const int32_t hash = key & 0x7fffffff;
         int32_t index = hash % length;
         consumed_free_ = false;
-        if (!full_[index]) {
+        Slot *sl = &slots_[(size_t)index];
+        if (sl->val < 0) {
             consumed_free_ = true;
-            keys_[index] = key; full_[index] = 1; *slot = index;
+            sl->key = key; *slot = sl;
             return true;
         }
-        if (keys_[index] == key) { *slot = index; return false; }
+        if (sl->key == key) { *slot = sl; return false; }
         const int32_t probe = 1 + (hash % (length - 2));
         for (;;) {
             index -= probe;
             if (index < 0) index += length;
-            if (!full_[index]) {
+            sl = &slots_[(size_t)index];
+            if (sl->val < 0) {
                 consumed_free_ = true;
-                keys_[index] = key; full_[index] = 1; *slot = index;
+                sl->key = key; *slot = sl;
                 return true;
             }
-            if (keys_[index] == key) { *slot = index; return false; }
+            if (sl->key == key) { *slot = sl; return false; }
         }
     }
     void rehash(int32_t newcap) {
-        std::vector<int32_t> ok, ov;
-        std::vector<uint8_t> of;
-        ok.swap(keys_);
-        ov.swap(vals_);
-        of.swap(full_);
+        std::vector<Slot> old;
+        old.swap(slots_);
         const int32_t oldcap = cap_;
         alloc(newcap);
         for (int32_t i = oldcap; i-- > 0;) {
-            if (of[i]) {
-                int32_t s;
-                probe_insert(ok[i], &s);
-                vals_[s] = ov[i];
+            if (old[(size_t)i].val >= 0) {
+                Slot *s;
+                probe_insert(old[(size_t)i].key, &s);
+                s->val = old[(size_t)i].val;
             }
         }
     }
 
-    std::vector<int32_t> keys_, vals_;
-    std::vector<uint8_t> full_;
+    std::vector<Slot> slots_;
     int32_t cap_ = 0, size_ = 0, free_ = 0, max_size_ = 0;
     bool consumed_free_ = false;
 };

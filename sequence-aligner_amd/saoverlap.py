@@ -114,11 +114,14 @@ def lib():
         L.sa_ctx_create_rank.argtypes = [P(Settings), C.c_int, C.c_int, C.c_int, C.c_char_p, P(vp)]
         L.sa_exchanged_bytes.argtypes = [vp]
         L.sa_exchanged_bytes.restype = C.c_uint64
-        L.sa_dist_buckets.argtypes = [vp, vp, P(C.c_uint64), P(C.c_uint64)]
-        L.sa_dist_plan.argtypes = [vp, C.c_uint64, P(C.c_uint32)]
-        L.sa_dist_count_pass.argtypes = [vp, C.c_uint32, C.c_uint32, P(C.c_uint64)]
-        L.sa_dist_reduce_pass.argtypes = [vp, vp, vp, vp, C.c_uint64, C.c_uint32, C.c_uint32]
-        L.sa_get_shard_info.argtypes = [vp, P(C.c_uint32), P(C.c_uint64), P(C.c_uint64)]
+        # (round 6 entry points; a library built from an older tree -- SA_OVERLAP_LIB,
+        # same-box A/B runs -- lacks them and the bindings stay unset)
+        if hasattr(L, "sa_get_shard_info"):
+            L.sa_dist_buckets.argtypes = [vp, vp, P(C.c_uint64), P(C.c_uint64)]
+            L.sa_dist_plan.argtypes = [vp, C.c_uint64, P(C.c_uint32)]
+            L.sa_dist_count_pass.argtypes = [vp, C.c_uint32, C.c_uint32, P(C.c_uint64)]
+            L.sa_dist_reduce_pass.argtypes = [vp, vp, vp, vp, C.c_uint64, C.c_uint32, C.c_uint32]
+            L.sa_get_shard_info.argtypes = [vp, P(C.c_uint32), P(C.c_uint64), P(C.c_uint64)]
         _lib = L
     return _lib
 
