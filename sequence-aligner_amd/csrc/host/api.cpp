@@ -1318,10 +1318,7 @@ int device_build(sa_ctx *c, bool readback) {
             // PairData: Trove layout of keys (fst<<16)^snd inserted in first-occurrence
             // order, each slot carrying its pair's index (the count without a lookup)
             TroveLayout pd;
-            for (uint64_t i = 0; i < np; ++i) {
-                const int32_t key = (int32_t)(((uint32_t)f[i] << 16) ^ (uint32_t)s[i]);
-                pd.insert(key, (int32_t)i);
-            }
+            for (uint64_t i = 0; i < np; ++i) pd.insert((int32_t)(((uint32_t)f[i] << 16) ^ (uint32_t)s[i]), (int32_t)i);
             // calcDispatchData (KmerTable.scala:155-187) over PairData iteration order:
             // DispatchData's Trove layout over the leads, each lead's (trail, count)
             // list in that order.  Decoded leads are 16-bit (key >> 16, E4): a lead's
