@@ -332,6 +332,12 @@ def main():
                     help="add a checksum of the dispatch list (lead, trail, count) to the line (cross-build checks)")
     ap.add_argument("--serial-shards", action="store_true",
                     help="virtual shards: run the shards one after another (clean per-shard stage times)")
+    ap.add_argument("--lean", action="store_true",
+                    help="sharded: SA_OPT_LEAN_MEMORY (free scratch between stages; virtual shards of a "
+                         "configs[3]-sized read set on one GPU)")
+    ap.add_argument("--pass-budget-mb", type=int, default=0,
+                    help="sharded: SA_OPT_PASS_BUDGET_MB (partials per shard and lead-range pass; 0 = from "
+                         "the free device memory)")
     ap.add_argument("--stage-steps", type=int, default=5,
                     help="steps of a second, instrumented loop (HIP events around every stage) for the stage "
                          "times and the rooflines; the timed loop itself runs without events")
@@ -372,11 +378,13 @@ def main():
                                         min_len=args.min_len)
         uid = [sao.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        ov = sao.Overlapper(device=local, rank=rank, nranks=ws, rccl_id=uid[0], **common)
+        ov = sao.Overlapper(device=local, rank=rank, nranks=ws, rccl_id=uid[0], lean_memory=args.lean,
+                            pass_budget_mb=args.pass_budget_mb, **common)
         ov.add_packed(bases.tobytes(), offsets)
     elif mode in ("process", "virtual"):
         P = n_gpus if mode == "process" else args.shards
-        ov = sao.Overlapper(gpus=n_gpus, shards=P, serial_shards=args.serial_shards, **common)
+        ov = sao.Overlapper(gpus=n_gpus, shards=P, serial_shards=args.serial_shards, lean_memory=args.lean,
+                            pass_budget_mb=args.pass_budget_mb, **common)
         for r in range(P):  # the same reads the torchrun ranks would hold, in rank order
             b_r, o_r = synth_workload(args.reads, args.len, G * P, args.gc, seed=1, shard=r, min_len=args.min_len)
             ov.add_packed(b_r.tobytes(), o_r)
@@ -753,6 +761,7 @@ def main():
             "roofline_pair_count": roofline_pc,
             "roofline_align": roofline_align,
             "exchange_bytes_per_step": int(xbytes) if sharded else None,
+            "shard_info": ov.shard_info() if sharded else None,
             "read_allgather_ms": round(t_gather * 1e3, 3) if t_gather is not None else None,
             "cpu_baseline": cpu,
             "config0": config0,

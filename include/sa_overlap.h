@@ -181,11 +181,12 @@ enum sa_option {
                                   per pass (sa_dist_plan).  0 (default): half of the free
                                   device memory after the bucket build, shared by the
                                   shards on the device, at ~40 B per entry */
-    SA_OPT_LEAN_MEMORY = 10    /* sharded context: free each shard's scratch between stages
-                                  (sort / bucket scratch after the bucket build, exchange
-                                  buffers after use, reduce scratch after each pass) so
-                                  that virtual shards of a large read set fit one device;
-                                  costs re-allocations every build */
+    SA_OPT_LEAN_MEMORY = 10    /* virtual shards (one device): the shards' transients (sort
+                                  and bucket-build scratch, pair-counter regions, reduce
+                                  scratch) come from one pool that each shard borrows for
+                                  the length of a call, instead of P copies, so that
+                                  virtual shards of a large read set fit one device; the
+                                  shards then run one after another */
 };
 
 /* Project4's fdAlign switch (Project4.scala:187-192, :585-604).

@@ -57,9 +57,10 @@ template <class T>
 int ensure(sa_ctx *c, DBuf &b, size_t count, T **out) {
     const size_t need = std::max<size_t>(count, 1) * sizeof(T);
     if (b.bytes < need) {
-        if (b.p) (void)hipFree(b.p);
+        if (b.p && !b.borrowed) (void)hipFree(b.p);
         b.p = nullptr;
         b.bytes = 0;
+        b.borrowed = false;
         const size_t alloc = need + need / 8;
         hipError_t e = hipMalloc(&b.p, alloc);
         if (e != hipSuccess) return fail(c, SA_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
@@ -1636,32 +1637,6 @@ int single_align(sa_ctx *c, bool readback) {
     return device_align(c, readback);
 }
 
-namespace sa {
-void dist_release(sa_ctx *c, int what) {
-    (void)hipSetDevice(c->device);
-    (void)hipStreamSynchronize(c->stream);
-    auto rel = [](std::initializer_list<DBuf *> bs) {
-        for (DBuf *b : bs) {
-            if (b->p) (void)hipFree(b->p);
-            b->p = nullptr;
-            b->bytes = 0;
-        }
-    };
-    if (what & DIST_RELEASE_BUCKET_SCRATCH)
-        rel({&c->d_keys, &c->d_keys2, &c->d_vals, &c->d_vals2, &c->d_sorttmp, &c->d_rl, &c->d_srl, &c->d_srl2,
-             &c->d_ogid, &c->d_bkttmp, &c->d_tmd, &c->d_ted, &c->d_bmdo, &c->d_bedo, &c->d_bstart, &c->d_gbid,
-             &c->d_gmds, &c->d_gede});
-    if (what & DIST_RELEASE_PAIR_OUTPUT) rel({&c->d_pf, &c->d_ps, &c->d_pc});
-    if (what & DIST_RELEASE_REDUCE_SCRATCH)
-        rel({&c->d_okeys, &c->d_okeys2, &c->d_ovals, &c->d_ovals2, &c->d_osort, &c->d_psum, &c->d_pkeep, &c->d_ppos,
-             &c->d_lr, &c->d_scan});
-    if (what & DIST_RELEASE_BUCKETS) {
-        rel({&c->d_rec, &c->d_md, &c->d_xrec, &c->d_pbound, &c->d_pitems, &c->d_items, &c->d_tier, &c->d_ovl,
-             &c->d_ovlrp});
-        c->dist_bkt = false;
-    }
-}
-}  // namespace sa
 
 // ===========================================================================
 // C ABI
@@ -1725,7 +1700,7 @@ void sa_ctx_destroy(sa_ctx *c) {
                     &c->d_shl, &c->d_sht, &c->d_shc, &c->d_rsh, &c->d_pbound, &c->d_pbown, &c->d_prange,
                     &c->d_pioff, &c->d_pitems};
     for (DBuf *b : bufs)
-        if (b->p) (void)hipFree(b->p);
+        if (b->p && !b->borrowed) (void)hipFree(b->p);
     for (auto &p : c->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->hcnt) (void)hipHostFree(c->hcnt);
@@ -2106,6 +2081,7 @@ int sa_dist_init(sa_ctx *c, int rank, int nranks, const uint32_t *starts, const 
         if (c->gocc[starts[r + 1]] - c->gocc[starts[r]] >= 0xFFFFFFF0ull)
             return fail(c, SA_E_OVERFLOW, "more than 2^32 k-mers on one rank");
     c->gnpr = uniform ? (uint32_t)(uni - k + 1) : 0;
+    c->dist_rho_ok = false;  // (a new read set: its partials / bound ratio is unknown)
     c->reads_dirty = true;  // loc tables come from all lengths now
     c->built = c->aligned = false;
     (void)hipSetDevice(c->device);
@@ -2219,9 +2195,10 @@ int ensure_keep(sa_ctx *c, DBuf &b, size_t count, size_t keep, T **out) {
         if (e != hipSuccess) return fail(c, SA_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
         if (keep && b.p) HIPCHK(hipMemcpyAsync(p, b.p, keep * sizeof(T), hipMemcpyDeviceToDevice, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
-        if (b.p) (void)hipFree(b.p);
+        if (b.p && !b.borrowed) (void)hipFree(b.p);
         b.p = p;
         b.bytes = alloc;
+        b.borrowed = false;
     }
     *out = (T *)b.p;
     return SA_OK;
@@ -2438,10 +2415,12 @@ int sa_dist_count_pass(sa_ctx *c, uint32_t pass, uint32_t npass, uint64_t *count
     }
     if (P > 1) HIPCHK(launch_pc_item_owners(istart, n_multi, dst, (uint32_t)P, iown, c->stream, iend));
     // output room: each owner's NSHARD regions hold 5/4 of that owner's bound spread
-    // evenly (the bound is the partner-list elements, >= the distinct partials); a
-    // region that still fills is grown and the pass recounted (pair_stage)
+    // evenly (the bound is the partner-list elements, >= the distinct partials) -- or,
+    // once a build of these reads has run, 1.5x its partials / bound ratio; a region
+    // that still fills is grown and the pass recounted (pair_stage)
     const uint64_t R = (uint64_t)NSHARD * (uint64_t)std::max(P, 1);
-    c->pair_cap = ((own_max + own_max / 4) / NSHARD + 1024) * R;
+    const double fcap = c->dist_rho_ok ? std::min(1.25, 1.5 * c->dist_rho + 0.01) : 1.25;
+    c->pair_cap = ((uint64_t)((double)own_max * fcap) / NSHARD + 1024) * R;
     EmitParams E = emit_params(c);
     E.occ_off = loff;  // occurrences of read a on this rank: [loff[a], loff[a+1])
     E.npr = 0;
@@ -2468,8 +2447,16 @@ int sa_dist_count_pass(sa_ctx *c, uint32_t pass, uint32_t npass, uint64_t *count
     c->part_off[fill.size()] = acc;
     c->part_np = acc;
     c->part_cap = cap_s;
-    if (pass + 1 == npass) c->stats.role_pairs = 0;  // (passes run from the last to the first)
+    if (pass + 1 == npass) {  // (passes run from the last to the first)
+        c->stats.role_pairs = 0;
+        c->dist_parts_acc = 0;
+    }
     c->stats.role_pairs += shard_sum(hc.role_pairs);
+    c->dist_parts_acc += acc;
+    if (pass == 0 && c->pbown[P] > 0) {  // the whole count ran: these reads' partials / bound
+        c->dist_rho = (double)c->dist_parts_acc / (double)c->pbown[P];
+        c->dist_rho_ok = true;
+    }
     return SA_OK;
 }
 

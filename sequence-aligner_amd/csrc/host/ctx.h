@@ -18,6 +18,9 @@ namespace sa {
 struct DBuf {
     void *p = nullptr;
     size_t bytes = 0;
+    // lent by the sharded context's pool (SA_OPT_LEAN_MEMORY, virtual shards): never freed
+    // by the child; a child that needs more allocates its own and the pool takes it back
+    bool borrowed = false;
 };
 
 // device-resident counters, one memset per build; the hot ones are NSHARD-way
@@ -136,6 +139,13 @@ struct sa_ctx {
     std::vector<unsigned long long> pbown; // partial bound per lead owner [nranks], total last
     std::vector<uint64_t> pbcum;           // host prefix sums of the per-read bounds (multi-pass plans)
     uint32_t dist_npass = 1;               // the last plan's pass count
+    // partials / bound of the last build of these reads (1 until one ran): the bound
+    // counts partner-list elements, ~20x the distinct partials at the bench shape
+    // (overlapping reads share many k-mers), ~1.3-2x at configs[4]'s k = 12 -- the
+    // pair regions and the pass plan are sized by bound x 1.5 rho
+    double dist_rho = 1.0;
+    bool dist_rho_ok = false;
+    uint64_t dist_parts_acc = 0;           // partials of the passes run so far
     uint64_t disp_acc = 0;                 // dispatched pairs the reduce passes appended so far
     DBuf d_pbound, d_pbown, d_prange, d_pioff, d_pitems;
     // k-mer table statistics (sa_kmer_histogram)
@@ -187,12 +197,4 @@ void multi_stage_times(const sa_ctx *c, double *ms, uint64_t *n);
 void multi_reset_stage_times(sa_ctx *c);
 int multi_sync(sa_ctx *c);
 uint64_t multi_exchanged_bytes(const sa_ctx *c);
-// sharded contexts with SA_OPT_LEAN_MEMORY: free a child's scratch between stages (api.cpp)
-enum : int {
-    DIST_RELEASE_BUCKET_SCRATCH = 1,  // emit keys, sort / bucket-build scratch (after sa_dist_buckets)
-    DIST_RELEASE_PAIR_OUTPUT = 2,     // the pair counter's owner regions (after sa_dist_partials)
-    DIST_RELEASE_REDUCE_SCRATCH = 4,  // the owner reduce's scratch (after sa_dist_reduce_pass)
-    DIST_RELEASE_BUCKETS = 8          // records, lists, bounds, items (after the last pass)
-};
-void dist_release(sa_ctx *c, int what);
 }  // namespace sa

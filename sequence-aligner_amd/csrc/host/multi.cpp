@@ -73,9 +73,10 @@ struct sa_multi {
     double x_ms = 0;                // exchange wall time (SA_STAGE_EXCHANGE)
     uint64_t x_n = 0, x_bytes = 0;
     // lead-range passes (SA_OPT_PASS_BUDGET_MB; 0 = from the free device memory) and
-    // scratch release between stages (SA_OPT_LEAN_MEMORY)
+    // one pool of the shards' transients (SA_OPT_LEAN_MEMORY, virtual shards)
     uint64_t budget_mb = 0;
     bool lean = false;
+    std::vector<DBuf> pool;         // one buffer per kPooled member (lean virtual shards)
     // the last sharded build: passes, partial entries over every shard and pass, and
     // their upper bound (sa_get_shard_info)
     uint32_t npass = 1;
@@ -83,6 +84,19 @@ struct sa_multi {
 };
 
 namespace {
+
+// The per-shard transients (sort / bucket-build scratch, pair-counter regions, reduce
+// scratch): with SA_OPT_LEAN_MEMORY on virtual shards -- which then run one after another --
+// the shards borrow them from one pool for the length of a call instead of holding P
+// copies (configs[3]'s real read set on 8 virtual shards: ~15 GB of sort scratch once, not
+// 8x).  Nothing is freed between builds: HIP allocations of this size cost ~1 s per 7 GB,
+// which a build that released and re-allocated them paid every time.
+DBuf sa_ctx::*const kPooled[] = {&sa_ctx::d_keys,   &sa_ctx::d_keys2,  &sa_ctx::d_vals,   &sa_ctx::d_vals2,
+                                 &sa_ctx::d_sorttmp, &sa_ctx::d_rl,    &sa_ctx::d_srl,    &sa_ctx::d_srl2,
+                                 &sa_ctx::d_pf,     &sa_ctx::d_ps,     &sa_ctx::d_pc,     &sa_ctx::d_okeys,
+                                 &sa_ctx::d_okeys2, &sa_ctx::d_ovals,  &sa_ctx::d_ovals2, &sa_ctx::d_osort,
+                                 &sa_ctx::d_psum,   &sa_ctx::d_pkeep,  &sa_ctx::d_ppos};
+constexpr size_t kNPooled = sizeof(kPooled) / sizeof(kPooled[0]);
 
 int set_err(sa_ctx *c, int code, const std::string &msg) {
     c->err = msg;
@@ -110,20 +124,61 @@ void release(DBuf &b, int device) {
     b.bytes = 0;
 }
 
+bool pooled(const sa_multi *m) { return m->lean && !m->rccl && m->sh.size() > 1; }
+
+// the pool's buffers into shard k for one call (a buffer the shard still owns -- e.g. the
+// aligner's sort scratch -- goes to the pool if larger, else is freed)
+void lend(sa_multi *m, sa_ctx *k) {
+    if (m->pool.size() != kNPooled) m->pool.assign(kNPooled, DBuf{});
+    for (size_t i = 0; i < kNPooled; ++i) {
+        DBuf &cb = k->*kPooled[i], &pb = m->pool[i];
+        if (cb.p && !cb.borrowed) {
+            if (cb.bytes > pb.bytes) {
+                if (pb.p) (void)hipFree(pb.p);
+                pb = cb;
+            } else {
+                (void)hipFree(cb.p);
+            }
+        }
+        cb = pb;
+        cb.borrowed = pb.p != nullptr;
+    }
+}
+// ... and back: a buffer the shard had to grow during the call replaces the pool's
+void reclaim(sa_multi *m, sa_ctx *k) {
+    for (size_t i = 0; i < kNPooled; ++i) {
+        DBuf &cb = k->*kPooled[i], &pb = m->pool[i];
+        if (cb.p && !cb.borrowed) {
+            if (pb.p) (void)hipFree(pb.p);
+            pb = cb;
+            pb.borrowed = false;
+        }
+        cb = DBuf{};
+    }
+}
+
 // Run f on every local shard (one host thread per shard when there are several),
 // each thread bound to its shard's device.  The first failure is reported.
+// lend_pool: the calls use the pooled transients (lean virtual shards; they then run one
+// after another)
 template <class F>
-int for_shards(sa_ctx *c, F f) {
+int for_shards(sa_ctx *c, F f, bool lend_pool = false) {
     sa_multi *m = c->multi;
     std::vector<int> rcs(m->sh.size(), SA_OK);
+    const bool pool = pooled(m) && lend_pool;
     auto run = [&](size_t i) {
         Shard &s = m->sh[i];
         s.err.clear();
         if (hipSetDevice(s.device) != hipSuccess) { rcs[i] = SA_E_HIP; s.err = "hipSetDevice"; return; }
+        if (pool) lend(m, s.child);
         rcs[i] = f(s);
         if (rcs[i] && s.err.empty()) s.err = s.child ? sa_last_error(s.child) : "";
+        if (pool) {
+            (void)sa_sync(s.child);
+            reclaim(m, s.child);
+        }
     };
-    if (m->sh.size() == 1 || m->serial) {
+    if (m->sh.size() == 1 || m->serial || pool) {
         for (size_t i = 0; i < m->sh.size(); ++i) {
             run(i);
             if (m->serial && m->sh[i].child) (void)sa_sync(m->sh[i].child);
@@ -255,11 +310,13 @@ int exchange_counts(sa_ctx *c) {
 
 bool is_pow2(int x) { return x > 0 && (x & (x - 1)) == 0; }
 
-// Partial entries one shard may produce per lead-range pass: SA_OPT_PASS_BUDGET_MB, or
-// from the free memory of its device after the bucket build.  An entry (counted by its
-// upper bound) takes ~15 B of pair-counter regions, 12 B of send and 12 B of receive
-// buffer and ~28 B of reduce scratch on every shard of the device, all of them held
-// across the passes.  Within [2^16, 2^31] entries.
+// Partial entries (counted by their upper bound) one shard may produce per lead-range
+// pass: SA_OPT_PASS_BUDGET_MB, or from the free memory of its device after the bucket
+// build.  A partial takes ~15 B of pair-counter regions, 12 B of send and 12 B of
+// receive buffer and ~28 B of reduce scratch on every shard of the device, all held
+// across the passes; per bound entry that is 67 B x rho, rho = 1.5 x the partials /
+// bound ratio of the last build of these reads (1 before one ran: the bound counts
+// partner-list elements, ~20x the partials at the bench shape).  Within [2^16, 2^31].
 // (The free memory is asked for only when the shards' bounds come near it: hipMemGetInfo
 // costs ~2 ms a call -- 8 serial shards of the bench shape took 35.6 -> 52.1 ms per step
 // with one query per shard and build, profiles/r06/ab/ab_sharded8_meminfo.txt.)
@@ -270,12 +327,14 @@ uint64_t pass_budget(const sa_multi *m, const Shard &s) {
         b = (m->budget_mb << 20) / 12;
     } else {
         const uint64_t per_dev = m->rccl ? 1 : m->sh.size();  // shards sharing this device
-        const uint64_t per_entry = 67 * per_dev;
+        const double rho = s.child->dist_rho_ok ? std::min(1.0, 1.5 * s.child->dist_rho + 0.01) : 1.0;
+        // (pooled: every shard holds its send and receive buffers, one the regions and scratch)
+        const double per_entry = rho * (pooled(m) ? 24.0 * (double)per_dev + 43.0 : 67.0 * (double)per_dev);
         if ((double)s.bound * per_entry <= 0.15 * (double)s.mem_total) return cap;  // far from the memory: one pass
         (void)hipSetDevice(s.device);
         size_t fr = 0, tot = 0;
         if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 0;
-        b = (uint64_t)((double)fr * 0.6) / per_entry;
+        b = (uint64_t)((double)fr * 0.6 / per_entry);
     }
     return std::min<uint64_t>(std::max<uint64_t>(b, 1ull << 16), cap);
 }
@@ -384,6 +443,7 @@ void multi_destroy(sa_ctx *c) {
     }
     release(m->gcodes, m->sh.empty() ? 0 : m->sh[0].device);
     release(m->gbad, m->sh.empty() ? 0 : m->sh[0].device);
+    for (DBuf &b : m->pool) release(b, m->sh.empty() ? 0 : m->sh[0].device);
     delete m;
     c->multi = nullptr;
 }
@@ -403,6 +463,18 @@ int multi_build(sa_ctx *c, bool readback, int (*single_build)(sa_ctx *, bool)) {
     const int P = m->P;
     c->built = c->aligned = false;
     m->sharded = true;
+    // (SA_DEBUG_PHASES=1: host wall clock of each phase of the build on stderr, diagnostics)
+    static const bool dbg = getenv("SA_DEBUG_PHASES") != nullptr;
+    auto tp = std::chrono::steady_clock::now();
+    std::string phases;
+    auto mark = [&](const char *name) {
+        if (!dbg) return;
+        const auto t = std::chrono::steady_clock::now();
+        char b[64];
+        snprintf(b, sizeof(b), " %s %.3f", name, std::chrono::duration<double, std::milli>(t - tp).count());
+        phases += b;
+        tp = t;
+    };
     // ---- emit: records grouped by owner shard
     rc = for_shards(c, [&](Shard &s) {
         uint64_t n = 0;
@@ -410,11 +482,10 @@ int multi_build(sa_ctx *c, bool readback, int (*single_build)(sa_ctx *, bool)) {
         if (r) return r;
         if (grow(s.sk, n * 8 + 8, s.device)) return (int)SA_E_NOMEM;
         s.cnt.assign(P, 0);
-        r = sa_dist_emit(s.child, s.sk.p, s.cnt.data());
-        if (m->lean) dist_release(s.child, DIST_RELEASE_BUCKET_SCRATCH);  // (the emit's sort scratch)
-        return r;
-    });
+        return sa_dist_emit(s.child, s.sk.p, s.cnt.data());
+    }, true);
     if (rc) return rc;
+    mark("emit");
     // ---- exchange 1: k-mer records to the shard owning their hash range
     if ((rc = exchange_counts(c))) return rc;
     std::vector<Plan> pl(m->sh.size());
@@ -428,19 +499,13 @@ int multi_build(sa_ctx *c, bool readback, int (*single_build)(sa_ctx *, bool)) {
         pl[l].rcnt = s.rcnt; pl[l].roff = prefix(s.rcnt);
     }
     if ((rc = exchange(c, pl, 8))) return rc;
-    if (m->lean) for (Shard &s : m->sh) release(s.sk, s.device);
+    mark("x1");
     // ---- buckets of this hash range (built once), the partials' upper bounds
-    rc = for_shards(c, [&](Shard &s) {
-        int r = sa_dist_buckets(s.child, s.rk.p, s.rcnt.data(), &s.bound);
-        if (m->lean) {  // the received records are consumed (they were the sort's keys)
-            release(s.rk, s.device);
-            dist_release(s.child, DIST_RELEASE_BUCKET_SCRATCH);
-        }
-        return r;
-    });
+    rc = for_shards(c, [&](Shard &s) { return sa_dist_buckets(s.child, s.rk.p, s.rcnt.data(), &s.bound); }, true);
     if (rc) return rc;
     // ---- lead-range passes: every pass holds the partials of 1/npass of every
     // owner's leads, within the budget on every shard (all ranks agree on npass)
+    mark("buckets");
     std::vector<uint64_t> budget(m->sh.size());
     for (size_t l = 0; l < m->sh.size(); ++l) budget[l] = pass_budget(m, m->sh[l]);
     uint32_t npass = 1;
@@ -453,6 +518,7 @@ int multi_build(sa_ctx *c, bool readback, int (*single_build)(sa_ctx *, bool)) {
         if ((rc = exchange_counts(c))) return rc;
         for (uint64_t v : s.rcnt) npass = std::max<uint32_t>(npass, (uint32_t)v);
     }
+    mark("plan");
     m->npass = npass;
     m->partials = 0;
     m->bound = 0;
@@ -471,8 +537,9 @@ int multi_build(sa_ctx *c, bool readback, int (*single_build)(sa_ctx *, bool)) {
                 grow(s.pc, s.n_part * 4 + 4, s.device))
                 return (int)SA_E_NOMEM;
             return sa_dist_partials(s.child, s.pf.p, s.ps.p, s.pc.p);
-        });
+        }, true);
         if (rc) return rc;
+        mark("count");
         for (Shard &s : m->sh) m->partials += s.n_part;
         // ---- exchange 2: partials to the shard owning the lead
         if ((rc = exchange_counts(c))) return rc;
@@ -494,23 +561,15 @@ int multi_build(sa_ctx *c, bool readback, int (*single_build)(sa_ctx *, bool)) {
                 parts[a].recv.push_back((m->sh[l].*dst[a]).p);
             }
         if ((rc = exchange_parts(c, pl, parts, 4))) return rc;
+        mark("x2");
         // ---- reduce + filter: this shard's leads of the pass, appended
         rc = for_shards(c, [&](Shard &s) {
             return sa_dist_reduce_pass(s.child, s.qf.p, s.qs.p, s.qc.p, s.n_recv, pass, npass);
-        });
+        }, true);
         if (rc) return rc;
+        mark("reduce");
     }
-    // lean: the pass buffers live across the passes (allocating and freeing tens of GB
-    // per pass and shard cost more than the passes -- hipFree synchronises), then go
-    // with the bucket structures at the end of the build
-    if (m->lean)
-        for (Shard &s : m->sh) {
-            for (int a = 0; a < 3; ++a) {
-                release(s.*src[a], s.device);
-                release(s.*dst[a], s.device);
-            }
-            dist_release(s.child, DIST_RELEASE_PAIR_OUTPUT | DIST_RELEASE_REDUCE_SCRATCH | DIST_RELEASE_BUCKETS);
-        }
+    if (dbg) fprintf(stderr, "[sa phases ms]%s\n", phases.c_str());
     c->stats = sa_stats{};
     uint64_t nd = 0;
     for (Shard &s : m->sh) {

@@ -353,10 +353,11 @@ def test_configs3_real_density_eight_shards(oracle_mod):
         "npass": info["npass"], "partials_total": info["partials"], "partials_per_shard": info["partials"] / 8,
         "partial_bound_total": info["bound"], "partials_projected_by_oracle": est,
         "exchanged_bytes_first_build": xb, "first_build_s": t_first, "second_build_s": t_second,
-        "per_shard_stage_ms_sum_over_8_serial_shards": times, "sampled_leads": int(len(leads)),
+        "per_shard_stage_ms": times, "sampled_leads": int(len(leads)),
         "sampled_pairdata_rows": rows, "sampled_dispatched_rows": int(len(sel)),
-        "note": "serial virtual shards, SA_OPT_LEAN_MEMORY, pass budget from free memory; stage times are the "
-                "sum over the 8 shards of one build (divide by 8 for one shard)"})
+        "note": "serial virtual shards, SA_OPT_LEAN_MEMORY, pass budget from free memory; stage times: per "
+                "stage the slowest shard of the second build, summed over its passes (exchange: the host "
+                "wall clock of every exchange)"})
 
 
 def test_configs4_shape_k12_eight_shards_in_passes(oracle_mod):
