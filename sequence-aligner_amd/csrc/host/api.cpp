@@ -2296,10 +2296,12 @@ int sa_dist_buckets(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uin
     HIPCHK(launch_read_bound(loff, N, PI, dst, (uint32_t)P, pb, pown, c->stream, &cnt->big_n));
     Counters *hp;
     if (int rc_p = pinned_counters(c, &hp)) return rc_p;
-    c->pbown.assign((size_t)P + 1, 0);
+    // (the owner bounds ride in the pinned counter copy's bound_own: one DMA, no
+    // pageable staging)
+    HIPCHK(hipMemcpyAsync(cnt->bound_own, pown, ((size_t)P + 1) * 8, hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(hp, cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(c->pbown.data(), pown, ((size_t)P + 1) * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    c->pbown.assign(hp->bound_own, hp->bound_own + P + 1);
     const unsigned long long lds_buckets = shard_sum(hp->bkt_counts);
     if (hp->big_n) {  // partitions above 4,096 records (high-copy repeats): the global path, then the bounds
         rc = bucket_stage(c, keys, keys2, vals, vals2, n, loff, N, 0, packed ? nullptr : rl, nullptr, false, stmp,
@@ -2307,8 +2309,9 @@ int sa_dist_buckets(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uin
         if (rc) return rc;
         PI.xrec = PA.xrec;
         HIPCHK(launch_read_bound(loff, N, PI, dst, (uint32_t)P, pb, pown, c->stream));
-        HIPCHK(hipMemcpyAsync(c->pbown.data(), pown, ((size_t)P + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(hp->bound_own, pown, ((size_t)P + 1) * 8, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
+        c->pbown.assign(hp->bound_own, hp->bound_own + P + 1);
     }
     resolve_timing(c);
     c->dist_in = PI;
@@ -2638,8 +2641,10 @@ int sa_dist_set_reads(sa_ctx *c, const void *codes, const void *bad, uint64_t nw
     ENSURE(c->d_glen, (size_t)N + 1, &glen);
     ENSURE(c->d_gbad, (size_t)N + 1, &gbad);
     HIPCHK(hipMemsetAsync(gcodes + nwords, 0, 8, c->stream));
-    if (nwords) HIPCHK(hipMemcpyAsync(gcodes, codes, nwords * 4, hipMemcpyDeviceToDevice, c->stream));
-    if (N) HIPCHK(hipMemcpyAsync(gbad, bad, (size_t)N * 4, hipMemcpyDeviceToDevice, c->stream));
+    // (a virtual shard's buffers may be the all-gathered copy itself, lent by multi.cpp)
+    if (nwords && gcodes != codes)
+        HIPCHK(hipMemcpyAsync(gcodes, codes, nwords * 4, hipMemcpyDeviceToDevice, c->stream));
+    if (N && gbad != bad) HIPCHK(hipMemcpyAsync(gbad, bad, (size_t)N * 4, hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(gwoff, gw.data(), gw.size() * 8, hipMemcpyHostToDevice, c->stream));
     if (N) HIPCHK(hipMemcpyAsync(glen, c->dlen.data(), (size_t)N * 4, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));

@@ -42,6 +42,7 @@ struct Counters {
     uint32_t xrec_n;     // escape records written (big partitions)
     uint32_t rtotal;     // per-read pair mode: dispatched pairs (scan total)
     uint32_t shard_off[NSHARD + 2];
+    unsigned long long bound_own[257];  // sharded: partial bound per lead owner + total (read back pinned)
 };
 
 inline unsigned long long shard_sum(const unsigned long long *v) {

@@ -95,7 +95,8 @@ DBuf sa_ctx::*const kPooled[] = {&sa_ctx::d_keys,   &sa_ctx::d_keys2,  &sa_ctx::
                                  &sa_ctx::d_sorttmp, &sa_ctx::d_rl,    &sa_ctx::d_srl,    &sa_ctx::d_srl2,
                                  &sa_ctx::d_pf,     &sa_ctx::d_ps,     &sa_ctx::d_pc,     &sa_ctx::d_okeys,
                                  &sa_ctx::d_okeys2, &sa_ctx::d_ovals,  &sa_ctx::d_ovals2, &sa_ctx::d_osort,
-                                 &sa_ctx::d_psum,   &sa_ctx::d_pkeep,  &sa_ctx::d_ppos};
+                                 &sa_ctx::d_psum,   &sa_ctx::d_pkeep,  &sa_ctx::d_ppos,   &sa_ctx::d_tb,
+                                 &sa_ctx::d_p1st,   &sa_ctx::d_ltb,    &sa_ctx::d_lmax};
 constexpr size_t kNPooled = sizeof(kPooled) / sizeof(kPooled[0]);
 
 int set_err(sa_ctx *c, int code, const std::string &msg) {
@@ -685,12 +686,20 @@ int multi_align(sa_ctx *c, bool readback, int (*single_align)(sa_ctx *, bool)) {
         rc = for_shards(c, [&](Shard &s) {
             const void *gc = m->rccl ? s.xbuf.p : m->gcodes.p;
             const void *gb = m->rccl ? (const void *)((const char *)s.xbuf.p + total_w * 4 + 8) : m->gbad.p;
+            if (!m->rccl) {  // virtual shards read the one all-gathered copy (no P copies of it)
+                for (DBuf sa_ctx::*mb : {&sa_ctx::d_gcodes, &sa_ctx::d_gbad}) {
+                    DBuf &cb = s.child->*mb;
+                    if (cb.p && !cb.borrowed) release(cb, s.device);
+                }
+                s.child->d_gcodes = DBuf{m->gcodes.p, m->gcodes.bytes, true};
+                s.child->d_gbad = DBuf{m->gbad.p, m->gbad.bytes, true};
+            }
             return sa_dist_set_reads(s.child, gc, gb, total_w);
         });
         if (rc) return rc;
         m->reads_gathered = true;
     }
-    rc = for_shards(c, [&](Shard &s) { return readback ? sa_align(s.child) : sa_device_align(s.child); });
+    rc = for_shards(c, [&](Shard &s) { return readback ? sa_align(s.child) : sa_device_align(s.child); }, true);
     if (rc) return rc;
     c->stats.aligned = c->stats.ovl_records = c->stats.dp_cells = 0;
     for (Shard &s : m->sh) {
