@@ -2184,6 +2184,14 @@ static void pass_range(const sa_ctx *c, int r, uint32_t pass, uint32_t npass, ui
     b = s + (uint32_t)(len * (pass + 1) / npass);
 }
 
+// an upper bound of the partials of leads [a, b): the bounds of the blocks of pb_gran reads
+// it touches (exact per read)
+static uint64_t bound_sum(const sa_ctx *c, uint32_t a, uint32_t b) {
+    if (a >= b) return 0;
+    const size_t g = c->pb_gran;
+    return c->pbcum[((size_t)b + g - 1) / g] - c->pbcum[a / g];
+}
+
 // grow a device buffer keeping its first `keep` elements (the reduce passes append)
 template <class T>
 int ensure_keep(sa_ctx *c, DBuf &b, size_t count, size_t keep, T **out) {
@@ -2290,7 +2298,7 @@ int sa_dist_buckets(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uin
     PI.rec = PA.rec; PI.xrec = PA.xrec; PI.lst = PA.lst;
     // per-read upper bounds of the partials (the pass plan), per lead owner on the host
     uint64_t *pb; unsigned long long *pown;
-    ENSURE(c->d_pbound, (size_t)N + 1, &pb);
+    ENSURE(c->d_pbound, (size_t)N + 1 + ((size_t)N + 63) / 64, &pb);  // per read, then per 64 reads
     ENSURE(c->d_pbown, (size_t)P + 1, &pown);
     const uint32_t *dst = (const uint32_t *)c->d_starts.p;
     HIPCHK(launch_read_bound(loff, N, PI, dst, (uint32_t)P, pb, pown, c->stream, &cnt->big_n));
@@ -2338,11 +2346,16 @@ int sa_dist_plan(sa_ctx *c, uint64_t budget, uint32_t *npass) {
     }
     (void)hipSetDevice(c->device);
     const uint32_t N = (uint32_t)c->dlen.size();
-    if (c->pbcum.size() != (size_t)N + 1) {  // the per-read bounds, prefix-summed on the host
-        std::vector<uint64_t> b(N);
-        if (N) HIPCHK(hipMemcpy(b.data(), c->d_pbound.p, (size_t)N * 8, hipMemcpyDeviceToHost));
-        c->pbcum.assign((size_t)N + 1, 0);
-        for (uint32_t i = 0; i < N; ++i) c->pbcum[i + 1] = c->pbcum[i] + b[i];
+    if (c->pbcum.empty()) {  // the bounds prefix-summed on the host: per read up to 2^20 reads,
+        // else per block of 64 reads (round 6: the per-read bounds of configs[3]'s 10M reads --
+        // 80 MB read back and summed on every shard -- cost 28 ms per shard and build)
+        c->pb_gran = N <= (1u << 20) ? 1 : 64;
+        const size_t nb = ((size_t)N + c->pb_gran - 1) / c->pb_gran;
+        std::vector<uint64_t> b(nb);
+        const uint64_t *src = (const uint64_t *)c->d_pbound.p + (c->pb_gran == 1 ? 0 : (size_t)N + 1);
+        if (nb) HIPCHK(hipMemcpy(b.data(), src, nb * 8, hipMemcpyDeviceToHost));
+        c->pbcum.assign(nb + 1, 0);
+        for (size_t i = 0; i < nb; ++i) c->pbcum[i + 1] = c->pbcum[i] + b[i];
     }
     uint64_t maxlen = 1;
     for (int r = 0; r < P; ++r) maxlen = std::max<uint64_t>(maxlen, c->dstarts[r + 1] - c->dstarts[r]);
@@ -2354,7 +2367,7 @@ int sa_dist_plan(sa_ctx *c, uint64_t budget, uint32_t *npass) {
             for (int r = 0; r < P; ++r) {
                 uint32_t a, b;
                 pass_range(c, r, (uint32_t)p, (uint32_t)np, a, b);
-                t += c->pbcum[b] - c->pbcum[a];
+                t += bound_sum(c, a, b);
             }
             w = std::max(w, t);
         }
@@ -2399,10 +2412,10 @@ int sa_dist_count_pass(sa_ctx *c, uint32_t pass, uint32_t npass, uint64_t *count
         for (int r = 0; r < P; ++r) own_max = std::max<uint64_t>(own_max, c->pbown[r]);
     } else {  // this pass's lead range of every owner
         std::vector<uint32_t> rg(2 * (size_t)P);
-        const bool cum = c->pbcum.size() == (size_t)N + 1;
+        const bool cum = !c->pbcum.empty();
         for (int r = 0; r < P; ++r) {
             pass_range(c, r, pass, npass, rg[2 * r], rg[2 * r + 1]);
-            own_max = std::max<uint64_t>(own_max, cum ? c->pbcum[rg[2 * r + 1]] - c->pbcum[rg[2 * r]] : c->pbown[r]);
+            own_max = std::max<uint64_t>(own_max, cum ? bound_sum(c, rg[2 * r], rg[2 * r + 1]) : c->pbown[r]);
         }
         uint32_t *drg, *ioff;
         ENSURE(c->d_prange, rg.size(), &drg);

@@ -138,7 +138,8 @@ struct sa_ctx {
     sa::PairIn dist_in{};                  // their records and lists (device)
     uint64_t dist_recv = 0;                // records received
     std::vector<unsigned long long> pbown; // partial bound per lead owner [nranks], total last
-    std::vector<uint64_t> pbcum;           // host prefix sums of the per-read bounds (multi-pass plans)
+    std::vector<uint64_t> pbcum;           // host prefix sums of the partial bounds (multi-pass plans),
+    uint32_t pb_gran = 1;                  // per block of pb_gran reads (1 or 64)
     uint32_t dist_npass = 1;               // the last plan's pass count
     // partials / bound of the last build of these reads (1 until one ran): the bound
     // counts partner-list elements, ~20x the distinct partials at the bench shape

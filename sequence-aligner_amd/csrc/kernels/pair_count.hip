@@ -1388,14 +1388,17 @@ __global__ __launch_bounds__(RB_WAVES * 64) void read_bound_kernel(const uint64_
     }
     __builtin_amdgcn_wave_barrier();
     const uint64_t s = lane < nr ? acc[wv][lane] : 0ull;
+    unsigned long long t = s;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
+    // per read, and per block of 64 reads after them (bound[n_reads + 1 + a0 / 64]): a plan
+    // over many reads reads back the blocks' (8 B per 64 reads)
     if (lane < nr) bound[a0 + lane] = s;
+    if (lane == 0) bound[n_reads + 1 + (a0 >> 6)] = t;
     // one atomic per wave and owner: a wave's reads are consecutive, so nearly always
     // one owner (the first and last read agree)
     const uint32_t ow0 = owner_of(starts, owners, a0), ow1 = owner_of(starts, owners, a0 + nr - 1);
     if (ow0 == ow1) {
-        unsigned long long t = s;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
         if (lane == 0) {
             atomicAdd(&own[ow0], t);
             atomicAdd(&own[owners], t);
