@@ -1193,16 +1193,20 @@ int device_build(sa_ctx *c, bool readback) {
             HIPCHK(hipMemcpy(head.data(), PA.is_head, n, hipMemcpyDeviceToHost));
             HIPCHK(hipMemcpy(first.data(), PA.bkt_first, n * 4, hipMemcpyDeviceToHost));
         }
-        std::vector<std::pair<uint32_t, uint32_t>> fh;  // (first g, head pos)
+        // the buckets in first-occurrence order: first occurrences are distinct indices < n,
+        // so each head lands at its own slot of a g-indexed table and one ascending walk
+        // reads them in order -- with the read of g advancing monotonically (no sort of the
+        // ~2M heads, no binary search per head)
+        std::vector<uint32_t> by_g(n, 0);  // head position + 1 of the bucket first met at g
         for (uint64_t i = 0; i < n; ++i)
-            if (head[i]) fh.push_back({first[i], (uint32_t)i});
-        std::sort(fh.begin(), fh.end());
+            if (head[i]) by_g[first[i]] = (uint32_t)i + 1;
         TroveLayout kd;
         const int k = c->set.kmer_size, mm = c->m;
-        for (auto &x : fh) {
-            const uint32_t g = x.first;
-            const uint32_t r = (uint32_t)(std::upper_bound(c->occ_off.begin(), c->occ_off.end(), (uint64_t)g) -
-                                          c->occ_off.begin()) - 1;
+        uint32_t r = 0;
+        for (uint64_t g = 0; g < n; ++g) {
+            const uint32_t hp = by_g[g];
+            if (!hp) continue;
+            while (c->occ_off[r + 1] <= g) ++r;  // the last read with occ_off[r] <= g
             const char *sq = c->bases.data() + c->boff[r] + (g - c->occ_off[r]);
             uint32_t h = 0;  // Kmer.seqHash (ObjectStore.scala:48-67)
             for (int q = 0; q < mm; ++q) {
@@ -1212,7 +1216,7 @@ int device_build(sa_ctx *c, bool readback) {
                 h ^= ch == 'C' ? 1u : ch == 'T' ? 2u : ch == 'G' ? 3u : 0u;
             }
             (void)k;
-            kd.insert((int32_t)h, (int32_t)x.second);  // (distinct hashes: every insert is fresh)
+            kd.insert((int32_t)h, (int32_t)(hp - 1));  // (distinct hashes: every insert is fresh)
         }
         std::vector<uint32_t> rank(n, 0);
         uint32_t rk = 0;
