@@ -32,3 +32,9 @@ pass lds SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE
 # keyed to the workload (bench.py's config.pmc_key): pmc_summary__<key>.csv
 KEY=$(python3 -c 'import json,sys; print(json.loads(open(sys.argv[1]).read())["config"]["pmc_key"])' $OUT/bench.json)
 python3 $R/tools/pmc_summary.py $OUT $OUT/pmc_summary__$KEY.csv
+# (SP_TRIM=1: drop the per-dispatch traces once summarised -- a large multi-shard run's
+# traces pass gpurun's 64 MiB copy-back limit)
+if [ -n "${SP_TRIM:-}" ]; then
+    rm -f $OUT/pmc_*/pmc_kernel_trace.csv $OUT/pmc_*/pmc_counter_collection.csv $OUT/prof/run_kernel_trace.csv
+    du -sh $OUT >> $R/gpurun_out/steps.txt
+fi
