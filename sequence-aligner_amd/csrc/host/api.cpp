@@ -2404,7 +2404,17 @@ int sa_dist_count_pass(sa_ctx *c, uint32_t pass, uint32_t npass, uint64_t *count
     // counted in 2.55 ms per step against 1.55 for multi-read items -- a read's
     // ~60 local occurrences do not pay for a wave's table setup; and partials
     // sorted by owner after the count cost an order stage of 0.3 ms more)
-    const uint32_t target = PMW_TARGET;
+    // Items are sized to the partials they will hold when the last build of these reads
+    // says how dense they are: ~96 expected partials per item, half the wave table's fill
+    // limit (round 6: at configs[3]'s real density a local occurrence yields ~1.5 partials,
+    // so 128-occurrence items overflowed the 192-partner table and went to the recount
+    // tiers -- 37 ms of a shard's 72 ms of pair counting, profiles/r06/big/c3real; at the
+    // bench shape, 0.33 per occurrence, the target stays 128)
+    uint32_t target = PMW_TARGET;
+    if (c->dist_rho_ok && n) {
+        const double per_occ = c->dist_rho * (double)c->pbown[P] / (double)n;
+        if (per_occ > 0.0) target = (uint32_t)std::min<double>(PMW_TARGET, std::max(16.0, 96.0 / per_occ));
+    }
     uint32_t n_multi = 0;
     uint32_t *istart, *iend = nullptr, *iown = nullptr;
     uint64_t own_max = 0;  // the largest owner's bound of this pass's partials
@@ -2564,7 +2574,7 @@ int sa_dist_reduce_pass(sa_ctx *c, const void *fst, const void *snd, const void 
     {
         uint32_t *lr;
         uint2 *seg = (uint2 *)ok;
-        ENSURE(c->d_lr, 6 * ((size_t)nl + 1), &lr);
+        ENSURE(c->d_lr, 7 * ((size_t)nl + 1), &lr);  // (big: the two tiers' lead lists)
         uint32_t *lcnt = lr, *loff = lr + ((size_t)nl + 1), *lcur = lr + 2 * ((size_t)nl + 1),
                  *kcnt = lr + 3 * ((size_t)nl + 1), *kex = lr + 4 * ((size_t)nl + 1), *big = lr + 5 * ((size_t)nl + 1);
         uint8_t *scan2 = scan;

@@ -240,84 +240,129 @@ __global__ __launch_bounds__(LT_THREADS) void lead_tile_kernel(const uint32_t *f
 
 constexpr int LR_SLOTS = 256, LR_FILL = 192;
 constexpr uint32_t LR_EMPTY = 0xFFFFFFFFu;
+// the second tier: one wave per listed lead, a 1,024-slot table (768 partners).  A lead
+// with more than 2 x 192 partials goes to it without trying the first table (round 6:
+// at configs[3]'s real density a lead meets ~510 distinct partners in ~740 partials, so
+// every lead overflowed the 192-partner table -- after hashing all its partials -- and
+// the block-per-lead pass took them one block each on a fixed 256-block grid: 3.8 ms per
+// shard and pass, profiles/r06/big/c3real)
+constexpr int LRM_SLOTS = 1024, LRM_FILL = 768;
+constexpr uint32_t LR_ROUTE = 2 * LR_FILL;
 
-// one wave per lead: partials into a wave-private 256-slot table (trail ->
-// count sum), then the kept entries compacted, ranked by trail and written
-// back over the start of the lead's own segment; kcnt[l] = kept, distinct
-// pairs counted (KmerTable.calcDispatchData's filter, :155-187)
+// One wave sums lead l's partials into a wave-private SLOTS-slot table (trail -> count
+// sum), then compacts the kept entries, ranks them by trail and writes them back over the
+// start of the lead's own segment; kcnt[l] = kept (KmerTable.calcDispatchData's filter,
+// :155-187).  More than FILL distinct partners (or a failed probe run): kcnt[l] = 0 and
+// the lead is listed for the next tier.  Returns the distinct partners counted.
+template <int SLOTS, int FILL>
+__device__ __forceinline__ uint32_t lead_wave(uint2 *seg, const uint32_t *loff, uint32_t l, uint32_t *key,
+                                              uint32_t *val, uint2 *kept, int lane, int32_t min_c, int32_t max_c,
+                                              uint32_t *kcnt, uint32_t *next_list, uint32_t *next_n) {
+    constexpr int LOG = SLOTS == 256 ? 8 : SLOTS == 1024 ? 10 : 12;
+    static_assert((1 << LOG) == SLOTS, "table size");
+    constexpr int PER = SLOTS / 64;
+    __builtin_amdgcn_wave_barrier();  // (the wave's previous lead is done with the table)
+    for (int j = lane; j < SLOTS; j += 64) { key[j] = LR_EMPTY; val[j] = 0; }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    const uint32_t s0 = loff[l], m = loff[l + 1] - s0;
+    bool ovf = false;
+    for (uint32_t j = lane; j < m; j += 64) {
+        const uint2 v = seg[s0 + j];
+        uint32_t h = (v.x * 0x9E3779B1u) >> (32 - LOG);
+        int probe = 0;
+        for (; probe < 64; ++probe) {
+            uint32_t old = lds_relaxed(&key[h]);
+            if (old == LR_EMPTY) old = atomicCAS(&key[h], LR_EMPTY, v.x);
+            if (old == LR_EMPTY || old == v.x) { atomicAdd(&val[h], v.y); break; }
+            h = (h + 1) & (SLOTS - 1);
+        }
+        if (probe == 64) ovf = true;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    // this lane's PER slots: distinct keys, kept ones compacted by wave prefix
+    uint32_t nd = 0, kp = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t kk = key[lane * PER + q], kc = val[lane * PER + q];
+        if (kk != LR_EMPTY) {
+            ++nd;
+            if ((int32_t)kc >= min_c && (int32_t)kc <= max_c) kp |= 1u << q;
+        }
+    }
+    const uint32_t tot_nd = (uint32_t)__shfl((int)wave_incl_add(nd), 63, 64);
+    if (tot_nd > (uint32_t)FILL || __any(ovf)) {
+        if (lane == 0) {
+            kcnt[l] = 0;
+            next_list[atomicAdd(next_n, 1u)] = l;
+        }
+        return 0;
+    }
+    const uint32_t mine = __popc(kp);
+    const uint32_t ex = wave_incl_add(mine) - mine;
+    const uint32_t k = (uint32_t)__shfl((int)(ex + mine), 63, 64);
+    uint32_t at = ex;
+#pragma unroll
+    for (int q = 0; q < PER; ++q)
+        if (kp & (1u << q)) kept[at++] = make_uint2(key[lane * PER + q], val[lane * PER + q]);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    for (uint32_t j = lane; j < k; j += 64) {
+        const uint2 e = kept[j];
+        uint32_t r = 0;
+        for (uint32_t q = 0; q < k; ++q) r += kept[q].x < e.x ? 1u : 0u;
+        seg[s0 + r] = e;  // (the segment's partials are all consumed)
+    }
+    if (lane == 0) kcnt[l] = k;
+    __builtin_amdgcn_wave_barrier();  // (kept / key are reused by the wave's next lead)
+    return tot_nd;
+}
+
+// one wave per lead (a lead with more than LR_ROUTE partials is listed for the second
+// tier straight away); distinct pairs counted once per block
 __global__ __launch_bounds__(256) void lead_reduce_kernel(uint2 *seg, const uint32_t *loff, uint32_t nl, int32_t min_c,
                                                           int32_t max_c, uint32_t *kcnt,
-                                                          unsigned long long *distinct, uint32_t *big_list,
-                                                          uint32_t *big_n) {
+                                                          unsigned long long *distinct, uint32_t *mid_list,
+                                                          uint32_t *mid_n) {
     __shared__ uint32_t key[4][LR_SLOTS], val[4][LR_SLOTS];
     __shared__ uint2 kept[4][LR_FILL];
     __shared__ uint32_t nd_blk;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t l = blockIdx.x * 4 + w;
     if (threadIdx.x == 0) nd_blk = 0;
-    for (int j = lane; j < LR_SLOTS; j += 64) { key[w][j] = LR_EMPTY; val[w][j] = 0; }
     __syncthreads();
-    uint32_t nd = 0;
     if (l < nl) {
-        const uint32_t s0 = loff[l], m = loff[l + 1] - s0;
-        bool ovf = false;
-        for (uint32_t j = lane; j < m; j += 64) {
-            const uint2 v = seg[s0 + j];
-            uint32_t h = (v.x * 0x9E3779B1u) >> 24;
-            int probe = 0;
-            for (; probe < 64; ++probe) {
-                uint32_t old = lds_relaxed(&key[w][h]);
-                if (old == LR_EMPTY) old = atomicCAS(&key[w][h], LR_EMPTY, v.x);
-                if (old == LR_EMPTY || old == v.x) { atomicAdd(&val[w][h], v.y); break; }
-                h = (h + 1) & (LR_SLOTS - 1);
-            }
-            if (probe == 64) ovf = true;
-        }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-        // this lane's 4 slots: distinct keys, kept ones compacted by wave prefix
-        uint32_t kk[4], kc[4], kp = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            kk[q] = key[w][lane * 4 + q];
-            kc[q] = val[w][lane * 4 + q];
-            if (kk[q] != LR_EMPTY) {
-                ++nd;
-                if ((int32_t)kc[q] >= min_c && (int32_t)kc[q] <= max_c) kp |= 1u << q;
-            }
-        }
-        const uint32_t tot_nd = (uint32_t)__shfl((int)wave_incl_add(nd), 63, 64);
-        if (tot_nd > LR_FILL || __any(ovf)) {
-            // a lead with more partners than the wave table (high-copy repeats):
-            // listed for the block-per-lead pass (lead_reduce_big_kernel)
+        uint32_t nd = 0;
+        if (loff[l + 1] - loff[l] > LR_ROUTE) {
             if (lane == 0) {
                 kcnt[l] = 0;
-                big_list[atomicAdd(big_n, 1u)] = l;
+                mid_list[atomicAdd(mid_n, 1u)] = l;
             }
         } else {
-            const uint32_t mine = __popc(kp);
-            const uint32_t ex = wave_incl_add(mine) - mine;
-            const uint32_t k = (uint32_t)__shfl((int)(ex + mine), 63, 64);
-            uint32_t at = ex;
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if (kp & (1u << q)) kept[w][at++] = make_uint2(kk[q], kc[q]);
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-            for (uint32_t j = lane; j < k; j += 64) {
-                const uint2 e = kept[w][j];
-                uint32_t r = 0;
-                for (uint32_t q = 0; q < k; ++q) r += kept[w][q].x < e.x ? 1u : 0u;
-                seg[s0 + r] = e;  // (the segment's partials are all consumed)
-            }
-            if (lane == 0) {
-                kcnt[l] = k;
-                atomicAdd(&nd_blk, tot_nd);  // (a listed lead is counted by the block pass)
-            }
+            nd = lead_wave<LR_SLOTS, LR_FILL>(seg, loff, l, key[w], val[w], kept[w], lane, min_c, max_c, kcnt,
+                                              mid_list, mid_n);
         }
+        if (lane == 0 && nd) atomicAdd(&nd_blk, nd);  // (a listed lead is counted by its tier)
     }
     __syncthreads();
     if (threadIdx.x == 0 && nd_blk) atomicAdd(&distinct[blockIdx.x % NSHARD], (unsigned long long)nd_blk);
+}
+
+// the second tier: one-wave blocks walking the listed leads (14 KB of LDS each: 11 per CU)
+__global__ __launch_bounds__(64) void lead_reduce_mid_kernel(uint2 *seg, const uint32_t *loff, const uint32_t *mid_list,
+                                                             const uint32_t *mid_n, int32_t min_c, int32_t max_c,
+                                                             uint32_t *kcnt, unsigned long long *distinct,
+                                                             uint32_t *big_list, uint32_t *big_n) {
+    __shared__ uint32_t key[LRM_SLOTS], val[LRM_SLOTS];
+    __shared__ uint2 kept[LRM_FILL];
+    const int lane = threadIdx.x;
+    const uint32_t nm = *mid_n;
+    unsigned long long nd = 0;
+    for (uint32_t it = blockIdx.x; it < nm; it += gridDim.x)
+        nd += lead_wave<LRM_SLOTS, LRM_FILL>(seg, loff, mid_list[it], key, val, kept, lane, min_c, max_c, kcnt,
+                                             big_list, big_n);
+    if (lane == 0 && nd) atomicAdd(&distinct[blockIdx.x % NSHARD], nd);
 }
 
 // the listed leads, one 256-thread block each (a fixed grid walks the list):
@@ -414,11 +459,18 @@ hipError_t launch_lead_reduce(const uint32_t *fst, const uint32_t *snd, const ui
     if ((e = hipMemcpyAsync(loff + nl, total_dev, 4, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
     if (n) hipLaunchKernelGGL(lead_tile_kernel<true>, tiles, dim3(LT_THREADS), 0, s, fst, snd, cnt, n, base, lcnt,
                               (const uint32_t *)loff, lcur, seg);
-    if ((e = hipMemsetAsync(big, 0, 4, s)) != hipSuccess) return e;
+    // lists: big[0] = count, big[1 ..] the second tier's leads; big[nl + 1] = count,
+    // big[nl + 2 ..] the block tier's (the caller sizes big for 2 (nl + 1) entries)
+    uint32_t *mid = big, *blk = big + (size_t)nl + 1;
+    if ((e = hipMemsetAsync(mid, 0, 4, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(blk, 0, 4, s)) != hipSuccess) return e;
     hipLaunchKernelGGL(lead_reduce_kernel, dim3((nl + 3) / 4), dim3(256), 0, s, seg, loff, nl, min_c, max_c, kcnt,
-                       distinct, big + 1, big);
-    hipLaunchKernelGGL(lead_reduce_big_kernel, dim3(256), dim3(256), 0, s, seg, loff, (const uint32_t *)(big + 1),
-                       (const uint32_t *)big, min_c, max_c, kcnt, distinct, overflow);
+                       distinct, mid + 1, mid);
+    hipLaunchKernelGGL(lead_reduce_mid_kernel, dim3(nl < 256u * 11u ? nl : 256u * 11u), dim3(64), 0, s, seg, loff,
+                       (const uint32_t *)(mid + 1), (const uint32_t *)mid, min_c, max_c, kcnt, distinct, blk + 1, blk);
+    // (56 KB of LDS per block: 2 per CU)
+    hipLaunchKernelGGL(lead_reduce_big_kernel, dim3(512), dim3(256), 0, s, seg, loff, (const uint32_t *)(blk + 1),
+                       (const uint32_t *)blk, min_c, max_c, kcnt, distinct, overflow);
     return hipGetLastError();
 }
 
