@@ -2574,7 +2574,7 @@ int sa_dist_reduce_pass(sa_ctx *c, const void *fst, const void *snd, const void 
     {
         uint32_t *lr;
         uint2 *seg = (uint2 *)ok;
-        ENSURE(c->d_lr, 7 * ((size_t)nl + 1), &lr);  // (big: the two tiers' lead lists)
+        ENSURE(c->d_lr, 6 * ((size_t)nl + 1), &lr);
         uint32_t *lcnt = lr, *loff = lr + ((size_t)nl + 1), *lcur = lr + 2 * ((size_t)nl + 1),
                  *kcnt = lr + 3 * ((size_t)nl + 1), *kex = lr + 4 * ((size_t)nl + 1), *big = lr + 5 * ((size_t)nl + 1);
         uint8_t *scan2 = scan;

@@ -294,8 +294,12 @@ __device__ __forceinline__ uint32_t lead_wave(uint2 *seg, const uint32_t *loff, 
     const uint32_t tot_nd = (uint32_t)__shfl((int)wave_incl_add(nd), 63, 64);
     if (tot_nd > (uint32_t)FILL || __any(ovf)) {
         if (lane == 0) {
-            kcnt[l] = 0;
-            next_list[atomicAdd(next_n, 1u)] = l;
+            if (next_list) {  // (a list: the block tier's leads are few)
+                kcnt[l] = 0;
+                next_list[atomicAdd(next_n, 1u)] = l;
+            } else {
+                kcnt[l] = 0xFFFFFFFFu;  // KC_MID: the second tier's mark
+            }
         }
         return 0;
     }
@@ -319,12 +323,14 @@ __device__ __forceinline__ uint32_t lead_wave(uint2 *seg, const uint32_t *loff, 
     return tot_nd;
 }
 
-// one wave per lead (a lead with more than LR_ROUTE partials is listed for the second
-// tier straight away); distinct pairs counted once per block
+// one wave per lead; a lead with more than LR_ROUTE partials, or whose partners overflow
+// the table, is marked KC_MID in kcnt for the second tier (a mark, not a list: at configs[3]'s
+// real density nearly every lead goes there, and one list cursor took ~89k same-address
+// atomics per shard and pass -- 0.9 ms); distinct pairs counted once per block
+constexpr uint32_t KC_MID = 0xFFFFFFFFu;
 __global__ __launch_bounds__(256) void lead_reduce_kernel(uint2 *seg, const uint32_t *loff, uint32_t nl, int32_t min_c,
                                                           int32_t max_c, uint32_t *kcnt,
-                                                          unsigned long long *distinct, uint32_t *mid_list,
-                                                          uint32_t *mid_n) {
+                                                          unsigned long long *distinct) {
     __shared__ uint32_t key[4][LR_SLOTS], val[4][LR_SLOTS];
     __shared__ uint2 kept[4][LR_FILL];
     __shared__ uint32_t nd_blk;
@@ -335,33 +341,37 @@ __global__ __launch_bounds__(256) void lead_reduce_kernel(uint2 *seg, const uint
     if (l < nl) {
         uint32_t nd = 0;
         if (loff[l + 1] - loff[l] > LR_ROUTE) {
-            if (lane == 0) {
-                kcnt[l] = 0;
-                mid_list[atomicAdd(mid_n, 1u)] = l;
-            }
+            if (lane == 0) kcnt[l] = KC_MID;
         } else {
             nd = lead_wave<LR_SLOTS, LR_FILL>(seg, loff, l, key[w], val[w], kept[w], lane, min_c, max_c, kcnt,
-                                              mid_list, mid_n);
+                                              nullptr, nullptr);
         }
-        if (lane == 0 && nd) atomicAdd(&nd_blk, nd);  // (a listed lead is counted by its tier)
+        if (lane == 0 && nd) atomicAdd(&nd_blk, nd);  // (a marked lead is counted by its tier)
     }
     __syncthreads();
     if (threadIdx.x == 0 && nd_blk) atomicAdd(&distinct[blockIdx.x % NSHARD], (unsigned long long)nd_blk);
 }
 
-// the second tier: one-wave blocks walking the listed leads (14 KB of LDS each: 11 per CU)
-__global__ __launch_bounds__(64) void lead_reduce_mid_kernel(uint2 *seg, const uint32_t *loff, const uint32_t *mid_list,
-                                                             const uint32_t *mid_n, int32_t min_c, int32_t max_c,
-                                                             uint32_t *kcnt, unsigned long long *distinct,
-                                                             uint32_t *big_list, uint32_t *big_n) {
+// the second tier: one-wave blocks (14 KB of LDS each: 11 per CU) striding over the
+// leads 64 at a time -- one coalesced load of their kcnt, a ballot of the marked ones
+__global__ __launch_bounds__(64) void lead_reduce_mid_kernel(uint2 *seg, const uint32_t *loff, uint32_t nl,
+                                                             int32_t min_c, int32_t max_c, uint32_t *kcnt,
+                                                             unsigned long long *distinct, uint32_t *big_list,
+                                                             uint32_t *big_n) {
     __shared__ uint32_t key[LRM_SLOTS], val[LRM_SLOTS];
     __shared__ uint2 kept[LRM_FILL];
     const int lane = threadIdx.x;
-    const uint32_t nm = *mid_n;
     unsigned long long nd = 0;
-    for (uint32_t it = blockIdx.x; it < nm; it += gridDim.x)
-        nd += lead_wave<LRM_SLOTS, LRM_FILL>(seg, loff, mid_list[it], key, val, kept, lane, min_c, max_c, kcnt,
-                                             big_list, big_n);
+    for (uint32_t c0 = blockIdx.x * 64u; c0 < nl; c0 += gridDim.x * 64u) {
+        const uint32_t l0 = c0 + (uint32_t)lane;
+        unsigned long long todo = __ballot(l0 < nl && kcnt[l0] == KC_MID);
+        while (todo) {
+            const int b = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            nd += lead_wave<LRM_SLOTS, LRM_FILL>(seg, loff, c0 + (uint32_t)b, key, val, kept, lane, min_c, max_c,
+                                                 kcnt, big_list, big_n);
+        }
+    }
     if (lane == 0 && nd) atomicAdd(&distinct[blockIdx.x % NSHARD], nd);
 }
 
@@ -459,15 +469,14 @@ hipError_t launch_lead_reduce(const uint32_t *fst, const uint32_t *snd, const ui
     if ((e = hipMemcpyAsync(loff + nl, total_dev, 4, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
     if (n) hipLaunchKernelGGL(lead_tile_kernel<true>, tiles, dim3(LT_THREADS), 0, s, fst, snd, cnt, n, base, lcnt,
                               (const uint32_t *)loff, lcur, seg);
-    // lists: big[0] = count, big[1 ..] the second tier's leads; big[nl + 1] = count,
-    // big[nl + 2 ..] the block tier's (the caller sizes big for 2 (nl + 1) entries)
-    uint32_t *mid = big, *blk = big + (size_t)nl + 1;
-    if ((e = hipMemsetAsync(mid, 0, 4, s)) != hipSuccess) return e;
+    // the block tier's list: big[0] = count, big[1 ..] the leads
+    uint32_t *blk = big;
     if ((e = hipMemsetAsync(blk, 0, 4, s)) != hipSuccess) return e;
     hipLaunchKernelGGL(lead_reduce_kernel, dim3((nl + 3) / 4), dim3(256), 0, s, seg, loff, nl, min_c, max_c, kcnt,
-                       distinct, mid + 1, mid);
-    hipLaunchKernelGGL(lead_reduce_mid_kernel, dim3(nl < 256u * 11u ? nl : 256u * 11u), dim3(64), 0, s, seg, loff,
-                       (const uint32_t *)(mid + 1), (const uint32_t *)mid, min_c, max_c, kcnt, distinct, blk + 1, blk);
+                       distinct);
+    const uint32_t chunks = (nl + 63) / 64;
+    hipLaunchKernelGGL(lead_reduce_mid_kernel, dim3(chunks < 256u * 11u ? chunks : 256u * 11u), dim3(64), 0, s, seg,
+                       loff, nl, min_c, max_c, kcnt, distinct, blk + 1, blk);
     // (56 KB of LDS per block: 2 per CU)
     hipLaunchKernelGGL(lead_reduce_big_kernel, dim3(512), dim3(256), 0, s, seg, loff, (const uint32_t *)(blk + 1),
                        (const uint32_t *)blk, min_c, max_c, kcnt, distinct, overflow);
