@@ -2574,9 +2574,9 @@ int sa_dist_reduce_pass(sa_ctx *c, const void *fst, const void *snd, const void 
     {
         uint32_t *lr;
         uint2 *seg = (uint2 *)ok;
-        ENSURE(c->d_lr, 6 * ((size_t)nl + 1), &lr);
+        ENSURE(c->d_lr, 5 * ((size_t)nl + 1), &lr);
         uint32_t *lcnt = lr, *loff = lr + ((size_t)nl + 1), *lcur = lr + 2 * ((size_t)nl + 1),
-                 *kcnt = lr + 3 * ((size_t)nl + 1), *kex = lr + 4 * ((size_t)nl + 1), *big = lr + 5 * ((size_t)nl + 1);
+                 *kcnt = lr + 3 * ((size_t)nl + 1), *kex = lr + 4 * ((size_t)nl + 1);
         uint8_t *scan2 = scan;
         Counters *hp;
         if (int rc_ = pinned_counters(c, &hp)) return rc_;
@@ -2584,7 +2584,8 @@ int sa_dist_reduce_pass(sa_ctx *c, const void *fst, const void *snd, const void 
             StageScope st(c, SA_STAGE_ORDER);
             HIPCHK(launch_lead_reduce((const uint32_t *)fst, (const uint32_t *)snd, (const uint32_t *)cnt_in, n, lbase,
                                       nl, c->set.min_collisions, c->set.max_collisions, lcnt, loff, lcur, seg, kcnt,
-                                      cnt->distinct, &cnt->overflow_n, big, scan2, &cnt->totals[1], c->stream));
+                                      cnt->distinct, &cnt->overflow_n, (uint32_t)c->nranks, scan2, &cnt->totals[1],
+                                      c->stream));
             HIPCHK(exclusive_scan_u32(kcnt, kex, nl, &cnt->totals[0], scan2, c->stream));
         }
         HIPCHK(hipMemcpyAsync(hp, cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));

@@ -257,7 +257,7 @@ constexpr uint32_t LR_ROUTE = 2 * LR_FILL;
 template <int SLOTS, int FILL>
 __device__ __forceinline__ uint32_t lead_wave(uint2 *seg, const uint32_t *loff, uint32_t l, uint32_t *key,
                                               uint32_t *val, uint2 *kept, int lane, int32_t min_c, int32_t max_c,
-                                              uint32_t *kcnt, uint32_t *next_list, uint32_t *next_n) {
+                                              uint32_t *kcnt, uint32_t next_mark) {
     constexpr int LOG = SLOTS == 256 ? 8 : SLOTS == 1024 ? 10 : 12;
     static_assert((1 << LOG) == SLOTS, "table size");
     constexpr int PER = SLOTS / 64;
@@ -293,14 +293,7 @@ __device__ __forceinline__ uint32_t lead_wave(uint2 *seg, const uint32_t *loff, 
     }
     const uint32_t tot_nd = (uint32_t)__shfl((int)wave_incl_add(nd), 63, 64);
     if (tot_nd > (uint32_t)FILL || __any(ovf)) {
-        if (lane == 0) {
-            if (next_list) {  // (a list: the block tier's leads are few)
-                kcnt[l] = 0;
-                next_list[atomicAdd(next_n, 1u)] = l;
-            } else {
-                kcnt[l] = 0xFFFFFFFFu;  // KC_MID: the second tier's mark
-            }
-        }
+        if (lane == 0) kcnt[l] = next_mark;
         return 0;
     }
     const uint32_t mine = __popc(kp);
@@ -323,14 +316,24 @@ __device__ __forceinline__ uint32_t lead_wave(uint2 *seg, const uint32_t *loff, 
     return tot_nd;
 }
 
-// one wave per lead; a lead with more than LR_ROUTE partials, or whose partners overflow
-// the table, is marked KC_MID in kcnt for the second tier (a mark, not a list: at configs[3]'s
-// real density nearly every lead goes there, and one list cursor took ~89k same-address
-// atomics per shard and pass -- 0.9 ms); distinct pairs counted once per block
-constexpr uint32_t KC_MID = 0xFFFFFFFFu;
+// The tiers' marks in kcnt: a lead the first table cannot take is marked KC_MID (the
+// 1,024-slot wave tier) or KC_BIG (the 4,096-slot block tier) -- a mark, not a list: at
+// configs[3]'s real density nearly every lead leaves the first tier, and one list cursor
+// took ~89k same-address atomics per shard and pass (0.9 ms).  Leads are routed by their
+// partial count m: a lead has at least m / ranks distinct partners (a partner meets it
+// on at most every rank once), so m > ranks x FILL cannot fit a tier and skips it, and
+// m > ranks x 3,072 sends the whole reduce to the sort at once (*overflow).
+constexpr uint32_t KC_MID = 0xFFFFFFFFu, KC_BIG = 0xFFFFFFFEu;
+constexpr int LRB_SLOTS = 4096, LRB_FILL = 3072;
+__device__ __forceinline__ void set_overflow(uint32_t *overflow) {
+    if (__hip_atomic_load(overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) atomicOr(overflow, 1u);
+}
+
+// one wave per lead; distinct pairs counted once per block
 __global__ __launch_bounds__(256) void lead_reduce_kernel(uint2 *seg, const uint32_t *loff, uint32_t nl, int32_t min_c,
                                                           int32_t max_c, uint32_t *kcnt,
-                                                          unsigned long long *distinct) {
+                                                          unsigned long long *distinct, uint32_t ranks,
+                                                          uint32_t *overflow) {
     __shared__ uint32_t key[4][LR_SLOTS], val[4][LR_SLOTS];
     __shared__ uint2 kept[4][LR_FILL];
     __shared__ uint32_t nd_blk;
@@ -340,11 +343,15 @@ __global__ __launch_bounds__(256) void lead_reduce_kernel(uint2 *seg, const uint
     __syncthreads();
     if (l < nl) {
         uint32_t nd = 0;
-        if (loff[l + 1] - loff[l] > LR_ROUTE) {
+        const uint64_t m = loff[l + 1] - loff[l];
+        if (m > (uint64_t)ranks * LRB_FILL) {
+            if (lane == 0) { kcnt[l] = 0; set_overflow(overflow); }
+        } else if (m > (uint64_t)ranks * LRM_FILL) {
+            if (lane == 0) kcnt[l] = KC_BIG;
+        } else if (m > LR_ROUTE) {
             if (lane == 0) kcnt[l] = KC_MID;
         } else {
-            nd = lead_wave<LR_SLOTS, LR_FILL>(seg, loff, l, key[w], val[w], kept[w], lane, min_c, max_c, kcnt,
-                                              nullptr, nullptr);
+            nd = lead_wave<LR_SLOTS, LR_FILL>(seg, loff, l, key[w], val[w], kept[w], lane, min_c, max_c, kcnt, KC_MID);
         }
         if (lane == 0 && nd) atomicAdd(&nd_blk, nd);  // (a marked lead is counted by its tier)
     }
@@ -356,82 +363,92 @@ __global__ __launch_bounds__(256) void lead_reduce_kernel(uint2 *seg, const uint
 // leads 64 at a time -- one coalesced load of their kcnt, a ballot of the marked ones
 __global__ __launch_bounds__(64) void lead_reduce_mid_kernel(uint2 *seg, const uint32_t *loff, uint32_t nl,
                                                              int32_t min_c, int32_t max_c, uint32_t *kcnt,
-                                                             unsigned long long *distinct, uint32_t *big_list,
-                                                             uint32_t *big_n) {
+                                                             unsigned long long *distinct, const uint32_t *overflow) {
     __shared__ uint32_t key[LRM_SLOTS], val[LRM_SLOTS];
     __shared__ uint2 kept[LRM_FILL];
     const int lane = threadIdx.x;
     unsigned long long nd = 0;
     for (uint32_t c0 = blockIdx.x * 64u; c0 < nl; c0 += gridDim.x * 64u) {
+        if (__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
+            break;  // (the sort takes over; wave-uniform)
         const uint32_t l0 = c0 + (uint32_t)lane;
         unsigned long long todo = __ballot(l0 < nl && kcnt[l0] == KC_MID);
         while (todo) {
             const int b = __builtin_ctzll(todo);
             todo &= todo - 1;
             nd += lead_wave<LRM_SLOTS, LRM_FILL>(seg, loff, c0 + (uint32_t)b, key, val, kept, lane, min_c, max_c,
-                                                 kcnt, big_list, big_n);
+                                                 kcnt, KC_BIG);
         }
     }
     if (lane == 0 && nd) atomicAdd(&distinct[blockIdx.x % NSHARD], nd);
 }
 
-// the listed leads, one 256-thread block each (a fixed grid walks the list):
-// a 4,096-slot table (3,072 partners) summed and filtered as above, the kept
-// entries ranked by trail over the block; beyond 3,072 partners *overflow
-// sends the caller to the sort
-constexpr int LRB_SLOTS = 4096, LRB_FILL = 3072;
-
-__global__ __launch_bounds__(256) void lead_reduce_big_kernel(uint2 *seg, const uint32_t *loff, const uint32_t *big_list,
-                                                              const uint32_t *big_n, int32_t min_c, int32_t max_c,
-                                                              uint32_t *kcnt, unsigned long long *distinct,
-                                                              uint32_t *overflow) {
+// the third tier: 256-thread blocks striding over the leads 256 at a time, each marked
+// KC_BIG lead summed by the whole block in a 4,096-slot table (3,072 partners) and filtered
+// as above, the kept entries ranked by trail over the block; beyond 3,072 partners
+// *overflow sends the caller to the sort
+__global__ __launch_bounds__(256) void lead_reduce_big_kernel(uint2 *seg, const uint32_t *loff, uint32_t nl,
+                                                              int32_t min_c, int32_t max_c, uint32_t *kcnt,
+                                                              unsigned long long *distinct, uint32_t *overflow) {
     __shared__ uint32_t key[LRB_SLOTS], val[LRB_SLOTS];
     __shared__ uint2 kept[LRB_FILL];
-    __shared__ uint32_t fill, bad, nk;
-    const uint32_t nb = *big_n;
-    for (uint32_t it = blockIdx.x; it < nb; it += gridDim.x) {
-        __syncthreads();  // the previous lead's LDS consumed
-        for (int j = threadIdx.x; j < LRB_SLOTS; j += 256) { key[j] = LR_EMPTY; val[j] = 0; }
-        if (threadIdx.x == 0) { fill = 0; bad = 0; nk = 0; }
+    __shared__ uint32_t fill, bad, nk, nlist, stop, list[256];
+    for (uint32_t c0 = blockIdx.x * 256u; c0 < nl; c0 += gridDim.x * 256u) {
+        __syncthreads();  // (list / nlist of the previous chunk consumed)
+        if (threadIdx.x == 0) nlist = 0;
         __syncthreads();
-        const uint32_t l = big_list[it];
-        const uint32_t s0 = loff[l], m = loff[l + 1] - s0;
-        for (uint32_t j = threadIdx.x; j < m; j += 256) {
-            const uint2 v = seg[s0 + j];
-            uint32_t h = (v.x * 0x9E3779B1u) >> 20;  // 12 bits: LRB_SLOTS
-            int probe = 0;
-            for (; probe < 256; ++probe) {
-                uint32_t old = lds_relaxed(&key[h]);
-                if (old == LR_EMPTY) old = atomicCAS(&key[h], LR_EMPTY, v.x);
-                if (old == LR_EMPTY || old == v.x) {
-                    if (old == LR_EMPTY && atomicAdd(&fill, 1u) >= LRB_FILL) bad = 1;
-                    atomicAdd(&val[h], v.y);
-                    break;
-                }
-                h = (h + 1) & (LRB_SLOTS - 1);
+        const uint32_t l0 = c0 + threadIdx.x;
+        if (l0 < nl && kcnt[l0] == KC_BIG) list[atomicAdd(&nlist, 1u)] = l0;
+        __syncthreads();
+        const uint32_t nb = nlist;
+        for (uint32_t it = 0; it < nb; ++it) {
+            __syncthreads();  // the previous lead's LDS consumed
+            for (int j = threadIdx.x; j < LRB_SLOTS; j += 256) { key[j] = LR_EMPTY; val[j] = 0; }
+            if (threadIdx.x == 0) {
+                fill = 0; bad = 0; nk = 0;
+                stop = __hip_atomic_load(overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            if (probe == 256) bad = 1;
-        }
-        __syncthreads();
-        if (bad) {
-            if (threadIdx.x == 0) atomicOr(overflow, 1u);
-            continue;
-        }
-        for (int j = threadIdx.x; j < LRB_SLOTS; j += 256) {
-            const uint32_t k = key[j], c = val[j];
-            if (k != LR_EMPTY && (int32_t)c >= min_c && (int32_t)c <= max_c) kept[atomicAdd(&nk, 1u)] = make_uint2(k, c);
-        }
-        __syncthreads();
-        const uint32_t k = nk;
-        for (uint32_t j = threadIdx.x; j < k; j += 256) {
-            const uint2 e = kept[j];
-            uint32_t r = 0;
-            for (uint32_t q = 0; q < k; ++q) r += kept[q].x < e.x ? 1u : 0u;
-            seg[s0 + r] = e;  // (every partial of the segment was read before the barrier)
-        }
-        if (threadIdx.x == 0) {
-            kcnt[l] = k;
-            atomicAdd(&distinct[blockIdx.x % NSHARD], (unsigned long long)fill);
+            __syncthreads();
+            if (stop) return;  // (block-uniform: the sort takes over, this block's work would be redone)
+            const uint32_t l = list[it];
+            const uint32_t s0 = loff[l], m = loff[l + 1] - s0;
+            for (uint32_t j = threadIdx.x; j < m; j += 256) {
+                const uint2 v = seg[s0 + j];
+                uint32_t h = (v.x * 0x9E3779B1u) >> 20;  // 12 bits: LRB_SLOTS
+                int probe = 0;
+                for (; probe < 256; ++probe) {
+                    uint32_t old = lds_relaxed(&key[h]);
+                    if (old == LR_EMPTY) old = atomicCAS(&key[h], LR_EMPTY, v.x);
+                    if (old == LR_EMPTY || old == v.x) {
+                        if (old == LR_EMPTY && atomicAdd(&fill, 1u) >= LRB_FILL) bad = 1;
+                        atomicAdd(&val[h], v.y);
+                        break;
+                    }
+                    h = (h + 1) & (LRB_SLOTS - 1);
+                }
+                if (probe == 256) bad = 1;
+            }
+            __syncthreads();
+            if (bad) {
+                if (threadIdx.x == 0) set_overflow(overflow);
+                continue;
+            }
+            for (int j = threadIdx.x; j < LRB_SLOTS; j += 256) {
+                const uint32_t k = key[j], c = val[j];
+                if (k != LR_EMPTY && (int32_t)c >= min_c && (int32_t)c <= max_c) kept[atomicAdd(&nk, 1u)] = make_uint2(k, c);
+            }
+            __syncthreads();
+            const uint32_t k = nk;
+            for (uint32_t j = threadIdx.x; j < k; j += 256) {
+                const uint2 e = kept[j];
+                uint32_t r = 0;
+                for (uint32_t q = 0; q < k; ++q) r += kept[q].x < e.x ? 1u : 0u;
+                seg[s0 + r] = e;  // (every partial of the segment was read before the barrier)
+            }
+            if (threadIdx.x == 0) {
+                kcnt[l] = k;
+                atomicAdd(&distinct[blockIdx.x % NSHARD], (unsigned long long)fill);
+            }
         }
     }
 }
@@ -456,7 +473,7 @@ __global__ void lead_copy_kernel(const uint2 *seg, const uint32_t *loff, const u
 hipError_t launch_lead_reduce(const uint32_t *fst, const uint32_t *snd, const uint32_t *cnt, uint64_t n, uint32_t base,
                               uint32_t nl, int32_t min_c, int32_t max_c, uint32_t *lcnt, uint32_t *loff, uint32_t *lcur,
                               uint2 *seg, uint32_t *kcnt, unsigned long long *distinct, uint32_t *overflow,
-                              uint32_t *big, void *scan_tmp, uint32_t *total_dev, hipStream_t s) {
+                              uint32_t ranks, void *scan_tmp, uint32_t *total_dev, hipStream_t s) {
     if (!nl) return hipSuccess;
     hipError_t e;
     if ((e = hipMemsetAsync(lcnt, 0, (size_t)nl * 4, s)) != hipSuccess) return e;
@@ -469,17 +486,14 @@ hipError_t launch_lead_reduce(const uint32_t *fst, const uint32_t *snd, const ui
     if ((e = hipMemcpyAsync(loff + nl, total_dev, 4, hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
     if (n) hipLaunchKernelGGL(lead_tile_kernel<true>, tiles, dim3(LT_THREADS), 0, s, fst, snd, cnt, n, base, lcnt,
                               (const uint32_t *)loff, lcur, seg);
-    // the block tier's list: big[0] = count, big[1 ..] the leads
-    uint32_t *blk = big;
-    if ((e = hipMemsetAsync(blk, 0, 4, s)) != hipSuccess) return e;
     hipLaunchKernelGGL(lead_reduce_kernel, dim3((nl + 3) / 4), dim3(256), 0, s, seg, loff, nl, min_c, max_c, kcnt,
-                       distinct);
-    const uint32_t chunks = (nl + 63) / 64;
-    hipLaunchKernelGGL(lead_reduce_mid_kernel, dim3(chunks < 256u * 11u ? chunks : 256u * 11u), dim3(64), 0, s, seg,
-                       loff, nl, min_c, max_c, kcnt, distinct, blk + 1, blk);
+                       distinct, ranks, overflow);
+    const uint32_t c64 = (nl + 63) / 64, c256 = (nl + 255) / 256;
+    hipLaunchKernelGGL(lead_reduce_mid_kernel, dim3(c64 < 256u * 11u ? c64 : 256u * 11u), dim3(64), 0, s, seg, loff, nl,
+                       min_c, max_c, kcnt, distinct, (const uint32_t *)overflow);
     // (56 KB of LDS per block: 2 per CU)
-    hipLaunchKernelGGL(lead_reduce_big_kernel, dim3(512), dim3(256), 0, s, seg, loff, (const uint32_t *)(blk + 1),
-                       (const uint32_t *)blk, min_c, max_c, kcnt, distinct, overflow);
+    hipLaunchKernelGGL(lead_reduce_big_kernel, dim3(c256 < 512u ? c256 : 512u), dim3(256), 0, s, seg, loff, nl, min_c,
+                       max_c, kcnt, distinct, overflow);
     return hipGetLastError();
 }
 

@@ -619,12 +619,12 @@ hipError_t launch_reduce_heads(const uint64_t *skeys, const uint32_t *sidx, uint
 // segment start): one wave per lead (192 partners), then one wave per lead with
 // 1,024 slots (768), the leads beyond one block each (3,072); *overflow set when a
 // lead has more (the caller then sorts); lcnt / lcur: nl u32, loff: nl + 1 u32,
-// seg: n uint2, big: nl + 1 u32 (the block tier's count + list), total_dev: n
-// (the scan total)
+// seg: n uint2, ranks: the partials' senders (routing: a lead has at least
+// m / ranks distinct partners), total_dev: n (the scan total)
 hipError_t launch_lead_reduce(const uint32_t *fst, const uint32_t *snd, const uint32_t *cnt, uint64_t n, uint32_t base,
                               uint32_t nl, int32_t min_c, int32_t max_c, uint32_t *lcnt, uint32_t *loff, uint32_t *lcur,
                               uint2 *seg, uint32_t *kcnt, unsigned long long *distinct, uint32_t *overflow,
-                              uint32_t *big, void *scan_tmp, uint32_t *total_dev, hipStream_t s);
+                              uint32_t ranks, void *scan_tmp, uint32_t *total_dev, hipStream_t s);
 // the lead-descending dispatch from the reduced segments (kex = exclusive scan
 // of kcnt, total = its sum); ids 1-based, lead = base + l + 1
 hipError_t launch_lead_copy(const uint2 *seg, const uint32_t *loff, const uint32_t *kcnt, const uint32_t *kex,
