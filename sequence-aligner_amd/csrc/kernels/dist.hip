@@ -247,7 +247,7 @@ constexpr uint32_t LR_EMPTY = 0xFFFFFFFFu;
 // the block-per-lead pass took them one block each on a fixed 256-block grid: 3.8 ms per
 // shard and pass, profiles/r06/big/c3real)
 constexpr int LRM_SLOTS = 1024, LRM_FILL = 768;
-constexpr uint32_t LR_ROUTE = 2 * LR_FILL;
+constexpr uint32_t LR_ROUTE = 2 * LR_FILL, LRM_CHUNK = 16;
 
 // One wave sums lead l's partials into a wave-private SLOTS-slot table (trail -> count
 // sum), then compacts the kept entries, ranks them by trail and writes them back over the
@@ -283,12 +283,15 @@ __device__ __forceinline__ uint32_t lead_wave(uint2 *seg, const uint32_t *loff, 
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
     // this lane's PER slots: distinct keys, kept ones compacted by wave prefix
     uint32_t nd = 0, kp = 0;
+    // (the lane's slots into registers first: kept may alias the table)
+    uint32_t kk[PER], kc[PER];
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
-        const uint32_t kk = key[lane * PER + q], kc = val[lane * PER + q];
-        if (kk != LR_EMPTY) {
+        kk[q] = key[lane * PER + q];
+        kc[q] = val[lane * PER + q];
+        if (kk[q] != LR_EMPTY) {
             ++nd;
-            if ((int32_t)kc >= min_c && (int32_t)kc <= max_c) kp |= 1u << q;
+            if ((int32_t)kc[q] >= min_c && (int32_t)kc[q] <= max_c) kp |= 1u << q;
         }
     }
     const uint32_t tot_nd = (uint32_t)__shfl((int)wave_incl_add(nd), 63, 64);
@@ -300,9 +303,11 @@ __device__ __forceinline__ uint32_t lead_wave(uint2 *seg, const uint32_t *loff, 
     const uint32_t ex = wave_incl_add(mine) - mine;
     const uint32_t k = (uint32_t)__shfl((int)(ex + mine), 63, 64);
     uint32_t at = ex;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
 #pragma unroll
     for (int q = 0; q < PER; ++q)
-        if (kp & (1u << q)) kept[at++] = make_uint2(key[lane * PER + q], val[lane * PER + q]);
+        if (kp & (1u << q)) kept[at++] = make_uint2(kk[q], kc[q]);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
     for (uint32_t j = lane; j < k; j += 64) {
@@ -359,20 +364,25 @@ __global__ __launch_bounds__(256) void lead_reduce_kernel(uint2 *seg, const uint
     if (threadIdx.x == 0 && nd_blk) atomicAdd(&distinct[blockIdx.x % NSHARD], (unsigned long long)nd_blk);
 }
 
-// the second tier: one-wave blocks (14 KB of LDS each: 11 per CU) striding over the
-// leads 64 at a time -- one coalesced load of their kcnt, a ballot of the marked ones
+// the second tier: one-wave blocks (8 KB of LDS each: 20 per CU) striding over the leads
+// LRM_CHUNK at a time -- one coalesced load of their kcnt, a ballot of the marked ones
 __global__ __launch_bounds__(64) void lead_reduce_mid_kernel(uint2 *seg, const uint32_t *loff, uint32_t nl,
                                                              int32_t min_c, int32_t max_c, uint32_t *kcnt,
                                                              unsigned long long *distinct, const uint32_t *overflow) {
-    __shared__ uint32_t key[LRM_SLOTS], val[LRM_SLOTS];
-    __shared__ uint2 kept[LRM_FILL];
+    // 8 KB: the kept entries (<= 768 x 8 B) alias the table once it is read into registers,
+    // so 20 one-wave blocks fit a CU (with a separate kept array, 14 KB: 11)
+    __shared__ uint32_t tab[2 * LRM_SLOTS];
+    uint32_t *key = tab, *val = tab + LRM_SLOTS;
+    uint2 *kept = reinterpret_cast<uint2 *>(tab);
     const int lane = threadIdx.x;
     unsigned long long nd = 0;
-    for (uint32_t c0 = blockIdx.x * 64u; c0 < nl; c0 += gridDim.x * 64u) {
+    // chunks of LRM_CHUNK leads: enough blocks to fill the CUs (one 64-lead chunk per block
+    // left ~5 waves per CU, each walking 64 dense leads in a row)
+    for (uint32_t c0 = blockIdx.x * LRM_CHUNK; c0 < nl; c0 += gridDim.x * LRM_CHUNK) {
         if (__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
             break;  // (the sort takes over; wave-uniform)
         const uint32_t l0 = c0 + (uint32_t)lane;
-        unsigned long long todo = __ballot(l0 < nl && kcnt[l0] == KC_MID);
+        unsigned long long todo = __ballot(lane < (int)LRM_CHUNK && l0 < nl && kcnt[l0] == KC_MID);
         while (todo) {
             const int b = __builtin_ctzll(todo);
             todo &= todo - 1;
@@ -488,8 +498,8 @@ hipError_t launch_lead_reduce(const uint32_t *fst, const uint32_t *snd, const ui
                               (const uint32_t *)loff, lcur, seg);
     hipLaunchKernelGGL(lead_reduce_kernel, dim3((nl + 3) / 4), dim3(256), 0, s, seg, loff, nl, min_c, max_c, kcnt,
                        distinct, ranks, overflow);
-    const uint32_t c64 = (nl + 63) / 64, c256 = (nl + 255) / 256;
-    hipLaunchKernelGGL(lead_reduce_mid_kernel, dim3(c64 < 256u * 11u ? c64 : 256u * 11u), dim3(64), 0, s, seg, loff, nl,
+    const uint32_t cm = (nl + LRM_CHUNK - 1) / LRM_CHUNK, c256 = (nl + 255) / 256;
+    hipLaunchKernelGGL(lead_reduce_mid_kernel, dim3(cm < 256u * 20u ? cm : 256u * 20u), dim3(64), 0, s, seg, loff, nl,
                        min_c, max_c, kcnt, distinct, (const uint32_t *)overflow);
     // (56 KB of LDS per block: 2 per CU)
     hipLaunchKernelGGL(lead_reduce_big_kernel, dim3(c256 < 512u ? c256 : 512u), dim3(256), 0, s, seg, loff, nl, min_c,
