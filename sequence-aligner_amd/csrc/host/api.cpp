@@ -505,6 +505,11 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
         PA.tagtab = (const uint8_t *)c->d_tagtab.p;
         PA.occ_off = occ_off;
         PA.n_reads = n_reads; PA.npr = npr; PA.rl = rl; PA.srl = srl; PA.pv = pv; PA.spv = spv;
+        if (pv && c->dist_src_shift) {  // (sharded, source-relative packed values: RecvGen::src_shift)
+            PA.src_shift = c->dist_src_shift;
+            PA.src_own = (uint32_t)c->rank << (c->dist_src_shift - 32);
+            PA.src_starts = (const uint32_t *)c->d_starts.p;
+        }
             PA.npr_magic = npr >= 2 ? ~0ull / npr + 1 : 0;
         PA.len = len;
         PA.lbase = (const uint32_t *)c->d_lbase.p;
@@ -2250,7 +2255,26 @@ int sa_dist_buckets(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uin
     // bits): the occurrence table is packed, 12-byte records in the partition
     // sort, written straight into the sort's value buffer (else {read, loc rank}
     // pairs, 16-byte records)
-    const bool packed = bits_for(N ? N - 1 : 0) + c->lb <= 32;
+    // ... or, when the global ids do not fit but every source's reads do, source-relative
+    // (read - the source's first read, the source in the key's top bits: RecvGen::src_shift;
+    // configs[3]'s 10M reads: 16-byte records through the sort otherwise -- the sort 31 ms per
+    // shard at its real density, profiles/r06/big/c3real)
+    static const bool fuse_env = !getenv("SA_RECV_FUSED") || atoi(getenv("SA_RECV_FUSED")) != 0;
+    // The fused pass counts digits on the raw received keys but ranks the relabelled ones
+    // (low word = local index, top bits the source when source-relative): the two agree only
+    // while the first pass's digit lies between them, i.e. its shift 64 - log_ranks - PB >= 32
+    // (PB up to 23: log_ranks <= 9)
+    const bool fuse_ok = fuse_env && n > 0 && 64 - c->log_ranks - part_bits(n) >= 32;
+    uint32_t max_src = 0;
+    for (int s = 0; s < P; ++s) max_src = std::max(max_src, c->dstarts[s + 1] - c->dstarts[s]);
+    const bool glob_fit = bits_for(N ? N - 1 : 0) + c->lb <= 32;
+    // (SA_SRC_REL = 1 / 0: source-relative whenever it fits / never -- A/B and the GPU tests of the mode at
+    // small sizes)
+    static const int src_env = getenv("SA_SRC_REL") ? atoi(getenv("SA_SRC_REL")) : -1;
+    const bool src_rel = (src_env == 1 || (src_env < 0 && !glob_fit)) && fuse_ok && c->log_ranks > 0 &&
+                         bits_for(max_src ? max_src - 1 : 0) + c->lb <= 32;
+    const bool packed = glob_fit || src_rel;
+    c->dist_src_shift = src_rel ? 64 - c->log_ranks : 0;
     rl = nullptr;
     if (!packed) ENSURE(c->d_rl, n, &rl);
     ENSURE(c->d_loff, (size_t)N + 1, &loff);
@@ -2266,11 +2290,7 @@ int sa_dist_buckets(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uin
     // first pass (RecvGen: the received records are read once, not rewritten
     // first -- 8 serial shards of the bench shape, emit + sort per shard
     // profiles/r05/sharded; SA_RECV_FUSED=0: the separate pass, A/B runs)
-    static const bool fuse_env = !getenv("SA_RECV_FUSED") || atoi(getenv("SA_RECV_FUSED")) != 0;
-    // The fused pass counts digits on the raw received keys but ranks the relabelled ones
-    // (low word = local index): the two agree only while the first pass's digit lies in
-    // the high word, i.e. its shift 64 - log_ranks - PB >= 32 (PB up to 23: log_ranks <= 9)
-    const bool fused = fuse_env && packed && n > 0 && 64 - c->log_ranks - part_bits(n) >= 32;
+    const bool fused = fuse_ok && packed;
     RecvGen RG{};
     if (fused) {
         RG.seg = dseg; RG.P = (uint32_t)P; RG.starts = (const uint32_t *)c->d_starts.p;
@@ -2282,6 +2302,7 @@ int sa_dist_buckets(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uin
         PartArgs sc{};  // (the uniform-length loc-rank identity, as the bucket build checks it)
         set_part_shortcuts(c, sc, c->gnpr);
         RG.lr_ident = sc.lr_ident;
+        RG.src_shift = c->dist_src_shift;
     } else {
         StageScope st(c, SA_STAGE_EMIT);
         HIPCHK(launch_prepare_received(keys, n, dseg, (uint32_t)P, (const uint32_t *)c->d_starts.p,

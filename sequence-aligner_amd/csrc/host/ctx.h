@@ -115,6 +115,7 @@ struct sa_ctx {
     // distributed mode (sa_dist_*): this rank's slice of a global read set
     bool dist = false, dist_reads = false;
     int rank = 0, nranks = 1, log_ranks = 0;
+    int dist_src_shift = 0;                // this build's packed values are source-relative (RecvGen)
     std::vector<uint32_t> dstarts;   // [nranks+1] first global read of each rank
     std::vector<int32_t> dlen;       // length of every global read
     std::vector<uint64_t> gocc;      // global occurrence offsets [N+1]

@@ -64,6 +64,12 @@ __device__ __forceinline__ unsigned long long record_key(uint64_t rec, const Par
         const uint32_t v = *pvp;
         lr = v & ((1u << A.lb) - 1u);
         rr = v >> A.lb;
+        if (A.src_shift) {  // source-relative: the source from the key's top bits, then the owner's bits back
+            const uint32_t s = (uint32_t)(rec >> A.src_shift);
+            rr += A.src_starts[s];
+            const uint64_t low = (1ull << A.src_shift) - 1ull;
+            rec = (rec & low) | ((uint64_t)A.src_own << 32);
+        }
     } else if (rlp) {
         const uint2 v = *rlp;
         lr = v.y;

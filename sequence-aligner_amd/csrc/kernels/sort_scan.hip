@@ -393,10 +393,20 @@ __global__ __launch_bounds__(RsDown<RS_ITEMS>::THREADS, 4) void rs_downsweep_ker
             const bool valid = i < n;
             s = (uint32_t)__builtin_amdgcn_readfirstlane((int)recv_source(rg, tab, s, sub + (uint64_t)j * 64));
             const uint32_t st0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)tab.starts[s]);
-            uint32_t r = 0, lr = 0;
-            if (valid) recv_decode(rg, tab, recv_source(rg, tab, s, i), s, st0, k[j], r, lr);
-            v[j] = (r << rg.lb) | lr;
-            if (valid) k[j] = (k[j] & 0xFFFFFFFF00000000ull) | (uint32_t)i;
+            uint32_t r = 0, lr = 0, sl = s;
+            if (valid) {
+                sl = recv_source(rg, tab, s, i);
+                recv_decode(rg, tab, sl, s, st0, k[j], r, lr);
+            }
+            if (rg.src_shift) {  // source-relative value, the source in the key's top bits
+                v[j] = ((r - (valid ? tab.starts[sl] : 0u)) << rg.lb) | lr;
+                if (valid)
+                    k[j] = (k[j] & (((1ull << rg.src_shift) - 1ull) & 0xFFFFFFFF00000000ull)) |
+                           ((uint64_t)sl << rg.src_shift) | (uint32_t)i;
+            } else {
+                v[j] = (r << rg.lb) | lr;
+                if (valid) k[j] = (k[j] & 0xFFFFFFFF00000000ull) | (uint32_t)i;
+            }
             // loff[a] = i for the reads (read(i - 1), read(i)] (read(-1) = -1)
             uint32_t prev = (uint32_t)__shfl_up((int)r, 1, 64);
             if (lane == 0) prev = rprev;

@@ -377,6 +377,12 @@ struct RecvGen {
     uint64_t *loff;
     uint32_t n_reads;
     int lr_ident;             // uniform lengths whose loc rank is the position (no table lookup)
+    // src_shift > 0: source-relative values -- (read - starts[s]) << lb | loc rank, and the
+    // record's top log2 P key bits (its owner's, the same on every record of this rank)
+    // replaced by the source s; PartArgs::src_shift undoes both (record_key).  For read sets
+    // whose global ids do not fit 32 - lb bits but every source's do (configs[3]: 10M reads
+    // of 486 k-mers, 24 + 9 bits; 1.25M per source, 21 + 9)
+    int src_shift;
 };
 // (key, u32 value) radix sort of received records, values generated (RecvGen)
 hipError_t radix_sort_recv(const RecvGen &g, uint64_t **keys, uint32_t **vals, uint64_t **keys_alt,
@@ -449,6 +455,12 @@ struct PartArgs {
     // the partition sort instead of 16): read << lb | loc rank, by occurrence
     // index (pv) and sorted with the records (spv)
     const uint32_t *pv, *spv;
+    // source-relative packed values (RecvGen::src_shift): the source s sits in the key's top
+    // bits from src_shift on; the read is src_starts[s] + (value >> lb) and the key's top bits
+    // are the owner's again (src_own: those bits of this rank's high key words)
+    int32_t src_shift;
+    uint32_t src_own;
+    const uint32_t *src_starts;
     // sk holds 8-byte records (mix32 << 32 | occurrence index); the loc rank is
     // rl[g].y when given (distributed mode, mixed lengths), else re-derived from
     // the read's length and the position (lrank[lbase[L - k] + pos])
