@@ -471,7 +471,11 @@ int bucket_stage(sa_ctx *c, uint64_t *&keys, uint64_t *&keys2, uint32_t *vals, u
                 // passes instead of 16 (vals / vals2 are free until the global path)
                 uint32_t *v0 = vals, *v1 = vals2;
                 if (recv) {  // received records: relabelled and decoded by the first pass
-                    HIPCHK(radix_sort_recv(*recv, &keys, &v0, &keys2, &v1, n, 64 - skip_bits - PB, 64 - skip_bits,
+                    // (source-relative records carry their source in the key's top bits, which a
+                    // last pass of fewer than 8 bits would read with its digit: the range is
+                    // widened downwards to whole passes -- the same pass count, a finer order)
+                    const int lo_r = recv->src_shift ? 64 - skip_bits - 8 * ((PB + 7) / 8) : 64 - skip_bits - PB;
+                    HIPCHK(radix_sort_recv(*recv, &keys, &v0, &keys2, &v1, n, lo_r, 64 - skip_bits,
                                            stmp, c->stream));
                 } else {
                     if (n && v0 != pv) HIPCHK(hipMemcpyAsync(v0, pv, n * 4, hipMemcpyDeviceToDevice, c->stream));
@@ -2272,6 +2276,7 @@ int sa_dist_buckets(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uin
     // small sizes)
     static const int src_env = getenv("SA_SRC_REL") ? atoi(getenv("SA_SRC_REL")) : -1;
     const bool src_rel = (src_env == 1 || (src_env < 0 && !glob_fit)) && fuse_ok && c->log_ranks > 0 &&
+                         64 - c->log_ranks - 8 * ((part_bits(n) + 7) / 8) >= 32 &&
                          bits_for(max_src ? max_src - 1 : 0) + c->lb <= 32;
     const bool packed = glob_fit || src_rel;
     c->dist_src_shift = src_rel ? 64 - c->log_ranks : 0;
