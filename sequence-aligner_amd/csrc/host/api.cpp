@@ -2436,10 +2436,15 @@ int sa_dist_count_pass(sa_ctx *c, uint32_t pass, uint32_t npass, uint64_t *count
     // so 128-occurrence items overflowed the 192-partner table and went to the recount
     // tiers -- 37 ms of a shard's 72 ms of pair counting, profiles/r06/big/c3real; at the
     // bench shape, 0.33 per occurrence, the target stays 128)
+    // ... and at most 256 occurrences (bench shape, 8 serial shards, same box, 2 rounds: pairs
+    // 1.20-1.27 ms per shard at 128, 1.04 at 256, 1.05 at 384: fewer table set-ups and claims;
+    // profiles/r06/ab/ab_pmw_cap.txt; SA_PMW_CAP for A/B).  The first build, density unknown,
+    // keeps PMW_TARGET.
+    static const uint32_t tcap = getenv("SA_PMW_CAP") ? (uint32_t)atoi(getenv("SA_PMW_CAP")) : 2 * PMW_TARGET;
     uint32_t target = PMW_TARGET;
     if (c->dist_rho_ok && n) {
         const double per_occ = c->dist_rho * (double)c->pbown[P] / (double)n;
-        if (per_occ > 0.0) target = (uint32_t)std::min<double>(PMW_TARGET, std::max(16.0, 96.0 / per_occ));
+        if (per_occ > 0.0) target = (uint32_t)std::min<double>(tcap, std::max(16.0, 96.0 / per_occ));
     }
     uint32_t n_multi = 0;
     uint32_t *istart, *iend = nullptr, *iown = nullptr;
