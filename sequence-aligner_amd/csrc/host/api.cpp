@@ -2197,6 +2197,22 @@ static void pass_range(const sa_ctx *c, int r, uint32_t pass, uint32_t npass, ui
     b = s + (uint32_t)(len * (pass + 1) / npass);
 }
 
+// the partial bounds prefix-summed on the host: per read up to 2^20 reads, else per block
+// of 64 reads (round 6: the per-read bounds of configs[3]'s 10M reads -- 80 MB read back and
+// summed on every shard -- cost 28 ms per shard and build)
+static int ensure_pbcum(sa_ctx *c) {
+    if (!c->pbcum.empty()) return SA_OK;
+    const uint32_t N = (uint32_t)c->dlen.size();
+    c->pb_gran = N <= (1u << 20) ? 1 : 64;
+    const size_t nb = ((size_t)N + c->pb_gran - 1) / c->pb_gran;
+    std::vector<uint64_t> b(nb);
+    const uint64_t *src = (const uint64_t *)c->d_pbound.p + (c->pb_gran == 1 ? 0 : (size_t)N + 1);
+    if (nb) HIPCHK(hipMemcpy(b.data(), src, nb * 8, hipMemcpyDeviceToHost));
+    c->pbcum.assign(nb + 1, 0);
+    for (size_t i = 0; i < nb; ++i) c->pbcum[i + 1] = c->pbcum[i] + b[i];
+    return SA_OK;
+}
+
 // an upper bound of the partials of leads [a, b): the bounds of the blocks of pb_gran reads
 // it touches (exact per read)
 static uint64_t bound_sum(const sa_ctx *c, uint32_t a, uint32_t b) {
@@ -2375,18 +2391,7 @@ int sa_dist_plan(sa_ctx *c, uint64_t budget, uint32_t *npass) {
         return SA_OK;
     }
     (void)hipSetDevice(c->device);
-    const uint32_t N = (uint32_t)c->dlen.size();
-    if (c->pbcum.empty()) {  // the bounds prefix-summed on the host: per read up to 2^20 reads,
-        // else per block of 64 reads (round 6: the per-read bounds of configs[3]'s 10M reads --
-        // 80 MB read back and summed on every shard -- cost 28 ms per shard and build)
-        c->pb_gran = N <= (1u << 20) ? 1 : 64;
-        const size_t nb = ((size_t)N + c->pb_gran - 1) / c->pb_gran;
-        std::vector<uint64_t> b(nb);
-        const uint64_t *src = (const uint64_t *)c->d_pbound.p + (c->pb_gran == 1 ? 0 : (size_t)N + 1);
-        if (nb) HIPCHK(hipMemcpy(b.data(), src, nb * 8, hipMemcpyDeviceToHost));
-        c->pbcum.assign(nb + 1, 0);
-        for (size_t i = 0; i < nb; ++i) c->pbcum[i + 1] = c->pbcum[i] + b[i];
-    }
+    if (int rc = ensure_pbcum(c)) return rc;
     uint64_t maxlen = 1;
     for (int r = 0; r < P; ++r) maxlen = std::max<uint64_t>(maxlen, c->dstarts[r + 1] - c->dstarts[r]);
     // the largest pass of an np-pass plan on this rank (every owner's range of the pass)
@@ -2520,6 +2525,43 @@ int sa_dist_count_pass(sa_ctx *c, uint32_t pass, uint32_t npass, uint64_t *count
     }
     return SA_OK;
 }
+
+extern "C++" {
+namespace sa {
+// The first build of a read set does not know its partials / bound ratio (rho: the pass
+// budget and the pair-count items are sized by it).  A probe counts the partials of the top
+// 1/64 of every owner's leads -- counted, not kept -- and takes their ratio to the same
+// leads' bound (round 6: configs[3]'s real read set on 8 virtual shards planned 23 passes
+// at rho = 1 instead of ~10, and its 128-occurrence items overflowed into the recount tier:
+// count 756 ms + reduce 236 ms in the first build against 316 + 161 once rho was known)
+int dist_probe_rho(sa_ctx *c) {
+    if (!c || !c->dist_bkt || c->dist_rho_ok) return SA_OK;
+    const int P = c->nranks;
+    if (c->pbown.size() != (size_t)P + 1 || c->pbown[P] == 0) return SA_OK;
+    (void)hipSetDevice(c->device);
+    if (int rc = ensure_pbcum(c)) return rc;
+    constexpr uint32_t NP = 64;
+    uint64_t b = 0;
+    for (int r = 0; r < P; ++r) {
+        uint32_t lo, hi;
+        pass_range(c, r, NP - 1, NP, lo, hi);
+        b += bound_sum(c, lo, hi);
+    }
+    if (b == 0) return SA_OK;
+    std::vector<uint64_t> counts((size_t)P);
+    const uint64_t rp = c->stats.role_pairs, acc = c->dist_parts_acc;
+    int rc = sa_dist_count_pass(c, NP - 1, NP, counts.data());
+    if (rc) return rc;
+    c->stats.role_pairs = rp;  // (the probe's counts belong to no build)
+    c->dist_parts_acc = acc;
+    uint64_t parts = 0;
+    for (uint64_t v : counts) parts += v;
+    c->dist_rho = std::max(0.02, (double)parts / (double)b);
+    c->dist_rho_ok = true;
+    return SA_OK;
+}
+}  // namespace sa
+}  // extern "C++"
 
 int sa_dist_count(sa_ctx *c, void *recv_recs, const uint64_t *recv_counts, uint64_t *counts) {
     if (!c || !counts || !recv_counts) return SA_E_ARG;

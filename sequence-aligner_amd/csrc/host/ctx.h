@@ -198,6 +198,8 @@ int multi_gather_ovl(sa_ctx *c, std::string &all);
 int multi_set_option(sa_ctx *c, int option, int64_t value);
 void multi_stage_times(const sa_ctx *c, double *ms, uint64_t *n);
 void multi_reset_stage_times(sa_ctx *c);
+// (api.cpp) the first build of a read set: its partials / bound ratio from a probe pass
+int dist_probe_rho(sa_ctx *c);
 int multi_sync(sa_ctx *c);
 uint64_t multi_exchanged_bytes(const sa_ctx *c);
 }  // namespace sa

@@ -507,6 +507,10 @@ int multi_build(sa_ctx *c, bool readback, int (*single_build)(sa_ctx *, bool)) {
     // ---- lead-range passes: every pass holds the partials of 1/npass of every
     // owner's leads, within the budget on every shard (all ranks agree on npass)
     mark("buckets");
+    // (the first build of a read set: its partials / bound ratio from a probe, api.cpp)
+    rc = for_shards(c, [&](Shard &s) { return sa::dist_probe_rho(s.child); }, true);
+    if (rc) return rc;
+    mark("probe");
     std::vector<uint64_t> budget(m->sh.size());
     for (size_t l = 0; l < m->sh.size(); ++l) budget[l] = pass_budget(m, m->sh[l]);
     uint32_t npass = 1;
