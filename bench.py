@@ -427,8 +427,9 @@ def main():
     ov.sync()
     t_first = max_over_ranks(time.perf_counter() - t0)
     note("first build done")
-    # the first build after the allocations: what a single CLI run pays
-    # (nothing is remembered between builds of one read set), then warm-up
+    # the first build after the allocations: what a single CLI run pays, then warm-up
+    # (nothing is remembered between builds of one read set except, on the sharded
+    # path, its partials / bound ratio -- which a first build estimates with a probe)
     t_second = None
     for i in range(args.warmup):
         ov.sync()
