@@ -2522,6 +2522,9 @@ int sa_dist_count_pass(sa_ctx *c, uint32_t pass, uint32_t npass, uint64_t *count
     if (pass == 0 && c->pbown[P] > 0) {  // the whole count ran: these reads' partials / bound
         c->dist_rho = (double)c->dist_parts_acc / (double)c->pbown[P];
         c->dist_rho_ok = true;
+        if (getenv("SA_DEBUG_PHASES"))
+            fprintf(stderr, "[sa rho] rank %d: %llu partials / %llu bound = %.4f\n", c->rank,
+                    (unsigned long long)c->dist_parts_acc, (unsigned long long)c->pbown[P], c->dist_rho);
     }
     return SA_OK;
 }
@@ -2558,6 +2561,9 @@ int dist_probe_rho(sa_ctx *c) {
     for (uint64_t v : counts) parts += v;
     c->dist_rho = std::max(0.02, (double)parts / (double)b);
     c->dist_rho_ok = true;
+    if (getenv("SA_DEBUG_PHASES"))
+        fprintf(stderr, "[sa probe] rank %d: %llu partials / %llu bound = %.4f (whole bound %llu)\n", c->rank,
+                (unsigned long long)parts, (unsigned long long)b, c->dist_rho, (unsigned long long)c->pbown[P]);
     return SA_OK;
 }
 }  // namespace sa
