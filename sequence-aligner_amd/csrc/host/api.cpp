@@ -1322,17 +1322,41 @@ int device_build(sa_ctx *c, bool readback) {
     } else {
         // every distinct pair came back (strict: in first-insertion order; wide: lead desc)
         HostScope hs(c, SA_STAGE_REPLAY);
+        // strict: PairData's Trove layout of the keys (fst << 16) ^ snd inserted in
+        // first-occurrence order is built on the device (trove_replay.hip: the host replay,
+        // one insert after another at DRAM latency, was ~170 ms of configs[0]'s 0.2 s end to
+        // end), and the pairs come back permuted into its iteration order
+        static const bool host_replay = getenv("SA_HOST_TROVE") && atoi(getenv("SA_HOST_TROVE")) != 0;  // (A/B)
+        const bool dev_replay = strict && !host_replay && np > 0;
+        const int32_t *rf = dlead, *rs = dtrail, *rk = dcount;
+        if (dev_replay) {
+            uint8_t *tb;
+            const size_t need = 5 * (size_t)np * 4 + trove_temp_bytes((uint32_t)np) + 256;
+            ENSURE(c->d_trove, need, &tb);
+            int32_t *keys = (int32_t *)tb, *fo = keys + np, *so = fo + np, *ko = so + np;
+            uint32_t *order = (uint32_t *)(ko + np);
+            void *ttmp = (void *)(order + np);
+            HIPCHK(launch_trove_pair_keys(dlead, dtrail, (uint32_t)np, keys, c->stream));
+            uint32_t tcap = 0;
+            HIPCHK(trove_layout_device(keys, (uint32_t)np, order, ttmp, c->stream, &tcap));
+            HIPCHK(launch_trove_gather3(order, (uint32_t)np, dlead, dtrail, dcount, fo, so, ko, c->stream));
+            rf = fo; rs = so; rk = ko;
+        }
         std::vector<int32_t> f(np), s(np), k(np);
         if (np) {
-            HIPCHK(hipMemcpy(f.data(), dlead, np * 4, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(s.data(), dtrail, np * 4, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(k.data(), dcount, np * 4, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpyAsync(f.data(), rf, np * 4, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipMemcpyAsync(s.data(), rs, np * 4, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipMemcpyAsync(k.data(), rk, np * 4, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
         }
         if (strict) {
             // PairData: Trove layout of keys (fst<<16)^snd inserted in first-occurrence
-            // order, each slot carrying its pair's index (the count without a lookup)
+            // order, each slot carrying its pair's index (the count without a lookup);
+            // with the device layout the pairs already are in its iteration order
             TroveLayout pd;
-            for (uint64_t i = 0; i < np; ++i) pd.insert((int32_t)(((uint32_t)f[i] << 16) ^ (uint32_t)s[i]), (int32_t)i);
+            if (!dev_replay)
+                for (uint64_t i = 0; i < np; ++i)
+                    pd.insert((int32_t)(((uint32_t)f[i] << 16) ^ (uint32_t)s[i]), (int32_t)i);
             // calcDispatchData (KmerTable.scala:155-187) over PairData iteration order:
             // DispatchData's Trove layout over the leads, each lead's (trail, count)
             // list in that order.  Decoded leads are 16-bit (key >> 16, E4): a lead's
@@ -1341,7 +1365,7 @@ int device_build(sa_ctx *c, bool readback) {
             std::vector<std::vector<std::pair<int32_t, int32_t>>> lists;
             std::vector<int32_t> list_of(1 << 16, -1);  // lead + 32,768 -> list index
             bool id_err = false;
-            pd.for_each_kv([&](int32_t key, int32_t ix) {
+            auto each_pair = [&](int32_t key, int32_t ix) {
                 const int32_t cnt_ = k[(uint32_t)ix];
                 const int32_t a = key >> 16;
                 const int32_t b = (int32_t)((uint32_t)key << 16) >> 16;
@@ -1356,7 +1380,13 @@ int device_build(sa_ctx *c, bool readback) {
                     lists[(size_t)li].push_back({b, cnt_});
                     if (a < 1 || a > (int32_t)nr || b < 1 || b > (int32_t)nr) id_err = true;
                 }
-            });
+            };
+            if (dev_replay) {
+                for (uint64_t j = 0; j < np; ++j)
+                    each_pair((int32_t)(((uint32_t)f[j] << 16) ^ (uint32_t)s[j]), (int32_t)j);
+            } else {
+                pd.for_each_kv(each_pair);
+            }
             if (id_err)
                 return fail(c, SA_E_ID_RANGE, "strict ids: a dispatched pair decodes to an id outside 1..N "
                                               "(reference NullPointerException, KmerTable.scala:263-265)");
@@ -1710,7 +1740,7 @@ void sa_ctx_destroy(sa_ctx *c) {
                     &c->d_tedi, &c->d_xrec, &c->d_tier, &c->d_ovlrp, &c->d_meta, &c->d_items, &c->d_pq, &c->d_ocur, &c->d_lr, &c->d_bigtot, &c->d_hk0, &c->d_hk1, &c->d_hflag,
                     &c->d_hidx, &c->d_hpos, &c->d_htmp, &c->d_hist, &c->d_hovf, &c->d_hsmall,
                     &c->d_ltb, &c->d_lmax, &c->d_rreg, &c->d_rcnt, &c->d_rex,
-                    &c->d_shl, &c->d_sht, &c->d_shc, &c->d_rsh, &c->d_pbound, &c->d_pbown, &c->d_prange,
+                    &c->d_shl, &c->d_sht, &c->d_shc, &c->d_rsh, &c->d_pbound, &c->d_pbown, &c->d_trove, &c->d_prange,
                     &c->d_pioff, &c->d_pitems};
     for (DBuf *b : bufs)
         if (b->p && !b->borrowed) (void)hipFree(b->p);

@@ -151,6 +151,7 @@ struct sa_ctx {
     uint64_t dist_parts_acc = 0;           // partials of the passes run so far
     uint64_t disp_acc = 0;                 // dispatched pairs the reduce passes appended so far
     DBuf d_pbound, d_pbown, d_prange, d_pioff, d_pitems;
+    DBuf d_trove;                          // strict ids: the device Trove layout's keys, order and scratch
     // k-mer table statistics (sa_kmer_histogram)
     DBuf d_hk0, d_hk1, d_hflag, d_hidx, d_hpos, d_htmp, d_hist, d_hovf, d_hsmall;
     std::vector<uint64_t> hsize, hcount;

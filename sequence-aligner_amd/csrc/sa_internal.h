@@ -388,6 +388,17 @@ struct RecvGen {
 hipError_t radix_sort_recv(const RecvGen &g, uint64_t **keys, uint32_t **vals, uint64_t **keys_alt,
                            uint32_t **vals_alt, uint64_t n, int lo, int hi, void *tmp, hipStream_t s);
 
+// GNU Trove 3.0.3 layout (csrc/host/trove.h semantics, rehash chain included) of m distinct
+// keys inserted in index order, built on the device (trove_replay.hip): out_order[j] = the
+// index of the key in the j-th slot of iteration order (slot cap - 1 down to 0).  tmp:
+// trove_temp_bytes(m); the final capacity in *final_cap
+size_t trove_temp_bytes(uint32_t m);
+hipError_t trove_layout_device(const int32_t *keys, uint32_t m, uint32_t *out_order, void *tmp, hipStream_t s,
+                               uint32_t *final_cap);
+hipError_t launch_trove_pair_keys(const int32_t *f, const int32_t *s, uint32_t n, int32_t *keys, hipStream_t st);
+hipError_t launch_trove_gather3(const uint32_t *order, uint32_t n, const int32_t *f, const int32_t *s, const int32_t *k,
+                                int32_t *fo, int32_t *so, int32_t *ko, hipStream_t st);
+
 // exclusive scan of u32 (in place allowed), returns total in *total_dev
 size_t scan_temp_bytes(uint64_t n);
 hipError_t exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *total_dev,
