@@ -1196,42 +1196,55 @@ int device_build(sa_ctx *c, bool readback) {
         // distinct hashes in first-occurrence order (KmerTable.scala:45-50).  A
         // bucket is named by the sorted position of its head record.
         HostScope hs(c, SA_STAGE_REPLAY);
-        std::vector<uint8_t> head(n);
-        std::vector<uint32_t> first(n);
-        if (n) {
-            HIPCHK(hipMemcpy(head.data(), PA.is_head, n, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(first.data(), PA.bkt_first, n * 4, hipMemcpyDeviceToHost));
-        }
-        // the buckets in first-occurrence order: first occurrences are distinct indices < n,
-        // so each head lands at its own slot of a g-indexed table and one ascending walk
-        // reads them in order -- with the read of g advancing monotonically (no sort of the
-        // ~2M heads, no binary search per head)
-        std::vector<uint32_t> by_g(n, 0);  // head position + 1 of the bucket first met at g
-        for (uint64_t i = 0; i < n; ++i)
-            if (head[i]) by_g[first[i]] = (uint32_t)i + 1;
-        TroveLayout kd;
-        const int k = c->set.kmer_size, mm = c->m;
-        uint32_t r = 0;
-        for (uint64_t g = 0; g < n; ++g) {
-            const uint32_t hp = by_g[g];
-            if (!hp) continue;
-            while (c->occ_off[r + 1] <= g) ++r;  // the last read with occ_off[r] <= g
-            const char *sq = c->bases.data() + c->boff[r] + (g - c->occ_off[r]);
-            uint32_t h = 0;  // Kmer.seqHash (ObjectStore.scala:48-67)
-            for (int q = 0; q < mm; ++q) {
-                char ch = sq[q];
-                if (ch >= 'a' && ch <= 'z') ch = (char)(ch - 32);
-                h <<= 2;
-                h ^= ch == 'C' ? 1u : ch == 'T' ? 2u : ch == 'G' ? 3u : 0u;
+        static const bool host_replay = getenv("SA_HOST_TROVE") && atoi(getenv("SA_HOST_TROVE")) != 0;  // (A/B)
+        if (!host_replay) {
+            // on the device (trove_replay.hip): heads by first occurrence, their seqHash from
+            // the packed reads, the layout, the ranks -- no readback of the 5 B per k-mer of
+            // head flags and first occurrences
+            uint8_t *kt;
+            ENSURE(c->d_trove, kmerdata_temp_bytes(n), &kt);
+            uint32_t heads = 0;
+            HIPCHK(kmerdata_rank_device(PA.is_head, PA.bkt_first, n, dev_reads(c), (const uint64_t *)c->d_occ_off.p, nr,
+                                        c->m, c->bkt_rank_dev, kt, c->stream, &heads));
+            if (heads >= (1u << 26)) return fail(c, SA_E_OVERFLOW, "strict ids: more than 2^26 distinct k-mers");
+        } else {
+            std::vector<uint8_t> head(n);
+            std::vector<uint32_t> first(n);
+            if (n) {
+                HIPCHK(hipMemcpy(head.data(), PA.is_head, n, hipMemcpyDeviceToHost));
+                HIPCHK(hipMemcpy(first.data(), PA.bkt_first, n * 4, hipMemcpyDeviceToHost));
             }
-            (void)k;
-            kd.insert((int32_t)h, (int32_t)(hp - 1));  // (distinct hashes: every insert is fresh)
+            // the buckets in first-occurrence order: first occurrences are distinct indices < n,
+            // so each head lands at its own slot of a g-indexed table and one ascending walk
+            // reads them in order -- with the read of g advancing monotonically (no sort of the
+            // ~2M heads, no binary search per head)
+            std::vector<uint32_t> by_g(n, 0);  // head position + 1 of the bucket first met at g
+            for (uint64_t i = 0; i < n; ++i)
+                if (head[i]) by_g[first[i]] = (uint32_t)i + 1;
+            TroveLayout kd;
+            const int k = c->set.kmer_size, mm = c->m;
+            uint32_t r = 0;
+            for (uint64_t g = 0; g < n; ++g) {
+                const uint32_t hp = by_g[g];
+                if (!hp) continue;
+                while (c->occ_off[r + 1] <= g) ++r;  // the last read with occ_off[r] <= g
+                const char *sq = c->bases.data() + c->boff[r] + (g - c->occ_off[r]);
+                uint32_t h = 0;  // Kmer.seqHash (ObjectStore.scala:48-67)
+                for (int q = 0; q < mm; ++q) {
+                    char ch = sq[q];
+                    if (ch >= 'a' && ch <= 'z') ch = (char)(ch - 32);
+                    h <<= 2;
+                    h ^= ch == 'C' ? 1u : ch == 'T' ? 2u : ch == 'G' ? 3u : 0u;
+                }
+                (void)k;
+                kd.insert((int32_t)h, (int32_t)(hp - 1));  // (distinct hashes: every insert is fresh)
+            }
+            std::vector<uint32_t> rank(n, 0);
+            uint32_t rk = 0;
+            kd.for_each_kv([&](int32_t, int32_t pos) { rank[(uint32_t)pos] = rk++; });
+            if (rk >= (1u << 26)) return fail(c, SA_E_OVERFLOW, "strict ids: more than 2^26 distinct k-mers");
+            if (n) HIPCHK(hipMemcpy(c->bkt_rank_dev, rank.data(), n * 4, hipMemcpyHostToDevice));
         }
-        std::vector<uint32_t> rank(n, 0);
-        uint32_t rk = 0;
-        kd.for_each_kv([&](int32_t, int32_t pos) { rank[(uint32_t)pos] = rk++; });
-        if (rk >= (1u << 26)) return fail(c, SA_E_OVERFLOW, "strict ids: more than 2^26 distinct k-mers");
-        if (n) HIPCHK(hipMemcpy(c->bkt_rank_dev, rank.data(), n * 4, hipMemcpyHostToDevice));
     }
     PairIn PI{};
     PI.rec = PA.rec; PI.xrec = PA.xrec; PI.lst = PA.lst;

@@ -179,3 +179,77 @@ hipError_t launch_trove_gather3(const uint32_t *order, uint32_t n, const int32_t
 }
 
 }  // namespace sa
+
+// ---------------------------------------------------------------------------
+// KmerData (KmerTable.scala:45-50): the buckets' iteration rank, from the Trove layout
+// of their seqHash values inserted in first-occurrence order.  A bucket is named by
+// the sorted position of its head record (is_head / bkt_first from the bucket build).
+// ---------------------------------------------------------------------------
+namespace sa {
+namespace {
+__global__ void kd_by_g_kernel(const uint8_t *head, const uint32_t *first, uint64_t n, uint32_t *by_g) {
+    const uint64_t i = (uint64_t)blockIdx.x * TR_T + threadIdx.x;
+    if (i < n && head[i]) by_g[first[i]] = (uint32_t)i + 1u;
+}
+__global__ void kd_flags_kernel(const uint32_t *by_g, uint64_t n, uint32_t *flag) {
+    const uint64_t g = (uint64_t)blockIdx.x * TR_T + threadIdx.x;
+    if (g < n) flag[g] = by_g[g] != 0 ? 1u : 0u;
+}
+// the heads in first-occurrence order: their positions and the seqHash of their k-mer
+// (ObjectStore.scala:48-67: the first min(16, k) bases, h = (h << 2) ^ code, A0 C1 T2 G3 --
+// the packed HOXD codes A0 C1 G2 T3 mapped by c ^ (c >> 1))
+__global__ void kd_keys_kernel(const uint32_t *by_g, const uint32_t *flag, const uint32_t *ex, uint64_t n,
+                               DevReads rd, const uint64_t *occ_off, uint32_t n_reads, int shift, uint32_t *hpos,
+                               int32_t *keys) {
+    const uint64_t g = (uint64_t)blockIdx.x * TR_T + threadIdx.x;
+    if (g >= n || !flag[g]) return;
+    uint32_t lo = 0, hi = n_reads;  // the read of occurrence g: the largest r with occ_off[r] <= g
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (occ_off[mid] <= g) lo = mid; else hi = mid;
+    }
+    const int32_t pos = (int32_t)(g - occ_off[lo]);
+    uint32_t x = window16(rd.codes + rd.woff[lo], pos);
+    x = shift == 32 ? 0u : (x >> shift);
+    x ^= (x >> 1) & 0x55555555u;
+    const uint32_t j = ex[g];
+    hpos[j] = by_g[g] - 1u;
+    keys[j] = (int32_t)x;
+}
+__global__ void kd_rank_kernel(const uint32_t *order, uint32_t m, const uint32_t *hpos, uint32_t *rank) {
+    const uint32_t j = blockIdx.x * TR_T + threadIdx.x;
+    if (j < m) rank[hpos[order[j]]] = j;
+}
+}  // namespace
+
+size_t kmerdata_temp_bytes(uint64_t n) {
+    // by_g, flag, ex, hpos, keys, order (n each), the head count, the layout's scratch
+    return (6 * n + 64) * 4 + std::max<size_t>(scan_temp_bytes(n), trove_temp_bytes((uint32_t)n)) + 256;
+}
+
+hipError_t kmerdata_rank_device(const uint8_t *is_head, const uint32_t *bkt_first, uint64_t n, const DevReads &rd,
+                                const uint64_t *occ_off, uint32_t n_reads, int m_hash, uint32_t *rank, void *tmp,
+                                hipStream_t s, uint32_t *n_heads) {
+    *n_heads = 0;
+    hipError_t e;
+    if ((e = hipMemsetAsync(rank, 0, n * 4, s)) != hipSuccess || n == 0) return e;
+    uint32_t *by_g = (uint32_t *)tmp, *flag = by_g + n, *ex = flag + n, *hpos = ex + n;
+    int32_t *keys = (int32_t *)(hpos + n);
+    uint32_t *order = (uint32_t *)(keys + n), *total = order + n;
+    void *stmp = (void *)(total + 64);
+    if ((e = hipMemsetAsync(by_g, 0, n * 4, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(kd_by_g_kernel, tr_grid(n), dim3(TR_T), 0, s, is_head, bkt_first, n, by_g);
+    hipLaunchKernelGGL(kd_flags_kernel, tr_grid(n), dim3(TR_T), 0, s, by_g, n, flag);
+    if ((e = exclusive_scan_u32(flag, ex, n, total, stmp, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(kd_keys_kernel, tr_grid(n), dim3(TR_T), 0, s, by_g, flag, ex, n, rd, occ_off, n_reads,
+                       32 - 2 * m_hash, hpos, keys);
+    uint32_t m = 0;
+    if ((e = hipMemcpyAsync(&m, total, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    *n_heads = m;
+    uint32_t cap = 0;
+    if ((e = trove_layout_device(keys, m, order, stmp, s, &cap)) != hipSuccess) return e;
+    if (m) hipLaunchKernelGGL(kd_rank_kernel, tr_grid(m), dim3(TR_T), 0, s, order, m, hpos, rank);
+    return hipGetLastError();
+}
+}  // namespace sa

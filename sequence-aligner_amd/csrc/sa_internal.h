@@ -395,6 +395,13 @@ hipError_t radix_sort_recv(const RecvGen &g, uint64_t **keys, uint32_t **vals, u
 size_t trove_temp_bytes(uint32_t m);
 hipError_t trove_layout_device(const int32_t *keys, uint32_t m, uint32_t *out_order, void *tmp, hipStream_t s,
                                uint32_t *final_cap);
+// KmerData's bucket iteration ranks (rank[head position] = its place in the Trove layout of
+// the buckets' seqHash values in first-occurrence order; 0 elsewhere), the head count in
+// *n_heads; tmp: kmerdata_temp_bytes(n)
+size_t kmerdata_temp_bytes(uint64_t n);
+hipError_t kmerdata_rank_device(const uint8_t *is_head, const uint32_t *bkt_first, uint64_t n, const DevReads &rd,
+                                const uint64_t *occ_off, uint32_t n_reads, int m_hash, uint32_t *rank, void *tmp,
+                                hipStream_t s, uint32_t *n_heads);
 hipError_t launch_trove_pair_keys(const int32_t *f, const int32_t *s, uint32_t n, int32_t *keys, hipStream_t st);
 hipError_t launch_trove_gather3(const uint32_t *order, uint32_t n, const int32_t *f, const int32_t *s, const int32_t *k,
                                 int32_t *fo, int32_t *so, int32_t *ko, hipStream_t st);
