@@ -7,7 +7,7 @@
 //   radix_sort      group by hash, loc order, g-stable          (KmerData, KmerTable.scala:41-53)
 //   build_buckets   middle / edge lists + partner ranges        (calcPairData split, :97-115)
 //   pair_count      per-read LDS aggregation + [min,max] filter (addKmerPair / calcDispatchData)
-//   order           wide: lead desc / trail asc; strict: first-occurrence rank -> host Trove replay
+//   order           wide: lead desc / trail asc; strict: first-occurrence rank -> Trove layouts (device)
 //   dovetail        banded two-phase DP + validity             (generateFastDovetailAlignmentSet)
 // then the .ovl writer (Project4.calcOverlaps) on the host.
 #include "../../../include/sa_overlap.h"
@@ -1344,7 +1344,11 @@ int device_build(sa_ctx *c, bool readback) {
         const int32_t *rf = dlead, *rs = dtrail, *rk = dcount;
         if (dev_replay) {
             uint8_t *tb;
-            const size_t need = 5 * (size_t)np * 4 + trove_temp_bytes((uint32_t)np) + 256;
+            // keys, fo / so / ko, order, then the layout's scratch -- which the dispatched pairs'
+            // compaction reuses afterwards (3 n + n + 64 words + a scan's scratch: within it)
+            const size_t need = 5 * (size_t)np * 4 +
+                                std::max(trove_temp_bytes((uint32_t)np), (4 * (size_t)np + 64) * 4 + scan_temp_bytes(np)) +
+                                256;
             ENSURE(c->d_trove, need, &tb);
             int32_t *keys = (int32_t *)tb, *fo = keys + np, *so = fo + np, *ko = so + np;
             uint32_t *order = (uint32_t *)(ko + np);
@@ -1355,11 +1359,28 @@ int device_build(sa_ctx *c, bool readback) {
             HIPCHK(launch_trove_gather3(order, (uint32_t)np, dlead, dtrail, dcount, fo, so, ko, c->stream));
             rf = fo; rs = so; rk = ko;
         }
-        std::vector<int32_t> f(np), s(np), k(np);
-        if (np) {
-            HIPCHK(hipMemcpyAsync(f.data(), rf, np * 4, hipMemcpyDeviceToHost, c->stream));
-            HIPCHK(hipMemcpyAsync(s.data(), rs, np * 4, hipMemcpyDeviceToHost, c->stream));
-            HIPCHK(hipMemcpyAsync(k.data(), rk, np * 4, hipMemcpyDeviceToHost, c->stream));
+        // (device layout without SA_OPT_KEEP_PAIRS: only the dispatched pairs come back --
+        // the filter and the compaction run on the device, in iteration order)
+        uint64_t nb = np;
+        if (dev_replay && !c->keep_pairs) {
+            int32_t *keys = (int32_t *)c->d_trove.p, *fo = keys + np, *so = fo + np, *ko = so + np;
+            uint32_t *order = (uint32_t *)(ko + np), *flag = (uint32_t *)keys, *tot = order;
+            int32_t *fk = (int32_t *)(order + np), *sk = fk + np, *kk = sk + np;
+            uint32_t *ex = (uint32_t *)(kk + np);
+            void *stmp = (void *)(ex + np + 64);
+            HIPCHK(launch_trove_keep(fo, so, ko, (uint32_t)np, c->set.min_collisions, c->set.max_collisions, flag, ex,
+                                     tot, stmp, fk, sk, kk, c->stream));
+            uint32_t nk = 0;
+            HIPCHK(hipMemcpyAsync(&nk, tot, 4, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            nb = nk;
+            rf = fk; rs = sk; rk = kk;
+        }
+        std::vector<int32_t> f(nb), s(nb), k(nb);
+        if (nb) {
+            HIPCHK(hipMemcpyAsync(f.data(), rf, nb * 4, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipMemcpyAsync(s.data(), rs, nb * 4, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipMemcpyAsync(k.data(), rk, nb * 4, hipMemcpyDeviceToHost, c->stream));
             HIPCHK(hipStreamSynchronize(c->stream));
         }
         if (strict) {
@@ -1395,7 +1416,7 @@ int device_build(sa_ctx *c, bool readback) {
                 }
             };
             if (dev_replay) {
-                for (uint64_t j = 0; j < np; ++j)
+                for (uint64_t j = 0; j < nb; ++j)
                     each_pair((int32_t)(((uint32_t)f[j] << 16) ^ (uint32_t)s[j]), (int32_t)j);
             } else {
                 pd.for_each_kv(each_pair);

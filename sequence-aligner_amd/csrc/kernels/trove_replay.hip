@@ -253,3 +253,34 @@ hipError_t kmerdata_rank_device(const uint8_t *is_head, const uint32_t *bkt_firs
     return hipGetLastError();
 }
 }  // namespace sa
+
+// the pairs of PairData's iteration order whose count passes [min_c, max_c]
+// (calcDispatchData's filter, KmerTable.scala:155-187), compacted in that order
+namespace sa {
+namespace {
+__global__ void tr_keep_kernel(const int32_t *k, uint32_t n, int32_t min_c, int32_t max_c, uint32_t *flag) {
+    const uint32_t j = blockIdx.x * TR_T + threadIdx.x;
+    if (j < n) flag[j] = (k[j] >= min_c && k[j] <= max_c) ? 1u : 0u;
+}
+__global__ void tr_compact3_kernel(const uint32_t *flag, const uint32_t *ex, uint32_t n, const int32_t *f,
+                                   const int32_t *s, const int32_t *k, int32_t *fo, int32_t *so, int32_t *ko) {
+    const uint32_t j = blockIdx.x * TR_T + threadIdx.x;
+    if (j >= n || !flag[j]) return;
+    const uint32_t q = ex[j];
+    fo[q] = f[j];
+    so[q] = s[j];
+    ko[q] = k[j];
+}
+}  // namespace
+
+hipError_t launch_trove_keep(const int32_t *f, const int32_t *s, const int32_t *k, uint32_t n, int32_t min_c,
+                             int32_t max_c, uint32_t *flag, uint32_t *ex, uint32_t *total, void *stmp, int32_t *fo,
+                             int32_t *so, int32_t *ko, hipStream_t st) {
+    if (!n) return hipMemsetAsync(total, 0, 4, st);
+    hipLaunchKernelGGL(tr_keep_kernel, tr_grid(n), dim3(TR_T), 0, st, k, n, min_c, max_c, flag);
+    hipError_t e = exclusive_scan_u32(flag, ex, n, total, stmp, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(tr_compact3_kernel, tr_grid(n), dim3(TR_T), 0, st, flag, ex, n, f, s, k, fo, so, ko);
+    return hipGetLastError();
+}
+}  // namespace sa

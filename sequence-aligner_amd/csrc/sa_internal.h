@@ -402,6 +402,11 @@ size_t kmerdata_temp_bytes(uint64_t n);
 hipError_t kmerdata_rank_device(const uint8_t *is_head, const uint32_t *bkt_first, uint64_t n, const DevReads &rd,
                                 const uint64_t *occ_off, uint32_t n_reads, int m_hash, uint32_t *rank, void *tmp,
                                 hipStream_t s, uint32_t *n_heads);
+// the pairs (f, s, k) whose count k is in [min_c, max_c], compacted in order into fo / so /
+// ko; their number in *total (device); flag / ex: n u32, stmp: scan_temp_bytes(n)
+hipError_t launch_trove_keep(const int32_t *f, const int32_t *s, const int32_t *k, uint32_t n, int32_t min_c,
+                             int32_t max_c, uint32_t *flag, uint32_t *ex, uint32_t *total, void *stmp, int32_t *fo,
+                             int32_t *so, int32_t *ko, hipStream_t st);
 hipError_t launch_trove_pair_keys(const int32_t *f, const int32_t *s, uint32_t n, int32_t *keys, hipStream_t st);
 hipError_t launch_trove_gather3(const uint32_t *order, uint32_t n, const int32_t *f, const int32_t *s, const int32_t *k,
                                 int32_t *fo, int32_t *so, int32_t *ko, hipStream_t st);
