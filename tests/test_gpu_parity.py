@@ -427,3 +427,27 @@ def test_wide_band_lane_kernels_match_oracle(oracle_mod, mixed, k):
     ov = gpu_run(reads=reads, wide=True, **st)
     assert ov.stats()["dispatched"] > 100
     compare_with_oracle(oracle_mod, ov, r, True)
+
+
+@pytest.mark.parametrize("k", [15, 12])
+def test_device_trove_layout_equals_host_replay(tmp_path, k):
+    """The strict-id output order comes from GNU Trove layouts built on the device
+    (trove_replay.hip: eviction-chain reservations per table of the rehash chain); the
+    host replay (csrc/host/trove.h, one insert after another) is kept behind
+    SA_HOST_TROVE=1.  On the c_ruddii reads (32,000 reads: ~2M KmerData and ~3M PairData
+    keys, 15-17 tables each) both give the same .ovl bytes, and with SA_OPT_KEEP_PAIRS off
+    only the dispatched pairs come back from the device."""
+    import subprocess
+    cli = os.path.join(os.path.dirname(sao.__file__), "build", "sa-overlap")
+    fa = tmp_path / "c_ruddii.seq"
+    fa.write_bytes(H.reads_fasta_bytes(H.c_ruddii_reads()))
+    outs = []
+    for host in ("0", "1"):
+        o = tmp_path / ("o%s.ovl" % host)
+        env = dict(os.environ, SA_HOST_TROVE=host)
+        r = subprocess.run([cli, "-i", str(fa), "-o", str(o), "-k", str(k), "--strict-ids"], capture_output=True,
+                           timeout=300, env=env)
+        assert r.returncode == 0, r.stderr
+        outs.append(o.read_bytes())
+    assert outs[0].count(b"{OVL") > 1000
+    assert outs[0] == outs[1]
