@@ -23,6 +23,7 @@
 #include <chrono>
 #include <string>
 #include <unordered_map>
+#include <thread>
 #include <vector>
 
 #include "../sa_internal.h"
@@ -1676,27 +1677,69 @@ int host_results(sa_ctx *c) {
     }
     HostScope hs(c, SA_STAGE_FORMAT);
     // "{OVL\nadj:N\nrds:" + lead + "," + trail + "\nscr:0\nahg:" + ahg + "\nbhg:" + bhg + "\n}" + "\n"
-    // (Overlap.print, ObjectStore.scala:127-135; Project4.scala:814-818), at most 88 bytes
-    uint64_t rec = 0;
-    for (uint64_t i = 0; i < nd; ++i) rec += (c->alns[i].flags & SA_ALN_OVL_VALID) != 0;
-    c->ovl.resize(rec * 88);
-    char *p = &c->ovl[0], *const p0 = p;
+    // (Overlap.print, ObjectStore.scala:127-135; Project4.scala:814-818).  In chunks on up to 8
+    // host threads: each chunk's exact byte count first, then every chunk formats straight into
+    // its place (round 6: 7 ms for configs[0]'s 366k records on one thread)
     static const char H1[] = "{OVL\nadj:N\nrds:", H2[] = "\nscr:0\nahg:", H3[] = "\nbhg:", H4[] = "\n}\n";
-    for (uint64_t i = 0; i < nd; ++i) {
-        const sa_alignment &a = c->alns[i];
-        if (!(a.flags & SA_ALN_OVL_VALID)) continue;
-        const int ra = (a.flags & SA_ALN_DUD) ? 0 : a.lead, rb = (a.flags & SA_ALN_DUD) ? 0 : a.trail;
-        memcpy(p, H1, sizeof(H1) - 1); p += sizeof(H1) - 1;
-        p = put_int(p, ra);
-        *p++ = ',';
-        p = put_int(p, rb);
-        memcpy(p, H2, sizeof(H2) - 1); p += sizeof(H2) - 1;
-        p = put_int(p, a.ahg);
-        memcpy(p, H3, sizeof(H3) - 1); p += sizeof(H3) - 1;
-        p = put_int(p, a.bhg);
-        memcpy(p, H4, sizeof(H4) - 1); p += sizeof(H4) - 1;
-    }
-    c->ovl.resize((size_t)(p - p0));
+    constexpr size_t FIXED = (sizeof(H1) - 1) + 1 + (sizeof(H2) - 1) + (sizeof(H3) - 1) + (sizeof(H4) - 1);
+    auto ndig = [](int32_t v) {
+        uint32_t u = v < 0 ? 0u - (uint32_t)v : (uint32_t)v;
+        size_t n = v < 0 ? 2 : 1;
+        while (u >= 10) { u /= 10; ++n; }
+        return n;
+    };
+    auto fields = [&](const sa_alignment &a, int &ra, int &rb) {
+        ra = (a.flags & SA_ALN_DUD) ? 0 : a.lead;
+        rb = (a.flags & SA_ALN_DUD) ? 0 : a.trail;
+    };
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const uint64_t T = std::max<uint64_t>(1, std::min<uint64_t>({8ull, (uint64_t)hw, nd / 20000 + 1}));
+    std::vector<uint64_t> cbytes(T + 1, 0), crec(T, 0);
+    auto chunk = [&](uint64_t t, uint64_t &a0, uint64_t &a1) { a0 = nd * t / T; a1 = nd * (t + 1) / T; };
+    auto run = [&](auto f) {
+        if (T == 1) { f(0); return; }
+        std::vector<std::thread> th;
+        for (uint64_t t = 0; t < T; ++t) th.emplace_back(f, t);
+        for (auto &x : th) x.join();
+    };
+    run([&](uint64_t t) {
+        uint64_t a0, a1, b = 0, r = 0;
+        chunk(t, a0, a1);
+        for (uint64_t i = a0; i < a1; ++i) {
+            const sa_alignment &a = c->alns[i];
+            if (!(a.flags & SA_ALN_OVL_VALID)) continue;
+            int ra, rb;
+            fields(a, ra, rb);
+            b += FIXED + ndig(ra) + ndig(rb) + ndig(a.ahg) + ndig(a.bhg);
+            ++r;
+        }
+        cbytes[t + 1] = b;
+        crec[t] = r;
+    });
+    uint64_t rec = 0;
+    for (uint64_t t = 0; t < T; ++t) { cbytes[t + 1] += cbytes[t]; rec += crec[t]; }
+    c->ovl.resize(cbytes[T]);
+    char *const base = &c->ovl[0];
+    run([&](uint64_t t) {
+        uint64_t a0, a1;
+        chunk(t, a0, a1);
+        char *p = base + cbytes[t];
+        for (uint64_t i = a0; i < a1; ++i) {
+            const sa_alignment &a = c->alns[i];
+            if (!(a.flags & SA_ALN_OVL_VALID)) continue;
+            int ra, rb;
+            fields(a, ra, rb);
+            memcpy(p, H1, sizeof(H1) - 1); p += sizeof(H1) - 1;
+            p = put_int(p, ra);
+            *p++ = ',';
+            p = put_int(p, rb);
+            memcpy(p, H2, sizeof(H2) - 1); p += sizeof(H2) - 1;
+            p = put_int(p, a.ahg);
+            memcpy(p, H3, sizeof(H3) - 1); p += sizeof(H3) - 1;
+            p = put_int(p, a.bhg);
+            memcpy(p, H4, sizeof(H4) - 1); p += sizeof(H4) - 1;
+        }
+    });
     c->stats.ovl_records = rec;
     c->host_valid = true;
     return SA_OK;
