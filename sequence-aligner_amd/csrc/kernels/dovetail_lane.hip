@@ -1016,7 +1016,10 @@ __device__ __forceinline__ void band_row_x2(BandX2 &S, const int32_t u, const ui
     S.sel[15] = x2_sel(bnew[0], bnew[1]);
 }
 
-__global__ __launch_bounds__(256) void dovetail_p2tbx2_kernel(DevReads rd, const int32_t *lead, const int32_t *trail,
+#ifndef SA_P2_WAVES  // (A/B builds: a minimum of waves per SIMD for the packed phase 2)
+#define SA_P2_WAVES 1
+#endif
+__global__ __launch_bounds__(256, SA_P2_WAVES) void dovetail_p2tbx2_kernel(DevReads rd, const int32_t *lead, const int32_t *trail,
                                                               uint64_t npairs, uint64_t t0, uint64_t nt, AlignParams P,
                                                               const int32_t *p1, const uint32_t *order,
                                                               DevAlignment *out, int32_t *err, uint32_t *tbbuf) {
