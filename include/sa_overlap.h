@@ -178,9 +178,12 @@ enum sa_option {
                                   entries (12 B each, counted by their upper bound) one
                                   shard may produce per lead-range pass; the shards then
                                   count, exchange and reduce 1/npass of every owner's leads
-                                  per pass (sa_dist_plan).  0 (default): half of the free
+                                  per pass (sa_dist_plan).  0 (default): 60 % of the free
                                   device memory after the bucket build, shared by the
-                                  shards on the device, at ~40 B per entry */
+                                  shards on the device, at 67 B x rho per bound entry
+                                  (rho = 1.5 x the partials / bound ratio of these reads,
+                                  probed on their first build; one pass whenever the
+                                  bound is far from the memory) */
     SA_OPT_LEAN_MEMORY = 10    /* virtual shards (one device): the shards' transients (sort
                                   and bucket-build scratch, pair-counter regions, reduce
                                   scratch) come from one pool that each shard borrows for
