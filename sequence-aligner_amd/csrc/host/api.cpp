@@ -2742,6 +2742,10 @@ int sa_dist_reduce_pass(sa_ctx *c, const void *fst, const void *snd, const void 
     HIPCHK(hipMemsetAsync(cnt->totals, 0, sizeof(cnt->totals), c->stream));
     HIPCHK(hipMemsetAsync(&cnt->overflow_n, 0, sizeof(cnt->overflow_n), c->stream));
     auto finish = [&](uint32_t nd, unsigned long long ndist) {
+        // (the next pass's tier routing, from the tiers or the sort alike; SA_LR_ROUTE=0:
+        // the m / ranks floor alone, A/B)
+        static const bool route_on = !getenv("SA_LR_ROUTE") || atoi(getenv("SA_LR_ROUTE")) != 0;
+        if (n && route_on) c->dist_route = (float)((double)ndist / (double)n);
         c->disp_acc = acc + nd;
         c->n_disp = c->disp_acc;
         c->stats.pairs += ndist;
@@ -2756,8 +2760,8 @@ int sa_dist_reduce_pass(sa_ctx *c, const void *fst, const void *snd, const void 
     // filtered in LDS (one wave per lead; one block for a lead with more than
     // 192 distinct partners), then one scan + one copy in lead-descending
     // order; a lead with more than 3,072 (high-copy repeats) falls back to the
-    // (lead, trail) radix sort below
-    {
+    // (lead, trail) radix sort below (SA_LR_FORCE_SORT=1 sends every pass there: tests)
+    if (!(getenv("SA_LR_FORCE_SORT") && atoi(getenv("SA_LR_FORCE_SORT")) != 0)) {
         uint32_t *lr;
         uint2 *seg = (uint2 *)ok;
         ENSURE(c->d_lr, 5 * ((size_t)nl + 1), &lr);
@@ -2770,8 +2774,8 @@ int sa_dist_reduce_pass(sa_ctx *c, const void *fst, const void *snd, const void 
             StageScope st(c, SA_STAGE_ORDER);
             HIPCHK(launch_lead_reduce((const uint32_t *)fst, (const uint32_t *)snd, (const uint32_t *)cnt_in, n, lbase,
                                       nl, c->set.min_collisions, c->set.max_collisions, lcnt, loff, lcur, seg, kcnt,
-                                      cnt->distinct, &cnt->overflow_n, (uint32_t)c->nranks, scan2, &cnt->totals[1],
-                                      c->stream));
+                                      cnt->distinct, &cnt->overflow_n, (uint32_t)c->nranks, c->dist_route, scan2,
+                                      &cnt->totals[1], c->stream));
             HIPCHK(exclusive_scan_u32(kcnt, kex, nl, &cnt->totals[0], scan2, c->stream));
         }
         HIPCHK(hipMemcpyAsync(hp, cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));

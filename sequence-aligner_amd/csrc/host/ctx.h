@@ -116,6 +116,7 @@ struct sa_ctx {
     bool dist = false, dist_reads = false;
     int rank = 0, nranks = 1, log_ranks = 0;
     int dist_src_shift = 0;                // this build's packed values are source-relative (RecvGen)
+    float dist_route = 0.f;                // distinct partners per partial of the last reduced pass (tier routing)
     std::vector<uint32_t> dstarts;   // [nranks+1] first global read of each rank
     std::vector<int32_t> dlen;       // length of every global read
     std::vector<uint64_t> gocc;      // global occurrence offsets [N+1]

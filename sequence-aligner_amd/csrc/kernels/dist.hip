@@ -254,7 +254,7 @@ constexpr uint32_t LR_ROUTE = 2 * LR_FILL, LRM_CHUNK = 16;
 // start of the lead's own segment; kcnt[l] = kept (KmerTable.calcDispatchData's filter,
 // :155-187).  More than FILL distinct partners (or a failed probe run): kcnt[l] = 0 and
 // the lead is listed for the next tier.  Returns the distinct partners counted.
-template <int SLOTS, int FILL>
+template <int SLOTS, int FILL, bool CHECK>
 __device__ __forceinline__ uint32_t lead_wave(uint2 *seg, const uint32_t *loff, uint32_t l, uint32_t *key,
                                               uint32_t *val, uint2 *kept, int lane, int32_t min_c, int32_t max_c,
                                               uint32_t *kcnt, uint32_t next_mark) {
@@ -267,17 +267,37 @@ __device__ __forceinline__ uint32_t lead_wave(uint2 *seg, const uint32_t *loff, 
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
     const uint32_t s0 = loff[l], m = loff[l + 1] - s0;
     bool ovf = false;
-    for (uint32_t j = lane; j < m; j += 64) {
-        const uint2 v = seg[s0 + j];
-        uint32_t h = (v.x * 0x9E3779B1u) >> (32 - LOG);
-        int probe = 0;
-        for (; probe < 64; ++probe) {
-            uint32_t old = lds_relaxed(&key[h]);
-            if (old == LR_EMPTY) old = atomicCAS(&key[h], LR_EMPTY, v.x);
-            if (old == LR_EMPTY || old == v.x) { atomicAdd(&val[h], v.y); break; }
-            h = (h + 1) & (SLOTS - 1);
+    // CHECK: stop once the wave has inserted more than FILL keys -- the lead cannot fit
+    // (round 6: at configs[4]-shape k = 12 the 1,024-slot tier hashed every partial of
+    // ~5,000-partial leads into a full table, 64-probe runs each -- 9.3 ms per shard and
+    // pass, the largest kernel of the build -- before handing them on).  Checked once per
+    // 8 x 64 partials, and only while the routing has no ratio to go by (the first pass of
+    // a context): the check cost the tiers 5-9 % at configs[3]'s real density, where the
+    // ratio keeps such leads out of them
+    uint32_t fresh = 0;
+    const uint32_t blk = CHECK ? 8 * 64 : m;
+    for (uint32_t b0 = 0; b0 < m; b0 += blk) {
+        const uint32_t b1 = m - b0 > blk ? b0 + blk : m;
+        for (uint32_t j = b0 + (uint32_t)lane; j < b1; j += 64) {
+            const uint2 v = seg[s0 + j];
+            uint32_t h = (v.x * 0x9E3779B1u) >> (32 - LOG);
+            int probe = 0;
+            for (; probe < 64; ++probe) {
+                uint32_t old = lds_relaxed(&key[h]);
+                if (old == LR_EMPTY) old = atomicCAS(&key[h], LR_EMPTY, v.x);
+                if (old == LR_EMPTY || old == v.x) {
+                    if (CHECK) fresh += old == LR_EMPTY ? 1u : 0u;
+                    atomicAdd(&val[h], v.y);
+                    break;
+                }
+                h = (h + 1) & (SLOTS - 1);
+            }
+            if (probe == 64) ovf = true;
         }
-        if (probe == 64) ovf = true;
+        if (CHECK && (__any(ovf) || (uint32_t)__shfl((int)wave_incl_add(fresh), 63, 64) > (uint32_t)FILL)) {
+            ovf = true;
+            break;
+        }
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
@@ -322,14 +342,22 @@ __device__ __forceinline__ uint32_t lead_wave(uint2 *seg, const uint32_t *loff, 
 }
 
 // The tiers' marks in kcnt: a lead the first table cannot take is marked KC_MID (the
-// 1,024-slot wave tier) or KC_BIG (the 4,096-slot block tier) -- a mark, not a list: at
-// configs[3]'s real density nearly every lead leaves the first tier, and one list cursor
-// took ~89k same-address atomics per shard and pass (0.9 ms).  Leads are routed by their
-// partial count m: a lead has at least m / ranks distinct partners (a partner meets it
-// on at most every rank once), so m > ranks x FILL cannot fit a tier and skips it, and
-// m > ranks x 3,072 sends the whole reduce to the sort at once (*overflow).
-constexpr uint32_t KC_MID = 0xFFFFFFFFu, KC_BIG = 0xFFFFFFFEu;
+// 1,024-slot wave tier), KC_BIG (the 4,096-slot block tier) or KC_HUGE (the 16,384-slot
+// block tier) -- a mark, not a list: at configs[3]'s real density nearly every lead
+// leaves the first tier, and one list cursor took ~89k same-address atomics per shard and
+// pass (0.9 ms).  Leads are routed by their partial count m: a lead has at least m / ranks
+// distinct partners (a partner meets it on at most every rank once), and about m x route
+// (the last pass's distinct partners per partial), so a lead whose estimate passes a
+// tier's FILL skips it, and one past 12,288 sends the whole reduce to the sort at once
+// (*overflow).  Only the m / ranks floor is a proof; a wrong estimate costs time.
+constexpr uint32_t KC_MID = 0xFFFFFFFFu, KC_BIG = 0xFFFFFFFEu, KC_HUGE = 0xFFFFFFFDu;
 constexpr int LRB_SLOTS = 4096, LRB_FILL = 3072;
+// the fourth tier (round 6): configs[4]-shape k = 12 leads meet ~4,000-8,000 distinct
+// partners, past the 4,096-slot table, and every pass went to the sort
+constexpr int LRH_SLOTS = 16384, LRH_FILL = 12288, LRH_THREADS = 1024;
+// leads per chunk of the block tiers: a pass holds ~10^4-10^5 leads, and 256-lead chunks
+// left most CUs without one
+constexpr uint32_t LRB_CHUNK = 64;
 __device__ __forceinline__ void set_overflow(uint32_t *overflow) {
     if (__hip_atomic_load(overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) atomicOr(overflow, 1u);
 }
@@ -338,7 +366,7 @@ __device__ __forceinline__ void set_overflow(uint32_t *overflow) {
 __global__ __launch_bounds__(256) void lead_reduce_kernel(uint2 *seg, const uint32_t *loff, uint32_t nl, int32_t min_c,
                                                           int32_t max_c, uint32_t *kcnt,
                                                           unsigned long long *distinct, uint32_t ranks,
-                                                          uint32_t *overflow) {
+                                                          float route, uint32_t *overflow) {
     __shared__ uint32_t key[4][LR_SLOTS], val[4][LR_SLOTS];
     __shared__ uint2 kept[4][LR_FILL];
     __shared__ uint32_t nd_blk;
@@ -349,14 +377,23 @@ __global__ __launch_bounds__(256) void lead_reduce_kernel(uint2 *seg, const uint
     if (l < nl) {
         uint32_t nd = 0;
         const uint64_t m = loff[l + 1] - loff[l];
-        if (m > (uint64_t)ranks * LRB_FILL) {
+        // est: the lead's expected distinct partners -- the m / ranks floor, or m x the
+        // last pass's distinct-per-partial ratio (x 0.85 for the spread between leads).  A
+        // lead routed past a tier it would have fit costs time, never results
+        const uint64_t lo = m / ranks, ex = (uint64_t)((float)m * route * 0.85f);
+        const uint64_t est = lo > ex ? lo : ex;
+        if (m > (uint64_t)ranks * LRH_FILL || est > (uint64_t)LRH_FILL) {
+            // (an estimate past the last tier sends the pass to the sort now: the tiers
+            // would hash the lead twice before failing on it)
             if (lane == 0) { kcnt[l] = 0; set_overflow(overflow); }
-        } else if (m > (uint64_t)ranks * LRM_FILL) {
+        } else if (est > (uint64_t)LRB_FILL) {
+            if (lane == 0) kcnt[l] = KC_HUGE;
+        } else if (est > (uint64_t)LRM_FILL) {
             if (lane == 0) kcnt[l] = KC_BIG;
         } else if (m > LR_ROUTE) {
             if (lane == 0) kcnt[l] = KC_MID;
         } else {
-            nd = lead_wave<LR_SLOTS, LR_FILL>(seg, loff, l, key[w], val[w], kept[w], lane, min_c, max_c, kcnt, KC_MID);
+            nd = lead_wave<LR_SLOTS, LR_FILL, false>(seg, loff, l, key[w], val[w], kept[w], lane, min_c, max_c, kcnt, KC_MID);
         }
         if (lane == 0 && nd) atomicAdd(&nd_blk, nd);  // (a marked lead is counted by its tier)
     }
@@ -366,6 +403,7 @@ __global__ __launch_bounds__(256) void lead_reduce_kernel(uint2 *seg, const uint
 
 // the second tier: one-wave blocks (8 KB of LDS each: 20 per CU) striding over the leads
 // LRM_CHUNK at a time -- one coalesced load of their kcnt, a ballot of the marked ones
+template <bool CHECK>
 __global__ __launch_bounds__(64) void lead_reduce_mid_kernel(uint2 *seg, const uint32_t *loff, uint32_t nl,
                                                              int32_t min_c, int32_t max_c, uint32_t *kcnt,
                                                              unsigned long long *distinct, const uint32_t *overflow) {
@@ -386,70 +424,91 @@ __global__ __launch_bounds__(64) void lead_reduce_mid_kernel(uint2 *seg, const u
         while (todo) {
             const int b = __builtin_ctzll(todo);
             todo &= todo - 1;
-            nd += lead_wave<LRM_SLOTS, LRM_FILL>(seg, loff, c0 + (uint32_t)b, key, val, kept, lane, min_c, max_c,
+            nd += lead_wave<LRM_SLOTS, LRM_FILL, CHECK>(seg, loff, c0 + (uint32_t)b, key, val, kept, lane, min_c, max_c,
                                                  kcnt, KC_BIG);
         }
     }
     if (lane == 0 && nd) atomicAdd(&distinct[blockIdx.x % NSHARD], nd);
 }
 
-// the third tier: 256-thread blocks striding over the leads 256 at a time, each marked
-// KC_BIG lead summed by the whole block in a 4,096-slot table (3,072 partners) and filtered
-// as above, the kept entries ranked by trail over the block; beyond 3,072 partners
-// *overflow sends the caller to the sort
-__global__ __launch_bounds__(256) void lead_reduce_big_kernel(uint2 *seg, const uint32_t *loff, uint32_t nl,
-                                                              int32_t min_c, int32_t max_c, uint32_t *kcnt,
-                                                              unsigned long long *distinct, uint32_t *overflow) {
-    __shared__ uint32_t key[LRB_SLOTS], val[LRB_SLOTS];
-    __shared__ uint2 kept[LRB_FILL];
-    __shared__ uint32_t fill, bad, nk, nlist, stop, list[256];
-    for (uint32_t c0 = blockIdx.x * 256u; c0 < nl; c0 += gridDim.x * 256u) {
-        __syncthreads();  // (list / nlist of the previous chunk consumed)
-        if (threadIdx.x == 0) nlist = 0;
+// The block tiers: blocks of NT threads striding over the leads LRB_CHUNK at a time, each
+// lead marked MARK summed by the whole block in a SLOTS-slot table (FILL partners) and
+// filtered as above, the kept entries ranked by trail over the block.  Past FILL partners
+// (or a failed probe run) the block stops hashing the lead at once and marks it NEXT, or
+// with NEXT == 0 sets *overflow, which sends the caller to the sort.  The kept entries
+// alias the table (read into registers first): 16,384 slots are 128 KB, one block per CU.
+template <int SLOTS, int FILL, int NT>
+__device__ __forceinline__ void lead_block_tier(uint2 *seg, const uint32_t *loff, uint32_t nl, int32_t min_c,
+                                                int32_t max_c, uint32_t *kcnt, unsigned long long *distinct,
+                                                uint32_t *overflow, uint32_t mark, uint32_t next, uint32_t *tab) {
+    constexpr int LOG = SLOTS == 4096 ? 12 : 14;
+    static_assert((1 << LOG) == SLOTS, "table size");
+    constexpr int PER = SLOTS / NT;
+    constexpr int MAXP = 256;
+    __shared__ uint32_t fill, bad, nk, stop;
+    __shared__ unsigned long long todo_s;
+    uint32_t *key = tab, *val = tab + SLOTS;
+    uint2 *kept = reinterpret_cast<uint2 *>(tab);
+    for (uint32_t c0 = blockIdx.x * LRB_CHUNK; c0 < nl; c0 += gridDim.x * LRB_CHUNK) {
+        __syncthreads();  // (todo_s of the previous chunk consumed)
+        if (threadIdx.x < 64) {
+            const uint32_t l0 = c0 + threadIdx.x;
+            const unsigned long long b = __ballot(l0 < nl && kcnt[l0] == mark);
+            if (threadIdx.x == 0) todo_s = b;
+        }
         __syncthreads();
-        const uint32_t l0 = c0 + threadIdx.x;
-        if (l0 < nl && kcnt[l0] == KC_BIG) list[atomicAdd(&nlist, 1u)] = l0;
-        __syncthreads();
-        const uint32_t nb = nlist;
-        for (uint32_t it = 0; it < nb; ++it) {
+        unsigned long long todo = todo_s;
+        while (todo) {
+            const uint32_t l = c0 + (uint32_t)__builtin_ctzll(todo);
+            todo &= todo - 1;
             __syncthreads();  // the previous lead's LDS consumed
-            for (int j = threadIdx.x; j < LRB_SLOTS; j += 256) { key[j] = LR_EMPTY; val[j] = 0; }
+            for (int j = threadIdx.x; j < SLOTS; j += NT) { key[j] = LR_EMPTY; val[j] = 0; }
             if (threadIdx.x == 0) {
                 fill = 0; bad = 0; nk = 0;
                 stop = __hip_atomic_load(overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             __syncthreads();
             if (stop) return;  // (block-uniform: the sort takes over, this block's work would be redone)
-            const uint32_t l = list[it];
             const uint32_t s0 = loff[l], m = loff[l + 1] - s0;
-            for (uint32_t j = threadIdx.x; j < m; j += 256) {
+            for (uint32_t j = threadIdx.x; j < m; j += NT) {
+                if (lds_relaxed(&bad)) break;  // (the lead cannot fit: stop hashing it)
                 const uint2 v = seg[s0 + j];
-                uint32_t h = (v.x * 0x9E3779B1u) >> 20;  // 12 bits: LRB_SLOTS
+                uint32_t h = (v.x * 0x9E3779B1u) >> (32 - LOG);
                 int probe = 0;
-                for (; probe < 256; ++probe) {
+                for (; probe < MAXP; ++probe) {
                     uint32_t old = lds_relaxed(&key[h]);
                     if (old == LR_EMPTY) old = atomicCAS(&key[h], LR_EMPTY, v.x);
                     if (old == LR_EMPTY || old == v.x) {
-                        if (old == LR_EMPTY && atomicAdd(&fill, 1u) >= LRB_FILL) bad = 1;
+                        if (old == LR_EMPTY && atomicAdd(&fill, 1u) >= (uint32_t)FILL) bad = 1;
                         atomicAdd(&val[h], v.y);
                         break;
                     }
-                    h = (h + 1) & (LRB_SLOTS - 1);
+                    h = (h + 1) & (SLOTS - 1);
                 }
-                if (probe == 256) bad = 1;
+                if (probe == MAXP) bad = 1;
             }
             __syncthreads();
             if (bad) {
-                if (threadIdx.x == 0) set_overflow(overflow);
+                if (threadIdx.x == 0) {
+                    if (next) kcnt[l] = next;
+                    else set_overflow(overflow);
+                }
                 continue;
             }
-            for (int j = threadIdx.x; j < LRB_SLOTS; j += 256) {
-                const uint32_t k = key[j], c = val[j];
-                if (k != LR_EMPTY && (int32_t)c >= min_c && (int32_t)c <= max_c) kept[atomicAdd(&nk, 1u)] = make_uint2(k, c);
+            uint32_t kk[PER], kc[PER];
+#pragma unroll
+            for (int q = 0; q < PER; ++q) {
+                kk[q] = key[q * NT + threadIdx.x];
+                kc[q] = val[q * NT + threadIdx.x];
             }
+            __syncthreads();  // (the table is read: kept overwrites it)
+#pragma unroll
+            for (int q = 0; q < PER; ++q)
+                if (kk[q] != LR_EMPTY && (int32_t)kc[q] >= min_c && (int32_t)kc[q] <= max_c)
+                    kept[atomicAdd(&nk, 1u)] = make_uint2(kk[q], kc[q]);
             __syncthreads();
             const uint32_t k = nk;
-            for (uint32_t j = threadIdx.x; j < k; j += 256) {
+            for (uint32_t j = threadIdx.x; j < k; j += NT) {
                 const uint2 e = kept[j];
                 uint32_t r = 0;
                 for (uint32_t q = 0; q < k; ++q) r += kept[q].x < e.x ? 1u : 0u;
@@ -461,6 +520,26 @@ __global__ __launch_bounds__(256) void lead_reduce_big_kernel(uint2 *seg, const 
             }
         }
     }
+}
+
+// the third tier: 4,096 slots (3,072 partners) per 256-thread block, 32 KB: 5 per CU
+__global__ __launch_bounds__(256) void lead_reduce_big_kernel(uint2 *seg, const uint32_t *loff, uint32_t nl,
+                                                              int32_t min_c, int32_t max_c, uint32_t *kcnt,
+                                                              unsigned long long *distinct, uint32_t *overflow) {
+    __shared__ uint32_t tab[2 * LRB_SLOTS];
+    lead_block_tier<LRB_SLOTS, LRB_FILL, 256>(seg, loff, nl, min_c, max_c, kcnt, distinct, overflow, KC_BIG, KC_HUGE,
+                                              tab);
+}
+
+// the fourth tier: 16,384 slots (12,288 partners) per 1,024-thread block, 128 KB of
+// dynamic LDS: one per CU
+__global__ __launch_bounds__(LRH_THREADS) void lead_reduce_huge_kernel(uint2 *seg, const uint32_t *loff, uint32_t nl,
+                                                                       int32_t min_c, int32_t max_c, uint32_t *kcnt,
+                                                                       unsigned long long *distinct,
+                                                                       uint32_t *overflow) {
+    extern __shared__ __align__(16) uint32_t htab[];
+    lead_block_tier<LRH_SLOTS, LRH_FILL, LRH_THREADS>(seg, loff, nl, min_c, max_c, kcnt, distinct, overflow, KC_HUGE,
+                                                      0u, htab);
 }
 
 // lead-descending dispatch: lead l's kept entries go to total - kex[l] - kcnt[l]
@@ -483,7 +562,7 @@ __global__ void lead_copy_kernel(const uint2 *seg, const uint32_t *loff, const u
 hipError_t launch_lead_reduce(const uint32_t *fst, const uint32_t *snd, const uint32_t *cnt, uint64_t n, uint32_t base,
                               uint32_t nl, int32_t min_c, int32_t max_c, uint32_t *lcnt, uint32_t *loff, uint32_t *lcur,
                               uint2 *seg, uint32_t *kcnt, unsigned long long *distinct, uint32_t *overflow,
-                              uint32_t ranks, void *scan_tmp, uint32_t *total_dev, hipStream_t s) {
+                              uint32_t ranks, float route, void *scan_tmp, uint32_t *total_dev, hipStream_t s) {
     if (!nl) return hipSuccess;
     hipError_t e;
     if ((e = hipMemsetAsync(lcnt, 0, (size_t)nl * 4, s)) != hipSuccess) return e;
@@ -497,13 +576,23 @@ hipError_t launch_lead_reduce(const uint32_t *fst, const uint32_t *snd, const ui
     if (n) hipLaunchKernelGGL(lead_tile_kernel<true>, tiles, dim3(LT_THREADS), 0, s, fst, snd, cnt, n, base, lcnt,
                               (const uint32_t *)loff, lcur, seg);
     hipLaunchKernelGGL(lead_reduce_kernel, dim3((nl + 3) / 4), dim3(256), 0, s, seg, loff, nl, min_c, max_c, kcnt,
-                       distinct, ranks, overflow);
-    const uint32_t cm = (nl + LRM_CHUNK - 1) / LRM_CHUNK, c256 = (nl + 255) / 256;
-    hipLaunchKernelGGL(lead_reduce_mid_kernel, dim3(cm < 256u * 20u ? cm : 256u * 20u), dim3(64), 0, s, seg, loff, nl,
-                       min_c, max_c, kcnt, distinct, (const uint32_t *)overflow);
-    // (56 KB of LDS per block: 2 per CU)
-    hipLaunchKernelGGL(lead_reduce_big_kernel, dim3(c256 < 512u ? c256 : 512u), dim3(256), 0, s, seg, loff, nl, min_c,
-                       max_c, kcnt, distinct, overflow);
+                       distinct, ranks, route, overflow);
+    const uint32_t cm = (nl + LRM_CHUNK - 1) / LRM_CHUNK;
+    const dim3 gm(cm < 256u * 20u ? cm : 256u * 20u);
+    if (route > 0.f)
+        hipLaunchKernelGGL(lead_reduce_mid_kernel<false>, gm, dim3(64), 0, s, seg, loff, nl, min_c, max_c, kcnt,
+                           distinct, (const uint32_t *)overflow);
+    else
+        hipLaunchKernelGGL(lead_reduce_mid_kernel<true>, gm, dim3(64), 0, s, seg, loff, nl, min_c, max_c, kcnt, distinct,
+                           (const uint32_t *)overflow);
+    const uint32_t cb = (nl + LRB_CHUNK - 1) / LRB_CHUNK;
+    hipLaunchKernelGGL(lead_reduce_big_kernel, dim3(cb < 256u * 5u ? cb : 256u * 5u), dim3(256), 0, s, seg, loff, nl,
+                       min_c, max_c, kcnt, distinct, overflow);
+    constexpr size_t hlds = 2u * LRH_SLOTS * 4u;
+    (void)hipFuncSetAttribute((const void *)lead_reduce_huge_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)hlds);
+    hipLaunchKernelGGL(lead_reduce_huge_kernel, dim3(cb < 256u ? cb : 256u), dim3(LRH_THREADS), hlds, s, seg, loff,
+                       nl, min_c, max_c, kcnt, distinct, overflow);
     return hipGetLastError();
 }
 

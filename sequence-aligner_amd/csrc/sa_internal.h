@@ -659,7 +659,7 @@ hipError_t launch_reduce_heads(const uint64_t *skeys, const uint32_t *sidx, uint
 hipError_t launch_lead_reduce(const uint32_t *fst, const uint32_t *snd, const uint32_t *cnt, uint64_t n, uint32_t base,
                               uint32_t nl, int32_t min_c, int32_t max_c, uint32_t *lcnt, uint32_t *loff, uint32_t *lcur,
                               uint2 *seg, uint32_t *kcnt, unsigned long long *distinct, uint32_t *overflow,
-                              uint32_t ranks, void *scan_tmp, uint32_t *total_dev, hipStream_t s);
+                              uint32_t ranks, float route, void *scan_tmp, uint32_t *total_dev, hipStream_t s);
 // the lead-descending dispatch from the reduced segments (kex = exclusive scan
 // of kcnt, total = its sum); ids 1-based, lead = base + l + 1
 hipError_t launch_lead_copy(const uint2 *seg, const uint32_t *loff, const uint32_t *kcnt, const uint32_t *kex,

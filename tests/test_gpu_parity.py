@@ -416,6 +416,38 @@ def test_sharded_hip_matches_single_gpu(P, repeat, budget, tmp_path):
     assert len(npass) == 1 and (npass.pop() > 1) == (budget is not None)
 
 
+@pytest.mark.parametrize("copies,force_sort", [(6000, False), (13000, False), (6000, True)])
+def test_virtual_shards_reduce_tiers(copies, force_sort, monkeypatch):
+    """The sharded reduce's lead tiers on 2 virtual shards: two 15-mers in `copies` short
+    reads give leads up to ~copies distinct partners, every pair kept (2 collisions) --
+    the 4,096- and 16,384-slot block tiers at 6,000, past the last tier (the whole pass
+    to the (lead, trail) sort) at 13,000, and SA_LR_FORCE_SORT=1 sends every pass to the
+    sort.  Dispatch equals the single context's exactly."""
+    rng = np.random.default_rng(90 + copies)
+    reads = mutate(H.synth_reads(600, 300, 9000, gc=0.5, seed=91, mixed=(250, 340)), rng, 3)
+    ma, mb = "ACGTTGCAACGTAGC", "TTGACCGATGCAAGT"
+    for i in range(copies):
+        s_ = "".join("ACGT"[x] for x in rng.integers(0, 4, 80))
+        p_ = 3 + i % 20
+        reads.append(s_[:p_] + ma + s_[p_ + 15:p_ + 30] + mb + s_[p_ + 45:])
+    st = dict(kmer_size=15, min_collisions=2)
+    if force_sort:
+        monkeypatch.setenv("SA_LR_FORCE_SORT", "1")
+    ov = sao.Overlapper(shards=2, id_mode=sao.SA_IDS_WIDE, **st)
+    ov.add_reads(reads)
+    ov.build()
+    got = ov.dispatch()
+    ov.close()
+    ref = sao.Overlapper(id_mode=sao.SA_IDS_WIDE, keep_pairs=False, **st)
+    ref.add_reads(reads)
+    ref.build()
+    want = ref.dispatch()
+    ref.close()
+    assert len(want[0]) > copies * copies // 8  # (most motif pairs kept)
+    for g, w in zip(got, want):
+        np.testing.assert_array_equal(g, w)
+
+
 @pytest.mark.parametrize("mixed,k", [((100, 1000), 15), ((600, 1500), 14)])
 def test_wide_band_lane_kernels_match_oracle(oracle_mod, mixed, k):
     """Reads up to 1,000-1,500 bp (configs[4]'s shape): bands of 16-31 cells run
