@@ -2757,10 +2757,10 @@ int sa_dist_reduce_pass(sa_ctx *c, const void *fst, const void *snd, const void 
         return (int)SA_OK;
     };
     // this rank's leads: per-lead segments of the received partials, summed and
-    // filtered in LDS (one wave per lead; one block for a lead with more than
-    // 192 distinct partners), then one scan + one copy in lead-descending
-    // order; a lead with more than 3,072 (high-copy repeats) falls back to the
-    // (lead, trail) radix sort below (SA_LR_FORCE_SORT=1 sends every pass there: tests)
+    // filtered in LDS (a wave per lead up to 768 distinct partners, a block per lead
+    // up to 12,288: dist.hip's four tiers), then one scan + one copy in lead-descending
+    // order; a lead with more than 12,288 (high-copy repeats, k = 12) sends the pass to
+    // the (lead, trail) radix sort below (SA_LR_FORCE_SORT=1 sends every pass there: tests)
     if (!(getenv("SA_LR_FORCE_SORT") && atoi(getenv("SA_LR_FORCE_SORT")) != 0)) {
         uint32_t *lr;
         uint2 *seg = (uint2 *)ok;
