@@ -358,6 +358,8 @@ constexpr int LRH_SLOTS = 16384, LRH_FILL = 12288, LRH_THREADS = 1024;
 // leads per chunk of the block tiers: a pass holds ~10^4-10^5 leads, and 256-lead chunks
 // left most CUs without one
 constexpr uint32_t LRB_CHUNK = 64;
+// kept entries past which a block tier sorts them (bitonic) instead of counting ranks
+constexpr int LRB_BITONIC = 512;
 __device__ __forceinline__ void set_overflow(uint32_t *overflow) {
     if (__hip_atomic_load(overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) atomicOr(overflow, 1u);
 }
@@ -508,11 +510,32 @@ __device__ __forceinline__ void lead_block_tier(uint2 *seg, const uint32_t *loff
                     kept[atomicAdd(&nk, 1u)] = make_uint2(kk[q], kc[q]);
             __syncthreads();
             const uint32_t k = nk;
-            for (uint32_t j = threadIdx.x; j < k; j += NT) {
-                const uint2 e = kept[j];
-                uint32_t r = 0;
-                for (uint32_t q = 0; q < k; ++q) r += kept[q].x < e.x ? 1u : 0u;
-                seg[s0 + r] = e;  // (every partial of the segment was read before the barrier)
+            if (k > (uint32_t)LRB_BITONIC) {
+                // many kept (high-copy repeats): a bitonic sort by trail over the next power
+                // of two (<= SLOTS entries of 8 B: the table's own bytes), pads last -- the
+                // rank count below is k^2 / NT reads each (6,000 kept: 11.6 -> 2.3 ms per
+                // 16,384-slot launch, profiles/r06/tiers/paths_*)
+                uint32_t P = 64;
+                while (P < k) P <<= 1;
+                for (uint32_t j = k + threadIdx.x; j < P; j += NT) kept[j] = make_uint2(LR_EMPTY, 0u);
+                __syncthreads();
+                for (uint32_t size = 2; size <= P; size <<= 1)
+                    for (uint32_t stride = size >> 1; stride; stride >>= 1) {
+                        for (uint32_t t = threadIdx.x; t < P / 2; t += NT) {
+                            const uint32_t i = 2 * t - (t & (stride - 1)), i2 = i + stride;
+                            const uint2 a = kept[i], b = kept[i2];
+                            if ((a.x > b.x) == ((i & size) == 0)) { kept[i] = b; kept[i2] = a; }
+                        }
+                        __syncthreads();
+                    }
+                for (uint32_t j = threadIdx.x; j < k; j += NT) seg[s0 + j] = kept[j];
+            } else {
+                for (uint32_t j = threadIdx.x; j < k; j += NT) {
+                    const uint2 e = kept[j];
+                    uint32_t r = 0;
+                    for (uint32_t q = 0; q < k; ++q) r += kept[q].x < e.x ? 1u : 0u;
+                    seg[s0 + r] = e;  // (every partial of the segment was read before the barrier)
+                }
             }
             if (threadIdx.x == 0) {
                 kcnt[l] = k;
